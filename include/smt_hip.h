@@ -1,0 +1,152 @@
+/*
+ * smt_hip.h — C-ABI of the MI355X (gfx950) SMT block-sparse fine-tuning hot path.
+ *
+ * Every entry point takes borrowed device pointers, sizes and a hipStream_t, never
+ * allocates or frees caller memory (workspaces are passed in), is enqueued on the
+ * given stream without a host synchronisation, and returns 0 on success or a
+ * negative SMT_E* code; smt_last_error() then returns a thread-local message.
+ *
+ * Reference interfaces each entry point replaces (paths relative to the
+ * yudaohai666/Sparse_Matrix_Tuning snapshot):
+ *   smt_tile_gather       deepspeed/smt/smt.py:317-325   tile copy W -> selected_weight
+ *   smt_tile_scatter      deepspeed/smt/smt.py:332-341   per-forward write-back tiles -> W
+ *                         (also smt.py:429-439, the merge in convert_matrix_sparsity_to_linear_layer)
+ *   smt_tile_wgrad        deepspeed/smt/smt.py:382-404   per-tile sum_b g[b,:,rows]^T x[b,:,cols]
+ *   smt_grad_accumulate   deepspeed/fine_tune.py:724-741, 751-764   warm-up fp32 grad harvest
+ *   smt_block_score       deepspeed/smt/smt_helper.py:67-78, 233-251   per-256x256-block scores
+ *   smt_sq_norm           DeepSpeed bf16/ZeRO global grad-norm for gradient_clipping=1.0
+ *                         (deepspeed/helpers/deepspeed_helpers.py:87; DeepSpeed 0.16.5, external)
+ *   smt_adamw_step        DeepSpeed FusedAdam(adam_w_mode=True) step over the tiles
+ *                         (deepspeed/fine_tune.py:352,361-363,773; DeepSpeed 0.16.5, external),
+ *                         fused with clip, bf16 cast and the tile -> W scatter
+ */
+#ifndef SMT_HIP_H
+#define SMT_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SMT_BLOCK_DIM 256           /* deepspeed/smt/smt.py:22 Block_dimension */
+
+/* status codes */
+#define SMT_OK 0
+#define SMT_E_INVALID (-1)          /* bad argument (null pointer, negative size, bad enum) */
+#define SMT_E_ALIGN (-2)            /* pointer / leading dimension not 16-byte aligned */
+#define SMT_E_WORKSPACE (-3)        /* workspace too small */
+#define SMT_E_LAUNCH (-4)           /* hipLaunchKernel / hipGetLastError failure */
+
+/* element dtypes */
+#define SMT_DTYPE_BF16 0
+#define SMT_DTYPE_FP32 1
+#define SMT_DTYPE_FP16 2
+
+/* block-score strategies, smt_helper.py:71-78 */
+#define SMT_SCORE_MEAN_ABS 0        /* mean(dim=(1,3)).abs()  -> raw sum of g      */
+#define SMT_SCORE_ABS_MEAN 1        /* abs().mean(dim=(1,3))  -> raw sum of |g|    */
+#define SMT_SCORE_L1 2              /* abs().sum(dim=(1,3))   -> raw sum of |g|    */
+#define SMT_SCORE_L2 3              /* sqrt(sum(abs()**2))    -> raw sum of g*g    */
+
+/* AdamW update formulas */
+#define SMT_ADAM_DEEPSPEED 0        /* DeepSpeed FusedAdam ADAM_MODE_1 (decoupled decay inside update) */
+#define SMT_ADAM_TORCH 1            /* torch.optim.AdamW (decay applied to p before the update)        */
+
+/* One 256x256 tile of a flat tile-major parameter buffer and where it lives in W. */
+typedef struct smt_tile_desc {
+    void* weight;                   /* W base (bf16, row-major) or NULL: no scatter   */
+    int64_t ld_weight;              /* W row stride in elements                       */
+    int32_t row_block;              /* index[0] of smt.py:318                         */
+    int32_t col_block;              /* index[1] of smt.py:318                         */
+    int64_t flat_offset;            /* element offset of the tile in the flat buffers */
+} smt_tile_desc;
+
+/* One warm-up accumulator update: dst[i] (+)= float(src[i]) for i < n. */
+typedef struct smt_accum_entry {
+    const void* src;                /* gradient (dtype src_dtype)                 */
+    float* dst;                     /* fp32 accumulator                           */
+    int64_t n;                      /* elements                                   */
+    int64_t chunk_begin;            /* exclusive prefix of ceil(n / 4096) chunks  */
+    int32_t src_dtype;              /* SMT_DTYPE_*                                */
+    int32_t assign;                 /* 1: dst = src (first step, fine_tune.py:731-734); 0: dst += src */
+} smt_accum_entry;
+
+/* One gradient matrix [d1*256, d2*256] (fp32, row stride ld) to score per 256x256 block. */
+typedef struct smt_score_entry {
+    const float* src;
+    int64_t ld;
+    int32_t d1, d2;                 /* block grid, smt_helper.py:57-58            */
+    int64_t block_begin;            /* exclusive prefix of d1*d2                  */
+    double* out;                    /* d1*d2 raw fp64 block sums, row-major       */
+    int32_t strategy;               /* SMT_SCORE_*                                */
+    int32_t pad_;
+} smt_score_entry;
+
+typedef struct smt_adamw_args {
+    float lr, beta1, beta2, eps, weight_decay;
+    float bias_correction1;         /* 1 - beta1^step (1.0 if bias_correction off) */
+    float bias_correction2;         /* 1 - beta2^step                              */
+    float max_grad_norm;            /* <= 0: no clipping                           */
+    float grad_scale;               /* multiplies every gradient (1/world for DP average) */
+    int32_t mode;                   /* SMT_ADAM_*                                  */
+    int32_t grad_dtype;             /* SMT_DTYPE_BF16 or SMT_DTYPE_FP32            */
+} smt_adamw_args;
+
+const char* smt_last_error(void);
+int smt_abi_version(void);
+
+/* Workspace bytes smt_tile_wgrad needs for T rows and n_tiles tiles. */
+size_t smt_wgrad_workspace_bytes(int64_t T, int32_t n_tiles);
+
+/*
+ * grad_tiles[i] (+)= sum_{t<T} grad_out[t, r_i*256 : r_i*256+256]^T  x[t, c_i*256 : c_i*256+256]
+ * grad_out [T, ld_grad_out], x [T, ld_x]: bf16 row-major; tile_rc_dev: device int32 [n_tiles][2];
+ * grad_tiles: [n_tiles*256, 256] row-major of out_dtype (bf16 or fp32). fp32 MFMA accumulation over
+ * the whole T, one rounding at the end (the reference rounds each per-sample partial to bf16 first).
+ */
+int smt_tile_wgrad(const void* grad_out, int64_t ld_grad_out,
+                   const void* x, int64_t ld_x, int64_t T,
+                   const int32_t* tile_rc_dev, int32_t n_tiles,
+                   void* grad_tiles, int32_t out_dtype, int32_t accumulate,
+                   void* workspace, size_t workspace_bytes, hipStream_t stream);
+
+/* tiles[i] = W[r_i*256:+256, c_i*256:+256]; elem_bytes 2 or 4. */
+int smt_tile_gather(const void* weight, int64_t ld_weight, int32_t elem_bytes,
+                    const int32_t* tile_rc_dev, int32_t n_tiles,
+                    void* tiles, hipStream_t stream);
+
+/* W[r_i*256:+256, c_i*256:+256] = tiles[i]; elem_bytes 2 or 4. */
+int smt_tile_scatter(void* weight, int64_t ld_weight, int32_t elem_bytes,
+                     const int32_t* tile_rc_dev, int32_t n_tiles,
+                     const void* tiles, hipStream_t stream);
+
+/* Multi-tensor warm-up accumulation; entries_dev is a device array of n_entries. */
+int smt_grad_accumulate(const smt_accum_entry* entries_dev, int32_t n_entries,
+                        int64_t total_chunks, hipStream_t stream);
+
+/* Multi-tensor block scoring; one fp64 raw sum per 256x256 block. */
+int smt_block_score(const smt_score_entry* entries_dev, int32_t n_entries,
+                    int64_t total_blocks, hipStream_t stream);
+
+/* out_dev[0] = sum x[i]^2 in fp64 (deterministic two-pass); partials_dev holds n_partials doubles. */
+int smt_sq_norm(const float* x, int64_t n, double* partials_dev, int32_t n_partials,
+                double* out_dev, hipStream_t stream);
+
+/*
+ * Fused clip + AdamW + bf16 cast (+ scatter into W) over flat tile-major buffers of
+ * n_tiles*65536 elements (tiles_dev != NULL) or n_elems plain elements (tiles_dev == NULL).
+ * grad_sq_norm_dev: device fp64 squared global norm of the effective gradient (grad * grad_scale,
+ * over every parameter the clip covers), or NULL for no clipping.
+ */
+int smt_adamw_step(const void* grad, float* master, float* exp_avg, float* exp_avg_sq,
+                   void* param_bf16, const smt_tile_desc* tiles_dev, int32_t n_tiles,
+                   int64_t n_elems, const double* grad_sq_norm_dev,
+                   const smt_adamw_args* args, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SMT_HIP_H */

@@ -1,0 +1,232 @@
+"""CPU restatement of the reference SMT hot path — TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import
+this module, and only as the checker / CPU baseline. The product (``sparse_matrix_tuning_amd``)
+never imports it and has no CPU path.
+
+Every function restates, with torch on the CPU (the library the reference itself computes with),
+the reference code at the cited ``file:line`` of yudaohai666/Sparse_Matrix_Tuning. Importing or
+running the reference was denied in this environment; the restatement is pinned by
+KAT-1 / KAT-2 (derived by reading the reference demos) and by dense-autograd identities,
+see tests/test_oracle.py. DeepSpeed's FusedAdam / clipping (external, DeepSpeed 0.16.5) are restated
+from their published algorithm: parity unpinned by the reference.
+"""
+from __future__ import annotations
+
+import heapq
+import re
+from collections import defaultdict
+from typing import Dict, Hashable, List, Sequence, Tuple
+
+import torch
+
+Block_dimension = 256                                   # smt.py:22
+_LAYER = re.compile(r'model\.layers\.(\d+)\.')          # smt.py:90, fine_tune.py:718
+
+
+# ------------------------------------------------------------------------------------------------
+# tiles, forward, backward (smt.py:302-413)
+# ------------------------------------------------------------------------------------------------
+def gather_tiles(weight: torch.Tensor, index_list: Sequence[Tuple[int, int]]) -> torch.Tensor:
+    """smt.py:312-325."""
+    B = Block_dimension
+    out = torch.empty(len(index_list) * B, B, dtype=weight.dtype)
+    for i, index in enumerate(index_list):
+        out[i * B:(i + 1) * B, :] = weight[index[0] * B:(index[0] + 1) * B, index[1] * B:(index[1] + 1) * B]
+    return out
+
+
+def writeback_tiles(weight: torch.Tensor, selected: torch.Tensor, index_list) -> None:
+    """smt.py:332-341 (in place on ``weight``)."""
+    B = Block_dimension
+    for i, index in enumerate(index_list):
+        weight[index[0] * B:(index[0] + 1) * B, index[1] * B:(index[1] + 1) * B] = selected[i * B:(i + 1) * B, :]
+
+
+def linearz_forward(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """smt.py:366."""
+    return torch.matmul(x, weight.t())
+
+
+def linearz_backward(grad_output: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, index_list):
+    """smt.py:382-406: per tile, a batched [B,256,S]x[B,S,256] matmul in the input dtype (each
+    per-sample partial rounded to that dtype), summed over the batch; ``grad_input = g @ W``."""
+    B = Block_dimension
+    grad_weight = torch.empty(len(index_list) * B, B, dtype=grad_output.dtype)
+    for i, index in enumerate(index_list):
+        grad_weight[i * B:(i + 1) * B, :] = torch.sum(torch.matmul(
+            grad_output.permute(0, 2, 1)[:, index[0] * B:(index[0] + 1) * B, :],
+            x[:, :, index[1] * B:(index[1] + 1) * B]), dim=0)
+    grad_input = torch.matmul(grad_output, weight)
+    return grad_input, grad_weight
+
+
+def tile_grads_fp64(grad_output: torch.Tensor, x: torch.Tensor, index_list) -> torch.Tensor:
+    """Exact-arithmetic truth for the tile gradients from the same (rounded) inputs."""
+    B = Block_dimension
+    g = grad_output.reshape(-1, grad_output.shape[-1]).double()
+    xx = x.reshape(-1, x.shape[-1]).double()
+    out = torch.empty(len(index_list) * B, B, dtype=torch.float64)
+    for i, (r, c) in enumerate(index_list):
+        out[i * B:(i + 1) * B] = g[:, r * B:(r + 1) * B].t() @ xx[:, c * B:(c + 1) * B]
+    return out
+
+
+# ------------------------------------------------------------------------------------------------
+# block statistics and selection (smt_helper.py:40-146, 149-251)
+# ------------------------------------------------------------------------------------------------
+def block_stat(grad: torch.Tensor, d1: int, d2: int, strategy: str) -> torch.Tensor:
+    """smt_helper.py:67-78 + 233-251, fp32 CPU reductions exactly as written there."""
+    g = grad.reshape(d1, Block_dimension, d2, Block_dimension)
+    if strategy == 'mean_abs':
+        return g.mean(dim=(1, 3)).abs()
+    if strategy == 'abs_mean':
+        return g.abs().mean(dim=(1, 3))
+    if strategy == 'L1':
+        return g.abs().sum(dim=(1, 3))
+    if strategy == 'L2':
+        return torch.sqrt(torch.sum(g.abs() ** 2, dim=(1, 3)))
+    return None
+
+
+def block_stat_fp64(grad: torch.Tensor, d1: int, d2: int, strategy: str) -> torch.Tensor:
+    """The same statistic with fp64 sums, rounded once to fp32 (what the GPU kernel computes)."""
+    g = grad.double().reshape(d1, Block_dimension, d2, Block_dimension)
+    n = float(Block_dimension * Block_dimension)
+    if strategy == 'mean_abs':
+        return (g.sum(dim=(1, 3)) / n).float().abs()
+    if strategy == 'abs_mean':
+        return (g.abs().sum(dim=(1, 3)) / n).float()
+    if strategy == 'L1':
+        return g.abs().sum(dim=(1, 3)).float()
+    if strategy == 'L2':
+        return torch.sqrt((g * g).sum(dim=(1, 3))).float()
+    return None
+
+
+def select_submatrix(grads: Dict[Hashable, torch.Tensor], targeted_module_dims, n=660,
+                     selection_strategy="no_restriction", calculate_strategy="mean_abs",
+                     stat=block_stat):
+    """smt_helper.py:40-146, including the heap loop of 111-119 and its UnboundLocalError paths."""
+    block_means = {}
+    for key, grad in grads.items():
+        d1 = int(targeted_module_dims[key[0]][0] / Block_dimension)
+        d2 = int(targeted_module_dims[key[0]][1] / Block_dimension)
+        grad.reshape(d1, Block_dimension, d2, Block_dimension)      # RuntimeError on bad dims
+        s = stat(grad, d1, d2, calculate_strategy)
+        if s is not None:
+            block_means[key] = s
+    if selection_strategy == "norm_dist":
+        ranked_blocks = defaultdict(list)
+        if not block_means:
+            raise UnboundLocalError("indices")
+        for key, block_mean in block_means.items():
+            indices = torch.argsort(block_mean.view(-1), descending=True, stable=True)
+            for idx in indices[:n]:
+                ranked_blocks[key].append(((idx // block_mean.shape[1]).item(), (idx % block_mean.shape[1]).item()))
+        return ranked_blocks
+    top_blocks = []
+    for key, block_mean in block_means.items():
+        for i in range(block_mean.shape[0]):
+            for j in range(block_mean.shape[1]):
+                abs_mean = block_mean[i, j].item()
+                if len(top_blocks) < n:
+                    heapq.heappush(top_blocks, (abs_mean, (key, i, j)))
+                else:
+                    heapq.heappushpop(top_blocks, (abs_mean, (key, i, j)))
+    top_blocks.sort(reverse=True)
+    if not top_blocks:
+        raise UnboundLocalError("mean")
+    ranked_blocks = defaultdict(list)
+    for _mean, (info, row, col) in top_blocks:
+        ranked_blocks[info].append((row, col))
+    return ranked_blocks
+
+
+def select_channel(activation: Dict[Hashable, torch.Tensor], n=660, selection_strategy="no_restriction",
+                   calculate_strategy="mean_abs"):
+    """smt_helper.py:149-230 (activation channel path; oracle only, product path is 'next')."""
+    column_means = {}
+    for key, act in activation.items():
+        act = torch.sum(act.abs(), dim=0)
+        if calculate_strategy == 'mean_abs':
+            column_means[key] = torch.mean(act.abs(), dim=0)
+        elif calculate_strategy == 'abs_mean':
+            column_means[key] = torch.abs(torch.mean(act, dim=0))
+        elif calculate_strategy == 'L1':
+            column_means[key] = torch.norm(act, p=1, dim=0)
+        elif calculate_strategy == 'L2':
+            column_means[key] = torch.norm(act, p=2, dim=0)
+    if selection_strategy == "norm_dist":
+        return {key: torch.argsort(cm, descending=True, stable=True)[:n].tolist() for key, cm in column_means.items()}
+    top_columns = []
+    for key, column_mean in column_means.items():
+        for idx in range(column_mean.shape[0]):
+            value = column_mean[idx].item()
+            if len(top_columns) < n:
+                heapq.heappush(top_columns, (value, (key, idx)))
+            else:
+                heapq.heappushpop(top_columns, (value, (key, idx)))
+    top_columns.sort(reverse=True)
+    ranked = defaultdict(list)
+    for _value, (key, idx) in top_columns:
+        ranked[key].append(idx)
+    return ranked
+
+
+# ------------------------------------------------------------------------------------------------
+# trainer segments (fine_tune.py:217-241, 714-767)
+# ------------------------------------------------------------------------------------------------
+def total_blocks_from_shapes(shapes: Sequence[Tuple[int, ...]]) -> float:
+    """fine_tune.py:231-234."""
+    total = 0
+    for s in shapes:
+        if len(s) == 2:
+            total += s[0] / 256 * s[1] / 256
+    return total
+
+
+def harvest(named_grads: Sequence[Tuple[str, torch.Tensor]], warmup_grads: dict, attention_warmup_grads: dict,
+            num_mlp_blocks: int, num_attention_blocks: int) -> None:
+    """fine_tune.py:716-767 on (name, grad) pairs in named_parameters() order (CPU fp32 dicts)."""
+    for name, grad in named_grads:
+        match = _LAYER.search(name)
+        layer_number = int(match.group(1)) if match else None
+        if 'mlp' in name and num_mlp_blocks > 0:
+            module_name = 'gate_proj' if 'gate_proj' in name else 'up_proj' if 'up_proj' in name else 'down_proj'
+            key = (module_name, layer_number)
+            if key not in warmup_grads:
+                warmup_grads[key] = grad.detach().cpu().to(torch.float32)
+            else:
+                warmup_grads[key] += grad.detach().cpu().to(torch.float32)
+        if 'self_attn' in name and 'weight' in name and num_attention_blocks > 0:
+            module_name = 'q_proj' if 'q_proj' in name else 'k_proj' if 'k_proj' in name else 'v_proj' if 'v_proj' in name else None
+            if module_name is not None:
+                key = (module_name, layer_number)
+                if key not in attention_warmup_grads:
+                    attention_warmup_grads[key] = grad.detach().cpu().to(torch.float32)
+                else:
+                    attention_warmup_grads[key] += grad.detach().cpu().to(torch.float32)
+
+
+# ------------------------------------------------------------------------------------------------
+# optimizer (DeepSpeed 0.16.5 FusedAdam ADAM_MODE_1 + gradient_clipping; external, restated)
+# ------------------------------------------------------------------------------------------------
+def clip_coef(grads: List[torch.Tensor], max_norm: float) -> float:
+    """DeepSpeed: clip = (||g|| + 1e-6) / max_norm, grads scaled by 1/clip when clip > 1."""
+    total = torch.sqrt(sum((g.double() ** 2).sum() for g in grads)).item()
+    clip = (total + 1e-6) / max_norm
+    return 1.0 / clip if clip > 1 else 1.0
+
+
+def fused_adam_step(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor, step: int,
+                    lr: float, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.0) -> None:
+    """In place on fp32 p, m, v (DeepSpeed multi_tensor_adam.cu, ADAM_MODE_1)."""
+    b1, b2 = betas
+    bc1 = 1 - b1 ** step
+    bc2 = 1 - b2 ** step
+    m.mul_(b1).add_((1 - b1) * g)
+    v.mul_(b2).add_((1 - b2) * g * g)
+    denom = torch.sqrt(v / bc2) + eps
+    update = (m / bc1) / denom + weight_decay * p
+    p.sub_(lr * update)

@@ -1,0 +1,294 @@
+"""ctypes binding of ``libsmt_hip.so`` (C ABI: ``include/smt_hip.h``).
+
+PyTorch is used only as plumbing here: device memory (the caching allocator) and the
+current HIP stream. Every compute call below goes to a gfx950 kernel; there is no CPU or
+eager-PyTorch fallback. If the library is missing or a tensor is not on a ROCm device the
+call raises, loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional, Sequence
+
+import torch  # imported first: its libamdhip64.so.7 is the HIP runtime the library binds to
+
+from . import build as _build
+
+BLOCK = 256
+TILE_ELEMS = BLOCK * BLOCK
+
+DTYPE_BF16, DTYPE_FP32, DTYPE_FP16 = 0, 1, 2
+SCORE_MEAN_ABS, SCORE_ABS_MEAN, SCORE_L1, SCORE_L2 = 0, 1, 2, 3
+ADAM_DEEPSPEED, ADAM_TORCH = 0, 1
+
+_DT = {torch.bfloat16: DTYPE_BF16, torch.float32: DTYPE_FP32, torch.float16: DTYPE_FP16}
+
+# Every function the header declares; tests check the library exports each of them.
+ABI_FUNCTIONS = (
+    "smt_last_error", "smt_abi_version", "smt_wgrad_workspace_bytes", "smt_tile_wgrad",
+    "smt_tile_gather", "smt_tile_scatter", "smt_grad_accumulate", "smt_block_score",
+    "smt_sq_norm", "smt_adamw_step",
+)
+
+
+class TileDesc(ctypes.Structure):
+    _fields_ = [("weight", ctypes.c_void_p), ("ld_weight", ctypes.c_int64),
+                ("row_block", ctypes.c_int32), ("col_block", ctypes.c_int32),
+                ("flat_offset", ctypes.c_int64)]
+
+
+class AccumEntry(ctypes.Structure):
+    _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("n", ctypes.c_int64),
+                ("chunk_begin", ctypes.c_int64), ("src_dtype", ctypes.c_int32), ("assign", ctypes.c_int32)]
+
+
+class ScoreEntry(ctypes.Structure):
+    _fields_ = [("src", ctypes.c_void_p), ("ld", ctypes.c_int64), ("d1", ctypes.c_int32),
+                ("d2", ctypes.c_int32), ("block_begin", ctypes.c_int64), ("out", ctypes.c_void_p),
+                ("strategy", ctypes.c_int32), ("pad_", ctypes.c_int32)]
+
+
+class AdamWArgs(ctypes.Structure):
+    _fields_ = [("lr", ctypes.c_float), ("beta1", ctypes.c_float), ("beta2", ctypes.c_float),
+                ("eps", ctypes.c_float), ("weight_decay", ctypes.c_float),
+                ("bias_correction1", ctypes.c_float), ("bias_correction2", ctypes.c_float),
+                ("max_grad_norm", ctypes.c_float), ("grad_scale", ctypes.c_float),
+                ("mode", ctypes.c_int32), ("grad_dtype", ctypes.c_int32)]
+
+
+ACC_CHUNK = 4096
+_lock = threading.Lock()
+_lib: Optional[ctypes.CDLL] = None
+
+_P, _I64, _I32, _SZ = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_size_t
+_SIGS = {
+    "smt_last_error": (ctypes.c_char_p, []),
+    "smt_abi_version": (ctypes.c_int, []),
+    "smt_wgrad_workspace_bytes": (_SZ, [_I64, _I32]),
+    "smt_tile_wgrad": (ctypes.c_int, [_P, _I64, _P, _I64, _I64, _P, _I32, _P, _I32, _I32, _P, _SZ, _P]),
+    "smt_tile_gather": (ctypes.c_int, [_P, _I64, _I32, _P, _I32, _P, _P]),
+    "smt_tile_scatter": (ctypes.c_int, [_P, _I64, _I32, _P, _I32, _P, _P]),
+    "smt_grad_accumulate": (ctypes.c_int, [_P, _I32, _I64, _P]),
+    "smt_block_score": (ctypes.c_int, [_P, _I32, _I64, _P]),
+    "smt_sq_norm": (ctypes.c_int, [_P, _I64, _P, _I32, _P, _P]),
+    "smt_adamw_step": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I32, _I64, _P, ctypes.POINTER(AdamWArgs), _P]),
+}
+
+
+def lib_path() -> str:
+    return _build.LIB_PATH
+
+
+def load(build_if_missing: bool = False) -> ctypes.CDLL:
+    """Load (and bind) ``libsmt_hip.so``. Raises if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if build_if_missing and _build.is_stale():
+                _build.build()
+            path = _build.LIB_PATH
+            if not os.path.exists(path):
+                raise RuntimeError(
+                    f"SMT HIP library not built ({path}); run `python -c 'import __graft_entry__ as g; g.build()'`"
+                    " or `python -m sparse_matrix_tuning_amd.build`")
+            lib = ctypes.CDLL(path)
+            for name, (res, args) in _SIGS.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().smt_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed (status {rc}): {msg}")
+
+
+def _require_device(*tensors: torch.Tensor) -> torch.device:
+    dev = None
+    for t in tensors:
+        if t is None:
+            continue
+        if t.device.type != "cuda":
+            raise RuntimeError(
+                f"SMT HIP path needs tensors on a ROCm device, got {t.device} "
+                "(there is no CPU fallback: the CPU restatement lives in oracle/ and is test-only)")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise RuntimeError(f"tensors on different devices: {dev} vs {t.device}")
+    return dev
+
+
+def _stream(dev: torch.device) -> int:
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _device_table(structs: Sequence[ctypes.Structure], cls, dev: torch.device) -> torch.Tensor:
+    """Copy an array of C structs into device memory (through the caching allocator)."""
+    n = len(structs)
+    arr = (cls * n)(*structs)
+    host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+    return host.to(dev, non_blocking=False)
+
+
+def tile_table(index_list: Sequence[Sequence[int]], device: torch.device) -> torch.Tensor:
+    """Device int32 [n, 2] table of (row_block, col_block)."""
+    flat = [int(v) for rc in index_list for v in (rc[0], rc[1])]
+    return torch.tensor(flat, dtype=torch.int32).view(-1, 2).to(device)
+
+
+# ---------------------------------------------------------------------------------------------
+# wrappers
+# ---------------------------------------------------------------------------------------------
+def wgrad_workspace_bytes(T: int, n_tiles: int) -> int:
+    return int(load().smt_wgrad_workspace_bytes(int(T), int(n_tiles)))
+
+
+def tile_wgrad(grad_out2d: torch.Tensor, x2d: torch.Tensor, tile_rc: torch.Tensor, out: torch.Tensor,
+               accumulate: bool = False) -> torch.Tensor:
+    """out[i] (+)= grad_out2d[:, r_i-block]^T @ x2d[:, c_i-block] for every tile (smt.py:397-404)."""
+    dev = _require_device(grad_out2d, x2d, tile_rc, out)
+    if grad_out2d.dtype != torch.bfloat16 or x2d.dtype != torch.bfloat16:
+        raise NotImplementedError(f"tile_wgrad: bf16 operands only (got {grad_out2d.dtype}, {x2d.dtype})")
+    if out.dtype not in (torch.bfloat16, torch.float32) or not out.is_contiguous():
+        raise ValueError("tile_wgrad: out must be a contiguous bf16/fp32 tensor")
+    n = tile_rc.shape[0]
+    if out.numel() != n * TILE_ELEMS:
+        raise ValueError(f"tile_wgrad: out has {out.numel()} elements, expected {n * TILE_ELEMS}")
+    T = grad_out2d.shape[0]
+    if x2d.shape[0] != T or grad_out2d.stride(1) != 1 or x2d.stride(1) != 1:
+        raise ValueError("tile_wgrad: operands must be [T, features] with unit feature stride")
+    ws_bytes = wgrad_workspace_bytes(T, n)
+    ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=dev)
+    rc = load().smt_tile_wgrad(_ptr(grad_out2d), grad_out2d.stride(0), _ptr(x2d), x2d.stride(0), T,
+                               _ptr(tile_rc), n, _ptr(out), _DT[out.dtype], int(bool(accumulate)),
+                               _ptr(ws), ws_bytes, _stream(dev))
+    _check(rc, "smt_tile_wgrad")
+    return out
+
+
+def tile_gather(weight: torch.Tensor, tile_rc: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    dev = _require_device(weight, tile_rc, out)
+    if weight.dim() != 2 or weight.stride(1) != 1 or out.dtype != weight.dtype or not out.is_contiguous():
+        raise ValueError("tile_gather: weight must be 2-D row-major and out contiguous of the same dtype")
+    rc = load().smt_tile_gather(_ptr(weight), weight.stride(0), weight.element_size(), _ptr(tile_rc),
+                                tile_rc.shape[0], _ptr(out), _stream(dev))
+    _check(rc, "smt_tile_gather")
+    return out
+
+
+def tile_scatter(weight: torch.Tensor, tile_rc: torch.Tensor, tiles: torch.Tensor) -> None:
+    dev = _require_device(weight, tile_rc, tiles)
+    if weight.dim() != 2 or weight.stride(1) != 1 or tiles.dtype != weight.dtype or not tiles.is_contiguous():
+        raise ValueError("tile_scatter: weight must be 2-D row-major and tiles contiguous of the same dtype")
+    rc = load().smt_tile_scatter(_ptr(weight), weight.stride(0), weight.element_size(), _ptr(tile_rc),
+                                 tile_rc.shape[0], _ptr(tiles), _stream(dev))
+    _check(rc, "smt_tile_scatter")
+
+
+class AccumulatePlan:
+    """Device descriptor table for one multi-tensor warm-up accumulation launch."""
+
+    def __init__(self, pairs: Sequence[tuple], assign: bool):
+        entries, chunk = [], 0
+        dev = None
+        for dst, src in pairs:
+            dev = _require_device(dst, src)
+            if dst.dtype != torch.float32 or not dst.is_contiguous() or not src.is_contiguous():
+                raise ValueError("accumulate: dst must be contiguous fp32 and src contiguous")
+            if dst.numel() != src.numel():
+                raise ValueError("accumulate: size mismatch")
+            n = dst.numel()
+            entries.append(AccumEntry(src.data_ptr(), dst.data_ptr(), n, chunk, _DT[src.dtype], int(assign)))
+            chunk += (n + ACC_CHUNK - 1) // ACC_CHUNK
+        self.n_entries = len(entries)
+        self.total_chunks = chunk
+        self.device = dev
+        self.table = _device_table(entries, AccumEntry, dev) if entries else None
+
+    def launch(self) -> None:
+        if not self.n_entries:
+            return
+        rc = load().smt_grad_accumulate(_ptr(self.table), self.n_entries, self.total_chunks, _stream(self.device))
+        _check(rc, "smt_grad_accumulate")
+
+
+def grad_accumulate(pairs: Sequence[tuple], assign: bool = False) -> None:
+    AccumulatePlan(pairs, assign).launch()
+
+
+def block_scores(grads: Sequence[torch.Tensor], dims: Sequence[tuple], strategy: int) -> list:
+    """Raw fp64 per-256x256-block sums for each fp32 gradient; one launch for all of them."""
+    entries, outs, blk = [], [], 0
+    dev = None
+    for g, (d1, d2) in zip(grads, dims):
+        dev = _require_device(g)
+        if g.dtype != torch.float32:
+            raise ValueError(f"block_scores: fp32 gradients only (got {g.dtype})")
+        g2 = g.reshape(d1 * BLOCK, d2 * BLOCK)
+        if g2.stride(1) != 1 or (g2.stride(0) % 4) or (g2.data_ptr() % 16):
+            g2 = g2.contiguous()
+        out = torch.empty(d1 * d2, dtype=torch.float64, device=dev)
+        outs.append((out, g2))
+        entries.append(ScoreEntry(g2.data_ptr(), g2.stride(0), d1, d2, blk, out.data_ptr(), strategy, 0))
+        blk += d1 * d2
+    if not entries:
+        return []
+    table = _device_table(entries, ScoreEntry, dev)
+    rc = load().smt_block_score(_ptr(table), len(entries), blk, _stream(dev))
+    _check(rc, "smt_block_score")
+    return [o for o, _ in outs]
+
+
+def sq_norm(x: torch.Tensor, out: Optional[torch.Tensor] = None, n_partials: int = 1024) -> torch.Tensor:
+    dev = _require_device(x)
+    if x.dtype != torch.float32 or not x.is_contiguous():
+        raise ValueError("sq_norm: contiguous fp32 only")
+    partials = torch.empty(n_partials, dtype=torch.float64, device=dev)
+    if out is None:
+        out = torch.empty(1, dtype=torch.float64, device=dev)
+    rc = load().smt_sq_norm(_ptr(x), x.numel(), _ptr(partials), n_partials, _ptr(out), _stream(dev))
+    _check(rc, "smt_sq_norm")
+    return out
+
+
+def adamw_step(grad: torch.Tensor, master: torch.Tensor, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor,
+               param_bf16: torch.Tensor, args: AdamWArgs, tiles: Optional[torch.Tensor] = None,
+               n_tiles: int = 0, grad_sq_norm: Optional[torch.Tensor] = None) -> None:
+    dev = _require_device(grad, master, exp_avg, exp_avg_sq, param_bf16, tiles, grad_sq_norm)
+    for t in (master, exp_avg, exp_avg_sq):
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            raise ValueError("adamw_step: master/exp_avg/exp_avg_sq must be contiguous fp32")
+    if param_bf16.dtype != torch.bfloat16 or not param_bf16.is_contiguous() or not grad.is_contiguous():
+        raise ValueError("adamw_step: param must be contiguous bf16 and grad contiguous")
+    n = master.numel()
+    if not (grad.numel() == n == exp_avg.numel() == exp_avg_sq.numel() == param_bf16.numel()):
+        raise ValueError("adamw_step: buffer sizes differ")
+    args.grad_dtype = _DT[grad.dtype]
+    rc = load().smt_adamw_step(_ptr(grad), _ptr(master), _ptr(exp_avg), _ptr(exp_avg_sq), _ptr(param_bf16),
+                               _ptr(tiles), int(n_tiles), n, _ptr(grad_sq_norm), ctypes.byref(args), _stream(dev))
+    _check(rc, "smt_adamw_step")
+
+
+def tile_descs(entries: Sequence[tuple], device: torch.device) -> torch.Tensor:
+    """entries: (weight tensor or None, row_block, col_block, flat_offset) -> device smt_tile_desc[]."""
+    descs = []
+    for w, r, c, off in entries:
+        if w is not None:
+            if w.dtype != torch.bfloat16 or w.stride(1) != 1:
+                raise ValueError("tile_descs: W must be bf16 row-major")
+            descs.append(TileDesc(w.data_ptr(), w.stride(0), int(r), int(c), int(off)))
+        else:
+            descs.append(TileDesc(None, 0, int(r), int(c), int(off)))
+    return _device_table(descs, TileDesc, device)

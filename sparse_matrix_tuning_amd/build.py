@@ -1,0 +1,59 @@
+"""Build the gfx950 HIP library ``_lib/libsmt_hip.so`` in-tree with hipcc.
+
+The library is the only native product code: ``csrc/smt_kernels.hip`` compiled for
+``--offload-arch=gfx950`` behind the C ABI in ``include/smt_hip.h``. It is loaded with
+ctypes by :mod:`sparse_matrix_tuning_amd._hip` (no torch types cross the boundary).
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_DIR = os.path.dirname(PKG_DIR)
+SRC = os.path.join(PKG_DIR, "csrc", "smt_kernels.hip")
+HEADER = os.path.join(REPO_DIR, "include", "smt_hip.h")
+LIB_DIR = os.path.join(PKG_DIR, "_lib")
+LIB_PATH = os.path.join(LIB_DIR, "libsmt_hip.so")
+ARCH = "gfx950"
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found (set HIPCC or install ROCm under /opt/rocm)")
+
+
+def is_stale() -> bool:
+    if not os.path.exists(LIB_PATH):
+        return True
+    t = os.path.getmtime(LIB_PATH)
+    return any(os.path.getmtime(p) > t for p in (SRC, HEADER, __file__))
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile the HIP library if it is missing or older than its sources; return its path."""
+    if not force and not is_stale():
+        return LIB_PATH
+    os.makedirs(LIB_DIR, exist_ok=True)
+    tmp = LIB_PATH + ".tmp"
+    cmd = [
+        hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
+        "-Wall", "-Wno-unused-function",
+        "-I", os.path.join(REPO_DIR, "include"),
+        "-o", tmp, SRC,
+    ]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"hipcc failed ({res.returncode}):\n{res.stdout}\n{res.stderr}")
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,748 @@
+// smt_kernels.hip — gfx950 (MI355X, CDNA4) kernels of the SMT block-sparse fine-tuning hot path
+// and the extern "C" ABI declared in include/smt_hip.h.
+//
+// Kernels (reference lines they restate, relative to yudaohai666/Sparse_Matrix_Tuning):
+//   wgrad_partial / wgrad_reduce   deepspeed/smt/smt.py:382-404  per-tile weight gradient, bf16 MFMA
+//   tile_copy<GATHER/SCATTER>      deepspeed/smt/smt.py:317-325 / 332-341
+//   grad_accumulate                deepspeed/fine_tune.py:724-741, 751-764
+//   block_score                    deepspeed/smt/smt_helper.py:67-78, 233-251
+//   sq_norm_partial / final        DeepSpeed gradient_clipping (deepspeed_helpers.py:87), external
+//   adamw_fused                    DeepSpeed FusedAdam (adam_w_mode) step, external, + W scatter
+//
+// Layout conventions: a "tile" is one 256x256 block; a tile buffer is [n_tiles*256, 256] row-major
+// (tile i occupies rows i*256..i*256+255, exactly the selected_weight layout of smt.py:312-325).
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "smt_hip.h"
+
+namespace {
+
+constexpr int kTile = SMT_BLOCK_DIM;          // 256
+constexpr int kTileElems = kTile * kTile;     // 65536
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+int check_launch(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(SMT_E_LAUNCH, "%s: %s", what, hipGetErrorString(e));
+    return SMT_OK;
+}
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
+
+__device__ __forceinline__ float bf16_bits_to_f32(uint32_t b) { return __uint_as_float(b << 16); }
+
+// Round-to-nearest-even f32 -> bf16 through the compiler's cast (v_cvt_pk_bf16_f32 on gfx950,
+// NaN-preserving; MI355X_MICROARCH.md "Correctness boundaries").
+__device__ __forceinline__ uint16_t f32_to_bf16_bits(float f) {
+    __bf16 b = (__bf16)f;
+    return __builtin_bit_cast(uint16_t, b);
+}
+
+__device__ __forceinline__ float half_bits_to_f32(uint16_t h) {
+    return (float)__builtin_bit_cast(_Float16, h);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Per-tile weight gradient (smt.py:397-404):
+//   C[m][n] = sum_t g[t][r*256+m] * x[t][c*256+n],  m,n in [0,256)
+// One 512-thread workgroup (8 waves as 2(M) x 4(N), 128x64 outputs per wave, 8 accumulators of
+// v_mfma_f32_32x32x16_bf16) owns a whole 256x256 tile for one contiguous chunk of T rows and
+// writes its fp32 partial to a slab; wgrad_reduce sums the slabs in a fixed order.
+// Both operands arrive K-major ([t][feature] rows of 512 B), so the LDS images are [k][256] and
+// every MFMA fragment is fetched by ds_read_b64_tr_b16 (transposed read, cdna_hip_programming T10).
+// Image swizzle: byte (k, b) -> k*512 + (b ^ ((k&3)<<6)). A 32-lane half of a tr read covers rows
+// k0..k0+3 x one aligned 64-B column chunk, which the XOR spreads over the four 64-B quarters of the
+// 256-B bank row: conflict-free. Staged through registers (global_load_dwordx4 -> ds_write_b128,
+// issue-early / write-late, T14) with one barrier per 64-row stage and two LDS buffers.
+// ------------------------------------------------------------------------------------------------
+constexpr int kWgThreads = 512;
+constexpr int kBK = 64;                        // T rows per stage
+constexpr int kRowBytes = kTile * 2;           // 512
+constexpr int kImgBytes = kBK * kRowBytes;     // 32 KiB per operand per stage
+constexpr int kChunksPerThread = (kImgBytes / 16) / kWgThreads;   // 4 x 16 B per operand
+static_assert(kChunksPerThread == 4, "staging geometry");
+
+__device__ __forceinline__ uint32_t img_off(uint32_t k, uint32_t byte_in_row) {
+    return k * kRowBytes + (byte_in_row ^ ((k & 3u) << 6));
+}
+
+__device__ __forceinline__ bf16x8_t tr_frag(const uint8_t* img, uint32_t k, uint32_t byte_in_row) {
+    s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(img + img_off(k, byte_in_row)));
+    s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(img + img_off(k + 4, byte_in_row)));
+    bf16x8_t f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        f[j] = __builtin_bit_cast(__bf16, lo[j]);
+        f[j + 4] = __builtin_bit_cast(__bf16, hi[j]);
+    }
+    return f;
+}
+
+__global__ __launch_bounds__(kWgThreads, 2)
+void wgrad_partial_kernel(const uint16_t* __restrict__ g, int64_t ldg,
+                          const uint16_t* __restrict__ x, int64_t ldx,
+                          int64_t T, int64_t chunk, int S,
+                          const int32_t* __restrict__ tile_rc,
+                          float* __restrict__ slab) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * 2 * kImgBytes];   // 128 KiB, one array
+
+    const int wg = blockIdx.x;
+    const int tile = wg / S;
+    const int s = wg - tile * S;
+    const int r = tile_rc[2 * tile];
+    const int c = tile_rc[2 * tile + 1];
+    const int64_t t_begin = (int64_t)s * chunk;
+    const int64_t t_end = (t_begin + chunk < T) ? (t_begin + chunk) : T;
+    const int nst = (t_end > t_begin) ? (int)((t_end - t_begin + kBK - 1) / kBK) : 0;
+
+    const uint16_t* gb = g + (int64_t)r * kTile;
+    const uint16_t* xb = x + (int64_t)c * kTile;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wm = wave >> 2;          // 0..1 -> rows wm*128
+    const int wn = wave & 3;           // 0..3 -> cols wn*64
+
+    uint4 ra[kChunksPerThread], rb[kChunksPerThread];
+
+    auto gload = [&](int st) {
+        const int64_t t0 = t_begin + (int64_t)st * kBK;
+        if (t0 + kBK <= t_end) {
+#pragma unroll
+            for (int i = 0; i < kChunksPerThread; ++i) {
+                const int cid = tid + kWgThreads * i;
+                const int64_t t = t0 + (cid >> 5);
+                const int e = (cid & 31) * 8;
+                ra[i] = *reinterpret_cast<const uint4*>(gb + t * ldg + e);
+                rb[i] = *reinterpret_cast<const uint4*>(xb + t * ldx + e);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < kChunksPerThread; ++i) {
+                const int cid = tid + kWgThreads * i;
+                const int64_t t = t0 + (cid >> 5);
+                const int e = (cid & 31) * 8;
+                if (t < t_end) {
+                    ra[i] = *reinterpret_cast<const uint4*>(gb + t * ldg + e);
+                    rb[i] = *reinterpret_cast<const uint4*>(xb + t * ldx + e);
+                } else {
+                    ra[i] = make_uint4(0, 0, 0, 0);
+                    rb[i] = make_uint4(0, 0, 0, 0);
+                }
+            }
+        }
+    };
+    auto swrite = [&](int buf) {
+        uint8_t* A = lds + buf * 2 * kImgBytes;
+        uint8_t* B = A + kImgBytes;
+#pragma unroll
+        for (int i = 0; i < kChunksPerThread; ++i) {
+            const int cid = tid + kWgThreads * i;
+            const uint32_t off = img_off((uint32_t)(cid >> 5), (uint32_t)(cid & 31) * 16u);
+            *reinterpret_cast<uint4*>(A + off) = ra[i];
+            *reinterpret_cast<uint4*>(B + off) = rb[i];
+        }
+    };
+
+    f32x16_t acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    // tr-read lane geometry: group gi = lane>>4 covers feature offset 16*(gi&1) and k offset
+    // 8*(gi>>1); lane 4q+p of the group supplies row q, features 4p..4p+3 (T10).
+    const int gi = lane >> 4;
+    const int q = (lane >> 2) & 3;
+    const int p = lane & 3;
+    const uint32_t feat_byte = 2u * (16u * (gi & 1) + 4u * p);
+    const uint32_t krow = 8u * (gi >> 1) + q;
+
+    if (nst > 0) {
+        gload(0);
+        swrite(0);
+    }
+    __syncthreads();
+
+    for (int st = 0; st < nst; ++st) {
+        const int buf = st & 1;
+        if (st + 1 < nst) gload(st + 1);
+        const uint8_t* A = lds + buf * 2 * kImgBytes;
+        const uint8_t* B = A + kImgBytes;
+#pragma unroll
+        for (int ks = 0; ks < kBK / 16; ++ks) {
+            bf16x8_t af[4], bfr[2];
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb)
+                af[mb] = tr_frag(A, ks * 16 + krow, 2u * (wm * 128 + mb * 32) + feat_byte);
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb)
+                bfr[nb] = tr_frag(B, ks * 16 + krow, 2u * (wn * 64 + nb * 32) + feat_byte);
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb)
+                    acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mb], bfr[nb], acc[mb][nb], 0, 0, 0);
+        }
+        if (st + 1 < nst) swrite(buf ^ 1);
+        __syncthreads();
+    }
+
+    // C/D map of 32x32x16: col = lane&31, row = (i&3) + 8*(i>>2) + 4*(lane>>5)
+    float* out = slab + (int64_t)(tile * S + s) * kTileElems;
+    const int col = lane & 31;
+    const int h = lane >> 5;
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int m = wm * 128 + mb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                const int n = wn * 64 + nb * 32 + col;
+                out[m * kTile + n] = acc[mb][nb][i];
+            }
+}
+
+// Sum the S partial slabs of each tile in order s = 0..S-1 (deterministic) and write the tile.
+// 64 workgroups x 256 threads x 4 elements per tile.
+template <bool OUT_F32>
+__global__ __launch_bounds__(256)
+void wgrad_reduce_kernel(const float* __restrict__ slab, int S, void* __restrict__ out, int accumulate) {
+    const int tile = blockIdx.x >> 6;
+    const int e = (((blockIdx.x & 63) << 8) + threadIdx.x) * 4;
+    const float* src = slab + (int64_t)tile * S * kTileElems + e;
+    float4 sum = *reinterpret_cast<const float4*>(src);
+    for (int s = 1; s < S; ++s) {
+        const float4 v = *reinterpret_cast<const float4*>(src + (int64_t)s * kTileElems);
+        sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
+    }
+    const int64_t o = (int64_t)tile * kTileElems + e;
+    if (OUT_F32) {
+        float4* dst = reinterpret_cast<float4*>(static_cast<float*>(out) + o);
+        if (accumulate) {
+            const float4 a = *dst;
+            sum.x += a.x; sum.y += a.y; sum.z += a.z; sum.w += a.w;
+        }
+        *dst = sum;
+    } else {
+        uint2* dst = reinterpret_cast<uint2*>(static_cast<uint16_t*>(out) + o);
+        if (accumulate) {
+            const uint2 a = *dst;
+            sum.x += bf16_bits_to_f32(a.x & 0xffffu);
+            sum.y += bf16_bits_to_f32(a.x >> 16);
+            sum.z += bf16_bits_to_f32(a.y & 0xffffu);
+            sum.w += bf16_bits_to_f32(a.y >> 16);
+        }
+        uint2 w;
+        w.x = (uint32_t)f32_to_bf16_bits(sum.x) | ((uint32_t)f32_to_bf16_bits(sum.y) << 16);
+        w.y = (uint32_t)f32_to_bf16_bits(sum.z) | ((uint32_t)f32_to_bf16_bits(sum.w) << 16);
+        *dst = w;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Tile gather / scatter (smt.py:317-325 and 332-341): 16 B per thread, 32 workgroups per tile.
+// ------------------------------------------------------------------------------------------------
+template <bool SCATTER, int ELEM_BYTES>
+__global__ __launch_bounds__(256)
+void tile_copy_kernel(uint8_t* __restrict__ weight, int64_t ld_weight, const int32_t* __restrict__ tile_rc,
+                      uint8_t* __restrict__ tiles) {
+    constexpr int kVec = 16 / ELEM_BYTES;                      // elements per 16 B
+    constexpr int kChunksPerRow = kTile / kVec;                // 32 or 64
+    constexpr int kChunksPerTile = kTile * kChunksPerRow;      // 8192 or 16384
+    constexpr int kWgPerTile = kChunksPerTile / 256;           // 32 or 64
+    const int tile = blockIdx.x / kWgPerTile;
+    const int chunk = (blockIdx.x - tile * kWgPerTile) * 256 + threadIdx.x;
+    const int m = chunk / kChunksPerRow;
+    const int n = (chunk - m * kChunksPerRow) * kVec;
+    const int r = tile_rc[2 * tile];
+    const int c = tile_rc[2 * tile + 1];
+    uint4* w = reinterpret_cast<uint4*>(weight + (((int64_t)r * kTile + m) * ld_weight + (int64_t)c * kTile + n) * ELEM_BYTES);
+    uint4* t = reinterpret_cast<uint4*>(tiles + ((int64_t)tile * kTileElems + (int64_t)m * kTile + n) * ELEM_BYTES);
+    if (SCATTER) *w = *t;
+    else *t = *w;
+}
+
+
+// ------------------------------------------------------------------------------------------------
+// Warm-up accumulation (fine_tune.py:731-741): dst = float(src) (first step) or dst += float(src).
+// 4096 elements per workgroup (256 threads x 2 passes x 8); entries found by binary search over
+// chunk_begin. One IEEE fp32 add of a widened bf16/fp16 value per element: bit-identical to the
+// CPU `acc += grad.cpu().to(torch.float32)` of the reference.
+// ------------------------------------------------------------------------------------------------
+constexpr int kAccChunk = 4096;
+
+__device__ __forceinline__ int find_acc_entry(const smt_accum_entry* e, int n, int64_t chunk) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (e[mid].chunk_begin <= chunk) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+template <int DT>
+__device__ __forceinline__ float load_elem(const void* p, int64_t i) {
+    if (DT == SMT_DTYPE_BF16) return bf16_bits_to_f32(static_cast<const uint16_t*>(p)[i]);
+    if (DT == SMT_DTYPE_FP16) return half_bits_to_f32(static_cast<const uint16_t*>(p)[i]);
+    return static_cast<const float*>(p)[i];
+}
+
+template <int DT>
+__device__ __forceinline__ void load8(const void* p, int64_t i, float (&v)[8]) {
+    if (DT == SMT_DTYPE_FP32) {
+        const float4 a = *reinterpret_cast<const float4*>(static_cast<const float*>(p) + i);
+        const float4 b = *reinterpret_cast<const float4*>(static_cast<const float*>(p) + i + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    } else {
+        const uint4 a = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(p) + i);
+        const uint32_t w[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (DT == SMT_DTYPE_BF16) {
+                v[2 * j] = bf16_bits_to_f32(w[j] & 0xffffu);
+                v[2 * j + 1] = bf16_bits_to_f32(w[j] >> 16);
+            } else {
+                v[2 * j] = half_bits_to_f32((uint16_t)(w[j] & 0xffffu));
+                v[2 * j + 1] = half_bits_to_f32((uint16_t)(w[j] >> 16));
+            }
+        }
+    }
+}
+
+template <int DT>
+__device__ void accumulate_chunk(const smt_accum_entry& ent, int64_t base) {
+    const bool vec = ((reinterpret_cast<uintptr_t>(ent.src) | reinterpret_cast<uintptr_t>(ent.dst)) & 15u) == 0;
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+        const int64_t i0 = base + pass * 2048 + threadIdx.x * 8;
+        if (i0 >= ent.n) continue;
+        if (vec && i0 + 8 <= ent.n) {
+            float v[8];
+            load8<DT>(ent.src, i0, v);
+            float4* d = reinterpret_cast<float4*>(ent.dst + i0);
+            float4 a = ent.assign ? make_float4(0.f, 0.f, 0.f, 0.f) : d[0];
+            float4 b = ent.assign ? make_float4(0.f, 0.f, 0.f, 0.f) : d[1];
+            if (ent.assign) {
+                a = make_float4(v[0], v[1], v[2], v[3]);
+                b = make_float4(v[4], v[5], v[6], v[7]);
+            } else {
+                a.x += v[0]; a.y += v[1]; a.z += v[2]; a.w += v[3];
+                b.x += v[4]; b.y += v[5]; b.z += v[6]; b.w += v[7];
+            }
+            d[0] = a;
+            d[1] = b;
+        } else {
+            for (int j = 0; j < 8; ++j) {
+                const int64_t i = i0 + j;
+                if (i < ent.n) {
+                    const float v = load_elem<DT>(ent.src, i);
+                    ent.dst[i] = ent.assign ? v : ent.dst[i] + v;
+                }
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256)
+void grad_accumulate_kernel(const smt_accum_entry* __restrict__ entries, int n_entries) {
+    const int64_t chunk = blockIdx.x;
+    const smt_accum_entry ent = entries[find_acc_entry(entries, n_entries, chunk)];
+    const int64_t base = (chunk - ent.chunk_begin) * kAccChunk;
+    if (ent.src_dtype == SMT_DTYPE_BF16) accumulate_chunk<SMT_DTYPE_BF16>(ent, base);
+    else if (ent.src_dtype == SMT_DTYPE_FP16) accumulate_chunk<SMT_DTYPE_FP16>(ent, base);
+    else accumulate_chunk<SMT_DTYPE_FP32>(ent, base);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Block scores (smt_helper.py:67-78, 233-251): one 256-thread workgroup per 256x256 block of an
+// fp32 gradient; float4 row loads (a wave covers one 1 KiB row), fp64 accumulation, wave shuffle
+// then LDS reduction in a fixed order. Writes the raw fp64 sum of g / |g| / g^2; the host turns it
+// into mean / abs / sqrt and rounds to fp32, the dtype the reference compares in.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ int find_score_entry(const smt_score_entry* e, int n, int64_t blk) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (e[mid].block_begin <= blk) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+template <int STRAT>
+__device__ __forceinline__ double score_term(float f) {
+    if (STRAT == SMT_SCORE_MEAN_ABS) return (double)f;
+    if (STRAT == SMT_SCORE_L2) return (double)f * (double)f;      // exact: 24-bit x 24-bit < 53 bits
+    return (double)fabsf(f);
+}
+
+template <int STRAT>
+__device__ double block_partial(const float* __restrict__ src, int64_t ld) {
+    const int col = (threadIdx.x & 63) * 4;
+    const int row0 = threadIdx.x >> 6;
+    double acc = 0.0;
+#pragma unroll 4
+    for (int it = 0; it < kTile / 4; ++it) {
+        const float4 v = *reinterpret_cast<const float4*>(src + (int64_t)(row0 + 4 * it) * ld + col);
+        acc += score_term<STRAT>(v.x) + score_term<STRAT>(v.y) + score_term<STRAT>(v.z) + score_term<STRAT>(v.w);
+    }
+    return acc;
+}
+
+__global__ __launch_bounds__(256)
+void block_score_kernel(const smt_score_entry* __restrict__ entries, int n_entries) {
+    __shared__ double part[4];
+    const int64_t blk = blockIdx.x;
+    const smt_score_entry ent = entries[find_score_entry(entries, n_entries, blk)];
+    const int64_t local = blk - ent.block_begin;
+    const int bi = (int)(local / ent.d2);
+    const int bj = (int)(local - (int64_t)bi * ent.d2);
+    const float* src = ent.src + (int64_t)bi * kTile * ent.ld + (int64_t)bj * kTile;
+    double acc;
+    switch (ent.strategy) {
+        case SMT_SCORE_MEAN_ABS: acc = block_partial<SMT_SCORE_MEAN_ABS>(src, ent.ld); break;
+        case SMT_SCORE_L2: acc = block_partial<SMT_SCORE_L2>(src, ent.ld); break;
+        default: acc = block_partial<SMT_SCORE_ABS_MEAN>(src, ent.ld); break;
+    }
+    acc = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) ent.out[local] = (part[0] + part[1]) + (part[2] + part[3]);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Global squared L2 norm of the flat fp32 gradient (deterministic two-pass, fp64).
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256)
+void sq_norm_partial_kernel(const float* __restrict__ x, int64_t n, double* __restrict__ partials) {
+    __shared__ double part[4];
+    double acc = 0.0;
+    const int64_t n4 = ((reinterpret_cast<uintptr_t>(x) & 15u) == 0) ? n / 4 : 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+        const float4 v = reinterpret_cast<const float4*>(x)[i];
+        acc += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+    }
+    for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        acc += (double)x[i] * x[i];
+    acc = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) partials[blockIdx.x] = (part[0] + part[1]) + (part[2] + part[3]);
+}
+
+__global__ __launch_bounds__(256)
+void sq_norm_final_kernel(const double* __restrict__ partials, int n, double* __restrict__ out) {
+    __shared__ double part[4];
+    double acc = 0.0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) acc += partials[i];
+    acc = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) out[0] = (part[0] + part[1]) + (part[2] + part[3]);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Fused clip + AdamW + bf16 cast + scatter into W. 8 elements per thread; in tile mode 32
+// workgroups per 256x256 tile (8 tile rows per workgroup) so the W destination is one scalar
+// descriptor per workgroup and every W store is a 16-B piece of a 512-B tile row.
+// ------------------------------------------------------------------------------------------------
+struct AdamStep {
+    float lr, b1, b2, eps, wd, bc1, bc2;
+    int mode;
+    __device__ __forceinline__ void apply(float g, float& p, float& m, float& v) const {
+        if (mode == SMT_ADAM_DEEPSPEED) {
+            m = b1 * m + (1.f - b1) * g;
+            v = b2 * v + (1.f - b2) * g * g;
+            const float denom = sqrtf(v / bc2) + eps;
+            const float update = (m / bc1) / denom + wd * p;
+            p = p - lr * update;
+        } else {
+            p = p * (1.f - lr * wd);
+            m = m + (1.f - b1) * (g - m);
+            v = v * b2 + (1.f - b2) * g * g;
+            const float denom = sqrtf(v) / sqrtf(bc2) + eps;
+            p = p - (lr / bc1) * (m / denom);
+        }
+    }
+};
+
+template <int GDT>
+__device__ __forceinline__ void adam8(const void* grad, float* master, float* m, float* v, uint16_t* param,
+                                      int64_t f, float gscale, const AdamStep& st, uint4* packed) {
+    float g[8];
+    load8<GDT>(grad, f, g);
+    float4* P = reinterpret_cast<float4*>(master + f);
+    float4* M = reinterpret_cast<float4*>(m + f);
+    float4* V = reinterpret_cast<float4*>(v + f);
+    float4 p0 = P[0], p1 = P[1], m0 = M[0], m1 = M[1], v0 = V[0], v1 = V[1];
+    float pp[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+    float mm[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
+    float vv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) st.apply(g[j] * gscale, pp[j], mm[j], vv[j]);
+    P[0] = make_float4(pp[0], pp[1], pp[2], pp[3]); P[1] = make_float4(pp[4], pp[5], pp[6], pp[7]);
+    M[0] = make_float4(mm[0], mm[1], mm[2], mm[3]); M[1] = make_float4(mm[4], mm[5], mm[6], mm[7]);
+    V[0] = make_float4(vv[0], vv[1], vv[2], vv[3]); V[1] = make_float4(vv[4], vv[5], vv[6], vv[7]);
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        w[j] = (uint32_t)f32_to_bf16_bits(pp[2 * j]) | ((uint32_t)f32_to_bf16_bits(pp[2 * j + 1]) << 16);
+    *packed = make_uint4(w[0], w[1], w[2], w[3]);
+    *reinterpret_cast<uint4*>(param + f) = *packed;
+}
+
+// norm_sq: squared global norm of the EFFECTIVE gradient (after grad_scale), fp64.
+__device__ __forceinline__ float clip_scale(const double* norm_sq, float max_norm, float grad_scale) {
+    float s = grad_scale;
+    if (norm_sq != nullptr && max_norm > 0.f) {
+        // DeepSpeed: clip = (total_norm + 1e-6) / max_norm; grads *= 1/clip when clip > 1.
+        const float total = (float)sqrt(*norm_sq);
+        const float clip = (total + 1e-6f) / max_norm;
+        if (clip > 1.f) s = grad_scale / clip;
+    }
+    return s;
+}
+
+template <int GDT>
+__global__ __launch_bounds__(256)
+void adamw_tiles_kernel(const void* __restrict__ grad, float* __restrict__ master, float* __restrict__ m,
+                        float* __restrict__ v, uint16_t* __restrict__ param,
+                        const smt_tile_desc* __restrict__ tiles, const double* __restrict__ norm_sq,
+                        smt_adamw_args a) {
+    const int tile = blockIdx.x >> 5;
+    const int local = (((blockIdx.x & 31) << 8) + threadIdx.x) * 8;   // element within the tile
+    const smt_tile_desc d = tiles[tile];
+    const int64_t f = d.flat_offset + local;
+    const AdamStep st{a.lr, a.beta1, a.beta2, a.eps, a.weight_decay, a.bias_correction1, a.bias_correction2, a.mode};
+    const float gscale = clip_scale(norm_sq, a.max_grad_norm, a.grad_scale);
+    uint4 packed;
+    adam8<GDT>(grad, master, m, v, param, f, gscale, st, &packed);
+    if (d.weight != nullptr) {
+        const int row = local >> 8;
+        const int col = local & 255;
+        uint16_t* w = static_cast<uint16_t*>(d.weight) +
+                      ((int64_t)d.row_block * kTile + row) * d.ld_weight + (int64_t)d.col_block * kTile + col;
+        *reinterpret_cast<uint4*>(w) = packed;
+    }
+}
+
+template <int GDT>
+__global__ __launch_bounds__(256)
+void adamw_flat_kernel(const void* __restrict__ grad, float* __restrict__ master, float* __restrict__ m,
+                       float* __restrict__ v, uint16_t* __restrict__ param, int64_t n,
+                       const double* __restrict__ norm_sq, smt_adamw_args a) {
+    const int64_t f = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
+    if (f >= n) return;
+    const AdamStep st{a.lr, a.beta1, a.beta2, a.eps, a.weight_decay, a.bias_correction1, a.bias_correction2, a.mode};
+    const float gscale = clip_scale(norm_sq, a.max_grad_norm, a.grad_scale);
+    if (f + 8 <= n) {
+        uint4 packed;
+        adam8<GDT>(grad, master, m, v, param, f, gscale, st, &packed);
+    } else {
+        for (int64_t i = f; i < n; ++i) {
+            float pp = master[i], mm = m[i], vv = v[i];
+            st.apply(load_elem<GDT>(grad, i) * gscale, pp, mm, vv);
+            master[i] = pp; m[i] = mm; v[i] = vv;
+            param[i] = f32_to_bf16_bits(pp);
+        }
+    }
+}
+
+// Split of T over workgroups for one tile set: about two workgroups per CU overall (256 CUs),
+// chunks of at least 512 rows and a multiple of the 64-row stage.
+struct WgradSplit { int S; int64_t chunk; };
+
+WgradSplit wgrad_split(int64_t T, int32_t n_tiles) {
+    WgradSplit sp{1, kBK};
+    if (T <= 0 || n_tiles <= 0) return sp;
+    int64_t S = (512 + n_tiles - 1) / n_tiles;
+    const int64_t s_max = (T + 511) / 512;
+    if (S > s_max) S = s_max;
+    if (S < 1) S = 1;
+    int64_t chunk = (T + S - 1) / S;
+    chunk = (chunk + kBK - 1) / kBK * kBK;
+    sp.S = (int)((T + chunk - 1) / chunk);
+    sp.chunk = chunk;
+    return sp;
+}
+
+}  // namespace
+
+// ================================================================================================
+// C ABI
+// ================================================================================================
+extern "C" {
+
+const char* smt_last_error(void) { return g_err; }
+
+int smt_abi_version(void) { return 1; }
+
+size_t smt_wgrad_workspace_bytes(int64_t T, int32_t n_tiles) {
+    if (T <= 0 || n_tiles <= 0) return 0;
+    const WgradSplit sp = wgrad_split(T, n_tiles);
+    return (size_t)n_tiles * (size_t)sp.S * (size_t)kTileElems * sizeof(float);
+}
+
+int smt_tile_wgrad(const void* grad_out, int64_t ld_grad_out, const void* x, int64_t ld_x, int64_t T,
+                   const int32_t* tile_rc_dev, int32_t n_tiles, void* grad_tiles, int32_t out_dtype,
+                   int32_t accumulate, void* workspace, size_t workspace_bytes, hipStream_t stream) {
+    if (n_tiles < 0 || T < 0) return fail(SMT_E_INVALID, "smt_tile_wgrad: negative size (T=%lld, n_tiles=%d)", (long long)T, n_tiles);
+    if (n_tiles == 0) return SMT_OK;
+    if (out_dtype != SMT_DTYPE_BF16 && out_dtype != SMT_DTYPE_FP32)
+        return fail(SMT_E_INVALID, "smt_tile_wgrad: out_dtype %d not supported", out_dtype);
+    if (!tile_rc_dev || !grad_tiles) return fail(SMT_E_INVALID, "smt_tile_wgrad: null tile table or output");
+    if (!aligned16(grad_tiles)) return fail(SMT_E_ALIGN, "smt_tile_wgrad: output not 16-byte aligned");
+    if (T == 0) {
+        if (accumulate) return SMT_OK;
+        const size_t bytes = (size_t)n_tiles * kTileElems * (out_dtype == SMT_DTYPE_FP32 ? 4 : 2);
+        hipError_t e = hipMemsetAsync(grad_tiles, 0, bytes, stream);
+        return e == hipSuccess ? SMT_OK : fail(SMT_E_LAUNCH, "smt_tile_wgrad: memset: %s", hipGetErrorString(e));
+    }
+    if (!grad_out || !x) return fail(SMT_E_INVALID, "smt_tile_wgrad: null operand");
+    if (!aligned16(grad_out) || !aligned16(x) || (ld_grad_out & 7) || (ld_x & 7))
+        return fail(SMT_E_ALIGN, "smt_tile_wgrad: operands need 16-byte aligned rows (ld %% 8 == 0)");
+    const WgradSplit sp = wgrad_split(T, n_tiles);
+    const size_t need = (size_t)n_tiles * sp.S * kTileElems * sizeof(float);
+    if (!workspace || workspace_bytes < need)
+        return fail(SMT_E_WORKSPACE, "smt_tile_wgrad: workspace %zu < %zu bytes", workspace_bytes, need);
+    if (!aligned16(workspace)) return fail(SMT_E_ALIGN, "smt_tile_wgrad: workspace not 16-byte aligned");
+    float* slab = static_cast<float*>(workspace);
+    hipLaunchKernelGGL(wgrad_partial_kernel, dim3(n_tiles * sp.S), dim3(kWgThreads), 0, stream,
+                       static_cast<const uint16_t*>(grad_out), ld_grad_out, static_cast<const uint16_t*>(x), ld_x,
+                       T, sp.chunk, sp.S, tile_rc_dev, slab);
+    int rc = check_launch("wgrad_partial_kernel");
+    if (rc) return rc;
+    if (out_dtype == SMT_DTYPE_FP32)
+        hipLaunchKernelGGL(wgrad_reduce_kernel<true>, dim3(n_tiles * 64), dim3(256), 0, stream, slab, sp.S, grad_tiles, accumulate);
+    else
+        hipLaunchKernelGGL(wgrad_reduce_kernel<false>, dim3(n_tiles * 64), dim3(256), 0, stream, slab, sp.S, grad_tiles, accumulate);
+    return check_launch("wgrad_reduce_kernel");
+}
+
+static int tile_copy(bool scatter, void* weight, int64_t ld_weight, int32_t elem_bytes, const int32_t* tile_rc_dev,
+                     int32_t n_tiles, void* tiles, hipStream_t stream) {
+    const char* name = scatter ? "smt_tile_scatter" : "smt_tile_gather";
+    if (n_tiles < 0) return fail(SMT_E_INVALID, "%s: negative n_tiles", name);
+    if (n_tiles == 0) return SMT_OK;
+    if (!weight || !tile_rc_dev || !tiles) return fail(SMT_E_INVALID, "%s: null pointer", name);
+    if (elem_bytes != 2 && elem_bytes != 4) return fail(SMT_E_INVALID, "%s: elem_bytes %d", name, elem_bytes);
+    if (!aligned16(weight) || !aligned16(tiles) || ((ld_weight * elem_bytes) & 15))
+        return fail(SMT_E_ALIGN, "%s: weight/tiles need 16-byte aligned rows", name);
+    uint8_t* w = static_cast<uint8_t*>(weight);
+    uint8_t* t = static_cast<uint8_t*>(tiles);
+    const int wg_per_tile = kTileElems * elem_bytes / 16 / 256;
+    dim3 grid(n_tiles * wg_per_tile);
+    if (elem_bytes == 2) {
+        if (scatter) hipLaunchKernelGGL((tile_copy_kernel<true, 2>), grid, dim3(256), 0, stream, w, ld_weight, tile_rc_dev, t);
+        else hipLaunchKernelGGL((tile_copy_kernel<false, 2>), grid, dim3(256), 0, stream, w, ld_weight, tile_rc_dev, t);
+    } else {
+        if (scatter) hipLaunchKernelGGL((tile_copy_kernel<true, 4>), grid, dim3(256), 0, stream, w, ld_weight, tile_rc_dev, t);
+        else hipLaunchKernelGGL((tile_copy_kernel<false, 4>), grid, dim3(256), 0, stream, w, ld_weight, tile_rc_dev, t);
+    }
+    return check_launch(name);
+}
+
+int smt_tile_gather(const void* weight, int64_t ld_weight, int32_t elem_bytes, const int32_t* tile_rc_dev,
+                    int32_t n_tiles, void* tiles, hipStream_t stream) {
+    return tile_copy(false, const_cast<void*>(weight), ld_weight, elem_bytes, tile_rc_dev, n_tiles, tiles, stream);
+}
+
+int smt_tile_scatter(void* weight, int64_t ld_weight, int32_t elem_bytes, const int32_t* tile_rc_dev,
+                     int32_t n_tiles, const void* tiles, hipStream_t stream) {
+    return tile_copy(true, weight, ld_weight, elem_bytes, tile_rc_dev, n_tiles, const_cast<void*>(tiles), stream);
+}
+
+int smt_grad_accumulate(const smt_accum_entry* entries_dev, int32_t n_entries, int64_t total_chunks, hipStream_t stream) {
+    if (n_entries < 0 || total_chunks < 0) return fail(SMT_E_INVALID, "smt_grad_accumulate: negative size");
+    if (n_entries == 0 || total_chunks == 0) return SMT_OK;
+    if (!entries_dev) return fail(SMT_E_INVALID, "smt_grad_accumulate: null entry table");
+    if (total_chunks > 0x7fffffffLL) return fail(SMT_E_INVALID, "smt_grad_accumulate: too many chunks");
+    hipLaunchKernelGGL(grad_accumulate_kernel, dim3((unsigned)total_chunks), dim3(256), 0, stream, entries_dev, n_entries);
+    return check_launch("grad_accumulate_kernel");
+}
+
+int smt_block_score(const smt_score_entry* entries_dev, int32_t n_entries, int64_t total_blocks, hipStream_t stream) {
+    if (n_entries < 0 || total_blocks < 0) return fail(SMT_E_INVALID, "smt_block_score: negative size");
+    if (n_entries == 0 || total_blocks == 0) return SMT_OK;
+    if (!entries_dev) return fail(SMT_E_INVALID, "smt_block_score: null entry table");
+    if (total_blocks > 0x7fffffffLL) return fail(SMT_E_INVALID, "smt_block_score: too many blocks");
+    hipLaunchKernelGGL(block_score_kernel, dim3((unsigned)total_blocks), dim3(256), 0, stream, entries_dev, n_entries);
+    return check_launch("block_score_kernel");
+}
+
+int smt_sq_norm(const float* x, int64_t n, double* partials_dev, int32_t n_partials, double* out_dev, hipStream_t stream) {
+    if (n < 0 || n_partials <= 0) return fail(SMT_E_INVALID, "smt_sq_norm: bad sizes (n=%lld, n_partials=%d)", (long long)n, n_partials);
+    if (!partials_dev || !out_dev || (n > 0 && !x)) return fail(SMT_E_INVALID, "smt_sq_norm: null pointer");
+    hipLaunchKernelGGL(sq_norm_partial_kernel, dim3(n_partials), dim3(256), 0, stream, x, n, partials_dev);
+    int rc = check_launch("sq_norm_partial_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(sq_norm_final_kernel, dim3(1), dim3(256), 0, stream, partials_dev, n_partials, out_dev);
+    return check_launch("sq_norm_final_kernel");
+}
+
+int smt_adamw_step(const void* grad, float* master, float* exp_avg, float* exp_avg_sq, void* param_bf16,
+                   const smt_tile_desc* tiles_dev, int32_t n_tiles, int64_t n_elems, const double* grad_sq_norm_dev,
+                   const smt_adamw_args* args, hipStream_t stream) {
+    if (!args) return fail(SMT_E_INVALID, "smt_adamw_step: null args");
+    if (args->grad_dtype != SMT_DTYPE_BF16 && args->grad_dtype != SMT_DTYPE_FP32)
+        return fail(SMT_E_INVALID, "smt_adamw_step: grad_dtype %d not supported", args->grad_dtype);
+    if (args->mode != SMT_ADAM_DEEPSPEED && args->mode != SMT_ADAM_TORCH)
+        return fail(SMT_E_INVALID, "smt_adamw_step: mode %d", args->mode);
+    if (!(args->bias_correction1 > 0.f) || !(args->bias_correction2 > 0.f))
+        return fail(SMT_E_INVALID, "smt_adamw_step: bias corrections must be > 0");
+    const bool tiled = tiles_dev != nullptr;
+    if (tiled ? n_tiles < 0 : n_elems < 0) return fail(SMT_E_INVALID, "smt_adamw_step: negative size");
+    if ((tiled && n_tiles == 0) || (!tiled && n_elems == 0)) return SMT_OK;
+    if (!grad || !master || !exp_avg || !exp_avg_sq || !param_bf16) return fail(SMT_E_INVALID, "smt_adamw_step: null buffer");
+    if (!aligned16(grad) || !aligned16(master) || !aligned16(exp_avg) || !aligned16(exp_avg_sq) || !aligned16(param_bf16))
+        return fail(SMT_E_ALIGN, "smt_adamw_step: buffers must be 16-byte aligned");
+    const smt_adamw_args a = *args;
+    uint16_t* p = static_cast<uint16_t*>(param_bf16);
+    if (tiled) {
+        dim3 grid(n_tiles * 32);
+        if (a.grad_dtype == SMT_DTYPE_FP32)
+            hipLaunchKernelGGL(adamw_tiles_kernel<SMT_DTYPE_FP32>, grid, dim3(256), 0, stream, grad, master, exp_avg, exp_avg_sq, p, tiles_dev, grad_sq_norm_dev, a);
+        else
+            hipLaunchKernelGGL(adamw_tiles_kernel<SMT_DTYPE_BF16>, grid, dim3(256), 0, stream, grad, master, exp_avg, exp_avg_sq, p, tiles_dev, grad_sq_norm_dev, a);
+        return check_launch("adamw_tiles_kernel");
+    }
+    const int64_t blocks = (n_elems + 2047) / 2048;
+    if (blocks > 0x7fffffffLL) return fail(SMT_E_INVALID, "smt_adamw_step: too many elements");
+    if (a.grad_dtype == SMT_DTYPE_FP32)
+        hipLaunchKernelGGL(adamw_flat_kernel<SMT_DTYPE_FP32>, dim3((unsigned)blocks), dim3(256), 0, stream, grad, master, exp_avg, exp_avg_sq, p, n_elems, grad_sq_norm_dev, a);
+    else
+        hipLaunchKernelGGL(adamw_flat_kernel<SMT_DTYPE_BF16>, dim3((unsigned)blocks), dim3(256), 0, stream, grad, master, exp_avg, exp_avg_sq, p, n_elems, grad_sq_norm_dev, a);
+    return check_launch("adamw_flat_kernel");
+}
+
+}  // extern "C"

@@ -1,0 +1,309 @@
+"""Minimal DeepSpeed-engine surface for the SMT hot path on MI355X.
+
+``fine_tune.py`` drives training through ``deepspeed.initialize`` (fine_tune.py:184-190,
+379-384), ``model.backward(loss)`` (:712), ``model.step()`` (:773), ``model.module`` and
+``safe_get_full_grad`` (:724, :751). DeepSpeed is not part of this build; :func:`initialize`
+returns an engine with that surface, designed for the SMT phase on one GPU per process:
+
+* Every trainable ``selected_weight`` of the model's SMT modules is re-pointed into ONE flat
+  bf16 buffer (tile-major, 65536 elements per tile). fp32 master / exp_avg / exp_avg_sq and an
+  fp32 gradient buffer of the same length sit beside it (57.1 M params at the LLaMA-3-8B
+  operating point: 0.92 GB).
+* ``linearZ.backward`` writes each module's tile gradients straight into that fp32 buffer through
+  the module's gradient sink (no autograd accumulation, no bf16 rounding).
+* At the gradient-accumulation boundary the engine issues ONE RCCL all-reduce (sum) of the flat
+  gradient buffer (torch.distributed "nccl" = RCCL over xGMI); averaging (1/world) is folded into
+  the optimizer kernels.
+* ``step()`` = one ``smt_sq_norm`` (global norm for ``gradient_clipping``) + one fused
+  ``smt_adamw_step`` launch per parameter group that clips, updates fp32 master/moments, writes the
+  bf16 tiles AND scatters them into the frozen ``W`` — so the modules skip the per-forward
+  write-back of smt.py:332-341. No host synchronisation anywhere in the step.
+
+Other trainable parameters (the full fine-tuning warm-up, fine_tune.py:160-190) take the dense
+path: autograd bf16 grads, one all-reduce per parameter, and the same fused AdamW kernel in flat
+mode over per-parameter fp32 masters. The ZeRO partitioning of the reference is not reproduced:
+at 288 GB per GPU the 57 M-parameter tile optimizer state is simply replicated.
+"""
+from __future__ import annotations
+
+import math
+from typing import Iterable, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from . import _hip
+from .smt.smt import LinearLayer_MatrixSparsity
+
+TILE_ELEMS = _hip.TILE_ELEMS
+
+
+class SMTFusedAdam(torch.optim.Optimizer):
+    """Constructor-compatible stand-in for DeepSpeed ``FusedAdam`` (fine_tune.py:352, 361-363).
+
+    Update rule (DeepSpeed multi_tensor_adam ADAM_MODE_1, adam_w_mode=True; external, restated):
+        m = b1*m + (1-b1)*g ;  v = b2*v + (1-b2)*g*g
+        p = p - lr * ( (m/bc1) / (sqrt(v/bc2) + eps) + wd*p )
+    ``adam_w_mode=False`` is not supported (the reference always uses AdamW). Used standalone,
+    ``step()`` runs the fused HIP kernel per parameter (flat mode) on ``p.grad``; under
+    :class:`SMTEngine` the engine owns packed buffers and drives the kernel itself.
+    """
+
+    def __init__(self, params, lr=1e-3, bias_correction=True, betas=(0.9, 0.999), eps=1e-8,
+                 adam_w_mode=True, weight_decay=0.0, amsgrad=False, set_grad_none=True):
+        if amsgrad:
+            raise RuntimeError("FusedAdam does not support the AMSGrad variant.")
+        if not adam_w_mode:
+            raise NotImplementedError("SMTFusedAdam implements adam_w_mode=True only")
+        defaults = dict(lr=lr, bias_correction=bias_correction, betas=betas, eps=eps, weight_decay=weight_decay)
+        super().__init__(params, defaults)
+        self.mode = _hip.ADAM_DEEPSPEED
+
+    def _args(self, group, step: int, max_norm: float = 0.0, grad_scale: float = 1.0) -> _hip.AdamWArgs:
+        b1, b2 = group["betas"]
+        bc1 = 1.0 - b1 ** step if group.get("bias_correction", True) else 1.0
+        bc2 = 1.0 - b2 ** step if group.get("bias_correction", True) else 1.0
+        return _hip.AdamWArgs(lr=group["lr"], beta1=b1, beta2=b2, eps=group["eps"],
+                              weight_decay=group["weight_decay"], bias_correction1=bc1,
+                              bias_correction2=bc2, max_grad_norm=max_norm, grad_scale=grad_scale,
+                              mode=self.mode, grad_dtype=0)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        for group in self.param_groups:
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                if p.dtype != torch.bfloat16:
+                    raise NotImplementedError("SMTFusedAdam: bf16 parameters only")
+                st = self.state[p]
+                if not st:
+                    st["step"] = 0
+                    st["master"] = p.detach().float()
+                    st["exp_avg"] = torch.zeros_like(st["master"])
+                    st["exp_avg_sq"] = torch.zeros_like(st["master"])
+                st["step"] += 1
+                _hip.adamw_step(p.grad.contiguous(), st["master"], st["exp_avg"], st["exp_avg_sq"], p.data,
+                                self._args(group, st["step"]))
+        return loss
+
+
+class _GradSink:
+    """Where ``linearZ.backward`` writes one module's fp32 tile gradients."""
+
+    __slots__ = ("buffer", "engine")
+
+    def __init__(self, buffer: torch.Tensor, engine: "SMTEngine"):
+        self.buffer = buffer
+        self.engine = engine
+
+    def take_accumulate(self) -> bool:
+        return self.engine._accumulate_tiles
+
+
+class _TileGroup:
+    """All SMT tiles of one optimizer parameter group, packed tile-major."""
+
+    def __init__(self, group: dict, modules: List[LinearLayer_MatrixSparsity], device, engine):
+        self.group = group
+        self.modules = modules
+        n_tiles = sum(len(m.tiles) for m in modules)
+        self.n_tiles = n_tiles
+        n = n_tiles * TILE_ELEMS
+        self.param = torch.empty(n, dtype=torch.bfloat16, device=device)
+        self.grad = torch.zeros(n, dtype=torch.float32, device=device)
+        descs, off = [], 0
+        for m in modules:
+            k = len(m.tiles)
+            view = self.param[off * TILE_ELEMS:(off + k) * TILE_ELEMS].view(k * 256, 256)
+            view.copy_(m.selected_weight.data)
+            m.selected_weight.data = view                       # re-point the Parameter's storage
+            m.selected_weight._smt_grad_sink = _GradSink(
+                self.grad[off * TILE_ELEMS:(off + k) * TILE_ELEMS].view(k * 256, 256), engine)
+            m.writeback_on_forward = False                      # the AdamW epilogue scatters into W
+            m.sync_weight()                                     # W consistent with the tiles now
+            for i, (r, c) in enumerate(m.tiles):
+                descs.append((m.weight.data, r, c, (off + i) * TILE_ELEMS))
+            off += k
+        self.master = self.param.float()
+        self.exp_avg = torch.zeros_like(self.master)
+        self.exp_avg_sq = torch.zeros_like(self.master)
+        self.descs = _hip.tile_descs(descs, device) if descs else None
+        self.step = 0
+
+
+class SMTEngine:
+    """``deepspeed.initialize`` result surface: ``backward``, ``step``, ``module``, ``train``/``eval``;
+    unknown attributes are forwarded to the module (e.g. ``gradient_checkpointing_enable``)."""
+
+    def __init__(self, model, optimizer: Optional[torch.optim.Optimizer], config: Optional[dict] = None,
+                 lr_scheduler=None):
+        self.module = model
+        self.optimizer = optimizer
+        self.lr_scheduler = lr_scheduler
+        cfg = dict(config or {})
+        self.config = cfg
+        self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+        micro = cfg.get("train_micro_batch_size_per_gpu")
+        total = cfg.get("train_batch_size")
+        gas = cfg.get("gradient_accumulation_steps")
+        if gas is None:
+            gas = max(1, int(total) // (int(micro) * self.world)) if (micro and total) else 1
+        self.gradient_accumulation_steps = int(gas)
+        self.max_grad_norm = float(cfg.get("gradient_clipping", 0.0) or 0.0)
+        self.micro_steps = 0
+        self.global_steps = 0
+        self._accumulate_tiles = False
+        self.device = next(model.parameters()).device
+
+        self.tile_groups: List[_TileGroup] = []
+        self.dense_groups: List[tuple] = []   # (group, [params])
+        self._dense_state = {}
+        if optimizer is not None:
+            owner = {}
+            for m in model.modules():
+                if isinstance(m, LinearLayer_MatrixSparsity) and m.selected_weight.requires_grad and len(m.tiles):
+                    owner[id(m.selected_weight)] = m
+            for group in optimizer.param_groups:
+                mods = [owner[id(p)] for p in group["params"] if id(p) in owner]
+                dense = [p for p in group["params"] if id(p) not in owner and p.requires_grad]
+                if mods:
+                    if any(m.weight.dtype != torch.bfloat16 for m in mods):
+                        raise NotImplementedError("SMT engine: bf16 models only")
+                    self.tile_groups.append(_TileGroup(group, mods, self.device, self))
+                if dense:
+                    self.dense_groups.append((group, dense))
+        self._norm_sq = torch.zeros(1, dtype=torch.float64, device=self.device)
+
+    # -- DeepSpeed surface ----------------------------------------------------------------------
+    def __call__(self, *args, **kwargs):
+        return self.module(*args, **kwargs)
+
+    forward = __call__
+
+    def __getattr__(self, name):
+        return getattr(self.__dict__["module"], name)
+
+    def train(self, mode: bool = True):
+        self.module.train(mode)
+        return self
+
+    def eval(self):
+        self.module.eval()
+        return self
+
+    def is_gradient_accumulation_boundary(self) -> bool:
+        return (self.micro_steps + 1) % self.gradient_accumulation_steps == 0
+
+    def backward(self, loss: torch.Tensor):
+        """Scale by 1/gas, run autograd (tile grads land in the packed fp32 buffer), and at the
+        accumulation boundary all-reduce the gradients across ranks."""
+        self._accumulate_tiles = (self.micro_steps % self.gradient_accumulation_steps) != 0
+        if self.gradient_accumulation_steps > 1:
+            loss = loss / self.gradient_accumulation_steps
+        loss.backward()
+        if self.is_gradient_accumulation_boundary() and self.world > 1:
+            for tg in self.tile_groups:
+                dist.all_reduce(tg.grad)            # sum; 1/world folded into the kernels
+            dense = [p.grad for _g, ps in self.dense_groups for p in ps if p.grad is not None]
+            for g in dense:
+                dist.all_reduce(g)
+            if dense:
+                torch._foreach_div_(dense, float(self.world))   # averaged, as safe_get_full_grad sees them
+        return loss
+
+    def _grad_scale(self) -> float:
+        return 1.0 / self.world
+
+    def step(self):
+        boundary = self.is_gradient_accumulation_boundary()
+        self.micro_steps += 1
+        if not boundary:
+            return
+        gs = self._grad_scale()
+        norm = None
+        if self.max_grad_norm > 0:
+            # squared global norm of the effective (DP-averaged) gradient, kept on the device
+            self._norm_sq.zero_()
+            for tg in self.tile_groups:
+                self._norm_sq += _hip.sq_norm(tg.grad) * (gs * gs)
+            dense_grads = [p.grad for _g, ps in self.dense_groups for p in ps if p.grad is not None]
+            if dense_grads:
+                norms = torch._foreach_norm(dense_grads, 2.0)
+                self._norm_sq += torch.stack([n.double() for n in norms]).pow(2).sum()
+            norm = self._norm_sq
+        for tg in self.tile_groups:
+            tg.step += 1
+            args = self.optimizer._args(tg.group, tg.step, self.max_grad_norm, gs)
+            _hip.adamw_step(tg.grad, tg.master, tg.exp_avg, tg.exp_avg_sq, tg.param, args,
+                            tiles=tg.descs, n_tiles=tg.n_tiles, grad_sq_norm=norm)
+        for group, params in self.dense_groups:
+            for p in params:
+                if p.grad is None:
+                    continue
+                st = self._dense_state.get(id(p))
+                if st is None:
+                    st = {"step": 0, "master": p.detach().float()}
+                    st["exp_avg"] = torch.zeros_like(st["master"])
+                    st["exp_avg_sq"] = torch.zeros_like(st["master"])
+                    self._dense_state[id(p)] = st
+                st["step"] += 1
+                args = self.optimizer._args(group, st["step"], self.max_grad_norm, 1.0)
+                _hip.adamw_step(p.grad.contiguous(), st["master"], st["exp_avg"], st["exp_avg_sq"], p.data, args,
+                                grad_sq_norm=norm)
+                p.grad = None
+        self.global_steps += 1
+        if self.lr_scheduler is not None:
+            self.lr_scheduler.step()
+
+    def zero_grad(self):
+        for _g, params in self.dense_groups:
+            for p in params:
+                p.grad = None
+
+    def tile_grad(self, param: torch.Tensor) -> Optional[torch.Tensor]:
+        """DP-averaged fp32 gradient of one ``selected_weight`` (``safe_get_full_grad`` semantics)."""
+        sink = getattr(param, "_smt_grad_sink", None)
+        if sink is None or sink.engine is not self:
+            return None
+        return sink.buffer * self._grad_scale()
+
+    def release(self):
+        """Drop optimizer state and packed buffers (e.g. the warm-up engine before SMT starts)."""
+        for tg in self.tile_groups:
+            for m in tg.modules:
+                if hasattr(m.selected_weight, "_smt_grad_sink"):
+                    del m.selected_weight._smt_grad_sink
+        self.tile_groups = []
+        self._dense_state = {}
+        for _g, ps in self.dense_groups:
+            for p in ps:
+                p.grad = None
+        self.dense_groups = []
+
+
+def initialize(model=None, optimizer=None, args=None, config=None, lr_scheduler=None,
+               model_parameters=None, dist_init_required=None, **_kw):
+    """``deepspeed.initialize`` signature; returns ``(engine, optimizer, None, lr_scheduler)``."""
+    if optimizer is None and model_parameters is not None:
+        optimizer = SMTFusedAdam(model_parameters)
+    engine = SMTEngine(model, optimizer, config=config, lr_scheduler=lr_scheduler)
+    return engine, optimizer, None, lr_scheduler
+
+
+def safe_get_full_grad(param: torch.Tensor, engine: Optional[SMTEngine] = None):
+    """DeepSpeed ``safe_get_full_grad`` (fine_tune.py:724, 751): the full, DP-averaged gradient."""
+    sink = getattr(param, "_smt_grad_sink", None)
+    if sink is not None:
+        return sink.engine.tile_grad(param)
+    return param.grad
+
+
+def linear_lr_lambda(num_warmup_steps: int, num_training_steps: int):
+    """HF ``get_scheduler('linear')`` (fine_tune.py:367-373) as a LambdaLR factor."""
+    def f(step: int) -> float:
+        if step < num_warmup_steps:
+            return float(step) / float(max(1, num_warmup_steps))
+        return max(0.0, float(num_training_steps - step) / float(max(1, num_training_steps - num_warmup_steps)))
+    return f

@@ -1,0 +1,388 @@
+"""MI355X drop-in for ``deepspeed/smt/smt.py`` (the matrix-sparsity path).
+
+Same names, signatures, argument meaning and error behaviour as the reference module that
+``deepspeed/fine_tune.py:39`` imports, re-implemented over the gfx950 kernels of
+``libsmt_hip.so``:
+
+* tile gather (smt.py:317-325) and the per-forward write-back (smt.py:332-341) are one HIP
+  launch per module instead of one copy per tile;
+* ``linearZ.backward``'s per-tile Python loop of batched GEMM + sum + copy (smt.py:386-404) is
+  one grouped bf16 MFMA launch over every tile of the module;
+* under :func:`sparse_matrix_tuning_amd.engine.initialize` the tile gradients land in fp32 in the
+  engine's packed buffer and the fused AdamW writes the tiles back into ``W``, so the forward
+  write-back is skipped.
+
+Differences from the reference, all deliberate:
+
+* no process-group initialisation or rank query at import (smt.py:20-21);
+* no ``print_rank_0`` spam;
+* the wgrad sums the whole batch in fp32 and rounds once, where the reference rounds every
+  per-sample ``[256, 256]`` partial to bf16 before summing (smt.py:397-404), so tile gradients
+  are closer to exact than the reference's (tolerance stated in tests/test_gpu_parity.py).
+
+There is no CPU or eager-PyTorch path: a module built on CPU tensors raises. ``meta`` tensors are
+accepted for shape-only construction (used by the CPU tests of the conversion logic).
+"""
+from __future__ import annotations
+
+import re
+from typing import Iterable, List, Optional, Sequence, Tuple
+
+import torch
+from torch import nn
+
+from .. import _hip
+
+Block_dimension = 256
+
+_LAYER_PATTERN = re.compile(r'model\.layers\.(\d+)\.')
+_NO_DECAY = ["bias", "layer_norm.weight", "layernorm.weight", "norm.weight", "ln_f.weight"]
+
+
+# ------------------------------------------------------------------------------------------------
+# naming helpers (the inline expressions of smt.py:105-107, 121-125, 651-653, 726-729)
+# ------------------------------------------------------------------------------------------------
+def recursive_getattr(model: nn.Module, module_name: str):
+    """Same contract as deepspeed.compression.helper.recursive_getattr (imported at smt.py:1)."""
+    output = model
+    for name in module_name.split('.'):
+        output = getattr(output, name)
+    return output
+
+
+def recursive_setattr(model: nn.Module, module_name: str, module: nn.Module) -> None:
+    """Same contract as deepspeed.compression.helper.recursive_setattr (imported at smt.py:1)."""
+    split_list = module_name.split('.')
+    output = model
+    for name in split_list[:-1]:
+        output = getattr(output, name)
+    output.__setattr__(split_list[-1], module)
+
+
+def _mlp_module_name(name: str) -> str:
+    return 'gate_proj' if 'gate_proj' in name else 'up_proj' if 'up_proj' in name else 'down_proj'
+
+
+def _attn_module_name(name: str) -> Optional[str]:
+    return ('q_proj' if 'q_proj' in name else 'k_proj' if 'k_proj' in name else
+            'v_proj' if 'v_proj' in name else 'o_proj' if 'o_proj' in name else None)
+
+
+def _layer_number(name: str) -> Optional[int]:
+    match = _LAYER_PATTERN.search(name)
+    return int(match.group(1)) if match else None
+
+
+# ------------------------------------------------------------------------------------------------
+# tile index: the reference's Python list plus its device copy
+# ------------------------------------------------------------------------------------------------
+class TileIndex:
+    """``index_list`` of smt.py:310 (list of ``(row_block, col_block)`` in selection order) with a
+    cached device ``int32 [n, 2]`` table for the kernels."""
+
+    def __init__(self, index_list: Iterable[Sequence[int]]):
+        self.index_list: List[Tuple[int, int]] = [(int(i[0]), int(i[1])) for i in index_list]
+        self._dev = {}
+
+    def __len__(self) -> int:
+        return len(self.index_list)
+
+    def __iter__(self):
+        return iter(self.index_list)
+
+    def __getitem__(self, i):
+        return self.index_list[i]
+
+    def device_table(self, device: torch.device) -> torch.Tensor:
+        key = (device.type, device.index)
+        t = self._dev.get(key)
+        if t is None:
+            t = _hip.tile_table(self.index_list, device)
+            self._dev[key] = t
+        return t
+
+    def validate(self, rows: int, cols: int) -> None:
+        rb, cb = rows // Block_dimension, cols // Block_dimension
+        for r, c in self.index_list:
+            if not (0 <= r < rb and 0 <= c < cb) or rows % Block_dimension or cols % Block_dimension:
+                # the reference's slice assignment fails with a shape-mismatch RuntimeError here
+                raise RuntimeError(
+                    f"tile ({r}, {c}) outside a [{rows}, {cols}] weight in {Block_dimension}-blocks")
+
+
+def _as_tile_index(index) -> TileIndex:
+    return index if isinstance(index, TileIndex) else TileIndex(index)
+
+
+# ------------------------------------------------------------------------------------------------
+# the SMT module (smt.py:302-344)
+# ------------------------------------------------------------------------------------------------
+class LinearLayer_MatrixSparsity(torch.nn.Module):
+    """Frozen dense ``W`` (aliased, not copied, smt.py:307) plus the trainable 256x256 tiles
+    ``selected_weight [n*256, 256]`` listed in ``index_list`` (smt.py:312-327)."""
+
+    def __init__(self, weight, bias=None, index_list=[]):
+        super().__init__()
+        self.weight = weight
+        self.weight.requires_grad = False
+        self.bias = bias
+        self.tiles = _as_tile_index(index_list)
+        self.index_list = self.tiles.index_list
+        # True: write the tiles into W at every forward (smt.py:332-341). The SMT engine clears it
+        # because its fused AdamW already scatters the updated tiles into W.
+        self.writeback_on_forward = True
+
+        w = self.weight.data
+        n = len(self.tiles)
+        dev = w.device
+        if dev.type not in ("cuda", "meta"):
+            raise RuntimeError(
+                f"LinearLayer_MatrixSparsity: weight on {dev}; the SMT path runs on ROCm devices only")
+        if w.dim() != 2:
+            raise RuntimeError(f"LinearLayer_MatrixSparsity: 2-D weight expected, got {tuple(w.shape)}")
+        self.tiles.validate(w.shape[0], w.shape[1])
+        selected = torch.empty(n * Block_dimension, Block_dimension, dtype=w.dtype, device=dev)
+        if dev.type == "cuda" and n:
+            _hip.tile_gather(w, self.tiles.device_table(dev), selected)
+        self.selected_weight = nn.Parameter(selected, requires_grad=True)
+        self.fn = linearZ.apply
+
+    def sync_weight(self) -> None:
+        """Scatter the tiles into W (smt.py:332-341) with one launch."""
+        w = self.weight.data
+        if len(self.tiles) and w.device.type == "cuda":
+            _hip.tile_scatter(w, self.tiles.device_table(w.device), self.selected_weight.data)
+
+    def forward(self, x):
+        if self.writeback_on_forward:
+            self.sync_weight()
+        return self.fn(x, self.selected_weight, self.tiles, self.weight)
+
+    def extra_repr(self) -> str:
+        return f"in_features={self.weight.shape[1]}, out_features={self.weight.shape[0]}, tiles={len(self.tiles)}"
+
+
+SMTLinear = LinearLayer_MatrixSparsity
+
+
+class linearZ(torch.autograd.Function):
+    """``y = x @ W^T`` (smt.py:350-373); backward returns ``(grad_input, grad_tiles, None, None)``
+    (smt.py:376-413) with every tile's gradient from one grouped MFMA launch.
+
+    If ``selected_weight`` carries an engine gradient sink (``_smt_grad_sink``), the fp32 tile
+    gradients are written straight into the engine's packed buffer and ``None`` is returned for
+    ``selected_weight`` (the engine, not autograd, owns those gradients)."""
+
+    @staticmethod
+    def forward(ctx, input, selected_weight, matrix_index_list, weight):
+        tiles = _as_tile_index(matrix_index_list)
+        if len(tiles) and input.dim() != 3:
+            # smt.py:354-356 slices input[:, :, cols]; anything but 3-D fails there
+            raise IndexError(f"too many indices for tensor of dimension {input.dim()}")
+        ctx.tiles = tiles
+        ctx.sink = getattr(selected_weight, "_smt_grad_sink", None)
+        ctx.save_for_backward(input, weight)
+        return torch.matmul(input, weight.t())
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        input, weight = ctx.saved_tensors
+        tiles = ctx.tiles
+        n = len(tiles)
+        grad_input = grad_weight = None
+        if ctx.needs_input_grad[1]:
+            out_f = weight.shape[0]
+            in_f = weight.shape[1]
+            g2 = grad_output.reshape(-1, out_f)
+            x2 = input.reshape(-1, in_f)
+            if g2.stride(1) != 1 or g2.stride(0) % 8 or g2.data_ptr() % 16:
+                g2 = g2.contiguous()
+            if x2.stride(1) != 1 or x2.stride(0) % 8 or x2.data_ptr() % 16:
+                x2 = x2.contiguous()
+            sink = ctx.sink
+            if sink is not None:
+                _hip.tile_wgrad(g2, x2, tiles.device_table(g2.device), sink.buffer, accumulate=sink.take_accumulate())
+            else:
+                grad_weight = torch.empty(n * Block_dimension, Block_dimension,
+                                          dtype=grad_output.dtype, device=grad_output.device)
+                if n:
+                    _hip.tile_wgrad(g2, x2, tiles.device_table(g2.device), grad_weight)
+        if ctx.needs_input_grad[0]:
+            grad_input = torch.matmul(grad_output, weight)
+        return grad_input, grad_weight, None, None
+
+
+# ------------------------------------------------------------------------------------------------
+# model surgery (smt.py:83-179, 416-457, 641-745)
+# ------------------------------------------------------------------------------------------------
+def _replace(model, name, index_list):
+    module = recursive_getattr(model, name)
+    tmp = LinearLayer_MatrixSparsity(module.weight, bias=None, index_list=index_list).to(
+        module.weight.device).to(module.weight.dtype)
+    recursive_setattr(model, name, tmp)
+
+
+def convert_linear_layer_to_matrix_sparsity(model,
+                                            selected_submatrix,
+                                            selected_submatrix_attention,
+                                            part_module_name=['.layers'],
+                                            mixture=False):
+    """smt.py:83-179. Replace every trainable ``nn.Linear`` under ``part_module_name`` by an SMT
+    module holding its selected tiles; keys are ``(module_name, layer)`` with the layer read by the
+    regex ``model\\.layers\\.(\\d+)\\.`` (``None`` when it does not match). Biases are dropped."""
+    replace_name = []
+    for name, module in model.named_modules():
+        if isinstance(module, nn.Linear) and any(part in name for part in part_module_name):
+            replace_name.append(name)
+
+    for name in replace_name:
+        if "mlp" in name:
+            module = recursive_getattr(model, name)
+            if module.weight.requires_grad:
+                key = (_mlp_module_name(name), _layer_number(name))
+                _replace(model, name, selected_submatrix[key])
+        if "self_attn" in name:
+            module = recursive_getattr(model, name)
+            if module.weight.requires_grad:
+                key = (_attn_module_name(name), _layer_number(name))
+                src = selected_submatrix if mixture else selected_submatrix_attention
+                _replace(model, name, src[key])
+        if mixture and "embed_tokens" in name:
+            module = recursive_getattr(model, name)
+            if module.weight.requires_grad:
+                _replace(model, name, selected_submatrix[('embed_tokens', None)])
+    return model
+
+
+def convert_matrix_sparsity_to_linear_layer(model, part_module_name=['.layers']):
+    """smt.py:416-457: scatter each module's tiles into W and swap back a bias-free ``nn.Linear``
+    that shares ``W`` (no copy)."""
+    replace_name = []
+    for name, module in model.named_modules():
+        if isinstance(module, LinearLayer_MatrixSparsity) and any(part in name for part in part_module_name):
+            replace_name.append(name)
+    for name in replace_name:
+        module = recursive_getattr(model, name)
+        module.sync_weight()
+        weight_shape = module.weight.shape
+        new_linear = nn.Linear(weight_shape[1], weight_shape[0], bias=False, device="meta")
+        new_linear.weight = module.weight
+        recursive_setattr(model, name, new_linear)
+        del module
+    return model
+
+
+def freeze_unselected_matrix_layer(model,
+                                   select_parameters,
+                                   select_attention_parameters,
+                                   mixture=False,
+                                   layernorm=False):
+    """smt.py:641-745: ``requires_grad`` is True exactly for the parameters of selected
+    ``(module, layer)`` keys (plus layernorms / embed_tokens in mixture mode)."""
+    for name, param in model.named_parameters():
+        if mixture:
+            if "mlp" in name:
+                param.requires_grad = (_mlp_module_name(name), _layer_number(name)) in select_parameters.keys()
+            elif "self_attn" in name:
+                param.requires_grad = (_attn_module_name(name), _layer_number(name)) in select_parameters.keys()
+            elif "embed_tokens" in name:
+                param.requires_grad = ('embed_tokens', None) in select_parameters.keys()
+            elif ("input_layernorm" in name) or ("post_attention_layernorm" in name):
+                param.requires_grad = bool(layernorm)
+            else:
+                param.requires_grad = False
+        else:
+            if "mlp" in name:
+                param.requires_grad = (_mlp_module_name(name), _layer_number(name)) in select_parameters.keys()
+            elif "self_attn" in name:
+                param.requires_grad = (_attn_module_name(name), _layer_number(name)) in select_attention_parameters.keys()
+            else:
+                param.requires_grad = False
+    return model
+
+
+# ------------------------------------------------------------------------------------------------
+# optimizer parameter groups (smt.py:465-549, 554-638)
+# ------------------------------------------------------------------------------------------------
+def _groups(model, weight_decay, lr0, lr1, special, no_decay):
+    named = list(model.named_parameters())
+    no_decay = list(_NO_DECAY if no_decay is None else no_decay)
+    groups = [
+        {"params": [p for n, p in named if not any(nd in n.lower() for nd in no_decay)
+                    and p.requires_grad and not any(nd in n.lower() for nd in special)],
+         "weight_decay": weight_decay, "lr": lr0},
+        {"params": [p for n, p in named if not any(nd in n.lower() for nd in no_decay)
+                    and p.requires_grad and any(nd in n.lower() for nd in special)],
+         "weight_decay": weight_decay, "lr": lr1},
+        {"params": [p for n, p in named if any(nd in n.lower() for nd in no_decay) and p.requires_grad],
+         "weight_decay": 0.0},
+    ]
+    return [g for g in groups if g["params"]]
+
+
+def get_optimizer_sparse_grouped_parameters(
+    model,
+    weight_decay,
+    smt_lr,
+    lora_lr=5e-4,
+    no_decay_name_list=None,
+    lora_name_list=("lora_right_weight", "lora_left_weight"),
+):
+    """smt.py:465-549: group 0 = trainable non-norm params at ``smt_lr``; empty groups dropped.
+    ``no_decay_name_list=None`` means the reference default (bias / *norm.weight / ln_f.weight)."""
+    return _groups(model, weight_decay, smt_lr, lora_lr, lora_name_list, no_decay_name_list)
+
+
+def get_optimizer_qk_augment_grouped_parameters(
+    model,
+    weight_decay,
+    ft_learning_rate,
+    module_lr=5e-4,
+    no_decay_name_list=None,
+    module_name_list=("q_proj", "k_proj"),
+):
+    """smt.py:554-638: q/k projections get ``module_lr`` (warm-up only, fine_tune.py:160-163)."""
+    return _groups(model, weight_decay, ft_learning_rate, module_lr, module_name_list, no_decay_name_list)
+
+
+# ------------------------------------------------------------------------------------------------
+# channel-sparsity path (smt.py:25-80, 185-296, 748-831): SURVEY §8(f) "next"
+# ------------------------------------------------------------------------------------------------
+def freeze_unselected_channel_layer(model, select_parameters, select_attention_parameters, mixture=False):
+    """smt.py:748-831 (host logic only; note o_proj is not a candidate on this path)."""
+    for name, param in model.named_parameters():
+        if "mlp" in name:
+            param.requires_grad = (_mlp_module_name(name), _layer_number(name)) in select_parameters.keys()
+        elif "self_attn" in name:
+            mod = ('q_proj' if 'q_proj' in name else 'k_proj' if 'k_proj' in name else
+                   'v_proj' if 'v_proj' in name else None)
+            sel = select_parameters if mixture else select_attention_parameters
+            param.requires_grad = (mod, _layer_number(name)) in sel.keys()
+        else:
+            param.requires_grad = False
+    return model
+
+
+def _channel_next(*_a, **_k):
+    raise NotImplementedError(
+        "channel-sparsity (activation-selected rows, smt.py:185-296) is SURVEY §8(f) 'next' and not "
+        "built yet; see DESIGN.md")
+
+
+convert_linear_layer_to_channel_sparsity = _channel_next
+
+
+class LinearLayer_ChannelSparsity(torch.nn.Module):
+    def __init__(self, *a, **k):
+        super().__init__()
+        _channel_next()
+
+
+class linearChannel(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, *a):
+        _channel_next()
+
+    @staticmethod
+    def backward(ctx, *a):
+        _channel_next()
