@@ -45,6 +45,7 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef short s16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
 
@@ -88,13 +89,10 @@ __device__ __forceinline__ uint32_t img_off(uint32_t k, uint32_t byte_in_row) {
 __device__ __forceinline__ bf16x8_t tr_frag(const uint8_t* img, uint32_t k, uint32_t byte_in_row) {
     s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(img + img_off(k, byte_in_row)));
     s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(img + img_off(k + 4, byte_in_row)));
-    bf16x8_t f;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        f[j] = __builtin_bit_cast(__bf16, lo[j]);
-        f[j + 4] = __builtin_bit_cast(__bf16, hi[j]);
-    }
-    return f;
+    // whole-vector bit casts: element-wise __bf16 bit_casts of vector lanes miscompile (all lanes
+    // came back equal to element 0 on ROCm 7.2 / gfx950)
+    const s16x8_t both = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8_t, both);
 }
 
 __global__ __launch_bounds__(kWgThreads, 2)
