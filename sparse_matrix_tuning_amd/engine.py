@@ -255,6 +255,8 @@ class SMTEngine:
                 p.grad = None
         self.global_steps += 1
         if self.lr_scheduler is not None:
+            if self.optimizer is not None:
+                self.optimizer._opt_called = True     # the engine, not optimizer.step(), applied the update
             self.lr_scheduler.step()
 
     def zero_grad(self):

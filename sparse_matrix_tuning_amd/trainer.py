@@ -156,6 +156,9 @@ def select_and_convert(engine, harvester: GradHarvester, targeted_module_dims: d
     if hasattr(model, "enable_input_require_grads"):     # make_model_gradient_checkpointing_compatible
         model.enable_input_require_grads()
     groups = get_optimizer_sparse_grouped_parameters(model, w_decay, smt_lr)
+    if not groups:
+        raise RuntimeError("SMT selection produced no trainable tile (block budgets "
+                           f"attention={num_attention_blocks}, mlp={num_mlp_blocks})")
     opt = SMTFusedAdam(groups, lr=ft_learning_rate if ft_learning_rate is not None else smt_lr, betas=(0.9, 0.95))
     sched = torch.optim.lr_scheduler.LambdaLR(opt, linear_lr_lambda(smt_lr_warmup_steps, num_training_steps))
     torch.cuda.empty_cache()
