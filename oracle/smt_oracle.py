@@ -230,3 +230,60 @@ def fused_adam_step(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.
     denom = torch.sqrt(v / bc2) + eps
     update = (m / bc1) / denom + weight_decay * p
     p.sub_(lr * update)
+
+
+# ------------------------------------------------------------------------------------------------
+# module-level restatement (smt.py:83-134, 302-413) for end-to-end CPU checks
+# ------------------------------------------------------------------------------------------------
+class RefLinearZ(torch.autograd.Function):
+    """smt.py:347-413."""
+
+    @staticmethod
+    def forward(ctx, input, selected_weight, matrix_index_list, weight):
+        ctx.save_for_backward(input, weight)
+        ctx.index_list = list(matrix_index_list)
+        return linearz_forward(input, weight)
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        input, weight = ctx.saved_tensors
+        grad_input, grad_weight = linearz_backward(grad_output, input, weight, ctx.index_list)
+        return grad_input, grad_weight, None, None
+
+
+class RefLinearLayer_MatrixSparsity(torch.nn.Module):
+    """smt.py:302-344 (CPU)."""
+
+    def __init__(self, weight, index_list):
+        super().__init__()
+        self.weight = weight
+        self.weight.requires_grad = False
+        self.index_list = list(index_list)
+        self.selected_weight = torch.nn.Parameter(gather_tiles(weight.data, self.index_list))
+
+    def forward(self, x):
+        writeback_tiles(self.weight.data, self.selected_weight.data, self.index_list)
+        return RefLinearZ.apply(x, self.selected_weight, self.index_list, self.weight)
+
+
+def ref_convert(model, selected_mlp, selected_att):
+    """smt.py:83-134 (non-mixture branch) with the restated module."""
+    names = [n for n, m in model.named_modules() if isinstance(m, torch.nn.Linear) and '.layers' in n]
+    for name in names:
+        parent = model
+        parts = name.split('.')
+        for p in parts[:-1]:
+            parent = getattr(parent, p)
+        module = getattr(parent, parts[-1])
+        if not module.weight.requires_grad:
+            continue
+        match = _LAYER.search(name)
+        layer = int(match.group(1)) if match else None
+        if "mlp" in name:
+            mod = 'gate_proj' if 'gate_proj' in name else 'up_proj' if 'up_proj' in name else 'down_proj'
+            setattr(parent, parts[-1], RefLinearLayer_MatrixSparsity(module.weight, selected_mlp[(mod, layer)]))
+        elif "self_attn" in name:
+            mod = ('q_proj' if 'q_proj' in name else 'k_proj' if 'k_proj' in name else
+                   'v_proj' if 'v_proj' in name else 'o_proj' if 'o_proj' in name else None)
+            setattr(parent, parts[-1], RefLinearLayer_MatrixSparsity(module.weight, selected_att[(mod, layer)]))
+    return model

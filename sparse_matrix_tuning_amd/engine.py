@@ -26,8 +26,7 @@ at 288 GB per GPU the 57 M-parameter tile optimizer state is simply replicated (
 """
 from __future__ import annotations
 
-import math
-from typing import Iterable, List, Optional
+from typing import List, Optional
 
 import torch
 import torch.distributed as dist
@@ -204,13 +203,8 @@ class SMTEngine:
             loss = loss / self.gradient_accumulation_steps
         loss.backward()
         if self.is_gradient_accumulation_boundary() and self.world > 1:
-            for tg in self.tile_groups:
-                dist.all_reduce(tg.grad)            # sum; 1/world folded into the kernels
             dense = [p.grad for _g, ps in self.dense_groups for p in ps if p.grad is not None]
-            for g in dense:
-                dist.all_reduce(g)
-            if dense:
-                torch._foreach_div_(dense, float(self.world))   # averaged, as safe_get_full_grad sees them
+            allreduce_gradients([tg.grad for tg in self.tile_groups], dense, self.world)
         return loss
 
     def _grad_scale(self) -> float:
@@ -283,6 +277,24 @@ class SMTEngine:
             for p in ps:
                 p.grad = None
         self.dense_groups = []
+
+
+def allreduce_gradients(tile_buffers: List[torch.Tensor], dense_grads: List[torch.Tensor], world: int) -> None:
+    """The DP exchange of one step.
+
+    * ``tile_buffers``: the packed fp32 tile-gradient buffers — ONE all-reduce (sum) each (one per
+      optimizer group, normally one); the 1/world average is folded into the sq-norm and AdamW
+      kernels, so no extra pass over the buffer.
+    * ``dense_grads``: warm-up (full fine-tuning) gradients — summed and divided by ``world`` in
+      place, so ``safe_get_full_grad`` sees DP-averaged values as in DeepSpeed.
+    Backend: whatever process group is initialised ("nccl" = RCCL over xGMI on MI355X; gloo in the
+    CPU tests)."""
+    for buf in tile_buffers:
+        dist.all_reduce(buf)
+    for g in dense_grads:
+        dist.all_reduce(g)
+    if dense_grads:
+        torch._foreach_div_(dense_grads, float(world))
 
 
 def initialize(model=None, optimizer=None, args=None, config=None, lr_scheduler=None,

@@ -1,0 +1,63 @@
+"""The C-ABI library builds for gfx950, loads, and exports every symbol include/smt_hip.h declares.
+Argument validation paths return error codes before any HIP call (safe without a GPU)."""
+import ctypes
+import os
+import re
+import subprocess
+
+from sparse_matrix_tuning_amd import _hip, build
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "smt_hip.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(smt_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_lists_the_binding_functions():
+    assert declared_functions() == sorted(_hip.ABI_FUNCTIONS)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _hip.load(build_if_missing=True)
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", _hip.lib_path()], capture_output=True, text=True).stdout
+    for name in declared_functions():
+        assert re.search(rf"\bT {name}$", out, re.M), name
+    assert lib.smt_abi_version() == 1
+
+
+def test_library_carries_gfx950_code_object():
+    blob = open(_hip.lib_path(), "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob          # the offload bundle's target id
+
+
+def test_struct_layouts_match_header():
+    assert ctypes.sizeof(_hip.TileDesc) == 32
+    assert ctypes.sizeof(_hip.AccumEntry) == 40
+    assert ctypes.sizeof(_hip.ScoreEntry) == 48
+    assert ctypes.sizeof(_hip.AdamWArgs) == 44
+
+
+def test_validation_errors_without_gpu():
+    lib = _hip.load()
+    assert lib.smt_tile_wgrad(None, 0, None, 0, 16, None, -1, None, 0, 0, None, 0, None) == -1
+    assert b"negative" in lib.smt_last_error()
+    assert lib.smt_tile_wgrad(None, 0, None, 0, 16, None, 0, None, 0, 0, None, 0, None) == 0   # no tiles: no-op
+    assert lib.smt_adamw_step(None, None, None, None, None, None, 0, 0, None, None, None) == -1
+    args = _hip.AdamWArgs(lr=1e-3, beta1=0.9, beta2=0.95, eps=1e-8, weight_decay=0.0, bias_correction1=0.0,
+                          bias_correction2=0.1, max_grad_norm=0.0, grad_scale=1.0, mode=0, grad_dtype=0)
+    assert lib.smt_adamw_step(None, None, None, None, None, None, 0, 8, None, ctypes.byref(args), None) == -1
+    assert b"bias" in lib.smt_last_error()
+    assert lib.smt_tile_gather(None, 256, 3, None, 1, None, None) == -1
+    assert lib.smt_sq_norm(None, 10, None, 0, None, None) == -1
+    assert lib.smt_wgrad_workspace_bytes(32768, 27) == 27 * 19 * 65536 * 4
+    assert lib.smt_wgrad_workspace_bytes(0, 27) == 0
+
+
+def test_build_is_up_to_date():
+    assert not build.is_stale()

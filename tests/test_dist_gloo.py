@@ -1,0 +1,56 @@
+"""The N>1 path on CPU with gloo, world_size 2: the packed tile-gradient all-reduce + dense averaging
+of the engine, and the rank-0 selection broadcast."""
+import os
+import socket
+from collections import defaultdict
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from sparse_matrix_tuning_amd.engine import allreduce_gradients
+    from sparse_matrix_tuning_amd.trainer import _broadcast
+    torch.manual_seed(rank)
+    tiles = torch.randn(3 * 65536)
+    dense = [torch.randn(7, 5), torch.randn(11)]
+    all_tiles = [torch.zeros_like(tiles) for _ in range(world)]
+    dist.all_gather(all_tiles, tiles)
+    all_dense = [[torch.zeros_like(d) for _ in range(world)] for d in dense]
+    for d, bucket in zip(dense, all_dense):
+        dist.all_gather(bucket, d)
+    allreduce_gradients([tiles], dense, world)
+    ok = torch.equal(tiles, sum(all_tiles))                      # raw sum; 1/world folded into kernels
+    ok &= all(torch.allclose(d, sum(b) / world) for d, b in zip(dense, all_dense))
+    # every rank proposes a different selection; rank 0's wins everywhere
+    sel = defaultdict(list, {("up_proj", rank): [(rank, 1), (0, 0)]})
+    got = _broadcast(sel, True)
+    ok &= dict(got) == {("up_proj", 0): [(0, 1), (0, 0)]}
+    q.put((rank, bool(ok)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_tile_allreduce_and_selection_broadcast():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: True, 1: True}
