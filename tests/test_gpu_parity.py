@@ -1,0 +1,256 @@
+"""GPU parity of the drop-in API (smt.smt / smt.smt_helper / engine / harvest) against the oracle.
+
+Tolerances (stated per SURVEY §8(c) / BASELINE north_star):
+* block-index selection: bit-exact (same keys, same order, same tile order);
+* tile gradients (bf16 output): relative Frobenius error vs fp64 truth from identical bf16 inputs
+  <= max(1e-3, 1.1 x the reference restatement's own error); fp32 sink output <= 1e-5;
+* losses of a whole model: relative <= 1e-3 vs the reference restatement on the same weights/inputs;
+* copies (gather / write-back / merge / harvest accumulation): bit-exact.
+"""
+import json
+import os
+from collections import defaultdict
+
+import numpy as np
+import pytest
+import torch
+from torch import nn
+
+from oracle import smt_oracle as ref
+from sparse_matrix_tuning_amd import _hip, trainer
+from sparse_matrix_tuning_amd.engine import SMTFusedAdam, initialize
+from sparse_matrix_tuning_amd.smt import smt, smt_helper
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-300)).item()
+
+
+# ------------------------------------------------------------------ module (smt.py:302-413)
+def test_module_forward_backward_matches_golden_fixture():
+    d = np.load(os.path.join(GOLDEN, "linearz_case.npz"))
+    bf = lambda a: torch.from_numpy(a).view(torch.bfloat16)
+    x, g, W = bf(d["x"]), bf(d["g"]), bf(d["W"])
+    tiles = [tuple(t) for t in d["tiles"].tolist()]
+    mod = smt.LinearLayer_MatrixSparsity(nn.Parameter(W.to(DEV)), index_list=tiles)
+    assert torch.equal(mod.selected_weight.detach().cpu(), ref.gather_tiles(W, tiles))
+    xd = x.to(DEV).requires_grad_(True)
+    y = mod(xd)
+    y.backward(g.to(DEV))
+    y_ref, gi_ref, gw_ref = bf(d["y"]), bf(d["grad_input"]), bf(d["grad_tiles_ref"])
+    assert _rel(y, y_ref) < 1e-2 and _rel(xd.grad, gi_ref) < 1e-2      # stock bf16 GEMMs, different order
+    truth = ref.tile_grads_fp64(g, x, tiles)
+    err = _rel(mod.selected_weight.grad, truth)
+    assert err <= max(1e-3, 1.1 * _rel(gw_ref, truth)), err
+
+
+def test_linearz_apply_with_python_index_list():
+    torch.manual_seed(3)
+    W = (torch.randn(768, 512) * 0.02).bfloat16().to(DEV)
+    sw = torch.zeros(2 * 256, 256, dtype=torch.bfloat16, device=DEV, requires_grad=True)
+    x = torch.randn(3, 40, 512).bfloat16().to(DEV).requires_grad_(True)
+    y = smt.linearZ.apply(x, sw, [(2, 1), (0, 0)], W)
+    y.sum().backward()
+    truth = ref.tile_grads_fp64(torch.ones(3, 40, 768).bfloat16(), x.detach().cpu(), [(2, 1), (0, 0)])
+    assert _rel(sw.grad, truth) < 2e-3
+    assert sw.grad.dtype == torch.bfloat16
+
+
+def test_forward_writeback_and_merge_back_bit_exact():
+    torch.manual_seed(4)
+    W0 = torch.randn(512, 768).bfloat16()
+    W = nn.Parameter(W0.to(DEV))
+    tiles = [(1, 2), (0, 1)]
+    mod = smt.LinearLayer_MatrixSparsity(W, index_list=tiles)
+    with torch.no_grad():
+        mod.selected_weight.add_(1.0)
+    mod(torch.randn(1, 4, 768).bfloat16().to(DEV))            # writes tiles into W (smt.py:332-341)
+    W_ref = W0.clone()
+    ref.writeback_tiles(W_ref, mod.selected_weight.detach().cpu(), tiles)
+    assert torch.equal(W.detach().cpu(), W_ref)
+    holder = nn.Module()
+    holder.model = nn.Module()
+    holder.model.layers = nn.Module()
+    holder.model.layers.proj = mod          # names must contain '.layers' (part_module_name)
+    smt.convert_matrix_sparsity_to_linear_layer(holder)
+    assert isinstance(holder.model.layers.proj, nn.Linear) and holder.model.layers.proj.weight is W
+
+
+def test_gradient_checkpoint_recompute_consistent():
+    from torch.utils.checkpoint import checkpoint
+    torch.manual_seed(5)
+    W = nn.Parameter((torch.randn(512, 512) * 0.05).bfloat16().to(DEV))
+    mod = smt.LinearLayer_MatrixSparsity(W, index_list=[(1, 0), (0, 1)])
+    x = torch.randn(2, 64, 512).bfloat16().to(DEV)
+    grads = []
+    for ckpt in (False, True):
+        mod.selected_weight.grad = None
+        xi = x.clone().requires_grad_(True)
+        y = checkpoint(mod, xi, use_reentrant=False) if ckpt else mod(xi)
+        (y.float() ** 2).sum().backward()
+        grads.append(mod.selected_weight.grad.clone())
+    assert torch.equal(grads[0], grads[1])
+
+
+# ------------------------------------------------------------------ selection (smt_helper.py)
+def test_selection_bit_exact_vs_golden():
+    from tests.golden.make_golden import selection_inputs
+    spec = json.load(open(os.path.join(GOLDEN, "selection_expected.json")))
+    grads = selection_inputs()
+    att = {k: v.to(DEV) for k, v in grads.items() if k[0] in ("q_proj", "k_proj", "v_proj")}
+    mlp = {k: v.to(DEV) for k, v in grads.items() if k[0] in ("gate_proj", "up_proj", "down_proj")}
+    for case in spec["cases"]:
+        pool = att if case["pool"] == "attention" else mlp
+        out = smt_helper.select_submatrix_based_on_grads(pool, spec["dims"], case["n"],
+                                                         selection_strategy=case["selection_strategy"],
+                                                         calculate_strategy=case["strategy"])
+        got = [[k[0], k[1], [list(t) for t in v]] for k, v in out.items()]
+        assert got == case["expected"], (case["pool"], case["strategy"], case["n"], case["selection_strategy"])
+
+
+def test_selection_kat1_on_gpu():
+    grads = {('gate_proj', 1): torch.zeros(11008, 4096), ('up_proj', 1): torch.zeros(11008, 4096),
+             ('down_proj', 2): torch.ones(4096, 11008)}
+    grads[('gate_proj', 1)][0:512, 0:256] = 10.0
+    grads[('up_proj', 1)][0:2560, 0:256] = 10.0
+    dims = {'gate_proj': [11008, 4096], 'up_proj': [11008, 4096], 'down_proj': [4096, 11008]}
+    out = smt_helper.select_submatrix_based_on_grads(grads, dims, n=20)          # CPU dicts are moved to the GPU
+    assert list(out.items()) == [(('up_proj', 1), [(i, 0) for i in range(9, -1, -1)]),
+                                 (('gate_proj', 1), [(1, 0), (0, 0)]),
+                                 (('down_proj', 2), [(15, j) for j in range(42, 34, -1)])]
+
+
+def test_stat_helpers_match_reference_names():
+    torch.manual_seed(6)
+    g = torch.randn(512, 768)
+    v = g.reshape(2, 256, 3, 256)
+    for fn, name in ((smt_helper.mean_abs, "mean_abs"), (smt_helper.abs_mean_, "abs_mean"),
+                     (smt_helper.L1_norm, "L1"), (smt_helper.L2_norm, "L2")):
+        got = fn(v.to(DEV))
+        assert torch.equal(got, ref.block_stat_fp64(g, 2, 3, name))
+        assert torch.allclose(got, ref.block_stat(g, 2, 3, name), rtol=1e-5, atol=0)
+
+
+# ------------------------------------------------------------------ warm-up harvest (fine_tune.py:714-767)
+def test_harvest_bit_exact_vs_reference_cpu_accumulation():
+    torch.manual_seed(7)
+    model = _mini_llama()
+    h = trainer.GradHarvester(model, num_mlp_blocks=1, num_attention_blocks=1)
+    mlp_ref, att_ref = {}, {}
+    for _ in range(3):
+        for p in model.parameters():
+            p.grad = (torch.randn(p.shape) * 1e-2).bfloat16().to(DEV)
+        h.harvest()
+        ref.harvest([(n, p.grad) for n, p in model.named_parameters()], mlp_ref, att_ref, 1, 1)
+    assert set(h.warmup_grads) == set(mlp_ref) and set(h.attention_warmup_grads) == set(att_ref)
+    for k in mlp_ref:
+        assert torch.equal(h.warmup_grads[k].cpu(), mlp_ref[k])
+    for k in att_ref:
+        assert torch.equal(h.attention_warmup_grads[k].cpu(), att_ref[k])
+    assert ('o_proj', 0) not in h.attention_warmup_grads
+
+
+# ------------------------------------------------------------------ engine step (fused sparse AdamW)
+def _mini_llama(layers=2):
+    import bench
+    cfg = dict(bench.MODELS["mini"])
+    cfg["num_hidden_layers"] = layers
+    bench.MODELS["_t"] = cfg
+    try:
+        return bench.build_model("_t", DEV)
+    finally:
+        del bench.MODELS["_t"]
+
+
+def test_engine_sparse_adamw_step_matches_oracle():
+    torch.manual_seed(8)
+    W1 = nn.Parameter((torch.randn(512, 512) * 0.05).bfloat16().to(DEV))
+    W2 = nn.Parameter((torch.randn(768, 512) * 0.05).bfloat16().to(DEV))
+    net = nn.Module()
+    net.layers = nn.ModuleList([smt.LinearLayer_MatrixSparsity(W1, index_list=[(1, 1), (0, 0)]),
+                                smt.LinearLayer_MatrixSparsity(W2, index_list=[(2, 0)])])
+    W1_0, W2_0 = W1.detach().cpu().clone(), W2.detach().cpu().clone()
+    opt = SMTFusedAdam([{"params": [m.selected_weight for m in net.layers], "weight_decay": 0.01, "lr": 1e-3}],
+                       lr=1e-3, betas=(0.9, 0.95))
+    engine, _, _, _ = initialize(model=net, optimizer=opt, config={"gradient_clipping": 1.0})
+    x = torch.randn(2, 32, 512).bfloat16()
+    masters = [ref.gather_tiles(W1_0, [(1, 1), (0, 0)]).float(), ref.gather_tiles(W2_0, [(2, 0)]).float()]
+    ms = [torch.zeros_like(t) for t in masters]
+    vs = [torch.zeros_like(t) for t in masters]
+    for step in range(1, 4):
+        xd = x.to(DEV)
+        y1 = net.layers[0](xd)
+        y2 = net.layers[1](y1)
+        loss = (y2.float() ** 2).mean() * 100.0
+        engine.backward(loss)
+        grads = [net.layers[0].selected_weight._smt_grad_sink.buffer.clone().cpu(),
+                 net.layers[1].selected_weight._smt_grad_sink.buffer.clone().cpu()]
+        engine.step()
+        coef = ref.clip_coef(grads, 1.0)
+        for t, g, m, v in zip(masters, grads, ms, vs):
+            ref.fused_adam_step(t, g * coef, m, v, step, 1e-3, (0.9, 0.95), 1e-8, 0.01)
+    torch.cuda.synchronize()
+    got = [engine.tile_groups[0].master[:2 * 65536].cpu(), engine.tile_groups[0].master[2 * 65536:].cpu()]
+    for a, b in zip(got, masters):
+        assert _rel(a, b.reshape(-1)) < 1e-5
+    # the fused epilogue scattered the bf16 tiles into W (no forward write-back needed)
+    assert torch.equal(ref.gather_tiles(W1.detach().cpu(), [(1, 1), (0, 0)]), net.layers[0].selected_weight.detach().cpu())
+    assert torch.equal(ref.gather_tiles(W2.detach().cpu(), [(2, 0)]), net.layers[1].selected_weight.detach().cpu())
+    # untouched blocks of W unchanged
+    assert torch.equal(W1.detach().cpu()[0:256, 256:512], W1_0[0:256, 256:512])
+
+
+def test_engine_sink_grads_are_fp32_and_exact():
+    torch.manual_seed(9)
+    W = nn.Parameter((torch.randn(512, 768) * 0.05).bfloat16().to(DEV))
+    mod = smt.LinearLayer_MatrixSparsity(W, index_list=[(0, 2), (1, 0)])
+    opt = SMTFusedAdam([mod.selected_weight], lr=1e-3)
+    engine, _, _, _ = initialize(model=mod, optimizer=opt, config={})
+    x = torch.randn(2, 96, 768).bfloat16()
+    g = torch.randn(2, 96, 512).bfloat16()
+    engine.backward((mod(x.to(DEV)).float() * g.to(DEV).float()).sum())
+    sink = mod.selected_weight._smt_grad_sink.buffer
+    assert sink.dtype == torch.float32 and mod.selected_weight.grad is None
+    assert _rel(sink, ref.tile_grads_fp64(g, x, [(0, 2), (1, 0)])) < 1e-5
+
+
+# ------------------------------------------------------------------ end to end: mini LLaMA vs oracle
+def test_end_to_end_mini_llama_loss_matches_reference_restatement():
+    """Same weights, same batch: loss of the SMT model on MI355X vs the CPU restatement of the
+    reference modules (smt.py:302-413); tile grads through the whole network."""
+    torch.manual_seed(10)
+    model = _mini_llama(2)
+    sd = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+    sel_mlp = defaultdict(list, {('up_proj', 1): [(2, 1), (0, 0)], ('down_proj', 0): [(1, 0)]})
+    sel_att = defaultdict(list, {('v_proj', 1): [(0, 1)], ('q_proj', 0): [(1, 1)]})
+    smt.freeze_unselected_matrix_layer(model, sel_mlp, sel_att)
+    smt.convert_linear_layer_to_matrix_sparsity(model, sel_mlp, sel_att)
+    ids = torch.randint(0, 4096, (2, 128), generator=torch.Generator().manual_seed(0))
+    out = model(input_ids=ids.to(DEV), labels=ids.to(DEV), use_cache=False)
+    out.loss.backward()
+
+    import bench
+    from transformers import LlamaConfig, LlamaForCausalLM
+    cfg = dict(bench.MODELS["mini"])
+    cfg["num_hidden_layers"] = 2
+    cpu_cfg = LlamaConfig(**cfg)
+    cpu_cfg._attn_implementation = "sdpa"
+    cpu = LlamaForCausalLM(cpu_cfg).to(torch.bfloat16)
+    cpu.load_state_dict(sd)
+    smt.freeze_unselected_matrix_layer(cpu, sel_mlp, sel_att)
+    ref.ref_convert(cpu, sel_mlp, sel_att)
+    out_ref = cpu(input_ids=ids, labels=ids, use_cache=False)
+    out_ref.loss.backward()
+    rel = abs(out.loss.item() - out_ref.loss.item()) / abs(out_ref.loss.item())
+    assert rel <= 1e-3, (out.loss.item(), out_ref.loss.item())
+    gpu_mods = {n: m for n, m in model.named_modules() if isinstance(m, smt.LinearLayer_MatrixSparsity)}
+    cpu_mods = {n: m for n, m in cpu.named_modules() if isinstance(m, ref.RefLinearLayer_MatrixSparsity)}
+    assert sorted(gpu_mods) == sorted(cpu_mods)
+    for n in gpu_mods:
+        e = _rel(gpu_mods[n].selected_weight.grad, cpu_mods[n].selected_weight.grad)
+        assert e < 3e-2, (n, e)      # whole-network bf16 pipelines on two devices
