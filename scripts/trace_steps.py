@@ -1,0 +1,52 @@
+"""Per-category kernel time of the SMT steps from a rocprofv3 kernel-trace CSV.
+
+SMT steps are delimited by adamw_tiles_kernel dispatches (one per step): the region between two
+consecutive ones is one step. Prints per-step wall (first start .. last end) and kernel-time by category."""
+import collections
+import csv
+import sys
+
+
+def cat(name):
+    n = name
+    if "wgrad_partial" in n or "wgrad_reduce" in n:
+        return "smt_wgrad"
+    if "adamw" in n or "sq_norm" in n or "tile_copy" in n:
+        return "smt_optimizer"
+    if n.startswith("Cijk") or n.startswith("Custom_Cijk"):
+        return "gemm(hipBLASLt)"
+    if "attn_fwd" in n or "bwd_kernel" in n or "bwd_preprocess" in n:
+        return "attention(aotriton)"
+    if "SoftMax" in n or "nll_loss" in n or "log_softmax" in n:
+        return "loss"
+    if "reduce_kernel" in n:
+        return "reductions"
+    if "elementwise" in n or "Copy" in n or "copy" in n or "Cat" in n:
+        return "elementwise"
+    return "other"
+
+
+def main(path):
+    rows = list(csv.DictReader(open(path)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    idx = [i for i, r in enumerate(rows) if "adamw_tiles_kernel" in r["Kernel_Name"]]
+    if len(idx) < 2:
+        print("need >= 2 SMT steps")
+        return
+    for a, b in zip(idx[:-1], idx[1:]):
+        seg = rows[a + 1:b + 1]
+        wall = (int(seg[-1]["End_Timestamp"]) - int(seg[0]["Start_Timestamp"])) / 1e6
+        by = collections.Counter()
+        cnt = collections.Counter()
+        for r in seg:
+            d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+            by[cat(r["Kernel_Name"])] += d
+            cnt[cat(r["Kernel_Name"])] += 1
+        busy = sum(by.values())
+        print(f"step: wall {wall:.1f} ms, kernel-busy {busy:.1f} ms, dispatches {len(seg)}")
+        for k, v in by.most_common():
+            print(f"   {k:22s} {v:8.1f} ms  {100 * v / wall:5.1f}%  n={cnt[k]}")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
