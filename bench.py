@@ -113,9 +113,9 @@ def install_wgrad_timer(timer: WgradTimer):
     from sparse_matrix_tuning_amd import _hip
     orig = _hip.tile_wgrad
 
-    def timed(g2, x2, rc, out, accumulate=False):
+    def timed(g2, x2, rc, out, accumulate=False, order=None):
         return timer.hook(g2.shape[0], rc.shape[0], out.element_size(),
-                          lambda: orig(g2, x2, rc, out, accumulate=accumulate))
+                          lambda: orig(g2, x2, rc, out, accumulate=accumulate, order=order))
     _hip.tile_wgrad = timed
 
 
@@ -142,6 +142,17 @@ def batches(n, B, S, vocab, rank, device, offset=0):
         ids = ids.to(device)
         out.append(dict(input_ids=ids, attention_mask=torch.ones_like(ids), labels=ids))
     return out
+
+
+def pmc_traffic(args):
+    """HBM bytes per wgrad launch from the committed rocprofv3 --pmc passes of this same bench
+    configuration (scripts/pmc_traffic.py; FETCH_SIZE x2 + WRITE_SIZE), or None."""
+    path = os.path.join(ROOT, "profiles", "r01_wgrad_pmc.json")
+    if args.model != "llama3-8b" or not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        d = json.load(f)
+    return round(d["hbm_bytes_per_launch"]), f"profiles/r01_wgrad_pmc.json ({d['correction']})"
 
 
 def cpu_baseline(seconds: float, selection_tiles: dict, model_name: str):
@@ -297,8 +308,9 @@ def main():
         roofline = None
         if w and w["seconds"] > 0:
             achieved = w["bytes"] / w["seconds"] / 1e9
+            traffic, tsrc = pmc_traffic(args)
             roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                        "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
+                        "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
                         "kernel": "smt_tile_wgrad (wgrad_partial_kernel + wgrad_reduce_kernel)",
                         "launches": w["launches"], "avg_launch_us": round(w["seconds"] / w["launches"] * 1e6, 2),
                         "algorithmic_bytes_per_launch": round(w["bytes"] / w["launches"]),

@@ -104,12 +104,15 @@ size_t smt_wgrad_workspace_bytes(int64_t T, int32_t n_tiles);
 /*
  * grad_tiles[i] (+)= sum_{t<T} grad_out[t, r_i*256 : r_i*256+256]^T  x[t, c_i*256 : c_i*256+256]
  * grad_out [T, ld_grad_out], x [T, ld_x]: bf16 row-major; tile_rc_dev: device int32 [n_tiles][2];
- * grad_tiles: [n_tiles*256, 256] row-major of out_dtype (bf16 or fp32). fp32 MFMA accumulation over
- * the whole T, one rounding at the end (the reference rounds each per-sample partial to bf16 first).
+ * order_dev: optional device int32 [n_tiles] permutation giving the SCHEDULE order of the tiles
+ * (tiles sharing a column / row block adjacent, for L2 reuse); NULL = index order. Results do not
+ * depend on it. grad_tiles: [n_tiles*256, 256] row-major of out_dtype (bf16 or fp32). fp32 MFMA
+ * accumulation over the whole T, one rounding at the end (the reference rounds each per-sample
+ * partial to bf16 first). Deterministic (fixed split and summation order).
  */
 int smt_tile_wgrad(const void* grad_out, int64_t ld_grad_out,
                    const void* x, int64_t ld_x, int64_t T,
-                   const int32_t* tile_rc_dev, int32_t n_tiles,
+                   const int32_t* tile_rc_dev, const int32_t* order_dev, int32_t n_tiles,
                    void* grad_tiles, int32_t out_dtype, int32_t accumulate,
                    void* workspace, size_t workspace_bytes, hipStream_t stream);
 

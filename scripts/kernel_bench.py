@@ -1,8 +1,12 @@
-"""Micro-benchmark of the SMT HIP kernels at LLaMA-3-8B shapes (HIP events on the launch stream)."""
+"""Micro-benchmark of smt_tile_wgrad at LLaMA-3-8B shapes (HIP events on the launch stream).
+
+Patterns: 'random' tiles over the [out/256 x in/256] block grid, and 'clustered' tiles confined to
+4 column blocks (selections concentrate). Reports algorithmic GB/s (each tile's two
+T x 256 bf16 slices + its fp32 output) and the MFMA rate."""
 import argparse
 import json
-import sys
 import os
+import sys
 
 import torch
 
@@ -28,7 +32,7 @@ def main():
     ap.add_argument("--T", type=int, default=32768)
     ap.add_argument("--out", type=int, default=14336)
     ap.add_argument("--inp", type=int, default=4096)
-    ap.add_argument("--tiles", type=int, nargs="*", default=[1, 8, 27, 64, 128])
+    ap.add_argument("--tiles", type=int, nargs="*", default=[1, 8, 27, 64, 128, 256])
     args = ap.parse_args()
     dev = torch.device("cuda")
     torch.manual_seed(0)
@@ -36,31 +40,37 @@ def main():
     g = torch.randn(T, args.out, device=dev).bfloat16()
     x = torch.randn(T, args.inp, device=dev).bfloat16()
     rb, cb = args.out // 256, args.inp // 256
-    res = []
-    for n in args.tiles:
-        gen = torch.Generator().manual_seed(n)
-        perm = torch.randperm(rb * cb, generator=gen)[:n].tolist()
-        tiles = [(p // cb, p % cb) for p in perm]
-        rc = _hip.tile_table(tiles, dev)
-        out = torch.empty(n * 256, 256, device=dev)
-        ws = torch.empty(_hip.wgrad_workspace_bytes(T, n), dtype=torch.uint8, device=dev)
-        lib = _hip.load()
-        st = torch.cuda.current_stream().cuda_stream
+    lib = _hip.load()
+    for pattern in ("random", "clustered"):
+        for n in args.tiles:
+          for use_order in (False, True):
+            gen = torch.Generator().manual_seed(n)
+            if pattern == "random":
+                perm = torch.randperm(rb * cb, generator=gen)[:n].tolist()
+                tiles = [(p // cb, p % cb) for p in perm]
+            else:
+                cells = [(r, c) for c in range(4) for r in range(rb)]
+                perm = torch.randperm(len(cells), generator=gen)[:n].tolist()
+                tiles = [cells[p] for p in perm]
+            n = len(tiles)
+            rc = _hip.tile_table(tiles, dev)
+            order = _hip.order_table(tiles, dev)
+            out = torch.empty(n * 256, 256, device=dev)
+            wsb = _hip.wgrad_workspace_bytes(T, n)
+            ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)
+            st = torch.cuda.current_stream().cuda_stream
 
-        def run():
-            rc_ = lib.smt_tile_wgrad(g.data_ptr(), g.stride(0), x.data_ptr(), x.stride(0), T, rc.data_ptr(), n,
-                                     out.data_ptr(), 1, 0, ws.data_ptr(), ws.numel(), st)
-            assert rc_ == 0
-        t = timeit(run)
-        flops = 2.0 * T * 65536 * n
-        bytes_alg = n * (T * 256 * 2 * 2 + 65536 * 4)
-        res.append(dict(tiles=n, ms=t * 1e3, tflops=flops / t / 1e12, gbs=bytes_alg / t / 1e9,
-                        ws_mb=ws.numel() / 2**20))
-        print(json.dumps(res[-1]), flush=True)
-    # gather / scatter / adamw
-    n = 872
-    W = torch.randn(14336, 4096, device=dev).bfloat16()
-    perm = torch.randperm(56 * 16)[:n % (56 * 16)].tolist()
+            def run():
+                assert lib.smt_tile_wgrad(g.data_ptr(), g.stride(0), x.data_ptr(), x.stride(0), T, rc.data_ptr(),
+                                          order.data_ptr() if use_order else None, n,
+                                          out.data_ptr(), 1, 0, ws.data_ptr(), wsb, st) == 0
+            t = timeit(run)
+            flops = 2.0 * T * 65536 * n
+            bytes_alg = n * (T * 256 * 2 * 2 + 65536 * 4)
+            uniq = (len({r for r, _ in tiles}) + len({c for _, c in tiles})) * T * 512 + n * 65536 * 4
+            print(json.dumps(dict(pattern=pattern, order=use_order, tiles=n, us=round(t * 1e6, 1), alg_tbs=round(bytes_alg / t / 1e12, 3),
+                                  unique_slice_tbs=round(uniq / t / 1e12, 3), tflops=round(flops / t / 1e12, 1),
+                                  ws_mb=round(wsb / 2**20, 1))), flush=True)
 
 
 if __name__ == "__main__":

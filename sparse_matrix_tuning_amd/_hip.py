@@ -67,7 +67,7 @@ _SIGS = {
     "smt_last_error": (ctypes.c_char_p, []),
     "smt_abi_version": (ctypes.c_int, []),
     "smt_wgrad_workspace_bytes": (_SZ, [_I64, _I32]),
-    "smt_tile_wgrad": (ctypes.c_int, [_P, _I64, _P, _I64, _I64, _P, _I32, _P, _I32, _I32, _P, _SZ, _P]),
+    "smt_tile_wgrad": (ctypes.c_int, [_P, _I64, _P, _I64, _I64, _P, _P, _I32, _P, _I32, _I32, _P, _SZ, _P]),
     "smt_tile_gather": (ctypes.c_int, [_P, _I64, _I32, _P, _I32, _P, _P]),
     "smt_tile_scatter": (ctypes.c_int, [_P, _I64, _I32, _P, _I32, _P, _P]),
     "smt_grad_accumulate": (ctypes.c_int, [_P, _I32, _I64, _P]),
@@ -148,6 +148,22 @@ def tile_table(index_list: Sequence[Sequence[int]], device: torch.device) -> tor
     return torch.tensor(flat, dtype=torch.int32).view(-1, 2).to(device)
 
 
+def schedule_order(index_list: Sequence[Sequence[int]]) -> list:
+    """wgrad schedule: tiles sharing the operand slice that is shared most (fewer distinct column
+    blocks -> group by column, else by row) become adjacent, so they run on one XCD together."""
+    rows = {int(rc[0]) for rc in index_list}
+    cols = {int(rc[1]) for rc in index_list}
+    if len(cols) <= len(rows):
+        key = lambda i: (int(index_list[i][1]), int(index_list[i][0]))
+    else:
+        key = lambda i: (int(index_list[i][0]), int(index_list[i][1]))
+    return sorted(range(len(index_list)), key=key)
+
+
+def order_table(index_list: Sequence[Sequence[int]], device: torch.device) -> torch.Tensor:
+    return torch.tensor(schedule_order(index_list), dtype=torch.int32).to(device)
+
+
 # ---------------------------------------------------------------------------------------------
 # wrappers
 # ---------------------------------------------------------------------------------------------
@@ -156,9 +172,10 @@ def wgrad_workspace_bytes(T: int, n_tiles: int) -> int:
 
 
 def tile_wgrad(grad_out2d: torch.Tensor, x2d: torch.Tensor, tile_rc: torch.Tensor, out: torch.Tensor,
-               accumulate: bool = False) -> torch.Tensor:
-    """out[i] (+)= grad_out2d[:, r_i-block]^T @ x2d[:, c_i-block] for every tile (smt.py:397-404)."""
-    dev = _require_device(grad_out2d, x2d, tile_rc, out)
+               accumulate: bool = False, order: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out[i] (+)= grad_out2d[:, r_i-block]^T @ x2d[:, c_i-block] for every tile (smt.py:397-404).
+    ``order``: optional device int32 schedule permutation (speed only)."""
+    dev = _require_device(grad_out2d, x2d, tile_rc, out, order)
     if grad_out2d.dtype != torch.bfloat16 or x2d.dtype != torch.bfloat16:
         raise NotImplementedError(f"tile_wgrad: bf16 operands only (got {grad_out2d.dtype}, {x2d.dtype})")
     if out.dtype not in (torch.bfloat16, torch.float32) or not out.is_contiguous():
@@ -171,8 +188,10 @@ def tile_wgrad(grad_out2d: torch.Tensor, x2d: torch.Tensor, tile_rc: torch.Tenso
         raise ValueError("tile_wgrad: operands must be [T, features] with unit feature stride")
     ws_bytes = wgrad_workspace_bytes(T, n)
     ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=dev)
+    if order is not None and (order.dtype != torch.int32 or order.numel() != n):
+        raise ValueError("tile_wgrad: order must be int32 [n_tiles]")
     rc = load().smt_tile_wgrad(_ptr(grad_out2d), grad_out2d.stride(0), _ptr(x2d), x2d.stride(0), T,
-                               _ptr(tile_rc), n, _ptr(out), _DT[out.dtype], int(bool(accumulate)),
+                               _ptr(tile_rc), _ptr(order), n, _ptr(out), _DT[out.dtype], int(bool(accumulate)),
                                _ptr(ws), ws_bytes, _stream(dev))
     _check(rc, "smt_tile_wgrad")
     return out

@@ -95,17 +95,31 @@ __device__ __forceinline__ bf16x8_t tr_frag(const uint8_t* img, uint32_t k, uint
     return __builtin_bit_cast(bf16x8_t, both);
 }
 
+// Epilogue modes: partial slab (S > 1), or the final tile written directly (S == 1).
+enum WgradOut { kOutSlab = 0, kOutF32 = 1, kOutBF16 = 2 };
+
+template <int OUT>
 __global__ __launch_bounds__(kWgThreads, 2)
 void wgrad_partial_kernel(const uint16_t* __restrict__ g, int64_t ldg,
                           const uint16_t* __restrict__ x, int64_t ldx,
-                          int64_t T, int64_t chunk, int S,
-                          const int32_t* __restrict__ tile_rc,
-                          float* __restrict__ slab) {
+                          int64_t T, int64_t chunk, int S, int n_tiles,
+                          const int32_t* __restrict__ tile_rc, const int32_t* __restrict__ order,
+                          void* __restrict__ out_ptr, int accumulate) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * 2 * kImgBytes];   // 128 KiB, one array
 
-    const int wg = blockIdx.x;
-    const int tile = wg / S;
-    const int s = wg - tile * S;
+    // XCD-aware, chunk-major schedule. Workgroups are dealt round-robin over the 8 XCDs (b and b+8
+    // share one); the bijective remap (cdna_hip_programming T1) gives each XCD a CONTIGUOUS run of
+    // logical ids L = s*n_tiles + i: the tiles of (about) one T-chunk, in `order` (the host sorts
+    // tiles so that those sharing an x column-block / g row-block are adjacent). Tiles running on
+    // one XCD therefore stream the same rows at the same time and re-read shared slices from that
+    // XCD's L2 instead of HBM. Placement only changes speed, never results.
+    const int total = n_tiles * S;
+    const int b = blockIdx.x;
+    const int q8 = total >> 3, r8 = total & 7, xcd = b & 7;
+    const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+    const int s = L / n_tiles;
+    const int li = L - s * n_tiles;
+    const int tile = order != nullptr ? order[li] : li;
     const int r = tile_rc[2 * tile];
     const int c = tile_rc[2 * tile + 1];
     const int64_t t_begin = (int64_t)s * chunk;
@@ -209,19 +223,49 @@ void wgrad_partial_kernel(const uint16_t* __restrict__ g, int64_t ldg,
     }
 
     // C/D map of 32x32x16: col = lane&31, row = (i&3) + 8*(i>>2) + 4*(lane>>5)
-    float* out = slab + (int64_t)(tile * S + s) * kTileElems;
     const int col = lane & 31;
     const int h = lane >> 5;
+    if (OUT == kOutSlab) {
+        float* out = static_cast<float*>(out_ptr) + (int64_t)(tile * S + s) * kTileElems;
 #pragma unroll
-    for (int mb = 0; mb < 4; ++mb)
+        for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
-        for (int nb = 0; nb < 2; ++nb)
+            for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int m = wm * 128 + mb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-                const int n = wn * 64 + nb * 32 + col;
-                out[m * kTile + n] = acc[mb][nb][i];
-            }
+                for (int i = 0; i < 16; ++i) {
+                    const int m = wm * 128 + mb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                    const int n = wn * 64 + nb * 32 + col;
+                    out[m * kTile + n] = acc[mb][nb][i];
+                }
+    } else if (OUT == kOutF32) {
+        float* out = static_cast<float*>(out_ptr) + (int64_t)tile * kTileElems;
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int m = wm * 128 + mb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                    const int n = wn * 64 + nb * 32 + col;
+                    float v = acc[mb][nb][i];
+                    if (accumulate) v += out[m * kTile + n];
+                    out[m * kTile + n] = v;
+                }
+    } else {
+        uint16_t* out = static_cast<uint16_t*>(out_ptr) + (int64_t)tile * kTileElems;
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int m = wm * 128 + mb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                    const int n = wn * 64 + nb * 32 + col;
+                    float v = acc[mb][nb][i];
+                    if (accumulate) v += bf16_bits_to_f32(out[m * kTile + n]);
+                    out[m * kTile + n] = f32_to_bf16_bits(v);
+                }
+    }
 }
 
 // Sum the S partial slabs of each tile in order s = 0..S-1 (deterministic) and write the tile.
@@ -576,14 +620,17 @@ void adamw_flat_kernel(const void* __restrict__ grad, float* __restrict__ master
     }
 }
 
-// Split of T over workgroups for one tile set: about two workgroups per CU overall (256 CUs),
-// chunks of at least 512 rows and a multiple of the 64-row stage.
+// Split of T over workgroups for one tile set. One 512-thread workgroup fits per CU (128 KiB LDS),
+// so fill the 256 CUs in ONE round: S = floor(256 / n_tiles) (no partial second round, fewer slab
+// bytes), chunks of at least 512 rows and a multiple of the 64-row stage. S == 1 (n_tiles > 128):
+// the tile is written straight from the accumulators.
+constexpr int kCUs = 256;
 struct WgradSplit { int S; int64_t chunk; };
 
 WgradSplit wgrad_split(int64_t T, int32_t n_tiles) {
     WgradSplit sp{1, kBK};
     if (T <= 0 || n_tiles <= 0) return sp;
-    int64_t S = (512 + n_tiles - 1) / n_tiles;
+    int64_t S = n_tiles >= kCUs ? 1 : kCUs / n_tiles;
     const int64_t s_max = (T + 511) / 512;
     if (S > s_max) S = s_max;
     if (S < 1) S = 1;
@@ -603,17 +650,18 @@ extern "C" {
 
 const char* smt_last_error(void) { return g_err; }
 
-int smt_abi_version(void) { return 1; }
+int smt_abi_version(void) { return 2; }
 
 size_t smt_wgrad_workspace_bytes(int64_t T, int32_t n_tiles) {
     if (T <= 0 || n_tiles <= 0) return 0;
     const WgradSplit sp = wgrad_split(T, n_tiles);
+    if (sp.S == 1) return 0;                      // written straight from the accumulators
     return (size_t)n_tiles * (size_t)sp.S * (size_t)kTileElems * sizeof(float);
 }
 
 int smt_tile_wgrad(const void* grad_out, int64_t ld_grad_out, const void* x, int64_t ld_x, int64_t T,
-                   const int32_t* tile_rc_dev, int32_t n_tiles, void* grad_tiles, int32_t out_dtype,
-                   int32_t accumulate, void* workspace, size_t workspace_bytes, hipStream_t stream) {
+                   const int32_t* tile_rc_dev, const int32_t* order_dev, int32_t n_tiles, void* grad_tiles,
+                   int32_t out_dtype, int32_t accumulate, void* workspace, size_t workspace_bytes, hipStream_t stream) {
     if (n_tiles < 0 || T < 0) return fail(SMT_E_INVALID, "smt_tile_wgrad: negative size (T=%lld, n_tiles=%d)", (long long)T, n_tiles);
     if (n_tiles == 0) return SMT_OK;
     if (out_dtype != SMT_DTYPE_BF16 && out_dtype != SMT_DTYPE_FP32)
@@ -630,14 +678,25 @@ int smt_tile_wgrad(const void* grad_out, int64_t ld_grad_out, const void* x, int
     if (!aligned16(grad_out) || !aligned16(x) || (ld_grad_out & 7) || (ld_x & 7))
         return fail(SMT_E_ALIGN, "smt_tile_wgrad: operands need 16-byte aligned rows (ld %% 8 == 0)");
     const WgradSplit sp = wgrad_split(T, n_tiles);
+    const uint16_t* gp = static_cast<const uint16_t*>(grad_out);
+    const uint16_t* xp = static_cast<const uint16_t*>(x);
+    const dim3 grid(n_tiles * sp.S), block(kWgThreads);
+    if (sp.S == 1) {
+        if (out_dtype == SMT_DTYPE_FP32)
+            hipLaunchKernelGGL(wgrad_partial_kernel<kOutF32>, grid, block, 0, stream, gp, ld_grad_out, xp, ld_x,
+                               T, sp.chunk, 1, n_tiles, tile_rc_dev, order_dev, grad_tiles, accumulate);
+        else
+            hipLaunchKernelGGL(wgrad_partial_kernel<kOutBF16>, grid, block, 0, stream, gp, ld_grad_out, xp, ld_x,
+                               T, sp.chunk, 1, n_tiles, tile_rc_dev, order_dev, grad_tiles, accumulate);
+        return check_launch("wgrad_partial_kernel");
+    }
     const size_t need = (size_t)n_tiles * sp.S * kTileElems * sizeof(float);
     if (!workspace || workspace_bytes < need)
         return fail(SMT_E_WORKSPACE, "smt_tile_wgrad: workspace %zu < %zu bytes", workspace_bytes, need);
     if (!aligned16(workspace)) return fail(SMT_E_ALIGN, "smt_tile_wgrad: workspace not 16-byte aligned");
     float* slab = static_cast<float*>(workspace);
-    hipLaunchKernelGGL(wgrad_partial_kernel, dim3(n_tiles * sp.S), dim3(kWgThreads), 0, stream,
-                       static_cast<const uint16_t*>(grad_out), ld_grad_out, static_cast<const uint16_t*>(x), ld_x,
-                       T, sp.chunk, sp.S, tile_rc_dev, slab);
+    hipLaunchKernelGGL(wgrad_partial_kernel<kOutSlab>, grid, block, 0, stream, gp, ld_grad_out, xp, ld_x,
+                       T, sp.chunk, sp.S, n_tiles, tile_rc_dev, order_dev, slab, 0);
     int rc = check_launch("wgrad_partial_kernel");
     if (rc) return rc;
     if (out_dtype == SMT_DTYPE_FP32)

@@ -101,6 +101,15 @@ class TileIndex:
             self._dev[key] = t
         return t
 
+    def schedule(self, device: torch.device) -> torch.Tensor:
+        """Device int32 schedule permutation for the wgrad kernel (L2 reuse; speed only)."""
+        key = ("order", device.type, device.index)
+        t = self._dev.get(key)
+        if t is None:
+            t = _hip.order_table(self.index_list, device)
+            self._dev[key] = t
+        return t
+
     def validate(self, rows: int, cols: int) -> None:
         rb, cb = rows // Block_dimension, cols // Block_dimension
         for r, c in self.index_list:
@@ -200,13 +209,15 @@ class linearZ(torch.autograd.Function):
             if x2.stride(1) != 1 or x2.stride(0) % 8 or x2.data_ptr() % 16:
                 x2 = x2.contiguous()
             sink = ctx.sink
+            dev = g2.device
             if sink is not None:
-                _hip.tile_wgrad(g2, x2, tiles.device_table(g2.device), sink.buffer, accumulate=sink.take_accumulate())
+                _hip.tile_wgrad(g2, x2, tiles.device_table(dev), sink.buffer, accumulate=sink.take_accumulate(),
+                                order=tiles.schedule(dev))
             else:
                 grad_weight = torch.empty(n * Block_dimension, Block_dimension,
                                           dtype=grad_output.dtype, device=grad_output.device)
                 if n:
-                    _hip.tile_wgrad(g2, x2, tiles.device_table(g2.device), grad_weight)
+                    _hip.tile_wgrad(g2, x2, tiles.device_table(dev), grad_weight, order=tiles.schedule(dev))
         if ctx.needs_input_grad[0]:
             grad_input = torch.matmul(grad_output, weight)
         return grad_input, grad_weight, None, None

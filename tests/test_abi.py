@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     out = subprocess.run(["nm", "-D", "--defined-only", _hip.lib_path()], capture_output=True, text=True).stdout
     for name in declared_functions():
         assert re.search(rf"\bT {name}$", out, re.M), name
-    assert lib.smt_abi_version() == 1
+    assert lib.smt_abi_version() == 2
 
 
 def test_library_carries_gfx950_code_object():
@@ -45,9 +45,9 @@ def test_struct_layouts_match_header():
 
 def test_validation_errors_without_gpu():
     lib = _hip.load()
-    assert lib.smt_tile_wgrad(None, 0, None, 0, 16, None, -1, None, 0, 0, None, 0, None) == -1
+    assert lib.smt_tile_wgrad(None, 0, None, 0, 16, None, None, -1, None, 0, 0, None, 0, None) == -1
     assert b"negative" in lib.smt_last_error()
-    assert lib.smt_tile_wgrad(None, 0, None, 0, 16, None, 0, None, 0, 0, None, 0, None) == 0   # no tiles: no-op
+    assert lib.smt_tile_wgrad(None, 0, None, 0, 16, None, None, 0, None, 0, 0, None, 0, None) == 0   # no tiles: no-op
     assert lib.smt_adamw_step(None, None, None, None, None, None, 0, 0, None, None, None) == -1
     args = _hip.AdamWArgs(lr=1e-3, beta1=0.9, beta2=0.95, eps=1e-8, weight_decay=0.0, bias_correction1=0.0,
                           bias_correction2=0.1, max_grad_norm=0.0, grad_scale=1.0, mode=0, grad_dtype=0)
@@ -55,7 +55,9 @@ def test_validation_errors_without_gpu():
     assert b"bias" in lib.smt_last_error()
     assert lib.smt_tile_gather(None, 256, 3, None, 1, None, None) == -1
     assert lib.smt_sq_norm(None, 10, None, 0, None, None) == -1
-    assert lib.smt_wgrad_workspace_bytes(32768, 27) == 27 * 19 * 65536 * 4
+    assert lib.smt_wgrad_workspace_bytes(32768, 27) == 27 * 9 * 65536 * 4
+    assert lib.smt_wgrad_workspace_bytes(32768, 200) == 0          # S == 1: no slabs
+    assert lib.smt_wgrad_workspace_bytes(32768, 128) == 128 * 2 * 65536 * 4
     assert lib.smt_wgrad_workspace_bytes(0, 27) == 0
 
 

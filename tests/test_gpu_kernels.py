@@ -29,6 +29,7 @@ WGRAD_CASES = [
     (1, 2048, 1024, 4096, [(3, 15), (0, 0), (2, 7), (3, 0), (1, 8)]),
     (3, 100, 256, 512, [(0, 1)]),                    # ragged T = 300 (not a multiple of 64)
     (4, 512, 768, 512, [(r, c) for r in range(3) for c in range(2)]),   # every tile of the matrix
+    (1, 192, 4096, 2048, [(r, c) for r in range(16) for c in range(8)] + [(0, 0), (15, 7)]),  # n >= 128: S == 1
 ]
 
 
@@ -51,6 +52,19 @@ def test_tile_wgrad_vs_fp64(B, S, out_f, in_f, tiles, out_dtype):
         # and never worse than the reference's own per-sample-rounded result (smt.py:397-404)
         _gi, ref_gw = ref.linearz_backward(g, x, torch.zeros(out_f, in_f, dtype=torch.bfloat16), tiles)
         assert err <= max(1e-3, 1.1 * _rel(ref_gw, truth))
+
+
+@pytest.mark.parametrize("out_dtype", [torch.bfloat16, torch.float32])
+def test_tile_wgrad_direct_epilogue_accumulate(out_dtype):
+    # 130 tiles -> S == 1: the partial kernel writes (and accumulates into) the output itself
+    tiles = [(r, c) for r in range(13) for c in range(10)]
+    x = torch.randn(2, 48, 2560).bfloat16()
+    g = torch.randn(2, 48, 3328).bfloat16()
+    out = torch.full((len(tiles) * 256, 256), 0.5, dtype=out_dtype, device=DEV)
+    _hip.tile_wgrad(g.reshape(-1, 3328).to(DEV), x.reshape(-1, 2560).to(DEV), _hip.tile_table(tiles, torch.device(DEV)),
+                    out, accumulate=True)
+    truth = ref.tile_grads_fp64(g, x, tiles) + 0.5
+    assert _rel(out, truth) < (1e-5 if out_dtype == torch.float32 else 2e-3)
 
 
 def test_tile_wgrad_accumulate_and_empty():
