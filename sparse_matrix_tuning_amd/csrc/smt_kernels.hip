@@ -18,6 +18,9 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
+#include <cmath>
+
 #include "smt_hip.h"
 
 namespace {
@@ -621,19 +624,30 @@ void adamw_flat_kernel(const void* __restrict__ grad, float* __restrict__ master
 }
 
 // Split of T over workgroups for one tile set. One 512-thread workgroup fits per CU (128 KiB LDS),
-// so fill the 256 CUs in ONE round: S = floor(256 / n_tiles) (no partial second round, fewer slab
-// bytes), chunks of at least 512 rows and a multiple of the 64-row stage. S == 1 (n_tiles > 128):
-// the tile is written straight from the accumulators.
+// so the launch runs in rounds of 256 workgroups; pick S in [1, 64] (chunks >= 512 rows, multiple of
+// the 64-row stage) minimising the modelled time below, ties to the smaller S. E.g. at T = 32768:
+// n = 27 -> S = 9 (243 workgroups, one round); n = 436 -> S = 4 (7 rounds of T/4 instead of 2 rounds
+// of T). S == 1: the tile is written straight from the accumulators.
 constexpr int kCUs = 256;
 struct WgradSplit { int S; int64_t chunk; };
 
 WgradSplit wgrad_split(int64_t T, int32_t n_tiles) {
     WgradSplit sp{1, kBK};
     if (T <= 0 || n_tiles <= 0) return sp;
-    int64_t S = n_tiles >= kCUs ? 1 : kCUs / n_tiles;
-    const int64_t s_max = (T + 511) / 512;
-    if (S > s_max) S = s_max;
-    if (S < 1) S = 1;
+    // Time model (measured rates): a workgroup streams its 1 KiB/row of g+x slices at ~25 GB/s per
+    // CU and, when S > 1, writes a 256 KiB fp32 slab; the reduce re-reads the n*S slabs (~5 TB/s).
+    const int64_t s_max = std::max<int64_t>(1, std::min<int64_t>(64, (T + 511) / 512));
+    double best = 1e30;
+    int64_t S = 1;
+    for (int64_t cand = 1; cand <= s_max; ++cand) {
+        const int64_t rounds = (n_tiles * cand + kCUs - 1) / kCUs;
+        const double rows = std::ceil((double)T / (double)cand);
+        const double slab = cand > 1 ? 262144.0 : 0.0;
+        const double t_wg = (rows * 1024.0 + slab) / 25e9;
+        const double t_red = cand > 1 ? (double)n_tiles * cand * 262144.0 * 2.0 / 5e12 : 0.0;
+        const double cost = (double)rounds * t_wg + t_red;
+        if (cost < best * (1.0 - 1e-6)) { best = cost; S = cand; }
+    }
     int64_t chunk = (T + S - 1) / S;
     chunk = (chunk + kBK - 1) / kBK * kBK;
     sp.S = (int)((T + chunk - 1) / chunk);

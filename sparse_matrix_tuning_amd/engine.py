@@ -265,6 +265,22 @@ class SMTEngine:
             return None
         return sink.buffer * self._grad_scale()
 
+    def save_checkpoint(self, save_dir: str, tag=None, client_state: Optional[dict] = None) -> str:
+        """DeepSpeed ``save_checkpoint`` surface: selection + tiles + tile optimizer state
+        (:mod:`sparse_matrix_tuning_amd.checkpoint`)."""
+        import os
+        from . import checkpoint
+        d = os.path.join(save_dir, str(tag)) if tag is not None else save_dir
+        return checkpoint.save_checkpoint(self, d, client_state)
+
+    def load_checkpoint(self, load_dir: str, tag=None) -> dict:
+        """Load the tile optimizer state / counters saved by :meth:`save_checkpoint` into this
+        engine. The model must have been restored first (``checkpoint.restore_model``)."""
+        import os
+        from . import checkpoint
+        d = os.path.join(load_dir, str(tag)) if tag is not None else load_dir
+        return checkpoint.load_optimizer_state(self, d)
+
     def release(self):
         """Drop optimizer state and packed buffers (e.g. the warm-up engine before SMT starts)."""
         for tg in self.tile_groups:

@@ -1,0 +1,116 @@
+"""Checkpoint / resume: an interrupted run resumed from an SMT checkpoint is
+bit-identical to the uninterrupted run (all kernels on the path are deterministic)."""
+import pytest
+import torch
+from torch import nn
+
+from oracle import smt_oracle as ref
+from sparse_matrix_tuning_amd import checkpoint
+from sparse_matrix_tuning_amd.engine import SMTFusedAdam, initialize, linear_lr_lambda
+from sparse_matrix_tuning_amd.smt import smt
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+SEL_MLP = {("up_proj", 0): [(2, 1), (0, 0)], ("down_proj", 1): [(1, 2)]}
+SEL_ATT = {("v_proj", 0): [(0, 1)]}
+
+
+class Block(nn.Module):
+    def __init__(self, i):
+        super().__init__()
+        self.self_attn = nn.Module()
+        self.self_attn.v_proj = nn.Linear(512, 256, bias=False)
+        self.mlp = nn.Module()
+        self.mlp.up_proj = nn.Linear(256, 768, bias=False)
+        self.mlp.down_proj = nn.Linear(768, 512, bias=False)
+
+    def forward(self, x):
+        return self.mlp.down_proj(torch.relu(self.mlp.up_proj(self.self_attn.v_proj(x))))
+
+
+class Net(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.model = nn.Module()
+        self.model.layers = nn.ModuleList([Block(0), Block(1)])
+
+    def forward(self, x):
+        for b in self.model.layers:
+            x = b(x)
+        return x
+
+
+def _base():
+    torch.manual_seed(0)
+    net = Net().to(torch.bfloat16)
+    with torch.no_grad():
+        for p in net.parameters():
+            p.mul_(4.0)
+    return net.to(DEV)
+
+
+def _engine(net):
+    smt.freeze_unselected_matrix_layer(net, SEL_MLP, SEL_ATT)
+    smt.convert_linear_layer_to_matrix_sparsity(net, SEL_MLP, SEL_ATT)
+    groups = smt.get_optimizer_sparse_grouped_parameters(net, 0.01, 2e-3)
+    opt = SMTFusedAdam(groups, lr=2e-3, betas=(0.9, 0.95))
+    sched = torch.optim.lr_scheduler.LambdaLR(opt, linear_lr_lambda(1, 10))
+    eng, _, _, _ = initialize(model=net, optimizer=opt, config={"gradient_clipping": 1.0}, lr_scheduler=sched)
+    return eng
+
+
+def _step(eng, i):
+    x = torch.randn(2, 32, 512, generator=torch.Generator().manual_seed(100 + i)).bfloat16().to(DEV)
+    loss = (eng(x).float() ** 2).mean()
+    eng.backward(loss)
+    eng.step()
+    return loss.item()
+
+
+def test_resume_is_bit_identical(tmp_path):
+    base_sd = {k: v.clone() for k, v in _base().state_dict().items()}
+    a = _engine(_base())
+    for i in range(4):
+        _step(a, i)
+    b = _engine(_base())
+    for i in range(2):
+        _step(b, i)
+    b.save_checkpoint(str(tmp_path), tag="step2", client_state={"epoch": 0})
+    del b
+    net = _base()
+    net.load_state_dict(base_sd)
+    checkpoint.restore_model(net, str(tmp_path / "step2"))
+    c = _engine_restored(net)
+    assert c.load_checkpoint(str(tmp_path), tag="step2") == {"epoch": 0}
+    for i in range(2, 4):
+        _step(c, i)
+    torch.cuda.synchronize()
+    for ta, tc in zip(a.tile_groups, c.tile_groups):
+        assert torch.equal(ta.master, tc.master) and torch.equal(ta.exp_avg_sq, tc.exp_avg_sq)
+    for (na, pa), (nc, pc) in zip(a.module.named_parameters(), c.module.named_parameters()):
+        assert na == nc and torch.equal(pa, pc), na
+    assert c.global_steps == 4 and c.lr_scheduler.last_epoch == a.lr_scheduler.last_epoch
+
+
+def _engine_restored(net):
+    groups = smt.get_optimizer_sparse_grouped_parameters(net, 0.01, 2e-3)
+    opt = SMTFusedAdam(groups, lr=2e-3, betas=(0.9, 0.95))
+    sched = torch.optim.lr_scheduler.LambdaLR(opt, linear_lr_lambda(1, 10))
+    eng, _, _, _ = initialize(model=net, optimizer=opt, config={"gradient_clipping": 1.0}, lr_scheduler=sched)
+    return eng
+
+
+def test_selection_roundtrip_and_merged_export(tmp_path):
+    eng = _engine(_base())
+    _step(eng, 0)
+    eng.save_checkpoint(str(tmp_path))
+    sel_mlp, sel_att = checkpoint.read_selection(str(tmp_path))
+    assert dict(sel_mlp) == SEL_MLP and dict(sel_att) == SEL_ATT
+    path = str(tmp_path / "merged.safetensors")
+    checkpoint.save_merged_model(eng.module, path)
+    from safetensors.torch import load_file
+    sd = load_file(path)
+    assert not any(k.endswith("selected_weight") for k in sd)
+    up = eng.module.model.layers[0].mlp.up_proj
+    w = sd["model.layers.0.mlp.up_proj.weight"]
+    assert torch.equal(ref.gather_tiles(w, up.index_list), up.selected_weight.detach().cpu())
