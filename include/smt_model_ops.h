@@ -1,0 +1,60 @@
+/*
+ * smt_model_ops.h — C-ABI of the fused LLaMA elementwise kernels used by the SMT training step
+ * (csrc/llama_kernels.hip, same library libsmt_hip.so). Auxiliary to the SMT hot path (smt_hip.h):
+ * they replace eager op chains of the HF transformers LLaMA decoder that carries the SMT modules
+ * (the reference trains that model through AutoModelForCausalLM, deepspeed/fine_tune.py:150-155):
+ *   smt_rmsnorm_fwd/bwd   transformers LlamaRMSNorm.forward (+ autograd of its op chain)
+ *   smt_rope_fwd/bwd      transformers apply_rotary_pos_emb
+ *   smt_swiglu_fwd/bwd    transformers LlamaMLP.forward: act_fn(gate_proj(x)) * up_proj(x), act = SiLU
+ * bf16 tensors, 16-byte aligned rows; every intermediate bf16 rounding of the eager chain is kept.
+ * Return 0 or a negative code; smt_model_ops_last_error() holds the message.
+ */
+#ifndef SMT_MODEL_OPS_H
+#define SMT_MODEL_OPS_H
+
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* A [B, heads, S, D] bf16 tensor and its output, element strides (d-stride 1). */
+typedef struct smt_rope_tensor {
+    const void* in;
+    void* out;
+    int64_t in_sb, in_sh, in_ss;
+    int64_t out_sb, out_sh, out_ss;
+    int32_t heads;
+    int32_t pad_;
+} smt_rope_tensor;
+
+const char* smt_model_ops_last_error(void);
+
+/* y = w * bf16(x * rsqrt(mean(x^2) + eps)); rstd[rows] (fp32) saved for the backward. */
+int smt_rmsnorm_fwd(const void* x, int64_t ld_x, const void* weight, void* y, int64_t ld_y, float* rstd,
+                    int64_t rows, int32_t hidden, float eps, hipStream_t stream);
+
+/* Number of waves (and rows of dw_partial) smt_rmsnorm_bwd uses for `rows` rows. */
+int smt_rmsnorm_bwd_waves(int64_t rows);
+
+/* dx (and, if dw != NULL, dw via dw_partial[smt_rmsnorm_bwd_waves(rows)][hidden] fp32). */
+int smt_rmsnorm_bwd(const void* dy, int64_t ld_dy, const void* x, int64_t ld_x, const void* weight, const float* rstd,
+                    void* dx, int64_t ld_dx, float* dw_partial, void* dw, int64_t rows, int32_t hidden,
+                    hipStream_t stream);
+
+/* q/k rotary embedding (one launch for both); cos/sin [B, S, D] with strides (cos_sb, cos_ss, 1). */
+int smt_rope_fwd(const smt_rope_tensor* q, const smt_rope_tensor* k, const void* cos, const void* sin,
+                 int64_t cos_sb, int64_t cos_ss, int64_t B, int32_t S, int32_t D, hipStream_t stream);
+int smt_rope_bwd(const smt_rope_tensor* dq, const smt_rope_tensor* dk, const void* cos, const void* sin,
+                 int64_t cos_sb, int64_t cos_ss, int64_t B, int32_t S, int32_t D, hipStream_t stream);
+
+/* out = bf16(silu(gate)) * up ; backward recomputes silu from gate. n % 8 == 0. */
+int smt_swiglu_fwd(const void* gate, const void* up, void* out, int64_t n, hipStream_t stream);
+int smt_swiglu_bwd(const void* gate, const void* up, const void* grad_out, void* grad_gate, void* grad_up, int64_t n,
+                   hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SMT_MODEL_OPS_H */

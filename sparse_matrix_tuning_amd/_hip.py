@@ -25,11 +25,14 @@ ADAM_DEEPSPEED, ADAM_TORCH = 0, 1
 
 _DT = {torch.bfloat16: DTYPE_BF16, torch.float32: DTYPE_FP32, torch.float16: DTYPE_FP16}
 
-# Every function the header declares; tests check the library exports each of them.
+# Every function the headers declare (include/smt_hip.h, include/smt_model_ops.h); tests check the
+# library exports each of them.
 ABI_FUNCTIONS = (
     "smt_last_error", "smt_abi_version", "smt_wgrad_workspace_bytes", "smt_tile_wgrad",
     "smt_tile_gather", "smt_tile_scatter", "smt_grad_accumulate", "smt_block_score",
     "smt_sq_norm", "smt_adamw_step",
+    "smt_model_ops_last_error", "smt_rmsnorm_fwd", "smt_rmsnorm_bwd_waves", "smt_rmsnorm_bwd",
+    "smt_rope_fwd", "smt_rope_bwd", "smt_swiglu_fwd", "smt_swiglu_bwd",
 )
 
 
@@ -58,6 +61,13 @@ class AdamWArgs(ctypes.Structure):
                 ("mode", ctypes.c_int32), ("grad_dtype", ctypes.c_int32)]
 
 
+class RopeTensor(ctypes.Structure):
+    _fields_ = [("inp", ctypes.c_void_p), ("out", ctypes.c_void_p),
+                ("in_sb", ctypes.c_int64), ("in_sh", ctypes.c_int64), ("in_ss", ctypes.c_int64),
+                ("out_sb", ctypes.c_int64), ("out_sh", ctypes.c_int64), ("out_ss", ctypes.c_int64),
+                ("heads", ctypes.c_int32), ("pad_", ctypes.c_int32)]
+
+
 ACC_CHUNK = 4096
 _lock = threading.Lock()
 _lib: Optional[ctypes.CDLL] = None
@@ -74,6 +84,14 @@ _SIGS = {
     "smt_block_score": (ctypes.c_int, [_P, _I32, _I64, _P]),
     "smt_sq_norm": (ctypes.c_int, [_P, _I64, _P, _I32, _P, _P]),
     "smt_adamw_step": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I32, _I64, _P, ctypes.POINTER(AdamWArgs), _P]),
+    "smt_model_ops_last_error": (ctypes.c_char_p, []),
+    "smt_rmsnorm_fwd": (ctypes.c_int, [_P, _I64, _P, _P, _I64, _P, _I64, _I32, ctypes.c_float, _P]),
+    "smt_rmsnorm_bwd_waves": (ctypes.c_int, [_I64]),
+    "smt_rmsnorm_bwd": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _P, _P, _I64, _P, _P, _I64, _I32, _P]),
+    "smt_rope_fwd": (ctypes.c_int, [ctypes.POINTER(RopeTensor), ctypes.POINTER(RopeTensor), _P, _P, _I64, _I64, _I64, _I32, _I32, _P]),
+    "smt_rope_bwd": (ctypes.c_int, [ctypes.POINTER(RopeTensor), ctypes.POINTER(RopeTensor), _P, _P, _I64, _I64, _I64, _I32, _I32, _P]),
+    "smt_swiglu_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _P]),
+    "smt_swiglu_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I64, _P]),
 }
 
 
@@ -106,8 +124,9 @@ def load(build_if_missing: bool = False) -> ctypes.CDLL:
 
 def _check(rc: int, what: str) -> None:
     if rc != 0:
-        msg = load().smt_last_error().decode(errors="replace")
-        raise RuntimeError(f"{what} failed (status {rc}): {msg}")
+        lib = load()
+        err = lib.smt_model_ops_last_error if what.startswith(("smt_rmsnorm", "smt_rope", "smt_swiglu")) else lib.smt_last_error
+        raise RuntimeError(f"{what} failed (status {rc}): {err().decode(errors='replace')}")
 
 
 def _require_device(*tensors: torch.Tensor) -> torch.device:

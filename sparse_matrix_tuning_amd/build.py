@@ -1,7 +1,8 @@
 """Build the gfx950 HIP library ``_lib/libsmt_hip.so`` in-tree with hipcc.
 
-The library is the only native product code: ``csrc/smt_kernels.hip`` compiled for
-``--offload-arch=gfx950`` behind the C ABI in ``include/smt_hip.h``. It is loaded with
+The library is the only native product code: ``csrc/smt_kernels.hip`` (the SMT hot path, C ABI
+``include/smt_hip.h``) and ``csrc/llama_kernels.hip`` (fused LLaMA elementwise ops, C ABI
+``include/smt_model_ops.h``) compiled for ``--offload-arch=gfx950``. It is loaded with
 ctypes by :mod:`sparse_matrix_tuning_amd._hip` (no torch types cross the boundary).
 """
 from __future__ import annotations
@@ -13,8 +14,8 @@ import sys
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
-SRC = os.path.join(PKG_DIR, "csrc", "smt_kernels.hip")
-HEADER = os.path.join(REPO_DIR, "include", "smt_hip.h")
+SRCS = [os.path.join(PKG_DIR, "csrc", "smt_kernels.hip"), os.path.join(PKG_DIR, "csrc", "llama_kernels.hip")]
+HEADERS = [os.path.join(REPO_DIR, "include", "smt_hip.h"), os.path.join(REPO_DIR, "include", "smt_model_ops.h")]
 LIB_DIR = os.path.join(PKG_DIR, "_lib")
 LIB_PATH = os.path.join(LIB_DIR, "libsmt_hip.so")
 ARCH = "gfx950"
@@ -31,7 +32,7 @@ def is_stale() -> bool:
     if not os.path.exists(LIB_PATH):
         return True
     t = os.path.getmtime(LIB_PATH)
-    return any(os.path.getmtime(p) > t for p in (SRC, HEADER, __file__))
+    return any(os.path.getmtime(p) > t for p in (*SRCS, *HEADERS, __file__))
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
@@ -44,7 +45,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
         "-Wall", "-Wno-unused-function",
         "-I", os.path.join(REPO_DIR, "include"),
-        "-o", tmp, SRC,
+        "-o", tmp, *SRCS,
     ]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)

@@ -1,0 +1,376 @@
+// llama_kernels.hip — gfx950 fused elementwise kernels for the HF LLaMA decoder that carries the SMT
+// modules in the training step (bench / trainer). They replace the eager op chains of
+// transformers' LlamaRMSNorm.forward, apply_rotary_pos_emb and LlamaMLP's act_fn(gate) * up, which
+// the rocprof step breakdown shows as ~27 % of an SMT step (3.6 k elementwise dispatches, each a full
+// HBM pass over [B*S, hidden] or [B*S, intermediate] tensors, several in fp32).
+//
+// Numerics follow the eager bf16 op sequence, including every intermediate bf16 rounding, so the
+// outputs match the eager module to (at most) an ulp from reduction order / exp implementation.
+// All loads and stores are 16 B per lane; rows are processed one wave (64 lanes) per row.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "smt_model_ops.h"
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+int check_launch(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(-4, "%s: %s", what, hipGetErrorString(e));
+    return 0;
+}
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+__device__ __forceinline__ float bf(uint32_t b16) { return __uint_as_float(b16 << 16); }
+__device__ __forceinline__ uint32_t tobf(float f) { return (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)f); }
+__device__ __forceinline__ float rbf(float f) { return bf(tobf(f)); }       // round through bf16
+
+struct F8 { float v[8]; };
+
+__device__ __forceinline__ F8 ld8(const uint16_t* p) {
+    const uint4 a = *reinterpret_cast<const uint4*>(p);
+    F8 r;
+    const uint32_t w[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { r.v[2 * j] = bf(w[j] & 0xffffu); r.v[2 * j + 1] = bf(w[j] >> 16); }
+    return r;
+}
+
+__device__ __forceinline__ void st8(uint16_t* p, const F8& r) {
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = tobf(r.v[2 * j]) | (tobf(r.v[2 * j + 1]) << 16);
+    *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__device__ __forceinline__ float wave_sum_f(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// ------------------------------------------------------------------------------------------------
+// RMSNorm (LlamaRMSNorm.forward):  xf = float(x); r = rsqrt(mean(xf^2) + eps);
+//                                  y = bf16(float(w) * float(bf16(xf * r)))
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256)
+void rmsnorm_fwd_kernel(const uint16_t* __restrict__ x, int64_t ldx, const uint16_t* __restrict__ w,
+                        uint16_t* __restrict__ y, int64_t ldy, float* __restrict__ rstd,
+                        int64_t rows, int H, float eps) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const uint16_t* xr = x + row * ldx;
+    const int nch = H >> 3;
+    float ss = 0.f;
+    for (int c = lane; c < nch; c += 64) {
+        const F8 v = ld8(xr + c * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ss += v.v[j] * v.v[j];
+    }
+    ss = wave_sum_f(ss);
+    const float r = 1.0f / sqrtf(ss / (float)H + eps);
+    if (lane == 0) rstd[row] = r;
+    uint16_t* yr = y + row * ldy;
+    for (int c = lane; c < nch; c += 64) {
+        const F8 v = ld8(xr + c * 8);
+        const F8 wv = ld8(w + c * 8);
+        F8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o.v[j] = wv.v[j] * rbf(v.v[j] * r);
+        st8(yr + c * 8, o);
+    }
+}
+
+// Backward of the eager chain: dn = bf16(dy * w); dx = bf16(r*dn - xf * r^3 * sum(dn*xf) / H);
+// optional weight grad: dw = bf16(sum_rows float(bf16(dy * bf16(xf*r)))) as per-wave fp32 partials
+// [n_waves][H] summed in a fixed order by rmsnorm_dw_kernel. Waves stride over rows.
+template <bool DW, int CPL>
+__global__ __launch_bounds__(256)
+void rmsnorm_bwd_kernel(const uint16_t* __restrict__ dy, int64_t lddy, const uint16_t* __restrict__ x, int64_t ldx,
+                        const uint16_t* __restrict__ w, const float* __restrict__ rstd,
+                        uint16_t* __restrict__ dx, int64_t lddx, float* __restrict__ dw_partial,
+                        int64_t rows, int H) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t n_waves = (int64_t)gridDim.x * 4;
+    const int nch = H >> 3;
+    float acc[DW ? CPL * 8 : 1];
+    if (DW) {
+#pragma unroll
+        for (int i = 0; i < CPL * 8; ++i) acc[i] = 0.f;
+    }
+    for (int64_t row = wave; row < rows; row += n_waves) {
+        const float r = rstd[row];
+        const uint16_t* xr = x + row * ldx;
+        const uint16_t* dyr = dy + row * lddy;
+        float dot = 0.f;
+        for (int c = lane; c < nch; c += 64) {
+            const F8 xv = ld8(xr + c * 8), gv = ld8(dyr + c * 8), wv = ld8(w + c * 8);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) dot += rbf(gv.v[j] * wv.v[j]) * xv.v[j];
+        }
+        dot = wave_sum_f(dot);
+        const float coef = r * r * r * dot / (float)H;
+        uint16_t* dxr = dx + row * lddx;
+        int k = 0;
+        for (int c = lane; c < nch; c += 64, ++k) {
+            const F8 xv = ld8(xr + c * 8), gv = ld8(dyr + c * 8), wv = ld8(w + c * 8);
+            F8 o;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o.v[j] = r * rbf(gv.v[j] * wv.v[j]) - xv.v[j] * coef;
+            st8(dxr + c * 8, o);
+            if (DW) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc[k * 8 + j] += rbf(gv.v[j] * rbf(xv.v[j] * r));
+            }
+        }
+    }
+    if (DW) {
+        float* pr = dw_partial + wave * H;
+        int k = 0;
+        for (int c = lane; c < nch; c += 64, ++k) {
+            float4* d = reinterpret_cast<float4*>(pr + c * 8);
+            d[0] = make_float4(acc[k * 8 + 0], acc[k * 8 + 1], acc[k * 8 + 2], acc[k * 8 + 3]);
+            d[1] = make_float4(acc[k * 8 + 4], acc[k * 8 + 5], acc[k * 8 + 6], acc[k * 8 + 7]);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256)
+void rmsnorm_dw_kernel(const float* __restrict__ partial, int64_t n_waves, int H, uint16_t* __restrict__ dw) {
+    const int col = blockIdx.x * 256 + threadIdx.x;
+    if (col >= H) return;
+    float s = 0.f;
+    for (int64_t i = 0; i < n_waves; ++i) s += partial[i * H + col];
+    dw[col] = (uint16_t)tobf(s);
+}
+
+// ------------------------------------------------------------------------------------------------
+// RoPE (apply_rotary_pos_emb): per element pair (d, d+D/2) of one head row,
+//   lo' = bf16(bf16(lo*c_lo) + bf16(-hi*s_lo)),  hi' = bf16(bf16(hi*c_hi) + bf16(lo*s_hi))
+// backward:
+//   dlo = bf16(bf16(dlo'*c_lo) + bf16(dhi'*s_hi)), dhi = bf16(bf16(dhi'*c_hi) - bf16(dlo'*s_lo))
+// Tensors are [B, H, S, D] with element strides (sb, sh, ss, 1); cos/sin [B, S, D] (cb, cs, 1).
+// One thread per 8 pairs; the q and k tensors share one launch.
+// ------------------------------------------------------------------------------------------------
+struct RopeT {
+    const uint16_t* in; uint16_t* out;
+    int64_t sb, sh, ss;     // input strides
+    int64_t ob, oh, os;     // output strides
+    int H;
+};
+
+template <bool BWD>
+__device__ __forceinline__ void rope_one(const RopeT& t, const uint16_t* cos, const uint16_t* sin, int64_t cb,
+                                         int64_t cs, int64_t idx, int S, int D) {
+    const int half = D >> 1;
+    const int cpr = half >> 3;                        // 8-pair chunks per head row
+    const int c = (int)(idx % cpr);
+    int64_t rest = idx / cpr;
+    const int s = (int)(rest % S); rest /= S;
+    const int h = (int)(rest % t.H);
+    const int64_t b = rest / t.H;
+    const int d = c * 8;
+    const uint16_t* ip = t.in + b * t.sb + h * t.sh + (int64_t)s * t.ss;
+    uint16_t* op = t.out + b * t.ob + h * t.oh + (int64_t)s * t.os;
+    const uint16_t* cp = cos + b * cb + (int64_t)s * cs;
+    const uint16_t* sp = sin + b * cb + (int64_t)s * cs;
+    const F8 lo = ld8(ip + d), hi = ld8(ip + half + d);
+    const F8 clo = ld8(cp + d), chi = ld8(cp + half + d), slo = ld8(sp + d), shi = ld8(sp + half + d);
+    F8 olo, ohi;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        if (!BWD) {
+            olo.v[j] = rbf(lo.v[j] * clo.v[j]) + rbf(-hi.v[j] * slo.v[j]);
+            ohi.v[j] = rbf(hi.v[j] * chi.v[j]) + rbf(lo.v[j] * shi.v[j]);
+        } else {
+            olo.v[j] = rbf(lo.v[j] * clo.v[j]) + rbf(hi.v[j] * shi.v[j]);
+            ohi.v[j] = rbf(hi.v[j] * chi.v[j]) - rbf(lo.v[j] * slo.v[j]);
+        }
+    }
+    st8(op + d, olo);
+    st8(op + half + d, ohi);
+}
+
+template <bool BWD>
+__global__ __launch_bounds__(256)
+void rope_kernel(RopeT q, RopeT k, const uint16_t* __restrict__ cos, const uint16_t* __restrict__ sin,
+                 int64_t cb, int64_t cs, int64_t B, int S, int D) {
+    const int64_t cpr = D >> 4;
+    const int64_t nq = B * q.H * (int64_t)S * cpr;
+    const int64_t nk = B * k.H * (int64_t)S * cpr;
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx < nq) rope_one<BWD>(q, cos, sin, cb, cs, idx, S, D);
+    else if (idx < nq + nk) rope_one<BWD>(k, cos, sin, cb, cs, idx - nq, S, D);
+}
+
+// ------------------------------------------------------------------------------------------------
+// SwiGLU (act_fn(gate) * up with act_fn = SiLU):
+//   s = bf16(g / (1 + exp(-g))), h = bf16(s * u)
+// backward: ds = bf16(dh*u), du = bf16(dh*s), dg = bf16(ds * sig * (1 + g*(1 - sig)))
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256)
+void swiglu_fwd_kernel(const uint16_t* __restrict__ g, const uint16_t* __restrict__ u, uint16_t* __restrict__ h,
+                       int64_t n8) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n8) return;
+    const F8 gv = ld8(g + i * 8), uv = ld8(u + i * 8);
+    F8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float s = rbf(gv.v[j] / (1.0f + expf(-gv.v[j])));
+        o.v[j] = s * uv.v[j];
+    }
+    st8(h + i * 8, o);
+}
+
+__global__ __launch_bounds__(256)
+void swiglu_bwd_kernel(const uint16_t* __restrict__ g, const uint16_t* __restrict__ u, const uint16_t* __restrict__ dh,
+                       uint16_t* __restrict__ dg, uint16_t* __restrict__ du, int64_t n8) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n8) return;
+    const F8 gv = ld8(g + i * 8), uv = ld8(u + i * 8), hv = ld8(dh + i * 8);
+    F8 og, ou;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float x = gv.v[j];
+        const float sig = 1.0f / (1.0f + expf(-x));
+        const float s = rbf(x / (1.0f + expf(-x)));
+        const float ds = rbf(hv.v[j] * uv.v[j]);
+        ou.v[j] = hv.v[j] * s;
+        og.v[j] = ds * sig * (1.0f + x * (1.0f - sig));
+    }
+    st8(dg + i * 8, og);
+    st8(du + i * 8, ou);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* smt_model_ops_last_error(void) { return g_err; }
+
+int smt_rmsnorm_fwd(const void* x, int64_t ld_x, const void* weight, void* y, int64_t ld_y, float* rstd,
+                    int64_t rows, int32_t hidden, float eps, hipStream_t stream) {
+    if (rows < 0 || hidden <= 0 || (hidden & 7)) return fail(-1, "smt_rmsnorm_fwd: bad sizes rows=%lld hidden=%d", (long long)rows, hidden);
+    if (rows == 0) return 0;
+    if (!x || !weight || !y || !rstd) return fail(-1, "smt_rmsnorm_fwd: null pointer");
+    if (!aligned16(x) || !aligned16(weight) || !aligned16(y) || (ld_x & 7) || (ld_y & 7))
+        return fail(-2, "smt_rmsnorm_fwd: 16-byte aligned rows required");
+    const int64_t blocks = (rows + 3) / 4;
+    hipLaunchKernelGGL(rmsnorm_fwd_kernel, dim3((unsigned)blocks), dim3(256), 0, stream,
+                       (const uint16_t*)x, ld_x, (const uint16_t*)weight, (uint16_t*)y, ld_y, rstd, rows, hidden, eps);
+    return check_launch("rmsnorm_fwd_kernel");
+}
+
+int smt_rmsnorm_bwd_waves(int64_t rows) {
+    const int64_t want = rows < 4096 ? rows : 4096;
+    return (int)(want < 4 ? 4 : (want + 3) / 4 * 4);
+}
+
+int smt_rmsnorm_bwd(const void* dy, int64_t ld_dy, const void* x, int64_t ld_x, const void* weight, const float* rstd,
+                    void* dx, int64_t ld_dx, float* dw_partial, void* dw, int64_t rows, int32_t hidden,
+                    hipStream_t stream) {
+    if (rows < 0 || hidden <= 0 || (hidden & 7)) return fail(-1, "smt_rmsnorm_bwd: bad sizes");
+    if (rows == 0) return 0;
+    if (!dy || !x || !weight || !rstd || !dx) return fail(-1, "smt_rmsnorm_bwd: null pointer");
+    if (!aligned16(dy) || !aligned16(x) || !aligned16(weight) || !aligned16(dx) || (ld_dy & 7) || (ld_x & 7) || (ld_dx & 7))
+        return fail(-2, "smt_rmsnorm_bwd: 16-byte aligned rows required");
+    const int n_waves = smt_rmsnorm_bwd_waves(rows);
+    const dim3 grid(n_waves / 4), block(256);
+    const uint16_t *pdy = (const uint16_t*)dy, *px = (const uint16_t*)x, *pw = (const uint16_t*)weight;
+    uint16_t* pdx = (uint16_t*)dx;
+    if (dw == nullptr) {
+        hipLaunchKernelGGL((rmsnorm_bwd_kernel<false, 1>), grid, block, 0, stream, pdy, ld_dy, px, ld_x, pw, rstd, pdx, ld_dx,
+                           nullptr, rows, hidden);
+        return check_launch("rmsnorm_bwd_kernel");
+    }
+    if (!dw_partial || (hidden % 512) || hidden > 8192)
+        return fail(-1, "smt_rmsnorm_bwd: weight grad needs hidden %% 512 == 0, <= 8192 and a partial buffer");
+    const int cpl = hidden / 512;
+#define RMS_DW(C) case C: hipLaunchKernelGGL((rmsnorm_bwd_kernel<true, C>), grid, block, 0, stream, pdy, ld_dy, px, ld_x, pw, rstd, pdx, ld_dx, dw_partial, rows, hidden); break;
+    switch (cpl) {
+        RMS_DW(1) RMS_DW(2) RMS_DW(3) RMS_DW(4) RMS_DW(5) RMS_DW(6) RMS_DW(7) RMS_DW(8)
+        RMS_DW(9) RMS_DW(10) RMS_DW(11) RMS_DW(12) RMS_DW(13) RMS_DW(14) RMS_DW(15) RMS_DW(16)
+        default: return fail(-1, "smt_rmsnorm_bwd: hidden %d", hidden);
+    }
+#undef RMS_DW
+    int rc = check_launch("rmsnorm_bwd_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(rmsnorm_dw_kernel, dim3((hidden + 255) / 256), dim3(256), 0, stream, dw_partial, (int64_t)n_waves,
+                       hidden, (uint16_t*)dw);
+    return check_launch("rmsnorm_dw_kernel");
+}
+
+static int rope(bool bwd, const smt_rope_tensor* q, const smt_rope_tensor* k, const void* cos, const void* sin,
+                int64_t cos_sb, int64_t cos_ss, int64_t B, int32_t S, int32_t D, hipStream_t stream) {
+    if (!q || !k || !cos || !sin) return fail(-1, "smt_rope: null pointer");
+    if (B < 0 || S < 0 || D <= 0 || (D & 15)) return fail(-1, "smt_rope: head_dim %d must be a multiple of 16", D);
+    RopeT tq{(const uint16_t*)q->in, (uint16_t*)q->out, q->in_sb, q->in_sh, q->in_ss, q->out_sb, q->out_sh, q->out_ss, q->heads};
+    RopeT tk{(const uint16_t*)k->in, (uint16_t*)k->out, k->in_sb, k->in_sh, k->in_ss, k->out_sb, k->out_sh, k->out_ss, k->heads};
+    const void* ptrs[] = {q->in, q->out, k->in, k->out, cos, sin};
+    for (const void* p : ptrs) if (!aligned16(p)) return fail(-2, "smt_rope: 16-byte alignment required");
+    const int64_t strides[] = {q->in_sb, q->in_sh, q->in_ss, q->out_sb, q->out_sh, q->out_ss,
+                               k->in_sb, k->in_sh, k->in_ss, k->out_sb, k->out_sh, k->out_ss, cos_sb, cos_ss};
+    for (int64_t s : strides) if (s & 7) return fail(-2, "smt_rope: strides must be multiples of 8 elements");
+    const int64_t total = B * (int64_t)(q->heads + k->heads) * S * (D / 16);
+    if (total == 0) return 0;
+    const int64_t blocks = (total + 255) / 256;
+    if (bwd)
+        hipLaunchKernelGGL(rope_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, stream, tq, tk, (const uint16_t*)cos,
+                           (const uint16_t*)sin, cos_sb, cos_ss, B, S, D);
+    else
+        hipLaunchKernelGGL(rope_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, stream, tq, tk, (const uint16_t*)cos,
+                           (const uint16_t*)sin, cos_sb, cos_ss, B, S, D);
+    return check_launch("rope_kernel");
+}
+
+int smt_rope_fwd(const smt_rope_tensor* q, const smt_rope_tensor* k, const void* cos, const void* sin,
+                 int64_t cos_sb, int64_t cos_ss, int64_t B, int32_t S, int32_t D, hipStream_t stream) {
+    return rope(false, q, k, cos, sin, cos_sb, cos_ss, B, S, D, stream);
+}
+
+int smt_rope_bwd(const smt_rope_tensor* dq, const smt_rope_tensor* dk, const void* cos, const void* sin,
+                 int64_t cos_sb, int64_t cos_ss, int64_t B, int32_t S, int32_t D, hipStream_t stream) {
+    return rope(true, dq, dk, cos, sin, cos_sb, cos_ss, B, S, D, stream);
+}
+
+int smt_swiglu_fwd(const void* gate, const void* up, void* out, int64_t n, hipStream_t stream) {
+    if (n < 0 || (n & 7)) return fail(-1, "smt_swiglu_fwd: n %lld must be a multiple of 8", (long long)n);
+    if (n == 0) return 0;
+    if (!aligned16(gate) || !aligned16(up) || !aligned16(out)) return fail(-2, "smt_swiglu_fwd: alignment");
+    const int64_t n8 = n / 8;
+    hipLaunchKernelGGL(swiglu_fwd_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, stream,
+                       (const uint16_t*)gate, (const uint16_t*)up, (uint16_t*)out, n8);
+    return check_launch("swiglu_fwd_kernel");
+}
+
+int smt_swiglu_bwd(const void* gate, const void* up, const void* grad_out, void* grad_gate, void* grad_up, int64_t n,
+                   hipStream_t stream) {
+    if (n < 0 || (n & 7)) return fail(-1, "smt_swiglu_bwd: n %lld must be a multiple of 8", (long long)n);
+    if (n == 0) return 0;
+    if (!aligned16(gate) || !aligned16(up) || !aligned16(grad_out) || !aligned16(grad_gate) || !aligned16(grad_up))
+        return fail(-2, "smt_swiglu_bwd: alignment");
+    const int64_t n8 = n / 8;
+    hipLaunchKernelGGL(swiglu_bwd_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, stream,
+                       (const uint16_t*)gate, (const uint16_t*)up, (const uint16_t*)grad_out, (uint16_t*)grad_gate,
+                       (uint16_t*)grad_up, n8);
+    return check_launch("swiglu_bwd_kernel");
+}
+
+}  // extern "C"

@@ -1,0 +1,231 @@
+"""Fused gfx950 replacements for the eager elementwise chains of the HF LLaMA decoder.
+
+The SMT step trains ``transformers`` ``LlamaForCausalLM`` (the reference loads it through
+``AutoModelForCausalLM``, ``fine_tune.py:150-155``). In eager mode its RMSNorm, rotary embedding and
+SwiGLU each run as chains of 4-8 elementwise kernels, several in fp32; on MI355X those chains are
+27 % of an SMT step (profiles/r01_bench_step_breakdown.txt). :func:`patch_llama` swaps them for
+one-pass HIP kernels (``csrc/llama_kernels.hip``, C ABI ``include/smt_model_ops.h``) wrapped in
+autograd Functions. Every intermediate bf16 rounding of the eager chain is reproduced, so results
+match the eager model up to reduction order / exp ulps (tests/test_gpu_fused_llama.py).
+
+Only bf16 CUDA tensors take the fused path; anything else raises (no silent fallback).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+from torch import nn
+
+from . import _hip
+
+
+def _stream(t):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _need(t: torch.Tensor, what: str):
+    if t.device.type != "cuda" or t.dtype != torch.bfloat16:
+        raise RuntimeError(f"fused {what}: bf16 ROCm tensors only (got {t.dtype} on {t.device})")
+
+
+def _rows2d(t: torch.Tensor):
+    t2 = t.reshape(-1, t.shape[-1])
+    if t2.stride(-1) != 1 or t2.stride(0) % 8 or t2.data_ptr() % 16:
+        t2 = t2.contiguous()
+    return t2
+
+
+# ------------------------------------------------------------------------------------------------
+# RMSNorm
+# ------------------------------------------------------------------------------------------------
+class FusedRMSNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, eps):
+        _need(x, "rmsnorm")
+        _need(weight, "rmsnorm")
+        x2 = _rows2d(x)
+        rows, H = x2.shape
+        y = torch.empty((rows, H), dtype=x.dtype, device=x.device)
+        rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+        w = weight.contiguous()
+        rc = _hip.load().smt_rmsnorm_fwd(x2.data_ptr(), x2.stride(0), w.data_ptr(), y.data_ptr(), y.stride(0),
+                                         rstd.data_ptr(), rows, H, float(eps), _stream(x))
+        _hip._check(rc, "smt_rmsnorm_fwd")
+        ctx.save_for_backward(x2, w, rstd)
+        ctx.shape = x.shape
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, rstd = ctx.saved_tensors
+        rows, H = x2.shape
+        dy2 = _rows2d(dy)
+        dx = torch.empty_like(x2)
+        lib = _hip.load()
+        dw = partial = None
+        if ctx.needs_input_grad[1]:
+            waves = lib.smt_rmsnorm_bwd_waves(rows)
+            partial = torch.empty(waves, H, dtype=torch.float32, device=x2.device)
+            dw = torch.empty(H, dtype=w.dtype, device=w.device)
+        rc = lib.smt_rmsnorm_bwd(dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0), w.data_ptr(),
+                                 rstd.data_ptr(), dx.data_ptr(), dx.stride(0),
+                                 None if partial is None else partial.data_ptr(),
+                                 None if dw is None else dw.data_ptr(), rows, H, _stream(x2))
+        _hip._check(rc, "smt_rmsnorm_bwd")
+        return dx.view(ctx.shape), dw, None
+
+
+def fused_rmsnorm_forward(self, hidden_states):
+    """Drop-in for ``LlamaRMSNorm.forward``."""
+    return FusedRMSNormFn.apply(hidden_states, self.weight, self.variance_epsilon)
+
+
+# ------------------------------------------------------------------------------------------------
+# RoPE
+# ------------------------------------------------------------------------------------------------
+def _rope_desc(inp: torch.Tensor, out: torch.Tensor) -> _hip.RopeTensor:
+    sb, sh, ss, sd = inp.stride()
+    ob, oh, os_, od = out.stride()
+    if sd != 1 or od != 1:
+        raise RuntimeError("fused rope: head_dim must be the innermost dimension")
+    return _hip.RopeTensor(inp.data_ptr(), out.data_ptr(), sb, sh, ss, ob, oh, os_, inp.shape[1], 0)
+
+
+def _rope_launch(fn_name, q, k, cos, sin, q_layout=None, k_layout=None):
+    """Launch the fused rope kernel on q and k; outputs take ``*_layout`` = (shape, stride) (default:
+    the input's own layout: [B, S, H, D] storage under the [B, H, S, D] view for HF q/k)."""
+    B, _Hq, S, D = q.shape
+    if cos.dim() != 3 or cos.stride(-1) != 1 or cos.shape != sin.shape or cos.stride() != sin.stride():
+        cos, sin = cos.contiguous(), sin.contiguous()
+    if cos.shape[0] != B:
+        cos, sin = cos.expand(B, -1, -1).contiguous(), sin.expand(B, -1, -1).contiguous()
+    q = _rope_ready(q)
+    k = _rope_ready(k)
+    qs, qst = q_layout or (q.shape, q.stride())
+    ks, kst = k_layout or (k.shape, k.stride())
+    qo = torch.empty_strided(qs, qst, dtype=q.dtype, device=q.device)
+    ko = torch.empty_strided(ks, kst, dtype=k.dtype, device=k.device)
+    dq, dk = _rope_desc(q, qo), _rope_desc(k, ko)
+    lib = _hip.load()
+    rc = getattr(lib, fn_name)(ctypes.byref(dq), ctypes.byref(dk), cos.data_ptr(), sin.data_ptr(), cos.stride(0),
+                               cos.stride(1), B, S, D, _stream(q))
+    _hip._check(rc, fn_name)
+    return qo, ko
+
+
+def _rope_ready(t: torch.Tensor) -> torch.Tensor:
+    """16-byte aligned rows and 8-element strides with head_dim innermost, else a contiguous copy."""
+    if t.stride(-1) == 1 and not any(s % 8 for s in t.stride()[:3]) and t.data_ptr() % 16 == 0:
+        return t
+    return t.contiguous()
+
+
+class FusedRoPEFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, cos, sin):
+        for t, n in ((q, "q"), (k, "k"), (cos, "cos"), (sin, "sin")):
+            _need(t, "rope " + n)
+        qo, ko = _rope_launch("smt_rope_fwd", q, k, cos, sin)
+        ctx.save_for_backward(cos, sin)
+        # grads go back in q/k's own layout, so the transpose/view backward of q_proj's output is free
+        ctx.layouts = ((q.shape, q.stride()), (k.shape, k.stride()))
+        return qo, ko
+
+    @staticmethod
+    def backward(ctx, dqo, dko):
+        cos, sin = ctx.saved_tensors
+        ql, kl = ctx.layouts
+        if dqo is None:
+            dqo = torch.zeros(ql[0], dtype=torch.bfloat16, device=cos.device)
+        if dko is None:
+            dko = torch.zeros(kl[0], dtype=torch.bfloat16, device=cos.device)
+        dq, dk = _rope_launch("smt_rope_bwd", dqo, dko, cos, sin, ql, kl)
+        return dq, dk, None, None
+
+
+def fused_apply_rotary_pos_emb(q, k, cos, sin, unsqueeze_dim=1):
+    """Drop-in for ``transformers.models.llama.modeling_llama.apply_rotary_pos_emb`` (q/k in
+    ``[B, heads, S, head_dim]``, cos/sin ``[B, S, head_dim]``)."""
+    if unsqueeze_dim != 1:
+        raise NotImplementedError("fused rope: unsqueeze_dim=1 layout only")
+    return FusedRoPEFn.apply(q, k, cos, sin)
+
+
+# ------------------------------------------------------------------------------------------------
+# SwiGLU
+# ------------------------------------------------------------------------------------------------
+class FusedSwiGLUFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gate, up):
+        _need(gate, "swiglu")
+        _need(up, "swiglu")
+        g = gate.contiguous()
+        u = up.contiguous()
+        h = torch.empty_like(g)
+        rc = _hip.load().smt_swiglu_fwd(g.data_ptr(), u.data_ptr(), h.data_ptr(), g.numel(), _stream(g))
+        _hip._check(rc, "smt_swiglu_fwd")
+        ctx.save_for_backward(g, u)
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        g, u = ctx.saved_tensors
+        dh = dh.contiguous()
+        dg = torch.empty_like(g)
+        du = torch.empty_like(u)
+        rc = _hip.load().smt_swiglu_bwd(g.data_ptr(), u.data_ptr(), dh.data_ptr(), dg.data_ptr(), du.data_ptr(),
+                                        g.numel(), _stream(g))
+        _hip._check(rc, "smt_swiglu_bwd")
+        return dg, du
+
+
+def fused_mlp_forward(self, x):
+    """Drop-in for ``LlamaMLP.forward`` (SiLU activation)."""
+    return self.down_proj(FusedSwiGLUFn.apply(self.gate_proj(x), self.up_proj(x)))
+
+
+# ------------------------------------------------------------------------------------------------
+_EAGER = {}
+
+
+def _ml():
+    from transformers.models.llama import modeling_llama as ml
+    if "rope" not in _EAGER:
+        _EAGER["rope"] = ml.apply_rotary_pos_emb
+    return ml
+
+
+def eager_apply_rotary_pos_emb(*a, **k):
+    """transformers' own apply_rotary_pos_emb (for comparisons while the module global is patched)."""
+    return _ml() and _EAGER["rope"](*a, **k)
+
+
+def patch_llama(model: nn.Module) -> dict:
+    """Route a transformers LLaMA model's RMSNorm / RoPE / SwiGLU through the fused kernels.
+    RoPE is patched at module level (``modeling_llama.apply_rotary_pos_emb``, looked up by
+    ``LlamaAttention.forward`` at call time). Returns counts of patched modules. Idempotent."""
+    ml = _ml()
+    counts = {"rmsnorm": 0, "mlp": 0, "rope": 1}
+    for m in model.modules():
+        if isinstance(m, ml.LlamaRMSNorm):
+            m.forward = fused_rmsnorm_forward.__get__(m, type(m))
+            counts["rmsnorm"] += 1
+        elif isinstance(m, ml.LlamaMLP):
+            act = getattr(m, "act_fn", None)
+            if act is None or "silu" not in type(act).__name__.lower():
+                raise NotImplementedError(f"fused MLP: SiLU activation only (got {type(act).__name__})")
+            m.forward = fused_mlp_forward.__get__(m, type(m))
+            counts["mlp"] += 1
+    ml.apply_rotary_pos_emb = fused_apply_rotary_pos_emb
+    return counts
+
+
+def unpatch_llama(model: nn.Module = None) -> None:
+    """Undo :func:`patch_llama` (module-level RoPE; per-instance forwards of ``model`` if given)."""
+    ml = _ml()
+    ml.apply_rotary_pos_emb = _EAGER["rope"]
+    if model is not None:
+        for m in model.modules():
+            if isinstance(m, (ml.LlamaRMSNorm, ml.LlamaMLP)) and "forward" in m.__dict__:
+                del m.__dict__["forward"]

@@ -8,13 +8,15 @@ import subprocess
 from sparse_matrix_tuning_amd import _hip, build
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(ROOT, "include", "smt_hip.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in sorted(os.listdir(os.path.join(ROOT, "include"))) if h.endswith(".h")]
 
 
 def declared_functions():
-    text = open(HEADER).read()
-    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(smt_[a-z0-9_]+)\s*\(", text)))
+    names = set()
+    for h in HEADERS:
+        text = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        names |= set(re.findall(r"\b(smt_[a-z0-9_]+)\s*\(", text))
+    return sorted(names)
 
 
 def test_header_lists_the_binding_functions():
@@ -41,6 +43,7 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(_hip.AccumEntry) == 40
     assert ctypes.sizeof(_hip.ScoreEntry) == 48
     assert ctypes.sizeof(_hip.AdamWArgs) == 44
+    assert ctypes.sizeof(_hip.RopeTensor) == 72
 
 
 def test_validation_errors_without_gpu():

@@ -11,7 +11,7 @@ from sparse_matrix_tuning_amd.smt import smt
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
-SEL_MLP = {("up_proj", 0): [(2, 1), (0, 0)], ("down_proj", 1): [(1, 2)]}
+SEL_MLP = {("up_proj", 0): [(2, 0), (0, 0)], ("down_proj", 1): [(1, 2)]}
 SEL_ATT = {("v_proj", 0): [(0, 1)]}
 
 

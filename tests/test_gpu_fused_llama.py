@@ -1,0 +1,120 @@
+"""Fused LLaMA elementwise kernels vs the eager transformers op chains they replace."""
+import pytest
+import torch
+
+from sparse_matrix_tuning_amd import fused_llama as fl
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def _ulp_close(a, b, max_ulp_frac=1e-3):
+    """bf16 tensors equal except for a small fraction differing by one rounding step."""
+    a, b = a.float(), b.float()
+    diff = (a - b).abs()
+    tol = b.abs() * 2 ** -7 + 1e-30            # one bf16 ulp (8 significant bits) relative
+    bad = (diff > tol).float().mean().item()
+    return bad <= max_ulp_frac, bad
+
+
+def test_rmsnorm_forward_backward_vs_eager():
+    from transformers.models.llama.modeling_llama import LlamaRMSNorm
+    torch.manual_seed(0)
+    H = 4096
+    norm = LlamaRMSNorm(H, eps=1e-5).to(DEV).bfloat16()
+    with torch.no_grad():
+        norm.weight.copy_(torch.randn(H) * 0.2 + 1.0)
+    x = (torch.randn(3, 257, H, device=DEV) * 3).bfloat16()
+    dy = torch.randn(3, 257, H, device=DEV).bfloat16()
+    xe = x.clone().requires_grad_(True)
+    ye = norm(xe)
+    ye.backward(dy)
+    dw_e = norm.weight.grad.clone()
+    norm.weight.grad = None
+    xf = x.clone().requires_grad_(True)
+    yf = fl.FusedRMSNormFn.apply(xf, norm.weight, norm.variance_epsilon)
+    yf.backward(dy)
+    ok, bad = _ulp_close(yf, ye)
+    assert ok, bad
+    rel = ((xf.grad.float() - xe.grad.float()).norm() / xe.grad.float().norm()).item()
+    assert rel < 5e-3, rel
+    relw = ((norm.weight.grad.float() - dw_e.float()).norm() / dw_e.float().norm()).item()
+    assert relw < 5e-3, relw
+
+
+def test_rmsnorm_without_weight_grad_small_hidden():
+    from transformers.models.llama.modeling_llama import LlamaRMSNorm
+    norm = LlamaRMSNorm(512, eps=1e-6).to(DEV).bfloat16()
+    norm.weight.requires_grad_(False)
+    x = torch.randn(64, 512, device=DEV).bfloat16().requires_grad_(True)
+    y = fl.FusedRMSNormFn.apply(x, norm.weight, norm.variance_epsilon)
+    y.sum().backward()
+    x2 = x.detach().clone().requires_grad_(True)
+    norm(x2).sum().backward()
+    assert ((x.grad.float() - x2.grad.float()).norm() / x2.grad.float().norm()).item() < 5e-3
+
+
+def _hf_qk(B=2, S=96, Hq=8, Hk=2, D=128):
+    # q/k as LlamaAttention builds them: proj(...).view(B, S, H, D).transpose(1, 2)
+    q = torch.randn(B, S, Hq * D, device=DEV).bfloat16().view(B, S, Hq, D).transpose(1, 2)
+    k = torch.randn(B, S, Hk * D, device=DEV).bfloat16().view(B, S, Hk, D).transpose(1, 2)
+    pos = torch.arange(S, device=DEV, dtype=torch.float32)
+    inv = 1.0 / (500000.0 ** (torch.arange(0, D, 2, device=DEV, dtype=torch.float32) / D))
+    freqs = torch.outer(pos, inv)
+    emb = torch.cat((freqs, freqs), dim=-1)
+    cos = emb.cos()[None].expand(B, -1, -1).bfloat16().contiguous()
+    sin = emb.sin()[None].expand(B, -1, -1).bfloat16().contiguous()
+    return q, k, cos, sin
+
+
+def test_rope_bit_exact_vs_eager_forward_and_backward():
+    torch.manual_seed(1)
+    q, k, cos, sin = _hf_qk()
+    qe, ke = q.clone().requires_grad_(True), k.clone().requires_grad_(True)
+    oq_e, ok_e = fl.eager_apply_rotary_pos_emb(qe, ke, cos, sin)
+    qf, kf = q.clone().requires_grad_(True), k.clone().requires_grad_(True)
+    oq_f, ok_f = fl.fused_apply_rotary_pos_emb(qf, kf, cos, sin)
+    assert torch.equal(oq_f, oq_e) and torch.equal(ok_f, ok_e)
+    gq, gk = torch.randn_like(oq_e), torch.randn_like(ok_e)
+    (oq_e.float() * gq.float()).sum().add((ok_e.float() * gk.float()).sum()).backward()
+    (oq_f.float() * gq.float()).sum().add((ok_f.float() * gk.float()).sum()).backward()
+    assert torch.equal(qf.grad, qe.grad) and torch.equal(kf.grad, ke.grad)
+
+
+def test_swiglu_vs_eager():
+    torch.manual_seed(2)
+    g = (torch.randn(4, 100, 1536, device=DEV) * 3).bfloat16()
+    u = torch.randn(4, 100, 1536, device=DEV).bfloat16()
+    dh = torch.randn(4, 100, 1536, device=DEV).bfloat16()
+    ge, ue = g.clone().requires_grad_(True), u.clone().requires_grad_(True)
+    he = torch.nn.functional.silu(ge) * ue
+    he.backward(dh)
+    gf, uf = g.clone().requires_grad_(True), u.clone().requires_grad_(True)
+    hf = fl.FusedSwiGLUFn.apply(gf, uf)
+    hf.backward(dh)
+    for a, b in ((hf, he), (gf.grad, ge.grad), (uf.grad, ue.grad)):
+        ok, bad = _ulp_close(a, b)
+        assert ok, bad
+
+
+def test_patched_mini_llama_matches_eager():
+    import bench
+    torch.manual_seed(3)
+    model = bench.build_model("mini", DEV)
+    ids = torch.randint(0, 4096, (2, 256), device=DEV)
+    out_e = model(input_ids=ids, labels=ids, use_cache=False)
+    out_e.loss.backward()
+    ge = {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None}
+    model.zero_grad(set_to_none=True)
+    try:
+        counts = fl.patch_llama(model)
+        assert counts["rmsnorm"] == 9 and counts["mlp"] == 4
+        out_f = model(input_ids=ids, labels=ids, use_cache=False)
+        out_f.loss.backward()
+    finally:
+        fl.unpatch_llama(model)
+    rel = abs(out_f.loss.item() - out_e.loss.item()) / abs(out_e.loss.item())
+    assert rel < 1e-3, (out_f.loss.item(), out_e.loss.item())
+    worst = max(((p.grad.float() - ge[n].float()).norm() / ge[n].float().norm()).item()
+                for n, p in model.named_parameters() if p.grad is not None)
+    assert worst < 5e-2, worst
