@@ -224,8 +224,9 @@ def main():
     if not args.eager_ops:
         from sparse_matrix_tuning_amd.fused_llama import patch_llama
         patch_llama(model)
-    if not args.no_grad_ckpt:
-        model.gradient_checkpointing_enable()
+    # warm-up (full fine-tuning: fp32 master/moments for all 8 B params) always checkpoints;
+    # --no-grad-ckpt turns it off for the SMT phase only (keeps activations in the 288 GB HBM)
+    model.gradient_checkpointing_enable()
     model.train()
     log(f"model built in {time.time() - t_setup:.1f}s, params {sum(p.numel() for p in model.parameters()) / 1e9:.3f} B")
     vocab = MODELS[args.model]["vocab_size"]
@@ -275,6 +276,8 @@ def main():
         f"({100.0 * trainable / total_params:.3f}% of {total_params})")
 
     # ---- SMT phase ----
+    if args.no_grad_ckpt:
+        engine.module.gradient_checkpointing_disable()
     smt_batches = batches(args.warmup + args.steps, B, S, vocab, rank, device)
     torch.cuda.reset_peak_memory_stats(device)
 

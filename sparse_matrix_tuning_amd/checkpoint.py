@@ -123,6 +123,8 @@ def load_optimizer_state(engine, load_dir: str) -> dict:
                 raise ValueError(f"{key}/{gi}: {src.numel()} elements, engine has {dst.numel()}")
             dst.copy_(src.to(dst.device))
         tg.step = int(g["step"])
+        for k, v in g["hyper"].items():       # current lr (set by the scheduler), betas, eps, decay
+            tg.group[k] = tuple(v) if isinstance(v, list) else v
     engine.global_steps = int(meta["global_steps"])
     engine.micro_steps = int(meta["micro_steps"])
     if engine.lr_scheduler is not None and meta.get("lr_scheduler") is not None:
