@@ -70,6 +70,7 @@ def parse():
                     help="keep transformers' eager RMSNorm/RoPE/SwiGLU instead of the fused HIP kernels")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0, help="0 disables the CPU leg")
     ap.add_argument("--out", default=None, help="also write the JSON line here")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm) or gloo (functional tests)")
     args = ap.parse_args()
     default_ratio = 0.00356 if args.model == "llama3-8b" else 0.03
     args.att_ratio = default_ratio if args.att_ratio is None else args.att_ratio
@@ -206,10 +207,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    # one process per GPU; more ranks than GPUs (functional multi-rank runs on a 1-GPU box with gloo)
+    # share devices round-robin
+    dev_index = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev_index)
+    device = torch.device("cuda", dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(args.dist_backend)
 
     from sparse_matrix_tuning_amd import _hip
     _hip.load(build_if_missing=True)
