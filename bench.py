@@ -18,7 +18,7 @@ One process per GPU (RCCL over xGMI for N > 1, weak scaling: B=16 x S=2048 per G
    bracketed by barrier + synchronize; the max over ranks is reported.
 
 Rank 0 prints ONE JSON line. ``roofline`` is for the dominant hand-written kernel (the grouped
-tile-wgrad, smt_tile_wgrad = wgrad_partial + wgrad_reduce), timed with HIP events on its launch
+tile-wgrad, smt_tile_wgrad = wgrad_dma + wgrad_reduce), timed with HIP events on its launch
 stream over the timed region. ``cpu_baseline`` times the oracle's restatement of the reference path
 (oracle/smt_oracle.py) on this host's cores.
 """
@@ -155,7 +155,7 @@ def pmc_traffic(args):
         return None, None
     with open(path) as f:
         d = json.load(f)
-    return round(d["hbm_bytes_per_launch"]), f"profiles/r01_wgrad_pmc.json ({d['correction']})"
+    return round(d.get("hbm_bytes_per_call", d.get("hbm_bytes_per_launch"))), f"profiles/r01_wgrad_pmc.json ({d['correction']})"
 
 
 def cpu_baseline(seconds: float, selection_tiles: dict, model_name: str):
@@ -326,7 +326,7 @@ def main():
             traffic, tsrc = pmc_traffic(args)
             roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                         "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
-                        "kernel": "smt_tile_wgrad (wgrad_partial_kernel + wgrad_reduce_kernel)",
+                        "kernel": "smt_tile_wgrad (wgrad_dma_kernel + wgrad_reduce_kernel)",
                         "launches": w["launches"], "avg_launch_us": round(w["seconds"] / w["launches"] * 1e6, 2),
                         "algorithmic_bytes_per_launch": round(w["bytes"] / w["launches"]),
                         "mfma_tflops": round(w["flops"] / w["seconds"] / 1e12, 1)}

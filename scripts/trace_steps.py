@@ -9,7 +9,7 @@ import sys
 
 def cat(name):
     n = name
-    if "wgrad_partial" in n or "wgrad_reduce" in n:
+    if "wgrad_" in n:
         return "smt_wgrad"
     if "adamw" in n or "sq_norm" in n or "tile_copy" in n:
         return "smt_optimizer"

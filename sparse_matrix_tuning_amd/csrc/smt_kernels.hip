@@ -16,6 +16,7 @@
 #include <stdint.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -100,6 +101,56 @@ __device__ __forceinline__ bf16x8_t tr_frag(const uint8_t* img, uint32_t k, uint
 
 // Epilogue modes: partial slab (S > 1), or the final tile written directly (S == 1).
 enum WgradOut { kOutSlab = 0, kOutF32 = 1, kOutBF16 = 2 };
+
+// Epilogue: C/D map of 32x32x16 (col = lane&31, row = (i&3) + 8*(i>>2) + 4*(lane>>5)) to the fp32
+// partial slab of (tile, s), or straight to the fp32 / bf16 output tile when S == 1.
+template <int OUT>
+__device__ __forceinline__ void wgrad_store(f32x16_t (&acc)[4][2], void* __restrict__ out_ptr, int tile, int s, int S,
+                                            int wm, int wn, int lane, int accumulate) {
+    const int col = lane & 31;
+    const int h = lane >> 5;
+    if (OUT == kOutSlab) {
+        float* out = static_cast<float*>(out_ptr) + (int64_t)(tile * S + s) * kTileElems;
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int m = wm * 128 + mb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                    const int n = wn * 64 + nb * 32 + col;
+                    out[m * kTile + n] = acc[mb][nb][i];
+                }
+    } else if (OUT == kOutF32) {
+        float* out = static_cast<float*>(out_ptr) + (int64_t)tile * kTileElems;
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int m = wm * 128 + mb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                    const int n = wn * 64 + nb * 32 + col;
+                    float v = acc[mb][nb][i];
+                    if (accumulate) v += out[m * kTile + n];
+                    out[m * kTile + n] = v;
+                }
+    } else {
+        uint16_t* out = static_cast<uint16_t*>(out_ptr) + (int64_t)tile * kTileElems;
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int m = wm * 128 + mb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                    const int n = wn * 64 + nb * 32 + col;
+                    float v = acc[mb][nb][i];
+                    if (accumulate) v += bf16_bits_to_f32(out[m * kTile + n]);
+                    out[m * kTile + n] = f32_to_bf16_bits(v);
+                }
+    }
+}
 
 template <int OUT>
 __global__ __launch_bounds__(kWgThreads, 2)
@@ -225,50 +276,154 @@ void wgrad_partial_kernel(const uint16_t* __restrict__ g, int64_t ldg,
         __syncthreads();
     }
 
-    // C/D map of 32x32x16: col = lane&31, row = (i&3) + 8*(i>>2) + 4*(lane>>5)
-    const int col = lane & 31;
-    const int h = lane >> 5;
-    if (OUT == kOutSlab) {
-        float* out = static_cast<float*>(out_ptr) + (int64_t)(tile * S + s) * kTileElems;
+    wgrad_store<OUT>(acc, out_ptr, tile, s, S, wm, wn, lane, accumulate);
+}
+
+// ------------------------------------------------------------------------------------------------
+// LDS-DMA variant of the same tile GEMM (default). Operands go HBM -> LDS with
+// buffer_load_dwordx4 ... lds (no VGPR staging), 32-row stages in a 4-slot LDS ring with TWO stages
+// in flight while one is computed (counted s_waitcnt vmcnt + raw s_barrier: cdna_hip_programming
+// §5 "Pipelining across barriers"). The register-staged kernel above keeps only one 64 KiB stage in
+// flight per CU, which measured as latency-bound at ~25 GB/s per CU.
+// The LDS image stays lane-linear per DMA instruction (1 KiB = two 512-B rows); the XOR swizzle of
+// the image is applied to each lane's SOURCE address instead (rule 21), so the transposed reads are
+// unchanged. Rows past the chunk end read as zeros through the buffer descriptor's range check.
+// ------------------------------------------------------------------------------------------------
+constexpr int kDmaBK = 32;                                 // rows per stage
+constexpr int kDmaImg = kDmaBK * kRowBytes;                // 16 KiB per operand per stage
+constexpr int kDmaSlots = 4;                               // ring slots (2 in flight + 1 computing + 1 WAR margin)
+constexpr int kDmaSlotBytes = 2 * kDmaImg;                 // A + B
+
+typedef __attribute__((address_space(3))) uint8_t lds_u8_t;
+
+// One 1 KiB LDS-DMA: lane l's 16 B from rsrc+voff land at LDS byte lds_base + 16*l. Inline asm on
+// purpose: hipcc then does not see an LDS write it cannot disambiguate from the ring slot being read
+// (with the builtin it puts s_waitcnt vmcnt(0) before every ds_read, draining the 2-deep pipeline);
+// completion is tracked by the hand-counted vmcnt in the loop. M0 is saved / restored inside the
+// statement (cdna_hip_programming §5.7).
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, uint32_t lds_base, int voff) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+                 "buffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(lds_base) : "memory");
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const uint8_t* p) {
+    return (uint32_t)(uintptr_t)(const lds_u8_t*)p;
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base, int64_t bytes) {
+    // every descriptor input made provably wave-uniform (T20): no waterfall loops
+    const uint64_t a = (uint64_t)(uintptr_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    const int n = __builtin_amdgcn_readfirstlane((int)bytes);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
+}
+
+template <int OUT>
+__global__ __launch_bounds__(kWgThreads, 2)
+void wgrad_dma_kernel(const uint16_t* __restrict__ g, int64_t ldg,
+                      const uint16_t* __restrict__ x, int64_t ldx,
+                      int64_t T, int64_t chunk, int S, int n_tiles,
+                      const int32_t* __restrict__ tile_rc, const int32_t* __restrict__ order,
+                      void* __restrict__ out_ptr, int accumulate) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kDmaSlots * kDmaSlotBytes];   // 128 KiB, one array
+
+    const int total = n_tiles * S;
+    const int b = blockIdx.x;
+    const int q8 = total >> 3, r8 = total & 7, xcd = b & 7;
+    const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+    const int s = L / n_tiles;
+    const int li = L - s * n_tiles;
+    const int tile = order != nullptr ? order[li] : li;
+    const int r = tile_rc[2 * tile];
+    const int c = tile_rc[2 * tile + 1];
+    const int64_t t_begin = (int64_t)s * chunk;
+    const int64_t t_end = (t_begin + chunk < T) ? (t_begin + chunk) : T;
+    const int rows = (t_end > t_begin) ? (int)(t_end - t_begin) : 0;
+    const int nst = (rows + kDmaBK - 1) / kDmaBK;
+
+    // descriptors over this chunk's rows of the two column slices (host guarantees rows*ld*2 < 2^31)
+    const __amdgpu_buffer_rsrc_t rg = uniform_rsrc(g + t_begin * ldg + (int64_t)r * kTile, (int64_t)rows * ldg * 2);
+    const __amdgpu_buffer_rsrc_t rx = uniform_rsrc(x + t_begin * ldx + (int64_t)c * kTile, (int64_t)rows * ldx * 2);
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2;
+    const int wn = wave & 3;
+
+    // DMA geometry: wave w fills image rows 4w .. 4w+3 of each operand (two 1 KiB instructions);
+    // lane l of instruction j lands at image row k = 4w + 2j + (l>>5), physical byte 16*(l&31),
+    // which holds logical byte (16*(l&31)) ^ ((k&3) << 6) of that row.
+    int voff_g[2], voff_x[2];
 #pragma unroll
-        for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const int m = wm * 128 + mb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-                    const int n = wn * 64 + nb * 32 + col;
-                    out[m * kTile + n] = acc[mb][nb][i];
-                }
-    } else if (OUT == kOutF32) {
-        float* out = static_cast<float*>(out_ptr) + (int64_t)tile * kTileElems;
-#pragma unroll
-        for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const int m = wm * 128 + mb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-                    const int n = wn * 64 + nb * 32 + col;
-                    float v = acc[mb][nb][i];
-                    if (accumulate) v += out[m * kTile + n];
-                    out[m * kTile + n] = v;
-                }
-    } else {
-        uint16_t* out = static_cast<uint16_t*>(out_ptr) + (int64_t)tile * kTileElems;
-#pragma unroll
-        for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const int m = wm * 128 + mb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-                    const int n = wn * 64 + nb * 32 + col;
-                    float v = acc[mb][nb][i];
-                    if (accumulate) v += bf16_bits_to_f32(out[m * kTile + n]);
-                    out[m * kTile + n] = f32_to_bf16_bits(v);
-                }
+    for (int j = 0; j < 2; ++j) {
+        const int k = 4 * wave + 2 * j + (lane >> 5);
+        const int lb = (16 * (lane & 31)) ^ ((k & 3) << 6);
+        voff_g[j] = (int)(k * ldg * 2) + lb;
+        voff_x[j] = (int)(k * ldx * 2) + lb;
     }
+    const int step_g = (int)(kDmaBK * ldg * 2), step_x = (int)(kDmaBK * ldx * 2);
+
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(lds));
+    auto issue = [&](int st) {
+        const uint32_t slot = lds0 + (uint32_t)((st % kDmaSlots) * kDmaSlotBytes);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const uint32_t row0 = (uint32_t)(4 * wave + 2 * j) * kRowBytes;
+            dma16(rg, __builtin_amdgcn_readfirstlane(slot + row0), voff_g[j] + st * step_g);
+            dma16(rx, __builtin_amdgcn_readfirstlane(slot + kDmaImg + row0), voff_x[j] + st * step_x);
+        }
+    };
+
+    f32x16_t acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    const int gi = lane >> 4;
+    const int q = (lane >> 2) & 3;
+    const int p = lane & 3;
+    const uint32_t feat_byte = 2u * (16u * (gi & 1) + 4u * p);
+    const uint32_t krow = 8u * (gi >> 1) + q;
+
+    if (nst > 0) issue(0);
+    if (nst > 1) issue(1);
+    for (int st = 0; st < nst; ++st) {
+        if (st + 2 < nst) {
+            issue(st + 2);
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");     // stage st landed (st+1, st+2 in flight)
+        } else if (st + 1 < nst) {
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();                              // every wave's DMA for stage st landed
+        __builtin_amdgcn_sched_barrier(0);
+        const uint8_t* A = lds + (st % kDmaSlots) * kDmaSlotBytes;
+        const uint8_t* B = A + kDmaImg;
+#pragma unroll
+        for (int ks = 0; ks < kDmaBK / 16; ++ks) {
+            bf16x8_t af[4], bfr[2];
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb)
+                af[mb] = tr_frag(A, ks * 16 + krow, 2u * (wm * 128 + mb * 32) + feat_byte);
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb)
+                bfr[nb] = tr_frag(B, ks * 16 + krow, 2u * (wn * 64 + nb * 32) + feat_byte);
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb)
+                    acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mb], bfr[nb], acc[mb][nb], 0, 0, 0);
+        }
+    }
+    wgrad_store<OUT>(acc, out_ptr, tile, s, S, wm, wn, lane, accumulate);
 }
 
 // Sum the S partial slabs of each tile in order s = 0..S-1 (deterministic) and write the tile.
@@ -695,13 +850,23 @@ int smt_tile_wgrad(const void* grad_out, int64_t ld_grad_out, const void* x, int
     const uint16_t* gp = static_cast<const uint16_t*>(grad_out);
     const uint16_t* xp = static_cast<const uint16_t*>(x);
     const dim3 grid(n_tiles * sp.S), block(kWgThreads);
+    // LDS-DMA kernel by default; its 32-bit buffer offsets need chunk * ld * 2 < 2^31, otherwise (and
+    // with SMT_WGRAD_IMPL=reg) the register-staged kernel, which addresses with 64 bits.
+    const int64_t max_ld = ld_grad_out > ld_x ? ld_grad_out : ld_x;
+    static const bool force_reg = [] { const char* e = getenv("SMT_WGRAD_IMPL"); return e && strcmp(e, "reg") == 0; }();
+    const bool dma = !force_reg && sp.chunk * max_ld * 2 < (int64_t)0x7fffffff;
     if (sp.S == 1) {
-        if (out_dtype == SMT_DTYPE_FP32)
-            hipLaunchKernelGGL(wgrad_partial_kernel<kOutF32>, grid, block, 0, stream, gp, ld_grad_out, xp, ld_x,
-                               T, sp.chunk, 1, n_tiles, tile_rc_dev, order_dev, grad_tiles, accumulate);
-        else
-            hipLaunchKernelGGL(wgrad_partial_kernel<kOutBF16>, grid, block, 0, stream, gp, ld_grad_out, xp, ld_x,
-                               T, sp.chunk, 1, n_tiles, tile_rc_dev, order_dev, grad_tiles, accumulate);
+        if (out_dtype == SMT_DTYPE_FP32) {
+            if (dma) hipLaunchKernelGGL(wgrad_dma_kernel<kOutF32>, grid, block, 0, stream, gp, ld_grad_out, xp, ld_x,
+                                        T, sp.chunk, 1, n_tiles, tile_rc_dev, order_dev, grad_tiles, accumulate);
+            else hipLaunchKernelGGL(wgrad_partial_kernel<kOutF32>, grid, block, 0, stream, gp, ld_grad_out, xp, ld_x,
+                                    T, sp.chunk, 1, n_tiles, tile_rc_dev, order_dev, grad_tiles, accumulate);
+        } else {
+            if (dma) hipLaunchKernelGGL(wgrad_dma_kernel<kOutBF16>, grid, block, 0, stream, gp, ld_grad_out, xp, ld_x,
+                                        T, sp.chunk, 1, n_tiles, tile_rc_dev, order_dev, grad_tiles, accumulate);
+            else hipLaunchKernelGGL(wgrad_partial_kernel<kOutBF16>, grid, block, 0, stream, gp, ld_grad_out, xp, ld_x,
+                                    T, sp.chunk, 1, n_tiles, tile_rc_dev, order_dev, grad_tiles, accumulate);
+        }
         return check_launch("wgrad_partial_kernel");
     }
     const size_t need = (size_t)n_tiles * sp.S * kTileElems * sizeof(float);
@@ -709,8 +874,12 @@ int smt_tile_wgrad(const void* grad_out, int64_t ld_grad_out, const void* x, int
         return fail(SMT_E_WORKSPACE, "smt_tile_wgrad: workspace %zu < %zu bytes", workspace_bytes, need);
     if (!aligned16(workspace)) return fail(SMT_E_ALIGN, "smt_tile_wgrad: workspace not 16-byte aligned");
     float* slab = static_cast<float*>(workspace);
-    hipLaunchKernelGGL(wgrad_partial_kernel<kOutSlab>, grid, block, 0, stream, gp, ld_grad_out, xp, ld_x,
-                       T, sp.chunk, sp.S, n_tiles, tile_rc_dev, order_dev, slab, 0);
+    if (dma)
+        hipLaunchKernelGGL(wgrad_dma_kernel<kOutSlab>, grid, block, 0, stream, gp, ld_grad_out, xp, ld_x,
+                           T, sp.chunk, sp.S, n_tiles, tile_rc_dev, order_dev, slab, 0);
+    else
+        hipLaunchKernelGGL(wgrad_partial_kernel<kOutSlab>, grid, block, 0, stream, gp, ld_grad_out, xp, ld_x,
+                           T, sp.chunk, sp.S, n_tiles, tile_rc_dev, order_dev, slab, 0);
     int rc = check_launch("wgrad_partial_kernel");
     if (rc) return rc;
     if (out_dtype == SMT_DTYPE_FP32)
