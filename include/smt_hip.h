@@ -19,6 +19,13 @@
  *   smt_adamw_step        DeepSpeed FusedAdam(adam_w_mode=True) step over the tiles
  *                         (deepspeed/fine_tune.py:352,361-363,773; DeepSpeed 0.16.5, external),
  *                         fused with clip, bf16 cast and the tile -> W scatter
+ *   Channel path (activation-selected rows; SURVEY §8(f) row 1, ABI v3):
+ *   smt_row_gather        deepspeed/smt/smt.py:200-204   selected_weight[i, :] = W[index_list[i], :]
+ *   smt_row_scatter       deepspeed/smt/smt.py:211-213   per-forward write-back rows -> W
+ *   smt_column_gather     deepspeed/smt/smt.py:225-233   partial_input[:, :, i] = input[:, :, index_list[i]]
+ *   smt_act_accumulate    deepspeed/fine_tune.py:636-667 (cache_input_hook: |x| summed over steps)
+ *                         + deepspeed/smt/smt_helper.py:170 (sum over the batch dimension)
+ *   smt_channel_score     deepspeed/smt/smt_helper.py:171-184   per-channel statistic over the sequence
  */
 #ifndef SMT_HIP_H
 #define SMT_HIP_H
@@ -148,6 +155,39 @@ int smt_adamw_step(const void* grad, float* master, float* exp_avg, float* exp_a
                    void* param_bf16, const smt_tile_desc* tiles_dev, int32_t n_tiles,
                    int64_t n_elems, const double* grad_sq_norm_dev,
                    const smt_adamw_args* args, hipStream_t stream);
+
+/* ---- channel path (ABI v3) ------------------------------------------------------------------- */
+
+/* rows[i, 0:n_cols] = W[rows_dev[i], 0:n_cols]; elem_bytes 2 or 4; rows 16-byte aligned. */
+int smt_row_gather(const void* weight, int64_t ld_weight, int32_t elem_bytes, int64_t n_cols,
+                   const int32_t* rows_dev, int32_t n_rows, void* rows, int64_t ld_rows, hipStream_t stream);
+
+/* W[rows_dev[i], 0:n_cols] = rows[i, 0:n_cols]; rows_dev must not repeat an index. */
+int smt_row_scatter(void* weight, int64_t ld_weight, int32_t elem_bytes, int64_t n_cols,
+                    const int32_t* rows_dev, int32_t n_rows, const void* rows, int64_t ld_rows, hipStream_t stream);
+
+/*
+ * out[t, j] = x[t, cols_dev[j]] for j < n_cols and 0 for n_cols <= j < ld_out (bf16/fp16 bits,
+ * 2-byte elements); x [T, ld_x], out [T, ld_out] row-major, ld_out % 8 == 0.
+ */
+int smt_column_gather(const void* x, int64_t ld_x, int64_t T, const int32_t* cols_dev, int32_t n_cols,
+                      void* out, int64_t ld_out, hipStream_t stream);
+
+/*
+ * acc[s, c] = (assign ? 0 : acc[s, c]) + sum_{b<B} |x[b, s, c]|, in fp64 with b ascending.
+ * x: element (b, s, c) at x + b*batch_stride + s*ld_x + c (dtype x_dtype); acc: fp64 [S, n_cols]
+ * row-major; n_cols % 8 == 0.
+ */
+int smt_act_accumulate(const void* x, int32_t x_dtype, int64_t ld_x, int64_t batch_stride, int32_t B, int32_t S,
+                       int32_t n_cols, double* acc, int32_t assign, hipStream_t stream);
+
+/*
+ * out[c] = sum_{s<S} acc[s, c] (strategy MEAN_ABS, ABS_MEAN, L1) or sum_{s<S} acc[s, c]^2 (L2),
+ * fp64, s ascending, unfused multiply-add. The caller divides by S (means) or takes the square root
+ * (L2) and rounds to fp32 once.
+ */
+int smt_channel_score(const double* acc, int32_t S, int32_t n_cols, int32_t strategy, double* out,
+                      hipStream_t stream);
 
 #ifdef __cplusplus
 }

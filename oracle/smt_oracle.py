@@ -158,6 +158,8 @@ def select_channel(activation: Dict[Hashable, torch.Tensor], n=660, selection_st
         elif calculate_strategy == 'L2':
             column_means[key] = torch.norm(act, p=2, dim=0)
     if selection_strategy == "norm_dist":
+        if not column_means:
+            raise UnboundLocalError("indices")          # `del indices` with nothing bound (smt_helper.py:194)
         return {key: torch.argsort(cm, descending=True, stable=True)[:n].tolist() for key, cm in column_means.items()}
     top_columns = []
     for key, column_mean in column_means.items():
@@ -168,10 +170,101 @@ def select_channel(activation: Dict[Hashable, torch.Tensor], n=660, selection_st
             else:
                 heapq.heappushpop(top_columns, (value, (key, idx)))
     top_columns.sort(reverse=True)
+    if not top_columns:
+        raise UnboundLocalError("value")                # `del value` with nothing bound (smt_helper.py:226)
     ranked = defaultdict(list)
     for _value, (key, idx) in top_columns:
         ranked[key].append(idx)
     return ranked
+
+
+def channel_hook_accumulate(feat: dict, key, x: torch.Tensor) -> None:
+    """fine_tune.py:636-667 cache_input_hook at world size 1: ``|x|`` -> fp32 CPU -> first step
+    assigns, later steps ``+=`` (the all-reduce over ranks is the identity there)."""
+    a = x.abs().detach().cpu().to(torch.float32)
+    if key not in feat:
+        feat[key] = a
+    else:
+        feat[key] += a
+
+
+def channel_acc_fp64(steps: Sequence[torch.Tensor]) -> torch.Tensor:
+    """The build's exact-arithmetic definition of the harvested statistic before scoring:
+    ``acc[s, c] = sum over steps (in order) of sum over b (ascending) of |x[b, s, c]|`` in fp64.
+    Written with the same operation order as ``smt_act_accumulate`` so the two agree bit for bit."""
+    acc = None
+    for x in steps:
+        xs = x.detach().cpu().to(torch.float64).abs()
+        part = torch.zeros(xs.shape[1], xs.shape[2], dtype=torch.float64)
+        for b in range(xs.shape[0]):
+            part = part + xs[b]
+        acc = part if acc is None else acc + part
+    return acc
+
+
+def channel_stat_fp64(acc: torch.Tensor, strategy: str) -> torch.Tensor:
+    """smt_helper.py:171-184 on an fp64 ``[S, C]`` accumulator: the sequence reduction in fp64
+    (s ascending, as ``smt_channel_score``), one division / sqrt, one rounding to fp32."""
+    tot = torch.zeros(acc.shape[1], dtype=torch.float64)
+    for s in range(acc.shape[0]):
+        v = acc[s]
+        tot = tot + (v * v if strategy == 'L2' else v)
+    if strategy in ('mean_abs', 'abs_mean'):
+        return (tot / acc.shape[0]).abs().to(torch.float32)
+    if strategy == 'L1':
+        return tot.to(torch.float32)
+    if strategy == 'L2':
+        return tot.sqrt().to(torch.float32)
+    raise ValueError(strategy)
+
+
+def rank_channels(column_means: Dict[Hashable, torch.Tensor], n: int, selection_strategy="no_restriction"):
+    """smt_helper.py:186-230 (the heap / argsort half of select_channel) on given fp32 statistics."""
+    if selection_strategy == "norm_dist":
+        return {key: torch.argsort(cm, descending=True, stable=True)[:n].tolist() for key, cm in column_means.items()}
+    top = []
+    for key, cm in column_means.items():
+        for idx in range(cm.shape[0]):
+            value = cm[idx].item()
+            if len(top) < n:
+                heapq.heappush(top, (value, (key, idx)))
+            else:
+                heapq.heappushpop(top, (value, (key, idx)))
+    top.sort(reverse=True)
+    ranked = defaultdict(list)
+    for _value, (key, idx) in top:
+        ranked[key].append(idx)
+    return ranked
+
+
+def gather_rows(weight: torch.Tensor, index_list: Sequence[int]) -> torch.Tensor:
+    """smt.py:196-204."""
+    out = torch.empty(len(index_list), weight.shape[1], dtype=weight.dtype)
+    for i, index in enumerate(index_list):
+        out[i, :] = weight[index, :]
+    return out
+
+
+def linearchannel_forward(x: torch.Tensor, weight: torch.Tensor, index_list: Sequence[int]):
+    """smt.py:221-253: ``(output, partial_input)``."""
+    partial = torch.empty(x.shape[0], x.shape[1], len(index_list), dtype=x.dtype)
+    for i, index in enumerate(index_list):
+        partial[:, :, i] = x[:, :, index]
+    return torch.matmul(x, weight.t()), partial
+
+
+def linearchannel_backward(grad_output: torch.Tensor, partial: torch.Tensor, weight: torch.Tensor):
+    """smt.py:256-296: ``grad_weight = sum_b partial[b]^T g[b]`` ([k, out], per-sample products in
+    the input dtype), ``grad_input = g @ W``."""
+    grad_weight = torch.sum(torch.matmul(partial.permute(0, 2, 1), grad_output), dim=0)
+    return torch.matmul(grad_output, weight), grad_weight
+
+
+def channel_grads_fp64(grad_output: torch.Tensor, x: torch.Tensor, index_list: Sequence[int]) -> torch.Tensor:
+    """Exact-arithmetic truth of linearChannel's grad_weight from the same (rounded) inputs."""
+    g = grad_output.reshape(-1, grad_output.shape[-1]).double()
+    xx = x.reshape(-1, x.shape[-1]).double()[:, list(index_list)]
+    return xx.t() @ g
 
 
 # ------------------------------------------------------------------------------------------------
@@ -286,4 +379,60 @@ def ref_convert(model, selected_mlp, selected_att):
             mod = ('q_proj' if 'q_proj' in name else 'k_proj' if 'k_proj' in name else
                    'v_proj' if 'v_proj' in name else 'o_proj' if 'o_proj' in name else None)
             setattr(parent, parts[-1], RefLinearLayer_MatrixSparsity(module.weight, selected_att[(mod, layer)]))
+    return model
+
+
+class RefLinearChannel(torch.autograd.Function):
+    """smt.py:217-296."""
+
+    @staticmethod
+    def forward(ctx, input, selected_weight, channel_index_list, weight):
+        out, partial = linearchannel_forward(input, weight, list(channel_index_list))
+        ctx.save_for_backward(partial, weight)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        partial, weight = ctx.saved_tensors
+        grad_input, grad_weight = linearchannel_backward(grad_output, partial, weight)
+        return grad_input, grad_weight, None, None
+
+
+class RefLinearLayer_ChannelSparsity(torch.nn.Module):
+    """smt.py:185-214 (CPU)."""
+
+    def __init__(self, weight, index_list):
+        super().__init__()
+        self.weight = weight
+        self.weight.requires_grad = False
+        self.index_list = list(index_list)
+        self.selected_weight = torch.nn.Parameter(gather_rows(weight.data, self.index_list))
+
+    def forward(self, x):
+        for i, index in enumerate(self.index_list):
+            self.weight.data[index, :] = self.selected_weight.data[i, :]
+        return RefLinearChannel.apply(x, self.selected_weight, self.index_list, self.weight)
+
+
+def ref_convert_channel(model, selected_channel, selected_channel_attention):
+    """smt.py:25-80 with the restated channel module."""
+    names = [n for n, m in model.named_modules() if isinstance(m, torch.nn.Linear) and '.layers' in n]
+    for name in names:
+        parent = model
+        parts = name.split('.')
+        for p in parts[:-1]:
+            parent = getattr(parent, p)
+        module = getattr(parent, parts[-1])
+        if not module.weight.requires_grad:
+            continue
+        match = _LAYER.search(name)
+        layer = int(match.group(1)) if match else None
+        if "mlp" in name:
+            mod = 'gate_proj' if 'gate_proj' in name else 'up_proj' if 'up_proj' in name else 'down_proj'
+            setattr(parent, parts[-1], RefLinearLayer_ChannelSparsity(module.weight, selected_channel[(mod, layer)]))
+        elif "self_attn" in name:
+            mod = ('q_proj' if 'q_proj' in name else 'k_proj' if 'k_proj' in name else
+                   'v_proj' if 'v_proj' in name else 'o_proj' if 'o_proj' in name else None)
+            setattr(parent, parts[-1], RefLinearLayer_ChannelSparsity(module.weight,
+                                                                      selected_channel_attention[(mod, layer)]))
     return model

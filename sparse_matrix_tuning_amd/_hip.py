@@ -31,6 +31,7 @@ ABI_FUNCTIONS = (
     "smt_last_error", "smt_abi_version", "smt_wgrad_workspace_bytes", "smt_tile_wgrad",
     "smt_tile_gather", "smt_tile_scatter", "smt_grad_accumulate", "smt_block_score",
     "smt_sq_norm", "smt_adamw_step",
+    "smt_row_gather", "smt_row_scatter", "smt_column_gather", "smt_act_accumulate", "smt_channel_score",
     "smt_model_ops_last_error", "smt_rmsnorm_fwd", "smt_rmsnorm_bwd_waves", "smt_rmsnorm_bwd",
     "smt_rope_fwd", "smt_rope_bwd", "smt_swiglu_fwd", "smt_swiglu_bwd",
 )
@@ -84,6 +85,11 @@ _SIGS = {
     "smt_block_score": (ctypes.c_int, [_P, _I32, _I64, _P]),
     "smt_sq_norm": (ctypes.c_int, [_P, _I64, _P, _I32, _P, _P]),
     "smt_adamw_step": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I32, _I64, _P, ctypes.POINTER(AdamWArgs), _P]),
+    "smt_row_gather": (ctypes.c_int, [_P, _I64, _I32, _I64, _P, _I32, _P, _I64, _P]),
+    "smt_row_scatter": (ctypes.c_int, [_P, _I64, _I32, _I64, _P, _I32, _P, _I64, _P]),
+    "smt_column_gather": (ctypes.c_int, [_P, _I64, _I64, _P, _I32, _P, _I64, _P]),
+    "smt_act_accumulate": (ctypes.c_int, [_P, _I32, _I64, _I64, _I32, _I32, _I32, _P, _I32, _P]),
+    "smt_channel_score": (ctypes.c_int, [_P, _I32, _I32, _I32, _P, _P]),
     "smt_model_ops_last_error": (ctypes.c_char_p, []),
     "smt_rmsnorm_fwd": (ctypes.c_int, [_P, _I64, _P, _P, _I64, _P, _I64, _I32, ctypes.c_float, _P]),
     "smt_rmsnorm_bwd_waves": (ctypes.c_int, [_I64]),
@@ -330,3 +336,69 @@ def tile_descs(entries: Sequence[tuple], device: torch.device) -> torch.Tensor:
         else:
             descs.append(TileDesc(None, 0, int(r), int(c), int(off)))
     return _device_table(descs, TileDesc, device)
+
+
+# ---------------------------------------------------------------------------------------------
+# channel path (ABI v3)
+# ---------------------------------------------------------------------------------------------
+def index_table(indices: Sequence[int], device: torch.device) -> torch.Tensor:
+    """Device int32 [n] table of row / column indices."""
+    return torch.tensor([int(i) for i in indices], dtype=torch.int32).to(device)
+
+
+def _row_copy(fn: str, weight: torch.Tensor, rows_dev: torch.Tensor, rows: torch.Tensor) -> None:
+    dev = _require_device(weight, rows_dev, rows)
+    if weight.dim() != 2 or rows.dim() != 2 or weight.stride(1) != 1 or rows.stride(1) != 1:
+        raise ValueError(f"{fn}: weight and rows must be 2-D row-major")
+    if rows.dtype != weight.dtype or rows.shape[1] != weight.shape[1] or rows.shape[0] != rows_dev.numel():
+        raise ValueError(f"{fn}: rows must be [{rows_dev.numel()}, {weight.shape[1]}] of {weight.dtype}")
+    rc = getattr(load(), fn)(_ptr(weight), weight.stride(0), weight.element_size(), weight.shape[1], _ptr(rows_dev),
+                             rows_dev.numel(), _ptr(rows), rows.stride(0), _stream(dev))
+    _check(rc, fn)
+
+
+def row_gather(weight: torch.Tensor, rows_dev: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """out[i, :] = weight[rows[i], :] (smt.py:200-204)."""
+    _row_copy("smt_row_gather", weight, rows_dev, out)
+    return out
+
+
+def row_scatter(weight: torch.Tensor, rows_dev: torch.Tensor, rows: torch.Tensor) -> None:
+    """weight[rows[i], :] = rows[i, :] (smt.py:211-213)."""
+    _row_copy("smt_row_scatter", weight, rows_dev, rows)
+
+
+def column_gather(x2d: torch.Tensor, cols_dev: torch.Tensor, n_cols: int, ld_out: int) -> torch.Tensor:
+    """[T, ld_out] with out[:, j] = x2d[:, cols[j]] for j < n_cols and zeros after (smt.py:225-233)."""
+    dev = _require_device(x2d, cols_dev)
+    if x2d.dim() != 2 or x2d.stride(1) != 1 or x2d.element_size() != 2:
+        raise ValueError("column_gather: x must be a 2-D row-major 16-bit tensor")
+    out = torch.empty(x2d.shape[0], ld_out, dtype=x2d.dtype, device=dev)
+    rc = load().smt_column_gather(_ptr(x2d), x2d.stride(0), x2d.shape[0], _ptr(cols_dev), int(n_cols), _ptr(out),
+                                  ld_out, _stream(dev))
+    _check(rc, "smt_column_gather")
+    return out
+
+
+def act_accumulate(x3d: torch.Tensor, acc: torch.Tensor, assign: bool) -> None:
+    """acc[s, c] (+)= sum_b |x3d[b, s, c]| in fp64 (fine_tune.py:636-667, smt_helper.py:170)."""
+    dev = _require_device(x3d, acc)
+    if x3d.dim() != 3 or x3d.stride(2) != 1:
+        raise ValueError("act_accumulate: x must be [B, S, C] with unit channel stride")
+    B, S, C = x3d.shape
+    if acc.dtype != torch.float64 or not acc.is_contiguous() or tuple(acc.shape) != (S, C):
+        raise ValueError(f"act_accumulate: acc must be contiguous fp64 [{S}, {C}]")
+    rc = load().smt_act_accumulate(_ptr(x3d), _DT[x3d.dtype], x3d.stride(1), x3d.stride(0), B, S, C, _ptr(acc),
+                                   int(bool(assign)), _stream(dev))
+    _check(rc, "smt_act_accumulate")
+
+
+def channel_scores(acc: torch.Tensor, strategy: int) -> torch.Tensor:
+    """Raw fp64 per-channel sums over the sequence dim of an fp64 [S, C] accumulator."""
+    dev = _require_device(acc)
+    if acc.dtype != torch.float64 or not acc.is_contiguous() or acc.dim() != 2:
+        raise ValueError("channel_scores: contiguous fp64 [S, C] accumulator expected")
+    out = torch.empty(acc.shape[1], dtype=torch.float64, device=dev)
+    rc = load().smt_channel_score(_ptr(acc), acc.shape[0], acc.shape[1], int(strategy), _ptr(out), _stream(dev))
+    _check(rc, "smt_channel_score")
+    return out

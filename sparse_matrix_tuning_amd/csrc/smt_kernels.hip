@@ -778,6 +778,102 @@ void adamw_flat_kernel(const void* __restrict__ grad, float* __restrict__ master
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Channel path (smt.py:185-296, smt_helper.py:149-230, fine_tune.py:636-667).
+// ------------------------------------------------------------------------------------------------
+// Row gather / scatter of the selected rows (smt.py:200-204 gather, 211-213 per-forward write-back):
+// rows_buf[i, :] <-> W[rows[i], :]. One workgroup per (row, 4 KiB slice), 16 B per thread.
+constexpr int kRowSliceBytes = 4096;
+
+template <bool SCATTER>
+__global__ __launch_bounds__(256)
+void row_copy_kernel(uint8_t* __restrict__ weight, int64_t ld_w_bytes, const int32_t* __restrict__ rows,
+                     uint8_t* __restrict__ buf, int64_t ld_b_bytes, int64_t row_bytes, int32_t slices) {
+    const int64_t i = blockIdx.x / slices;
+    const int64_t off = (int64_t)(blockIdx.x - i * slices) * kRowSliceBytes + threadIdx.x * 16;
+    if (off >= row_bytes) return;
+    const int64_t r = rows[i];
+    uint4* w = reinterpret_cast<uint4*>(weight + r * ld_w_bytes + off);
+    uint4* b = reinterpret_cast<uint4*>(buf + i * ld_b_bytes + off);
+    if (SCATTER) *w = *b;
+    else *b = *w;
+}
+
+// partial_input of linearChannel.forward (smt.py:225-233): out[t, j] = x[t, cols[j]] for j < n_cols,
+// 0 for n_cols <= j < ld_out (zero columns pad the operand to a whole number of 256-blocks for the
+// tile wgrad). Each thread writes 8 consecutive outputs (one 16 B store, coalesced across the wave);
+// the 8 reads are 2 B gathers inside row t, served from L2 (a row is <= 28 KiB).
+__global__ __launch_bounds__(256)
+void column_gather_kernel(const uint16_t* __restrict__ x, int64_t ld_x, int64_t T, const int32_t* __restrict__ cols,
+                          int32_t n_cols, uint16_t* __restrict__ out, int64_t ld_out) {
+    const int64_t vec_per_row = ld_out >> 3;
+    const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t t = v / vec_per_row;
+    if (t >= T) return;
+    const int j0 = (int)(v - t * vec_per_row) * 8;
+    const uint16_t* xr = x + t * ld_x;
+    uint32_t w[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int ja = j0 + 2 * q, jb = ja + 1;
+        const uint32_t lo = ja < n_cols ? xr[cols[ja]] : 0u;
+        const uint32_t hi = jb < n_cols ? xr[cols[jb]] : 0u;
+        w[q] = lo | (hi << 16);
+    }
+    *reinterpret_cast<uint4*>(out + t * ld_out + j0) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// Activation harvest (the forward hook of fine_tune.py:636-667 plus the batch sum of
+// smt_helper.py:170): acc[s, c] (+)= sum_{b < B} |x[b, s, c]| in fp64, b ascending, then added to acc.
+// One thread per (s, 8 columns): B 16-byte loads, 64 B read-modify-write of acc.
+template <int DT>
+__global__ __launch_bounds__(256)
+void act_accumulate_kernel(const void* __restrict__ x, int64_t ld_x, int64_t sb, int32_t B, int32_t S,
+                           int32_t n_cols, double* __restrict__ acc, int32_t assign) {
+    const int64_t groups = n_cols >> 3;
+    const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t s = v / groups;
+    if (s >= S) return;
+    const int64_t c0 = (v - s * groups) * 8;
+    double sum[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) sum[q] = 0.0;
+    for (int b = 0; b < B; ++b) {
+        float e[8];
+        load8<DT>(x, (int64_t)b * sb + s * ld_x + c0, e);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) sum[q] += (double)fabsf(e[q]);
+    }
+    double2* a = reinterpret_cast<double2*>(acc + s * n_cols + c0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        double2 cur = assign ? make_double2(0.0, 0.0) : a[q];
+        cur.x = assign ? sum[2 * q] : cur.x + sum[2 * q];
+        cur.y = assign ? sum[2 * q + 1] : cur.y + sum[2 * q + 1];
+        a[q] = cur;
+    }
+}
+
+// Column statistic of the harvested activations (smt_helper.py:170-184): out[c] = sum_s acc[s, c]
+// (mean_abs / abs_mean / L1) or sum_s acc[s, c]^2 (L2), fp64, s ascending, no contraction (the
+// oracle restates this exact order; the host divides / takes sqrt and rounds to fp32 once).
+#pragma clang fp contract(off)
+__global__ __launch_bounds__(256)
+void channel_score_kernel(const double* __restrict__ acc, int32_t S, int32_t n_cols, int32_t square,
+                          double* __restrict__ out) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= n_cols) return;
+    double tot = 0.0;
+    const double* p = acc + c;
+    if (square) {
+        for (int s = 0; s < S; ++s) { const double v = p[(int64_t)s * n_cols]; tot = tot + v * v; }
+    } else {
+        for (int s = 0; s < S; ++s) tot = tot + p[(int64_t)s * n_cols];
+    }
+    out[c] = tot;
+}
+#pragma clang fp contract(on)
+
 // Split of T over workgroups for one tile set. One 512-thread workgroup fits per CU (128 KiB LDS),
 // so the launch runs in rounds of 256 workgroups; pick S in [1, 64] (chunks >= 512 rows, multiple of
 // the 64-row stage) minimising the modelled time below, ties to the smaller S. E.g. at T = 32768:
@@ -819,7 +915,7 @@ extern "C" {
 
 const char* smt_last_error(void) { return g_err; }
 
-int smt_abi_version(void) { return 2; }
+int smt_abi_version(void) { return 3; }
 
 size_t smt_wgrad_workspace_bytes(int64_t T, int32_t n_tiles) {
     if (T <= 0 || n_tiles <= 0) return 0;
@@ -983,6 +1079,86 @@ int smt_adamw_step(const void* grad, float* master, float* exp_avg, float* exp_a
     else
         hipLaunchKernelGGL(adamw_flat_kernel<SMT_DTYPE_BF16>, dim3((unsigned)blocks), dim3(256), 0, stream, grad, master, exp_avg, exp_avg_sq, p, n_elems, grad_sq_norm_dev, a);
     return check_launch("adamw_flat_kernel");
+}
+
+static int row_copy(bool scatter, void* weight, int64_t ld_weight, int32_t elem_bytes, int64_t n_cols,
+                    const int32_t* rows_dev, int32_t n_rows, void* rows, int64_t ld_rows, hipStream_t stream) {
+    const char* name = scatter ? "smt_row_scatter" : "smt_row_gather";
+    if (n_rows < 0 || n_cols < 0) return fail(SMT_E_INVALID, "%s: negative size", name);
+    if (n_rows == 0 || n_cols == 0) return SMT_OK;
+    if (!weight || !rows_dev || !rows) return fail(SMT_E_INVALID, "%s: null pointer", name);
+    if (elem_bytes != 2 && elem_bytes != 4) return fail(SMT_E_INVALID, "%s: elem_bytes %d", name, elem_bytes);
+    if (ld_weight < n_cols || ld_rows < n_cols) return fail(SMT_E_INVALID, "%s: leading dimension < n_cols", name);
+    const int64_t row_bytes = n_cols * elem_bytes;
+    if (!aligned16(weight) || !aligned16(rows) || ((ld_weight * elem_bytes) & 15) || ((ld_rows * elem_bytes) & 15) ||
+        (row_bytes & 15))
+        return fail(SMT_E_ALIGN, "%s: rows must be 16-byte aligned and a multiple of 16 bytes", name);
+    const int64_t slices = (row_bytes + kRowSliceBytes - 1) / kRowSliceBytes;
+    const int64_t blocks = slices * n_rows;
+    if (blocks > 0x7fffffffLL) return fail(SMT_E_INVALID, "%s: too many rows", name);
+    uint8_t* w = static_cast<uint8_t*>(weight);
+    uint8_t* b = static_cast<uint8_t*>(rows);
+    if (scatter)
+        hipLaunchKernelGGL(row_copy_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, stream, w, ld_weight * elem_bytes,
+                           rows_dev, b, ld_rows * elem_bytes, row_bytes, (int32_t)slices);
+    else
+        hipLaunchKernelGGL(row_copy_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, stream, w, ld_weight * elem_bytes,
+                           rows_dev, b, ld_rows * elem_bytes, row_bytes, (int32_t)slices);
+    return check_launch(name);
+}
+
+int smt_row_gather(const void* weight, int64_t ld_weight, int32_t elem_bytes, int64_t n_cols,
+                   const int32_t* rows_dev, int32_t n_rows, void* rows, int64_t ld_rows, hipStream_t stream) {
+    return row_copy(false, const_cast<void*>(weight), ld_weight, elem_bytes, n_cols, rows_dev, n_rows, rows, ld_rows, stream);
+}
+
+int smt_row_scatter(void* weight, int64_t ld_weight, int32_t elem_bytes, int64_t n_cols,
+                    const int32_t* rows_dev, int32_t n_rows, const void* rows, int64_t ld_rows, hipStream_t stream) {
+    return row_copy(true, weight, ld_weight, elem_bytes, n_cols, rows_dev, n_rows, const_cast<void*>(rows), ld_rows, stream);
+}
+
+int smt_column_gather(const void* x, int64_t ld_x, int64_t T, const int32_t* cols_dev, int32_t n_cols,
+                      void* out, int64_t ld_out, hipStream_t stream) {
+    if (T < 0 || n_cols < 0 || ld_out < n_cols) return fail(SMT_E_INVALID, "smt_column_gather: bad sizes");
+    if (T == 0 || ld_out == 0) return SMT_OK;
+    if (!x || !out || (n_cols > 0 && !cols_dev)) return fail(SMT_E_INVALID, "smt_column_gather: null pointer");
+    if (!aligned16(out) || (ld_out & 7)) return fail(SMT_E_ALIGN, "smt_column_gather: out rows must be 16-byte aligned (ld_out %% 8 == 0)");
+    const int64_t blocks = (T * (ld_out >> 3) + 255) / 256;
+    if (blocks > 0x7fffffffLL) return fail(SMT_E_INVALID, "smt_column_gather: too large");
+    hipLaunchKernelGGL(column_gather_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, static_cast<const uint16_t*>(x),
+                       ld_x, T, cols_dev, n_cols, static_cast<uint16_t*>(out), ld_out);
+    return check_launch("column_gather_kernel");
+}
+
+int smt_act_accumulate(const void* x, int32_t x_dtype, int64_t ld_x, int64_t batch_stride, int32_t B, int32_t S,
+                       int32_t n_cols, double* acc, int32_t assign, hipStream_t stream) {
+    if (B < 0 || S < 0 || n_cols < 0) return fail(SMT_E_INVALID, "smt_act_accumulate: negative size");
+    if (S == 0 || n_cols == 0) return SMT_OK;
+    if (!acc || (B > 0 && !x)) return fail(SMT_E_INVALID, "smt_act_accumulate: null pointer");
+    if (x_dtype != SMT_DTYPE_BF16 && x_dtype != SMT_DTYPE_FP16 && x_dtype != SMT_DTYPE_FP32)
+        return fail(SMT_E_INVALID, "smt_act_accumulate: x_dtype %d", x_dtype);
+    const int64_t vec = x_dtype == SMT_DTYPE_FP32 ? 4 : 8;
+    if ((n_cols & 7) || !aligned16(acc) || (B > 0 && (!aligned16(x) || (ld_x % vec) || (batch_stride % vec))))
+        return fail(SMT_E_ALIGN, "smt_act_accumulate: needs n_cols %% 8 == 0 and 16-byte aligned rows");
+    const int64_t blocks = ((int64_t)S * (n_cols >> 3) + 255) / 256;
+    const dim3 grid((unsigned)blocks), block(256);
+    if (x_dtype == SMT_DTYPE_BF16)
+        hipLaunchKernelGGL(act_accumulate_kernel<SMT_DTYPE_BF16>, grid, block, 0, stream, x, ld_x, batch_stride, B, S, n_cols, acc, assign);
+    else if (x_dtype == SMT_DTYPE_FP16)
+        hipLaunchKernelGGL(act_accumulate_kernel<SMT_DTYPE_FP16>, grid, block, 0, stream, x, ld_x, batch_stride, B, S, n_cols, acc, assign);
+    else
+        hipLaunchKernelGGL(act_accumulate_kernel<SMT_DTYPE_FP32>, grid, block, 0, stream, x, ld_x, batch_stride, B, S, n_cols, acc, assign);
+    return check_launch("act_accumulate_kernel");
+}
+
+int smt_channel_score(const double* acc, int32_t S, int32_t n_cols, int32_t strategy, double* out, hipStream_t stream) {
+    if (S < 0 || n_cols < 0) return fail(SMT_E_INVALID, "smt_channel_score: negative size");
+    if (strategy < SMT_SCORE_MEAN_ABS || strategy > SMT_SCORE_L2) return fail(SMT_E_INVALID, "smt_channel_score: strategy %d", strategy);
+    if (n_cols == 0) return SMT_OK;
+    if (!out || (S > 0 && !acc)) return fail(SMT_E_INVALID, "smt_channel_score: null pointer");
+    hipLaunchKernelGGL(channel_score_kernel, dim3((n_cols + 255) / 256), dim3(256), 0, stream, acc, S, n_cols,
+                       (int32_t)(strategy == SMT_SCORE_L2), out);
+    return check_launch("channel_score_kernel");
 }
 
 }  // extern "C"

@@ -357,10 +357,204 @@ def get_optimizer_qk_augment_grouped_parameters(
 
 
 # ------------------------------------------------------------------------------------------------
-# channel-sparsity path (smt.py:25-80, 185-296, 748-831): SURVEY §8(f) "next"
+# channel-sparsity path (smt.py:25-80, 185-296, 748-831): SURVEY §8(f) row 1
 # ------------------------------------------------------------------------------------------------
+class ChannelIndex:
+    """``index_list`` of smt.py:186-196 (row / channel indices in selection order) with cached
+    device tables: the int32 index table and the all-tiles table of the channel wgrad."""
+
+    def __init__(self, index_list: Iterable[int]):
+        self.index_list: List[int] = [int(i) for i in index_list]
+        self._dev = {}
+
+    def __len__(self) -> int:
+        return len(self.index_list)
+
+    def __iter__(self):
+        return iter(self.index_list)
+
+    def __getitem__(self, i):
+        return self.index_list[i]
+
+    @property
+    def padded(self) -> int:
+        """Channel count rounded up to whole 256-blocks (the wgrad operand width)."""
+        return -(-len(self.index_list) // Block_dimension) * Block_dimension
+
+    def device_table(self, device: torch.device) -> torch.Tensor:
+        key = ("idx", device.type, device.index)
+        t = self._dev.get(key)
+        if t is None:
+            t = _hip.index_table(self.index_list, device)
+            self._dev[key] = t
+        return t
+
+    def wgrad_tiles(self, out_features: int, device: torch.device) -> torch.Tensor:
+        """int32 [(k_pad/256) * (out/256), 2] table covering the [k_pad, out] channel gradient."""
+        key = ("tiles", out_features, device.type, device.index)
+        t = self._dev.get(key)
+        if t is None:
+            rc = [(r, c) for r in range(self.padded // Block_dimension)
+                  for c in range(out_features // Block_dimension)]
+            t = _hip.tile_table(rc, device)
+            self._dev[key] = t
+        return t
+
+    def validate(self, rows: int) -> None:
+        seen = set()
+        for i in self.index_list:
+            if not -rows <= i < rows:
+                # W.data[index, :] in smt.py:203 raises exactly this
+                raise IndexError(f"index {i} is out of bounds for dimension 0 with size {rows}")
+            if i % rows in seen:
+                raise ValueError(f"channel index {i} repeated: the row write-back (smt.py:211-213) would "
+                                 "depend on write order")
+            seen.add(i % rows)
+        self.index_list = [i % rows for i in self.index_list]
+
+
+def _as_channel_index(index) -> ChannelIndex:
+    return index if isinstance(index, ChannelIndex) else ChannelIndex(index)
+
+
+class LinearLayer_ChannelSparsity(torch.nn.Module):
+    """smt.py:185-214: frozen dense ``W`` (aliased) plus the trainable rows
+    ``selected_weight[i, :] = W[index_list[i], :]``; every forward writes the rows back into ``W``
+    (one launch) and runs :class:`linearChannel`."""
+
+    def __init__(self, weight, bias=None, index_list=[]):
+        super().__init__()
+        self.weight = weight
+        self.weight.requires_grad = False
+        self.bias = bias
+        self.channels = _as_channel_index(index_list)
+        w = self.weight.data
+        dev = w.device
+        if dev.type not in ("cuda", "meta"):
+            raise RuntimeError(
+                f"LinearLayer_ChannelSparsity: weight on {dev}; the SMT path runs on ROCm devices only")
+        if w.dim() != 2:
+            raise RuntimeError(f"LinearLayer_ChannelSparsity: 2-D weight expected, got {tuple(w.shape)}")
+        self.channels.validate(w.shape[0])
+        self.index_list = self.channels.index_list
+        self.writeback_on_forward = True
+        k = len(self.channels)
+        selected = torch.empty(k, w.shape[1], dtype=w.dtype, device=dev)
+        if dev.type == "cuda" and k:
+            _hip.row_gather(w, self.channels.device_table(dev), selected)
+        self.selected_weight = nn.Parameter(selected, requires_grad=True)
+        self.fn = linearChannel.apply
+
+    def sync_weight(self) -> None:
+        """Scatter the rows into W (smt.py:208-213) with one launch."""
+        w = self.weight.data
+        if len(self.channels) and w.device.type == "cuda":
+            _hip.row_scatter(w, self.channels.device_table(w.device), self.selected_weight.data)
+
+    def forward(self, x):
+        if self.writeback_on_forward:
+            self.sync_weight()
+        return self.fn(x, self.selected_weight, self.channels, self.weight)
+
+    def extra_repr(self) -> str:
+        return f"in_features={self.weight.shape[1]}, out_features={self.weight.shape[0]}, channels={len(self.channels)}"
+
+
+class linearChannel(torch.autograd.Function):
+    """smt.py:217-296. Forward: ``y = x @ W^T``, saving only ``partial_input = x[:, :, index_list]``
+    (one gather launch) and ``W``. Backward: ``grad_input = g @ W`` and, as the reference computes
+    it, ``grad_weight = sum_b partial_input[b]^T g[b]`` of shape ``[k, out]`` — the tile wgrad
+    kernel over the all-tiles grid of the zero-padded ``[T, k_pad]`` operand, then one scatter into
+    the dense layout.
+
+    The reference's gradient is ``[k, out]`` while its parameter is ``[k, in]`` (rows of ``W``):
+    it only runs for square ``W``, and then it applies the gradient of *column* ``idx`` of ``W`` to
+    *row* ``idx``. Both are reproduced: non-square ``W`` raises the same
+    autograd shape error, square ``W`` gets the reference's gradient. The batch sum is fp32 with one
+    rounding (the reference rounds each per-sample product to bf16 first)."""
+
+    @staticmethod
+    def forward(ctx, input, selected_weight, channel_index_list, weight):
+        ch = _as_channel_index(channel_index_list)
+        if input.dim() != 3:
+            # smt.py:226-233 builds [input.shape[0], input.shape[1], k] and slices input[:, :, index]
+            raise IndexError(f"too many indices for tensor of dimension {input.dim()}")
+        ctx.channels = ch
+        ctx.shape = input.shape
+        partial = None
+        if ctx.needs_input_grad[1] and len(ch):
+            x2 = input.reshape(-1, input.shape[-1])
+            if x2.stride(1) != 1:
+                x2 = x2.contiguous()
+            partial = _hip.column_gather(x2, ch.device_table(x2.device), len(ch), ch.padded)
+        ctx.save_for_backward(partial, weight)
+        return torch.matmul(input, weight.t())
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        partial, weight = ctx.saved_tensors
+        ch = ctx.channels
+        out_f, in_f = weight.shape
+        grad_input = grad_weight = None
+        if ctx.needs_input_grad[1]:
+            k = len(ch)
+            if out_f != in_f:
+                raise RuntimeError(
+                    f"Function linearChannelBackward returned an invalid gradient at index 1 - got [{k}, {out_f}] "
+                    f"but expected shape compatible with [{k}, {in_f}]")
+            if out_f % Block_dimension:
+                raise NotImplementedError(f"linearChannel: out_features {out_f} not a multiple of {Block_dimension}")
+            grad_weight = torch.empty(k, out_f, dtype=grad_output.dtype, device=grad_output.device)
+            if k:
+                g2 = grad_output.reshape(-1, out_f)
+                if g2.stride(1) != 1 or g2.stride(0) % 8 or g2.data_ptr() % 16:
+                    g2 = g2.contiguous()
+                dev = g2.device
+                table = ch.wgrad_tiles(out_f, dev)
+                tiles = torch.empty(table.shape[0] * Block_dimension, Block_dimension, dtype=grad_output.dtype,
+                                    device=dev)
+                _hip.tile_wgrad(partial, g2, table, tiles)
+                dense = torch.empty(ch.padded, out_f, dtype=grad_output.dtype, device=dev)
+                _hip.tile_scatter(dense, table, tiles)
+                grad_weight = dense[:k]
+        if ctx.needs_input_grad[0]:
+            grad_input = torch.matmul(grad_output, weight)
+        return grad_input, grad_weight, None, None
+
+
+def _replace_channel(model, name, index_list):
+    module = recursive_getattr(model, name)
+    tmp = LinearLayer_ChannelSparsity(module.weight, bias=None, index_list=index_list).to(
+        module.weight.device).to(module.weight.dtype)
+    recursive_setattr(model, name, tmp)
+
+
+def convert_linear_layer_to_channel_sparsity(model, selected_channel, selected_channel_attention,
+                                             part_module_name=['.layers']):
+    """smt.py:25-80: every trainable ``nn.Linear`` under ``part_module_name`` becomes a
+    :class:`LinearLayer_ChannelSparsity` with ``selected_channel[(gate|up|down_proj, layer)]`` (MLP)
+    or ``selected_channel_attention[(q|k|v|o_proj, layer)]`` (attention). Biases are dropped."""
+    replace_name = []
+    for name, module in model.named_modules():
+        if isinstance(module, nn.Linear) and any(part in name for part in part_module_name):
+            replace_name.append(name)
+    for name in replace_name:
+        if "mlp" in name:
+            module = recursive_getattr(model, name)
+            if module.weight.requires_grad:
+                _replace_channel(model, name, selected_channel[(_mlp_module_name(name), _layer_number(name))])
+        if "self_attn" in name:
+            module = recursive_getattr(model, name)
+            if module.weight.requires_grad:
+                key = (_attn_module_name(name), _layer_number(name))
+                _replace_channel(model, name, selected_channel_attention[key])
+    return model
+
+
 def freeze_unselected_channel_layer(model, select_parameters, select_attention_parameters, mixture=False):
-    """smt.py:748-831 (host logic only; note o_proj is not a candidate on this path)."""
+    """smt.py:748-831. Same as the matrix freeze without the layernorm / embedding branches; the
+    attention module name has no ``o_proj`` case (so o_proj is never trainable here), and in
+    ``mixture`` mode attention keys are looked up in the MLP selection (smt.py:774-777)."""
     for name, param in model.named_parameters():
         if "mlp" in name:
             param.requires_grad = (_mlp_module_name(name), _layer_number(name)) in select_parameters.keys()
@@ -372,28 +566,3 @@ def freeze_unselected_channel_layer(model, select_parameters, select_attention_p
         else:
             param.requires_grad = False
     return model
-
-
-def _channel_next(*_a, **_k):
-    raise NotImplementedError(
-        "channel-sparsity (activation-selected rows, smt.py:185-296) is SURVEY §8(f) 'next' and not "
-        "built yet; see DESIGN.md")
-
-
-convert_linear_layer_to_channel_sparsity = _channel_next
-
-
-class LinearLayer_ChannelSparsity(torch.nn.Module):
-    def __init__(self, *a, **k):
-        super().__init__()
-        _channel_next()
-
-
-class linearChannel(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, *a):
-        _channel_next()
-
-    @staticmethod
-    def backward(ctx, *a):
-        _channel_next()

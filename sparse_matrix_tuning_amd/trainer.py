@@ -11,6 +11,11 @@ GPU parity tests drive the exact same sequence:
                                         updated by one multi-tensor HIP launch per step instead of a
                                         D2H copy + CPU add per parameter)
 * :func:`select_and_convert`            fine_tune.py:257-384
+* :class:`ActivationHarvester`          fine_tune.py:584-709 (channel path: |x| of every targeted
+                                        linear's input summed over steps in fp64 HBM accumulators
+                                        by one HIP launch per hook; ONE all-reduce at selection
+                                        instead of one per hook per step)
+* :func:`select_and_convert_channels`   fine_tune.py:406-575
 """
 from __future__ import annotations
 
@@ -22,9 +27,11 @@ import torch
 from . import _hip
 from .engine import SMTFusedAdam, initialize, linear_lr_lambda, safe_get_full_grad
 from .smt.smt import (_attn_module_name, _layer_number, _mlp_module_name,
-                      convert_linear_layer_to_matrix_sparsity, freeze_unselected_matrix_layer,
+                      convert_linear_layer_to_channel_sparsity, convert_linear_layer_to_matrix_sparsity,
+                      freeze_unselected_channel_layer, freeze_unselected_matrix_layer,
                       get_optimizer_sparse_grouped_parameters)
-from .smt.smt_helper import select_submatrix_based_on_grads
+from .smt.smt_helper import (ChannelActivation, get_named_linears, select_channel_based_on_activation,
+                             select_submatrix_based_on_grads)
 
 TARGET_MODULE_NAMES = ('gate_proj', 'up_proj', 'down_proj', 'q_proj', 'k_proj', 'v_proj')
 
@@ -177,3 +184,150 @@ def _broadcast(selection, enabled: bool):
     for k, v in obj[0].items():
         out[k] = list(v)
     return out
+
+
+# ------------------------------------------------------------------------------------------------
+# channel path
+# ------------------------------------------------------------------------------------------------
+class ActivationHarvester:
+    """Activation collection of fine_tune.py:584-709, kept on the GPU.
+
+    The reference walks ``model.model.layers`` one by one under ``no_grad`` (a Catcher grabs layer
+    0's input), with a forward hook on every ``nn.Linear`` of the layer that takes ``|x|``,
+    all-reduces it over ranks, copies it to the CPU in fp32 and adds it to ``activation[(m, i)]``
+    (MLP: gate/up/down_proj when ``num_mlp_channel > 0``) or ``attention_activation[(m, i)]``
+    (q/k/v_proj when ``num_attention_channel > 0``; o_proj is skipped). The layer index ``i`` is the
+    position in ``model.model.layers``.
+
+    Here the hooks stay registered on those linears and one ordinary ``no_grad`` forward of the
+    model feeds them the same inputs. Each hook is one ``smt_act_accumulate`` launch into an fp64
+    ``[S, in]`` accumulator (the batch sum the reference does at selection, smt_helper.py:170, is
+    folded in); ranks are summed once, in :meth:`finalize`, with one all-reduce of all accumulators."""
+
+    def __init__(self, model, num_mlp_channel: int, num_attention_channel: int):
+        self.model = model
+        self.activation: Dict[tuple, ChannelActivation] = {}
+        self.attention_activation: Dict[tuple, ChannelActivation] = {}
+        self._handles = []
+        self._reduced = False
+        layers = model.model.layers
+        for i, layer in enumerate(layers):
+            for name, lin in get_named_linears(layer).items():
+                store = key = None
+                if 'mlp' in name and num_mlp_channel > 0:
+                    store, key = self.activation, (_mlp_module_name(name), i)
+                if 'self_attn' in name and num_attention_channel > 0:
+                    mod = ('q_proj' if 'q_proj' in name else 'k_proj' if 'k_proj' in name else
+                           'v_proj' if 'v_proj' in name else None)
+                    if mod is not None:
+                        store, key = self.attention_activation, (mod, i)
+                if store is not None:
+                    self._handles.append(lin.register_forward_hook(self._hook(store, key)))
+
+    @staticmethod
+    def _hook(store: dict, key: tuple):
+        def hook(_module, inputs, _output):
+            x = inputs[0].detach()
+            if x.stride(-1) != 1 or x.data_ptr() % 16 or any(st % 8 for st in x.stride()[:-1]):
+                x = x.contiguous()
+            ent = store.get(key)
+            if ent is None:
+                ent = store[key] = ChannelActivation(
+                    torch.empty(x.shape[1], x.shape[2], dtype=torch.float64, device=x.device))
+            elif tuple(ent.acc.shape) != (x.shape[1], x.shape[2]):
+                # the reference's `feat_dict[key] += x` needs equal shapes across steps too
+                raise RuntimeError(f"activation shape {tuple(x.shape)} differs from earlier steps "
+                                   f"({tuple(ent.acc.shape)}) for {key}")
+            _hip.act_accumulate(x, ent.acc, assign=ent.steps == 0)
+            ent.steps += 1
+        return hook
+
+    @torch.no_grad()
+    def collect(self, batch: dict) -> None:
+        """One activation step (fine_tune.py:586-709): eval-mode no-grad forward, back to train."""
+        was_training = self.model.training
+        self.model.eval()
+        try:
+            self.model(**batch, use_cache=False)
+        finally:
+            self.model.train(was_training)
+
+    def finalize(self) -> None:
+        """Sum the accumulators over ranks (the per-hook all-reduce of the reference, done once)."""
+        import torch.distributed as dist
+        if self._reduced:
+            return
+        self._reduced = True
+        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+            return
+        accs = [e.acc for d in (self.activation, self.attention_activation) for e in d.values()]
+        if not accs:
+            return
+        flat = torch.cat([a.reshape(-1) for a in accs])
+        dist.all_reduce(flat)
+        off = 0
+        for a in accs:
+            a.copy_(flat[off:off + a.numel()].view_as(a))
+            off += a.numel()
+
+    def remove(self) -> None:
+        for h in self._handles:
+            h.remove()
+        self._handles = []
+
+    def release(self) -> None:
+        self.remove()
+        self.activation = {}
+        self.attention_activation = {}
+
+
+def select_and_convert_channels(model, harvester: ActivationHarvester, num_attention_channel: int,
+                                num_mlp_channel: int, *, selection_strategy="no_restriction",
+                                calculate_strategy="mean_abs", no_limit_mixture=False, w_decay=0.0,
+                                smt_lr=9.865e-6, ft_learning_rate=None, smt_lr_warmup_steps=0,
+                                num_training_steps=1000, ds_config: Optional[dict] = None,
+                                broadcast_selection: bool = True):
+    """fine_tune.py:406-575 (channel path). Returns ``(engine, optimizer, lr_scheduler,
+    selected_channel, selected_channel_attention)``.
+
+    As in the reference: with ``no_limit_mixture`` the channels come from the MLP activations only
+    with the summed budget; otherwise attention is scored with the default ``mean_abs``
+    (fine_tune.py:472-476 does not pass ``calculate_strategy``) and MLP with ``calculate_strategy``;
+    the optimizer is FusedAdam at ``ft_learning_rate`` with betas (0.95, 0.999) (fine_tune.py:536-538).
+    The selected rows are ordinary dense parameters for the engine (autograd bf16 gradients, fused
+    AdamW in flat mode); each forward writes them back into W (smt.py:208-213)."""
+    harvester.finalize()
+    selected_att: dict = {}
+    selected_mlp: dict = {}
+    if no_limit_mixture:
+        selected_mlp = select_channel_based_on_activation(
+            harvester.activation, num_attention_channel + num_mlp_channel,
+            selection_strategy=selection_strategy, calculate_strategy=calculate_strategy)
+        selected_mlp = _broadcast(selected_mlp, broadcast_selection)
+        model = freeze_unselected_channel_layer(model, selected_mlp, {}, mixture=True)
+    else:
+        if num_attention_channel > 0:
+            selected_att = select_channel_based_on_activation(
+                harvester.attention_activation, num_attention_channel, selection_strategy=selection_strategy)
+        if num_mlp_channel > 0:
+            selected_mlp = select_channel_based_on_activation(
+                harvester.activation, num_mlp_channel, selection_strategy=selection_strategy,
+                calculate_strategy=calculate_strategy)
+        # fine_tune.py:506-507 synchronises the attention selection from rank 0 (a file broadcast)
+        selected_att = _broadcast(selected_att, broadcast_selection)
+        selected_mlp = _broadcast(selected_mlp, broadcast_selection)
+        model = freeze_unselected_channel_layer(model, selected_mlp, selected_att)
+    harvester.release()
+    model = convert_linear_layer_to_channel_sparsity(model, selected_mlp, selected_att)
+    if hasattr(model, "enable_input_require_grads"):
+        model.enable_input_require_grads()
+    groups = get_optimizer_sparse_grouped_parameters(model, w_decay, smt_lr)
+    if not groups:
+        raise RuntimeError("channel selection produced no trainable row (channel budgets "
+                           f"attention={num_attention_channel}, mlp={num_mlp_channel})")
+    opt = SMTFusedAdam(groups, lr=ft_learning_rate if ft_learning_rate is not None else smt_lr, betas=(0.95, 0.999))
+    sched = torch.optim.lr_scheduler.LambdaLR(opt, linear_lr_lambda(smt_lr_warmup_steps, num_training_steps))
+    torch.cuda.empty_cache()
+    engine, opt, _, sched = initialize(model=model, optimizer=opt, config=ds_config or {"gradient_clipping": 1.0},
+                                       lr_scheduler=sched)
+    return engine, opt, sched, selected_mlp, selected_att

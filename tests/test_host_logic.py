@@ -237,3 +237,88 @@ def test_harvest_rounds_preserve_reference_add_order(monkeypatch):
     assert set(h.attention_warmup_grads) == set(att_ref) == {('q_proj', None), ('k_proj', None), ('v_proj', None)}
     for k in att_ref:
         assert torch.equal(h.attention_warmup_grads[k], att_ref[k])
+
+
+# ------------------------------------------------------------------ channel path host logic
+def test_rank_channels_matches_reference_heap_on_golden_cases():
+    from tests.golden.make_golden import channel_inputs
+    spec = json.load(open(os.path.join(GOLDEN, "channel_selection_expected.json")))
+    act = channel_inputs()
+    accs = {k: ref.channel_acc_fp64([v]) for k, v in act.items()}
+    for case in spec["cases"]:
+        pool = {k: a for k, a in accs.items()
+                if (k[0] in ("q_proj", "k_proj", "v_proj")) == (case["pool"] == "attention")}
+        stats = {k: ref.channel_stat_fp64(a, case["strategy"]).numpy() for k, a in pool.items()}
+        out = smt_helper.rank_channels(stats, case["n"], case["selection_strategy"])
+        assert [[k[0], k[1], list(v)] for k, v in out.items()] == case["expected"], case["n"]
+
+
+def test_rank_channels_ties_and_errors():
+    s = {('q_proj', 0): np.array([1.0, 1.0, 2.0], np.float32), ('v_proj', 0): np.array([1.0], np.float32)}
+    out = smt_helper.rank_channels(s, 3)
+    # (2.0, q/2) first; the 1.0 ties go to the larger key ('v_proj' > 'q_proj'), then the larger index
+    assert list(out.items()) == [(('q_proj', 0), [2, 1]), (('v_proj', 0), [0])]
+    ref_out = ref.rank_channels({k: torch.from_numpy(v) for k, v in s.items()}, 3)
+    assert list(out.items()) == list(ref_out.items())
+    with pytest.raises(UnboundLocalError):
+        smt_helper.rank_channels({}, 3)
+    with pytest.raises(UnboundLocalError):
+        smt_helper.rank_channels(s, 0)
+    assert dict(smt_helper.rank_channels(s, 2, "norm_dist")) == {('q_proj', 0): [2, 0], ('v_proj', 0): [0]}
+    assert smt_helper.score_channels({('q_proj', 0): torch.zeros(1, 2, 8)}, "bogus") == {}
+
+
+def test_finalize_channel_scores():
+    raw = np.array([6.0, 0.0, 2.0 ** -40], np.float64)
+    assert smt_helper.finalize_channel_scores(raw, 3, "mean_abs").tolist() == [2.0, 0.0, np.float32(2.0 ** -40 / 3)]
+    assert smt_helper.finalize_channel_scores(raw, 3, "abs_mean").tolist() == [2.0, 0.0, np.float32(2.0 ** -40 / 3)]
+    assert smt_helper.finalize_channel_scores(raw, 3, "L1").tolist() == [6.0, 0.0, np.float32(2.0 ** -40)]
+    assert smt_helper.finalize_channel_scores(np.array([9.0]), 3, "L2").tolist() == [3.0]
+
+
+def test_channel_freeze_and_convert_on_meta():
+    m = TinyLlama(kv=512)                   # square q/k/v/o: the only shapes the reference path trains
+    sel_mlp = defaultdict(list)
+    sel_att = defaultdict(list, {('q_proj', 0): [5, 300, 1], ('v_proj', 1): [511], ('o_proj', 0): [3]})
+    smt.freeze_unselected_channel_layer(m, sel_mlp, sel_att)
+    trainable = sorted(n for n, p in m.named_parameters() if p.requires_grad)
+    # o_proj has no name on this path (smt.py:796-797): never trainable
+    assert trainable == ['model.layers.0.self_attn.q_proj.weight', 'model.layers.1.self_attn.v_proj.weight']
+    smt.convert_linear_layer_to_channel_sparsity(m, sel_mlp, sel_att)
+    conv = {n: mod for n, mod in m.named_modules() if isinstance(mod, smt.LinearLayer_ChannelSparsity)}
+    assert sorted(conv) == ['model.layers.0.self_attn.q_proj', 'model.layers.1.self_attn.v_proj']
+    q = conv['model.layers.0.self_attn.q_proj']
+    assert q.index_list == [5, 300, 1] and tuple(q.selected_weight.shape) == (3, 512)
+    assert q.channels.padded == 256 and q.bias is None and q.weight.requires_grad is False
+    groups = smt.get_optimizer_sparse_grouped_parameters(m, 0.0, 1e-5)
+    assert sum(p.numel() for p in groups[0]["params"]) == 4 * 512
+    # mixture: attention keys are looked up in the MLP selection
+    m2 = TinyLlama(kv=512)
+    smt.freeze_unselected_channel_layer(m2, {('k_proj', 1): [0], ('gate_proj', 0): [1]}, {}, mixture=True)
+    assert sorted(n for n, p in m2.named_parameters() if p.requires_grad) == [
+        'model.layers.0.mlp.gate_proj.weight', 'model.layers.1.self_attn.k_proj.weight']
+
+
+def test_channel_module_errors():
+    with pytest.raises(RuntimeError, match="ROCm"):
+        smt.LinearLayer_ChannelSparsity(nn.Parameter(torch.zeros(512, 512)), index_list=[0])
+    meta = lambda: nn.Parameter(torch.zeros(512, 512, device="meta"))
+    with pytest.raises(IndexError):
+        smt.LinearLayer_ChannelSparsity(meta(), index_list=[512])
+    with pytest.raises(ValueError):
+        smt.LinearLayer_ChannelSparsity(meta(), index_list=[3, 3])
+    assert smt.LinearLayer_ChannelSparsity(meta(), index_list=[-1]).index_list == [511]
+    with pytest.raises(IndexError):
+        smt.linearChannel.apply(torch.zeros(4, 512, device="meta"), torch.zeros(1, 512, device="meta"), [0],
+                                torch.zeros(512, 512, device="meta"))
+
+
+def test_activation_harvester_hook_keys_on_meta():
+    m = TinyLlama(kv=512)
+    h = trainer.ActivationHarvester(m, num_mlp_channel=1, num_attention_channel=1)
+    assert len(h._handles) == 2 * 6            # q, k, v, gate, up, down per layer; o_proj skipped
+    h.remove()
+    h2 = trainer.ActivationHarvester(m, num_mlp_channel=0, num_attention_channel=4)
+    assert len(h2._handles) == 2 * 3
+    h2.release()
+    assert not h2._handles and h2.attention_activation == {}

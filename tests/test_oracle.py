@@ -144,3 +144,67 @@ def test_harvest_keying_opt_naming_collapses_layers():
     assert set(att) == {('q_proj', None), ('k_proj', None)}
     assert att[('q_proj', None)][0, 0].item() == 1 + 4 + 7
     assert not mlp
+
+
+# ------------------------------------------------------------------ channel path (smt.py:185-296, smt_helper.py:149-230)
+def test_kat2_exact_fp64_channel_pipeline_agrees():
+    """KAT-2 through the build's exact-arithmetic definition (fp64 batch + sequence sums, one
+    rounding) selects exactly what the ATen fp32 restatement selects."""
+    act = {
+        ('gate_proj', 1): torch.zeros(3, 11008, 4096),
+        ('up_proj', 1): torch.zeros(3, 11008, 4096),
+        ('down_proj', 2): torch.ones(3, 4096, 11008),
+    }
+    act[('gate_proj', 1)][:, :, 0:256] = torch.ones(3, 11008, 256) * 1
+    act[('gate_proj', 1)][:, :, 0:4] = torch.ones(3, 11008, 4) * 10
+    act[('up_proj', 1)][:, :, 3:6] = torch.ones(3, 11008, 3) * 100
+    act[('down_proj', 2)][:, :, 3:6] = torch.ones(3, 4096, 3) * 100
+    stats = {k: ref.channel_stat_fp64(ref.channel_acc_fp64([v]), "mean_abs") for k, v in act.items()}
+    assert dict(ref.rank_channels(stats, 100)) == dict(ref.select_channel(act, n=100))
+
+
+def test_golden_channel_fixtures_reproduce():
+    from tests.golden.make_golden import channel_inputs, digest
+    spec = json.load(open(os.path.join(GOLDEN, "channel_selection_expected.json")))
+    act = channel_inputs()
+    assert digest(act) == spec["inputs_sha256"], "seeded generator drifted: regenerate goldens"
+    att = {k: v for k, v in act.items() if k[0] in ("q_proj", "k_proj", "v_proj")}
+    mlp = {k: v for k, v in act.items() if k[0] in ("gate_proj", "up_proj", "down_proj")}
+    for case in spec["cases"][::5]:
+        pool = att if case["pool"] == "attention" else mlp
+        out = ref.select_channel(pool, case["n"], selection_strategy=case["selection_strategy"],
+                                 calculate_strategy=case["strategy"])
+        assert [[k[0], k[1], list(v)] for k, v in out.items()] == case["expected"]
+    d = np.load(os.path.join(GOLDEN, "linearchannel_case.npz"))
+    bf = lambda a: torch.from_numpy(a).view(torch.bfloat16)
+    x, g, W, idx = bf(d["x"]), bf(d["g"]), bf(d["W"]), d["idx"].tolist()
+    y, partial = ref.linearchannel_forward(x, W, idx)
+    gi, gw = ref.linearchannel_backward(g, partial, W)
+    assert torch.equal(y, bf(d["y"])) and torch.equal(gi, bf(d["grad_input"])) and torch.equal(gw, bf(d["grad_weight_ref"]))
+
+
+def test_linearchannel_grad_is_the_column_gradient_fp64():
+    """The reference's channel gradient (smt.py:285-286) is dL/dW[:, idx]^T, i.e. the gradient of
+    the COLUMNS idx of W, stored against the ROWS idx: pinned by dense autograd."""
+    torch.manual_seed(1)
+    B, S, d = 2, 12, 64
+    x = torch.randn(B, S, d, dtype=torch.float64, requires_grad=True)
+    W = torch.randn(d, d, dtype=torch.float64, requires_grad=True)
+    g = torch.randn(B, S, d, dtype=torch.float64)
+    idx = [5, 0, 63, 17]
+    (x @ W.t()).backward(g)
+    y, partial = ref.linearchannel_forward(x.detach(), W.detach(), idx)
+    gi, gw = ref.linearchannel_backward(g, partial, W.detach())
+    assert torch.allclose(gi, x.grad, rtol=1e-12, atol=1e-12)
+    assert torch.allclose(gw, W.grad[:, idx].t(), rtol=1e-12, atol=1e-12)
+    assert torch.allclose(ref.channel_grads_fp64(g, x.detach(), idx), gw, rtol=1e-12, atol=1e-12)
+
+
+def test_channel_selection_error_paths():
+    act = {('q_proj', 0): torch.rand(1, 4, 16)}
+    with pytest.raises(UnboundLocalError):
+        ref.select_channel({}, n=3)
+    with pytest.raises(UnboundLocalError):
+        ref.select_channel(act, n=3, calculate_strategy="bogus")
+    with pytest.raises(UnboundLocalError):
+        ref.select_channel(act, n=0)
