@@ -1,38 +1,61 @@
-"""Compare ROCm SDPA flash backends (aotriton vs CK) at the LLaMA-3-8B step shape."""
+"""Time the gfx950 flash attention (fused_llama.flash_attention) against torch sdpa (aotriton) at
+the LLaMA-3-8B step shape: B=16, Hq=32, Hkv=8, S=2048, D=128, causal, q/k/v in the HF layout
+(transposed views of [B, S, H, D]). FLOPs: fwd 4*B*Hq*S^2*D/2, bwd 2.5x fwd."""
+import argparse
+import json
+import os
 import sys
-import time
+
 import torch
 import torch.nn.functional as F
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from sparse_matrix_tuning_amd.fused_llama import flash_attention  # noqa: E402
 
-def run(lib, B=16, H=32, S=2048, D=128, iters=5):
-    torch.backends.cuda.preferred_rocm_fa_library(lib)
-    q = torch.randn(B, H, S, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
-    k = torch.randn(B, H, S, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
-    v = torch.randn(B, H, S, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
-    g = torch.randn(B, H, S, D, device="cuda", dtype=torch.bfloat16)
-    def step():
-        o = F.scaled_dot_product_attention(q, k, v, is_causal=True)
-        o.backward(g)
-    for _ in range(2):
-        step()
+
+def timed(fn, iters):
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    fn()
     torch.cuda.synchronize()
-    e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
-    fwd = bwd = 0.0
+    e[0].record()
     for _ in range(iters):
-        e0.record()
-        o = F.scaled_dot_product_attention(q, k, v, is_causal=True)
-        e1.record()
-        o.backward(g)
-        e2.record()
-        torch.cuda.synchronize()
-        fwd += e0.elapsed_time(e1); bwd += e1.elapsed_time(e2)
-    fl = 4 * B * H * S * S * D / 2
-    print(f"{lib}: fwd {fwd/iters:.2f} ms ({fl/(fwd/iters*1e-3)/1e12:.0f} TF/s)  bwd {bwd/iters:.2f} ms ({2.5*fl/(bwd/iters*1e-3)/1e12:.0f} TF/s)", flush=True)
+        fn()
+    e[1].record()
+    torch.cuda.synchronize()
+    return e[0].elapsed_time(e[1]) / iters
 
 
-for lib in sys.argv[1:] or ["aotriton", "ck"]:
-    try:
-        run(lib)
-    except Exception as e:
-        print(lib, "failed:", repr(e)[:300])
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--B", type=int, default=16)
+    ap.add_argument("--Hq", type=int, default=32)
+    ap.add_argument("--Hkv", type=int, default=8)
+    ap.add_argument("--S", type=int, default=2048)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--impl", nargs="*", default=["smt", "sdpa"])
+    a = ap.parse_args()
+    B, Hq, Hkv, S, D = a.B, a.Hq, a.Hkv, a.S, 128
+    torch.manual_seed(0)
+    mk = lambda H: torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16).transpose(1, 2).requires_grad_(True)
+    q, k, v = mk(Hq), mk(Hkv), mk(Hkv)
+    g = torch.randn(B, S, Hq, D, device="cuda", dtype=torch.bfloat16)
+    fl = 4 * B * Hq * S * S * D / 2
+    for impl in a.impl:
+        if impl == "smt":
+            f = lambda: flash_attention(q, k, v)
+        else:
+            f = lambda: F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=True).transpose(1, 2)
+        o = f()
+        fwd = timed(f, a.iters)
+        def fb():
+            out = f()
+            out.backward(g)
+        tot = timed(fb, a.iters)
+        bwd = tot - fwd
+        print(json.dumps({"impl": impl, "B": B, "Hq": Hq, "Hkv": Hkv, "S": S, "fwd_ms": round(fwd, 3),
+                          "bwd_ms": round(bwd, 3), "fwd_tflops": round(fl / fwd / 1e9, 1),
+                          "bwd_tflops": round(2.5 * fl / bwd / 1e9, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

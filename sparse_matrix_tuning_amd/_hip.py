@@ -25,7 +25,7 @@ ADAM_DEEPSPEED, ADAM_TORCH = 0, 1
 
 _DT = {torch.bfloat16: DTYPE_BF16, torch.float32: DTYPE_FP32, torch.float16: DTYPE_FP16}
 
-# Every function the headers declare (include/smt_hip.h, include/smt_model_ops.h); tests check the
+# Every function the headers declare (include/smt_hip.h, smt_model_ops.h, smt_attention.h); tests check the
 # library exports each of them.
 ABI_FUNCTIONS = (
     "smt_last_error", "smt_abi_version", "smt_wgrad_workspace_bytes", "smt_tile_wgrad",
@@ -34,6 +34,7 @@ ABI_FUNCTIONS = (
     "smt_row_gather", "smt_row_scatter", "smt_column_gather", "smt_act_accumulate", "smt_channel_score",
     "smt_model_ops_last_error", "smt_rmsnorm_fwd", "smt_rmsnorm_bwd_waves", "smt_rmsnorm_bwd",
     "smt_rope_fwd", "smt_rope_bwd", "smt_swiglu_fwd", "smt_swiglu_bwd",
+    "smt_attn_last_error", "smt_attn_fwd", "smt_attn_bwd",
 )
 
 
@@ -69,6 +70,15 @@ class RopeTensor(ctypes.Structure):
                 ("heads", ctypes.c_int32), ("pad_", ctypes.c_int32)]
 
 
+class AttnTensor(ctypes.Structure):
+    _fields_ = [("ptr", ctypes.c_void_p), ("sb", ctypes.c_int64), ("sh", ctypes.c_int64), ("ss", ctypes.c_int64)]
+
+
+class AttnShape(ctypes.Structure):
+    _fields_ = [("B", ctypes.c_int32), ("Hq", ctypes.c_int32), ("Hkv", ctypes.c_int32), ("S", ctypes.c_int32),
+                ("scale", ctypes.c_float), ("pad_", ctypes.c_int32)]
+
+
 ACC_CHUNK = 4096
 _lock = threading.Lock()
 _lib: Optional[ctypes.CDLL] = None
@@ -90,6 +100,10 @@ _SIGS = {
     "smt_column_gather": (ctypes.c_int, [_P, _I64, _I64, _P, _I32, _P, _I64, _P]),
     "smt_act_accumulate": (ctypes.c_int, [_P, _I32, _I64, _I64, _I32, _I32, _I32, _P, _I32, _P]),
     "smt_channel_score": (ctypes.c_int, [_P, _I32, _I32, _I32, _P, _P]),
+    "smt_attn_last_error": (ctypes.c_char_p, []),
+    "smt_attn_fwd": (ctypes.c_int, [ctypes.POINTER(AttnTensor)] * 4 + [_P, ctypes.POINTER(AttnShape), _P]),
+    "smt_attn_bwd": (ctypes.c_int, [ctypes.POINTER(AttnTensor)] * 5 + [_P, _P] + [ctypes.POINTER(AttnTensor)] * 3
+                     + [ctypes.POINTER(AttnShape), _P]),
     "smt_model_ops_last_error": (ctypes.c_char_p, []),
     "smt_rmsnorm_fwd": (ctypes.c_int, [_P, _I64, _P, _P, _I64, _P, _I64, _I32, ctypes.c_float, _P]),
     "smt_rmsnorm_bwd_waves": (ctypes.c_int, [_I64]),
@@ -131,7 +145,12 @@ def load(build_if_missing: bool = False) -> ctypes.CDLL:
 def _check(rc: int, what: str) -> None:
     if rc != 0:
         lib = load()
-        err = lib.smt_model_ops_last_error if what.startswith(("smt_rmsnorm", "smt_rope", "smt_swiglu")) else lib.smt_last_error
+        if what.startswith(("smt_rmsnorm", "smt_rope", "smt_swiglu")):
+            err = lib.smt_model_ops_last_error
+        elif what.startswith("smt_attn"):
+            err = lib.smt_attn_last_error
+        else:
+            err = lib.smt_last_error
         raise RuntimeError(f"{what} failed (status {rc}): {err().decode(errors='replace')}")
 
 

@@ -1,0 +1,707 @@
+// Causal grouped-query flash attention for gfx950 (CDNA4), head_dim 128, bf16 I/O, fp32 softmax.
+// C ABI: include/smt_attention.h. Replaces transformers' sdpa attention (aotriton on this torch
+// build) in the LLaMA decoder that carries the SMT modules.
+//
+// MFMA v_mfma_f32_32x32x16_bf16 lane maps (verified on gfx950):
+//   A[m][k]: lane l holds m = l&31, k = 8*(l>>5) + j (j = 0..7)     B[k][n]: n = l&31, same k
+//   C[m][n]: lane l holds n = l&31, m = (i&3) + 8*(i>>2) + 4*(l>>5) (i = 0..15)
+// All products are arranged so that a softmax row lives on ONE lane pair (l, l^32):
+//   forward   S^T[key][q] = K Q^T,  O^T[d][q] += V^T P^T          (q on the lane)
+//   dQ        S^T, dP^T = V dO^T,   dQ^T[d][q] += K^T dS^T          (q on the lane)
+//   dK, dV    S[q][key] = Q K^T, dP = dO V^T, dV^T += dO^T P, dK^T += Q^T dS   (key on the lane)
+// so row statistics are per-lane scalars and the probability tile, packed to bf16 and exchanged
+// once between the two wave halves (v_permlane32_swap), IS the next product's B operand.
+// LDS images are [row][128 d] bf16 rows of 256 B, swizzled by 16-B chunk:
+//   chunk' = chunk ^ (((row & 3) << 2) | ((row >> 2) & 3))
+// which is conflict-free both for ds_read_b128 row reads (16 consecutive rows, same chunk) and for
+// ds_read_b64_tr_b16 transposed reads (4 consecutive rows land in 4 different 64-B quarters).
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "smt_attention.h"
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+int check_launch(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(-4, "%s: %s", what, hipGetErrorString(e));
+    return 0;
+}
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef short s16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
+
+constexpr int kD = 128;
+constexpr int kRowB = 256;                 // one [d] row in LDS
+constexpr float kNegInf = -__builtin_huge_valf();
+
+struct Tns {
+    const uint16_t* p;
+    int64_t sb, sh, ss;
+};
+
+__device__ __forceinline__ uint32_t swz(uint32_t row) { return ((row & 3u) << 2) | ((row >> 2) & 3u); }
+__device__ __forceinline__ uint32_t lds_off(uint32_t row, uint32_t byte) { return row * kRowB + (byte ^ (swz(row) << 4)); }
+
+// 8 consecutive d of one row (ds_read_b128): A[m=row][k] or B[k][n=row] fragments of row-major data.
+__device__ __forceinline__ bf16x8_t row_frag(const uint8_t* img, uint32_t row, uint32_t byte) {
+    return *reinterpret_cast<const bf16x8_t*>(img + lds_off(row, byte));
+}
+
+// Transposed fragment (two ds_read_b64_tr_b16): lane l gets column (col0 + l&31) at rows
+// row0 + 8*(l>>5) + 0..7, i.e. the A[m=col][k=row] operand of row-major data.
+struct TrLane {
+    uint32_t krow, feat_byte;
+};
+__device__ __forceinline__ TrLane tr_lane(int lane) {
+    const int gi = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    return TrLane{8u * (gi >> 1) + q, 2u * (16u * (gi & 1) + 4u * p)};
+}
+__device__ __forceinline__ bf16x8_t tr_frag(const uint8_t* img, TrLane tl, uint32_t row0, uint32_t col0) {
+    const uint32_t r = row0 + tl.krow, byte = 2u * col0 + tl.feat_byte;
+    s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(img + lds_off(r, byte)));
+    s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(img + lds_off(r + 4, byte)));
+    const s16x8_t both = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8_t, both);
+}
+
+__device__ __forceinline__ f32x16_t mfma(bf16x8_t a, bf16x8_t b, f32x16_t c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+    f32x2_t v = {a, b};
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
+}
+
+__device__ __forceinline__ float other_half_max(float x) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float halves_sum(float x) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// C-layout probabilities of one 32-column tile (16 fp32 per lane: column = lane's n, rows
+// (i&3)+8(i>>2)+4hi) -> two B fragments for k-steps of 16 rows, rows 8hi..8hi+7 per lane.
+__device__ __forceinline__ void pack_b_frags(const float (&p)[16], bf16x8_t& f0, bf16x8_t& f1) {
+    uint32_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = pk_bf16(p[2 * i], p[2 * i + 1]);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        auto a = __builtin_amdgcn_permlane32_swap(w[4 * h + 0], w[4 * h + 2], false, false);
+        auto b = __builtin_amdgcn_permlane32_swap(w[4 * h + 1], w[4 * h + 3], false, false);
+        u32x4_t v = {a[0], b[0], a[1], b[1]};
+        if (h == 0) f0 = __builtin_bit_cast(bf16x8_t, v);
+        else f1 = __builtin_bit_cast(bf16x8_t, v);
+    }
+}
+
+// XCD-aware bijective remap (workgroups are dealt round-robin over the 8 XCDs): consecutive logical
+// ids run on one XCD, so workgroups that share K/V (or Q/dO) share that XCD's L2.
+__device__ __forceinline__ int xcd_logical(int bid, int total) {
+    const int q8 = total >> 3, r8 = total & 7, xcd = bid & 7;
+    return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+}
+
+// LDS-DMA: lane l's 16 B from rsrc + voff land at LDS byte lds_base + 16*l (buffer_load ... lds).
+// Inline asm so that hipcc does not treat it as an LDS write aliasing every ds_read (it then drains
+// vmcnt before each read); completion is waited for explicitly (s_waitcnt vmcnt(0) + barrier).
+// M0 is saved / restored inside the statement. Out-of-range offsets read as zeros.
+typedef __attribute__((address_space(3))) uint8_t lds_u8_t;
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, uint32_t lds_base, int voff) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+                 "buffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(lds_base) : "memory");
+}
+__device__ __forceinline__ uint32_t lds_addr(const uint8_t* p) { return (uint32_t)(uintptr_t)(const lds_u8_t*)p; }
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base, int64_t bytes) {
+    const uint64_t a = (uint64_t)(uintptr_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    const int n = __builtin_amdgcn_readfirstlane((int)bytes);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
+}
+__device__ __forceinline__ void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// One wave copies `pieces` x 4 rows [row0, row0 + 4*pieces) of a [rows][128] bf16 operand (row stride
+// ss elements, rows counted from the rsrc base) into a swizzled LDS image at img (image row = row - img_row0).
+__device__ __forceinline__ void dma_rows(__amdgpu_buffer_rsrc_t rsrc, int64_t ss, uint32_t img, int img_row0,
+                                         int row0, int pieces, int lane) {
+#pragma unroll 4
+    for (int i = 0; i < pieces; ++i) {
+        const int r = row0 + 4 * i + (lane >> 4);             // source row of this lane
+        const uint32_t ir = (uint32_t)(r - img_row0);          // image row
+        const uint32_t ch = (uint32_t)(lane & 15) ^ swz(ir);   // logical chunk stored at this lane's slot
+        const uint32_t base = __builtin_amdgcn_readfirstlane(img + (uint32_t)(r - (lane >> 4) - img_row0) * kRowB);
+        dma16(rsrc, base, (int)((int64_t)r * ss * 2 + ch * 16));
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Forward: a workgroup = 4 waves x 32 query rows of one (b, q head); K/V tiles of 64 keys staged
+// through registers into a double-buffered LDS ring (issue-early / write-late), one barrier per tile.
+// ------------------------------------------------------------------------------------------------
+constexpr int kFwdQW = 32, kFwdWaves = 4, kFwdQB = kFwdQW * kFwdWaves, kKV = 64;
+constexpr int kTileB = kKV * kRowB;        // 16 KiB per operand tile
+
+struct FwdArgs {
+    Tns q, k, v;
+    uint16_t* o;
+    int64_t o_sb, o_sh, o_ss;
+    float* lse;
+    int B, Hq, Hkv, S;
+    float sl2;                             // scale * log2(e)
+};
+
+__global__ __launch_bounds__(256, 2)
+void attn_fwd_kernel(FwdArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * 2 * kTileB];      // 64 KiB
+    const int nqb = (a.S + kFwdQB - 1) / kFwdQB;
+    const int G = a.Hq / a.Hkv;
+    const int total = nqb * a.Hq * a.B;
+    const int L = xcd_logical(blockIdx.x, total);
+    const int per_group = G * nqb;
+    const int grp = L / per_group;
+    const int rem = L - grp * per_group;
+    const int qb = nqb - 1 - rem / G;                  // heaviest (longest causal row) first
+    const int h = (grp % a.Hkv) * G + rem % G;
+    const int b = grp / a.Hkv, hk = grp % a.Hkv;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int hi = lane >> 5, l32 = lane & 31;
+    const int q0 = qb * kFwdQB, qw = q0 + wave * kFwdQW;
+    const uint16_t* qp = a.q.p + b * a.q.sb + h * a.q.sh;
+    const uint16_t* kp = a.k.p + b * a.k.sb + hk * a.k.sh;
+    const uint16_t* vp = a.v.p + b * a.v.sb + hk * a.v.sh;
+
+    const int qrow = qw + l32;
+    bf16x8_t qf[8];
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+        if (qrow < a.S) qf[ks] = *reinterpret_cast<const bf16x8_t*>(qp + qrow * a.q.ss + 16 * ks + 8 * hi);
+        else qf[ks] = __builtin_bit_cast(bf16x8_t, u32x4_t{0u, 0u, 0u, 0u});
+    }
+
+    const int kv_end = min(a.S, q0 + kFwdQB);
+    const int nt = (kv_end + kKV - 1) / kKV;
+    const __amdgpu_buffer_rsrc_t rk = uniform_rsrc(kp, (int64_t)a.S * a.k.ss * 2);
+    const __amdgpu_buffer_rsrc_t rv = uniform_rsrc(vp, (int64_t)a.S * a.v.ss * 2);
+    const uint32_t lds0 = lds_addr(lds);
+    auto issue = [&](int t) {            // wave w: rows [16w, 16w+16) of the K and V tiles
+        const uint32_t slot = lds0 + (uint32_t)((t & 1) * 2 * kTileB);
+        dma_rows(rk, a.k.ss, slot, t * kKV, t * kKV + 16 * wave, 4, lane);
+        dma_rows(rv, a.v.ss, slot + kTileB, t * kKV, t * kKV + 16 * wave, 4, lane);
+    };
+
+    const TrLane tl = tr_lane(lane);
+    f32x16_t o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[dt][i] = 0.f;
+    float m_run = kNegInf, l_run = 0.f;
+
+    if (nt > 0) issue(0);
+    vm_wait_all();
+    __syncthreads();
+    for (int t = 0; t < nt; ++t) {
+        if (t + 1 < nt) issue(t + 1);
+        const uint8_t* K = lds + (t & 1) * 2 * kTileB;
+        const uint8_t* V = K + kTileB;
+        const int k0 = t * kKV;
+        if (k0 <= qw + kFwdQW - 1) {
+            f32x16_t s0, s1;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) { s0[i] = 0.f; s1[i] = 0.f; }
+#pragma unroll
+            for (int ks = 0; ks < 8; ++ks) {
+                const bf16x8_t a0 = row_frag(K, l32, 32 * ks + 16 * hi);
+                const bf16x8_t a1 = row_frag(K, 32 + l32, 32 * ks + 16 * hi);
+                s0 = mfma(a0, qf[ks], s0);
+                s1 = mfma(a1, qf[ks], s1);
+            }
+            float x[32];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) { x[i] = s0[i] * a.sl2; x[16 + i] = s1[i] * a.sl2; }
+            if (k0 + kKV - 1 > qw) {                               // tile crosses this wave's diagonal
+#pragma unroll
+                for (int i = 0; i < 32; ++i) {
+                    const int key = k0 + 32 * (i >> 4) + (i & 3) + 8 * ((i & 15) >> 2) + 4 * hi;
+                    if (key > qrow) x[i] = kNegInf;
+                }
+            }
+            float mloc = x[0];
+#pragma unroll
+            for (int i = 1; i < 32; ++i) mloc = fmaxf(mloc, x[i]);
+            const float m_new = fmaxf(m_run, other_half_max(mloc));
+            const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+            float p[32];
+            float sum = 0.f;
+#pragma unroll
+            for (int i = 0; i < 32; ++i) {
+                p[i] = __builtin_amdgcn_exp2f(x[i] - m_new);
+                sum += p[i];
+            }
+            l_run = l_run * alpha + sum;
+            m_run = m_new;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+            bf16x8_t pf[4];
+            pack_b_frags(*reinterpret_cast<const float(*)[16]>(&p[0]), pf[0], pf[1]);
+            pack_b_frags(*reinterpret_cast<const float(*)[16]>(&p[16]), pf[2], pf[3]);
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int kst = 0; kst < 4; ++kst) o[dt] = mfma(tr_frag(V, tl, 16 * kst, 32 * dt), pf[kst], o[dt]);
+        }
+        vm_wait_all();
+        __syncthreads();
+    }
+
+    const float l_tot = halves_sum(l_run);
+    if (qrow < a.S) {
+        const float inv = 1.f / l_tot;
+        uint16_t* op = a.o + b * a.o_sb + h * a.o_sh + (int64_t)qrow * a.o_ss;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int d = 32 * dt + 8 * g + 4 * hi;
+                uint2 w;
+                w.x = pk_bf16(o[dt][4 * g] * inv, o[dt][4 * g + 1] * inv);
+                w.y = pk_bf16(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
+                *reinterpret_cast<uint2*>(op + d) = w;
+            }
+        if (hi == 0) a.lse[((int64_t)b * a.Hq + h) * a.S + qrow] = m_run + __log2f(l_tot);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Backward preprocess: delta[b, h, q] = sum_d dO * O (fp32 of the bf16 values). 16 lanes per row.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256)
+void attn_delta_kernel(Tns o, Tns dout, float* __restrict__ delta, int Hq, int S, int64_t rows) {
+    const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
+    const int part = threadIdx.x & 15;
+    float acc = 0.f;
+    if (row < rows) {
+        const int64_t s = row % S;
+        const int64_t bh = row / S;
+        const int64_t h = bh % Hq, b = bh / Hq;
+        const uint4 x = *reinterpret_cast<const uint4*>(o.p + b * o.sb + h * o.sh + s * o.ss + part * 8);
+        const uint4 y = *reinterpret_cast<const uint4*>(dout.p + b * dout.sb + h * dout.sh + s * dout.ss + part * 8);
+        const uint32_t xa[4] = {x.x, x.y, x.z, x.w}, ya[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            acc += __uint_as_float(xa[j] << 16) * __uint_as_float(ya[j] << 16);
+            acc += __uint_as_float(xa[j] & 0xffff0000u) * __uint_as_float(ya[j] & 0xffff0000u);
+        }
+    }
+#pragma unroll
+    for (int off = 8; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 16);
+    if (row < rows && part == 0) delta[row] = acc;
+}
+
+// ------------------------------------------------------------------------------------------------
+// dQ: a workgroup = 4 waves x 32 query rows of one (b, q head), sweeping the K/V tiles up to the
+// diagonal (staged as in the forward). Per tile: S^T = K Q^T, dP^T = V dO^T, P = exp2(S*c - lse),
+// dS = P (dP - delta), dQ^T += K^T dS^T.
+// ------------------------------------------------------------------------------------------------
+struct DqArgs {
+    Tns q, k, v, dout;
+    uint16_t* dq;
+    int64_t dq_sb, dq_sh, dq_ss;
+    const float* lse;
+    const float* delta;
+    int B, Hq, Hkv, S;
+    float sl2, scale;
+};
+
+__global__ __launch_bounds__(256, 2)
+void attn_dq_kernel(DqArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * 2 * kTileB];      // 64 KiB
+    const int nqb = (a.S + kFwdQB - 1) / kFwdQB;
+    const int G = a.Hq / a.Hkv;
+    const int total = nqb * a.Hq * a.B;
+    const int L = xcd_logical(blockIdx.x, total);
+    const int per_group = G * nqb;
+    const int grp = L / per_group;
+    const int rem = L - grp * per_group;
+    const int qb = nqb - 1 - rem / G;
+    const int h = (grp % a.Hkv) * G + rem % G;
+    const int b = grp / a.Hkv, hk = grp % a.Hkv;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int hi = lane >> 5, l32 = lane & 31;
+    const int q0 = qb * kFwdQB, qw = q0 + wave * kFwdQW;
+    const uint16_t* qp = a.q.p + b * a.q.sb + h * a.q.sh;
+    const uint16_t* dop = a.dout.p + b * a.dout.sb + h * a.dout.sh;
+    const uint16_t* kp = a.k.p + b * a.k.sb + hk * a.k.sh;
+    const uint16_t* vp = a.v.p + b * a.v.sb + hk * a.v.sh;
+
+    const int qrow = qw + l32;
+    const bool qvalid = qrow < a.S;
+    bf16x8_t qf[8], df[8];
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+        if (qvalid) {
+            qf[ks] = *reinterpret_cast<const bf16x8_t*>(qp + qrow * a.q.ss + 16 * ks + 8 * hi);
+            df[ks] = *reinterpret_cast<const bf16x8_t*>(dop + qrow * a.dout.ss + 16 * ks + 8 * hi);
+        } else {
+            qf[ks] = __builtin_bit_cast(bf16x8_t, u32x4_t{0u, 0u, 0u, 0u});
+            df[ks] = qf[ks];
+        }
+    }
+    const int64_t srow = ((int64_t)b * a.Hq + h) * a.S + (qvalid ? qrow : 0);
+    const float lse = qvalid ? a.lse[srow] : 0.f;
+    const float dlt = qvalid ? a.delta[srow] : 0.f;
+
+    const int kv_end = min(a.S, q0 + kFwdQB);
+    const int nt = (kv_end + kKV - 1) / kKV;
+    const __amdgpu_buffer_rsrc_t rk = uniform_rsrc(kp, (int64_t)a.S * a.k.ss * 2);
+    const __amdgpu_buffer_rsrc_t rv = uniform_rsrc(vp, (int64_t)a.S * a.v.ss * 2);
+    const uint32_t lds0 = lds_addr(lds);
+    auto issue = [&](int t) {
+        const uint32_t slot = lds0 + (uint32_t)((t & 1) * 2 * kTileB);
+        dma_rows(rk, a.k.ss, slot, t * kKV, t * kKV + 16 * wave, 4, lane);
+        dma_rows(rv, a.v.ss, slot + kTileB, t * kKV, t * kKV + 16 * wave, 4, lane);
+    };
+
+    const TrLane tl = tr_lane(lane);
+    f32x16_t dq[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dq[dt][i] = 0.f;
+
+    if (nt > 0) issue(0);
+    vm_wait_all();
+    __syncthreads();
+    for (int t = 0; t < nt; ++t) {
+        if (t + 1 < nt) issue(t + 1);
+        const uint8_t* K = lds + (t & 1) * 2 * kTileB;
+        const uint8_t* V = K + kTileB;
+        const int k0 = t * kKV;
+        if (k0 <= qw + kFwdQW - 1) {
+            f32x16_t s[2], dp[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) { s[j][i] = 0.f; dp[j][i] = 0.f; }
+#pragma unroll
+            for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    s[j] = mfma(row_frag(K, 32 * j + l32, 32 * ks + 16 * hi), qf[ks], s[j]);
+                    dp[j] = mfma(row_frag(V, 32 * j + l32, 32 * ks + 16 * hi), df[ks], dp[j]);
+                }
+            const bool diag = k0 + kKV - 1 > qw;
+            float ds[32];
+#pragma unroll
+            for (int i = 0; i < 32; ++i) {
+                const int j = i >> 4, ii = i & 15;
+                float pv = __builtin_amdgcn_exp2f(s[j][ii] * a.sl2 - lse);
+                if (diag) {
+                    const int key = k0 + 32 * j + (ii & 3) + 8 * (ii >> 2) + 4 * hi;
+                    if (key > qrow) pv = 0.f;
+                }
+                ds[i] = pv * (dp[j][ii] - dlt);
+            }
+            bf16x8_t sf[4];
+            pack_b_frags(*reinterpret_cast<const float(*)[16]>(&ds[0]), sf[0], sf[1]);
+            pack_b_frags(*reinterpret_cast<const float(*)[16]>(&ds[16]), sf[2], sf[3]);
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int kst = 0; kst < 4; ++kst) dq[dt] = mfma(tr_frag(K, tl, 16 * kst, 32 * dt), sf[kst], dq[dt]);
+        }
+        vm_wait_all();
+        __syncthreads();
+    }
+
+    if (qvalid) {
+        uint16_t* out = a.dq + b * a.dq_sb + h * a.dq_sh + (int64_t)qrow * a.dq_ss;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int d = 32 * dt + 8 * g + 4 * hi;
+                uint2 w;
+                w.x = pk_bf16(dq[dt][4 * g] * a.scale, dq[dt][4 * g + 1] * a.scale);
+                w.y = pk_bf16(dq[dt][4 * g + 2] * a.scale, dq[dt][4 * g + 3] * a.scale);
+                *reinterpret_cast<uint2*>(out + d) = w;
+            }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// dK, dV: a workgroup = 8 waves x 32 keys (256 keys) of one (b, kv head); it sweeps the G query
+// heads x 32-row query slices from the block's first key to S, so the G heads' contributions are
+// summed in registers (no atomics). K fragments live in registers, V rows in LDS (64 KiB); the
+// Q / dO slices (+ their lse / delta) arrive by LDS-DMA into a double-buffered ring.
+// Per slice and wave: S = Q K^T and dP = dO V^T with the row constants (-lse/c, -delta) as the
+// initial accumulators, P = exp2(c S'), dS = P dP', dV^T += dO^T P, dK^T += Q^T dS.
+// ------------------------------------------------------------------------------------------------
+constexpr int kKB = 256, kKW = 32, kDkvWaves = kKB / kKW, kSlice = 32;
+constexpr int kSliceB = kSlice * kRowB;            // 8 KiB per operand slice
+constexpr int kSliceBuf = 2 * kSliceB + 256;       // Q, dO, 32 lse + 32 delta
+constexpr int kVImg = kKB * kRowB;                 // 64 KiB
+
+struct DkvArgs {
+    Tns q, k, v, dout;
+    uint16_t* dk;
+    int64_t dk_sb, dk_sh, dk_ss;
+    uint16_t* dv;
+    int64_t dv_sb, dv_sh, dv_ss;
+    const float* lse;
+    const float* delta;
+    int B, Hq, Hkv, S;
+    float sl2, scale;
+};
+
+__global__ __launch_bounds__(kDkvWaves * 64, 2)
+void attn_dkdv_kernel(DkvArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kVImg + 2 * kSliceBuf];
+    const int nkb = (a.S + kKB - 1) / kKB;
+    const int total = nkb * a.Hkv * a.B;
+    const int L = xcd_logical(blockIdx.x, total);
+    const int grp = L / nkb;
+    const int kb = L - grp * nkb;                      // kb = 0 (longest causal sweep) first
+    const int b = grp / a.Hkv, hk = grp % a.Hkv;
+    const int G = a.Hq / a.Hkv;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int hi = lane >> 5, l32 = lane & 31;
+    const int k0 = kb * kKB, kw = k0 + wave * kKW;
+    const int key = kw + l32;
+    const uint16_t* kp = a.k.p + b * a.k.sb + hk * a.k.sh;
+    const uint16_t* vp = a.v.p + b * a.v.sb + hk * a.v.sh;
+    const uint32_t lds0 = lds_addr(lds);
+
+    // V image of the block's 256 keys (each wave its own 32 rows), by DMA
+    dma_rows(uniform_rsrc(vp, (int64_t)a.S * a.v.ss * 2), a.v.ss, lds0, k0, kw, kKW / 4, lane);
+
+    // K fragments (B operand of S = Q K^T): key = kw + l32, d = 16ks + 8hi
+    bf16x8_t kf[8];
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+        if (key < a.S) kf[ks] = *reinterpret_cast<const bf16x8_t*>(kp + (int64_t)key * a.k.ss + 16 * ks + 8 * hi);
+        else kf[ks] = __builtin_bit_cast(bf16x8_t, u32x4_t{0u, 0u, 0u, 0u});
+    }
+
+    const int n_sl = (a.S - k0 + kSlice - 1) / kSlice;     // query slices per head, from q = k0
+    const int n_it = G * n_sl;
+    // Slice staging by DMA: waves 0-3 bring Q rows 8w..8w+7, waves 4-7 dO rows; waves 0 / 1 also
+    // the slice's 32 lse / 32 delta values (8 lanes x 16 B).
+    auto issue = [&](int it) {
+        const int hh = it / n_sl, sl = it - hh * n_sl;
+        const int h = hk * G + hh;
+        const int s0 = k0 + sl * kSlice;
+        const uint32_t buf = lds0 + kVImg + (uint32_t)((it & 1) * kSliceBuf);
+        const bool is_q = wave < 4;
+        const Tns& src = is_q ? a.q : a.dout;
+        const uint16_t* base = src.p + b * src.sb + h * src.sh;
+        dma_rows(uniform_rsrc(base, (int64_t)a.S * src.ss * 2), src.ss, buf + (is_q ? 0u : (uint32_t)kSliceB), s0,
+                 s0 + 8 * (wave & 3), 2, lane);
+        if (wave < 2 && lane < 8) {
+            const float* row = (wave == 0 ? a.lse : a.delta) + ((int64_t)b * a.Hq + h) * a.S;
+            dma16(uniform_rsrc(row, (int64_t)a.S * 4), __builtin_amdgcn_readfirstlane(buf + 2 * kSliceB + 128 * wave),
+                  (s0 + 4 * lane) * 4);
+        }
+    };
+
+    const TrLane tl = tr_lane(lane);
+    f32x16_t dvt[4], dkt[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { dvt[dt][i] = 0.f; dkt[dt][i] = 0.f; }
+    const float inv_sl2 = 1.f / a.sl2;
+
+    if (n_it > 0) issue(0);
+    vm_wait_all();
+    __syncthreads();
+    for (int it = 0; it < n_it; ++it) {
+        if (it + 1 < n_it) issue(it + 1);
+        const uint8_t* Qs = lds + kVImg + (it & 1) * kSliceBuf;
+        const uint8_t* Ds = Qs + kSliceB;
+        const float* cst = reinterpret_cast<const float*>(Qs + 2 * kSliceB);     // lse[32], delta[32]
+        const int sl = it % n_sl;
+        const int s0 = k0 + sl * kSlice;
+        if (s0 + kSlice - 1 >= kw) {                        // some q of the slice sees some key of the wave
+            // row constants as initial accumulators: rows q = (i&3) + 8(i>>2) + 4hi
+            f32x16_t s, dp;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const float4 lz = *reinterpret_cast<const float4*>(cst + 8 * g + 4 * hi);
+                const float4 dz = *reinterpret_cast<const float4*>(cst + 32 + 8 * g + 4 * hi);
+                s[4 * g] = -lz.x * inv_sl2; s[4 * g + 1] = -lz.y * inv_sl2;
+                s[4 * g + 2] = -lz.z * inv_sl2; s[4 * g + 3] = -lz.w * inv_sl2;
+                dp[4 * g] = -dz.x; dp[4 * g + 1] = -dz.y; dp[4 * g + 2] = -dz.z; dp[4 * g + 3] = -dz.w;
+            }
+#pragma unroll
+            for (int ks = 0; ks < 8; ++ks) {
+                s = mfma(row_frag(Qs, l32, 32 * ks + 16 * hi), kf[ks], s);
+                dp = mfma(row_frag(Ds, l32, 32 * ks + 16 * hi), row_frag(lds, wave * kKW + l32, 32 * ks + 16 * hi), dp);
+            }
+            const bool diag = s0 < kw + kKW - 1;
+            float p[16], ds[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                float pv = __builtin_amdgcn_exp2f(s[i] * a.sl2);
+                if (diag) {
+                    const int q = s0 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+                    if (key > q) pv = 0.f;
+                }
+                p[i] = pv;
+                ds[i] = pv * dp[i];
+            }
+            bf16x8_t pf[2], sf[2];
+            pack_b_frags(p, pf[0], pf[1]);
+            pack_b_frags(ds, sf[0], sf[1]);
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int kq = 0; kq < 2; ++kq) {
+                    dvt[dt] = mfma(tr_frag(Ds, tl, 16 * kq, 32 * dt), pf[kq], dvt[dt]);
+                    dkt[dt] = mfma(tr_frag(Qs, tl, 16 * kq, 32 * dt), sf[kq], dkt[dt]);
+                }
+        }
+        vm_wait_all();
+        __syncthreads();
+    }
+
+    // dK = scale * (dK^T)^T, dV = (dV^T)^T: the lane's key row, 4 consecutive d per register group
+    if (key < a.S) {
+        uint16_t* dkr = a.dk + b * a.dk_sb + hk * a.dk_sh + (int64_t)key * a.dk_ss;
+        uint16_t* dvr = a.dv + b * a.dv_sb + hk * a.dv_sh + (int64_t)key * a.dv_ss;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int d = 32 * dt + 8 * g + 4 * hi;
+                uint2 w;
+                w.x = pk_bf16(dkt[dt][4 * g] * a.scale, dkt[dt][4 * g + 1] * a.scale);
+                w.y = pk_bf16(dkt[dt][4 * g + 2] * a.scale, dkt[dt][4 * g + 3] * a.scale);
+                *reinterpret_cast<uint2*>(dkr + d) = w;
+                w.x = pk_bf16(dvt[dt][4 * g], dvt[dt][4 * g + 1]);
+                w.y = pk_bf16(dvt[dt][4 * g + 2], dvt[dt][4 * g + 3]);
+                *reinterpret_cast<uint2*>(dvr + d) = w;
+            }
+    }
+}
+
+inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+int check_tensor(const smt_attn_tensor* t, const char* what, const char* fn) {
+    if (!t || !t->ptr) return fail(-1, "%s: null %s", fn, what);
+    if (!al16(t->ptr) || (t->sb & 7) || (t->sh & 7) || (t->ss & 7))
+        return fail(-2, "%s: %s needs 16-byte aligned rows (strides %% 8 == 0)", fn, what);
+    return 0;
+}
+
+int check_shape(const smt_attn_shape* s, const char* fn) {
+    if (!s) return fail(-1, "%s: null shape", fn);
+    if (s->B <= 0 || s->Hq <= 0 || s->Hkv <= 0 || s->S <= 0 || s->Hq % s->Hkv)
+        return fail(-1, "%s: bad shape B=%d Hq=%d Hkv=%d S=%d", fn, s->B, s->Hq, s->Hkv, s->S);
+    if (!(s->scale > 0.f)) return fail(-1, "%s: scale must be > 0", fn);
+    return 0;
+}
+
+Tns tns(const smt_attn_tensor* t) { return Tns{static_cast<const uint16_t*>(t->ptr), t->sb, t->sh, t->ss}; }
+
+}  // namespace
+
+extern "C" {
+
+const char* smt_attn_last_error(void) { return g_err; }
+
+int smt_attn_fwd(const smt_attn_tensor* q, const smt_attn_tensor* k, const smt_attn_tensor* v,
+                 const smt_attn_tensor* o, float* lse, const smt_attn_shape* shape, hipStream_t stream) {
+    int rc;
+    if ((rc = check_shape(shape, "smt_attn_fwd")) || (rc = check_tensor(q, "q", "smt_attn_fwd")) ||
+        (rc = check_tensor(k, "k", "smt_attn_fwd")) || (rc = check_tensor(v, "v", "smt_attn_fwd")) ||
+        (rc = check_tensor(o, "o", "smt_attn_fwd")))
+        return rc;
+    if (!lse) return fail(-1, "smt_attn_fwd: null lse");
+    FwdArgs a;
+    a.q = tns(q); a.k = tns(k); a.v = tns(v);
+    a.o = static_cast<uint16_t*>(o->ptr); a.o_sb = o->sb; a.o_sh = o->sh; a.o_ss = o->ss;
+    a.lse = lse;
+    a.B = shape->B; a.Hq = shape->Hq; a.Hkv = shape->Hkv; a.S = shape->S;
+    a.sl2 = shape->scale * 1.4426950408889634f;
+    const int64_t nqb = (shape->S + kFwdQB - 1) / kFwdQB;
+    const int64_t blocks = nqb * shape->Hq * shape->B;
+    if (blocks > 0x7fffffffLL) return fail(-1, "smt_attn_fwd: too many blocks");
+    hipLaunchKernelGGL(attn_fwd_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, a);
+    return check_launch("attn_fwd_kernel");
+}
+
+int smt_attn_bwd(const smt_attn_tensor* q, const smt_attn_tensor* k, const smt_attn_tensor* v,
+                 const smt_attn_tensor* o, const smt_attn_tensor* d_o, const float* lse, float* delta_ws,
+                 const smt_attn_tensor* dq, const smt_attn_tensor* dk, const smt_attn_tensor* dv,
+                 const smt_attn_shape* shape, hipStream_t stream) {
+    int rc;
+    const char* fn = "smt_attn_bwd";
+    if ((rc = check_shape(shape, fn)) || (rc = check_tensor(q, "q", fn)) || (rc = check_tensor(k, "k", fn)) ||
+        (rc = check_tensor(v, "v", fn)) || (rc = check_tensor(o, "o", fn)) || (rc = check_tensor(d_o, "do", fn)) ||
+        (rc = check_tensor(dq, "dq", fn)) || (rc = check_tensor(dk, "dk", fn)) || (rc = check_tensor(dv, "dv", fn)))
+        return rc;
+    if (!lse || !delta_ws) return fail(-1, "%s: null lse / delta workspace", fn);
+    if (!al16(lse) || !al16(delta_ws) || (shape->S & 3)) return fail(-2, "%s: lse / delta need 16-byte rows (S %% 4 == 0)", fn);
+    const int B = shape->B, Hq = shape->Hq, Hkv = shape->Hkv, S = shape->S;
+    const float sl2 = shape->scale * 1.4426950408889634f;
+
+    const int64_t rows = (int64_t)B * Hq * S;
+    hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((rows * 16 + 255) / 256)), dim3(256), 0, stream,
+                       tns(o), tns(d_o), delta_ws, Hq, S, rows);
+    if ((rc = check_launch("attn_delta_kernel"))) return rc;
+
+    DqArgs qa;
+    qa.q = tns(q); qa.k = tns(k); qa.v = tns(v); qa.dout = tns(d_o);
+    qa.dq = static_cast<uint16_t*>(dq->ptr); qa.dq_sb = dq->sb; qa.dq_sh = dq->sh; qa.dq_ss = dq->ss;
+    qa.lse = lse; qa.delta = delta_ws;
+    qa.B = B; qa.Hq = Hq; qa.Hkv = Hkv; qa.S = S; qa.sl2 = sl2; qa.scale = shape->scale;
+    const int64_t nqb = (S + kFwdQB - 1) / kFwdQB;
+    hipLaunchKernelGGL(attn_dq_kernel, dim3((unsigned)(nqb * Hq * B)), dim3(256), 0, stream, qa);
+    if ((rc = check_launch("attn_dq_kernel"))) return rc;
+
+    DkvArgs ka;
+    ka.q = tns(q); ka.k = tns(k); ka.v = tns(v); ka.dout = tns(d_o);
+    ka.dk = static_cast<uint16_t*>(dk->ptr); ka.dk_sb = dk->sb; ka.dk_sh = dk->sh; ka.dk_ss = dk->ss;
+    ka.dv = static_cast<uint16_t*>(dv->ptr); ka.dv_sb = dv->sb; ka.dv_sh = dv->sh; ka.dv_ss = dv->ss;
+    ka.lse = lse; ka.delta = delta_ws;
+    ka.B = B; ka.Hq = Hq; ka.Hkv = Hkv; ka.S = S; ka.sl2 = sl2; ka.scale = shape->scale;
+    const int64_t nkb = (S + kKB - 1) / kKB;
+    hipLaunchKernelGGL(attn_dkdv_kernel, dim3((unsigned)(nkb * Hkv * B)), dim3(kDkvWaves * 64), 0, stream, ka);
+    return check_launch("attn_dkdv_kernel");
+}
+
+}  // extern "C"

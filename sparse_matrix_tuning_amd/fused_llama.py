@@ -8,6 +8,11 @@ one-pass HIP kernels (``csrc/llama_kernels.hip``, C ABI ``include/smt_model_ops.
 autograd Functions. Every intermediate bf16 rounding of the eager chain is reproduced, so results
 match the eager model up to reduction order / exp ulps (tests/test_gpu_fused_llama.py).
 
+It also routes the decoder's attention to a gfx950 causal flash attention (forward + backward,
+``csrc/attn_kernels.hip``, C ABI ``include/smt_attention.h``), registered with transformers'
+``AttentionInterface`` as ``"smt_flash"``; sdpa on this torch build runs aotriton at 25-27 % of the
+step. Tolerances vs an fp32 reference are in tests/test_gpu_attention.py.
+
 Only bf16 CUDA tensors take the fused path; anything else raises (no silent fallback).
 """
 from __future__ import annotations
@@ -186,6 +191,104 @@ def fused_mlp_forward(self, x):
 
 
 # ------------------------------------------------------------------------------------------------
+# causal flash attention
+# ------------------------------------------------------------------------------------------------
+def _attn_tensor(t: torch.Tensor) -> _hip.AttnTensor:
+    sb, sh, ss, sd = t.stride()
+    if sd != 1:
+        raise RuntimeError("flash attention: head_dim must be the innermost dimension")
+    return _hip.AttnTensor(t.data_ptr(), sb, sh, ss)
+
+
+def _attn_ready(t: torch.Tensor) -> torch.Tensor:
+    if t.stride(-1) == 1 and not any(s % 8 for s in t.stride()[:3]) and t.data_ptr() % 16 == 0:
+        return t
+    return t.contiguous()
+
+
+class FlashAttnFn(torch.autograd.Function):
+    """Causal GQA attention: q [B, Hq, S, 128], k / v [B, Hkv, S, 128] (any strides with head_dim
+    innermost) -> o [B, S, Hq, 128] (the layout transformers' attention functions return)."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, scale):
+        for t, n in ((q, "q"), (k, "k"), (v, "v")):
+            _need(t, "flash attention " + n)
+        B, Hq, S, D = q.shape
+        Hkv = k.shape[1]
+        if D != 128 or k.shape != (B, Hkv, S, D) or v.shape != k.shape or Hq % Hkv or S % 4:
+            raise NotImplementedError(f"flash attention: head_dim 128, Hq % Hkv == 0, S % 4 == 0 "
+                                      f"(q {tuple(q.shape)}, k {tuple(k.shape)})")
+        q, k, v = _attn_ready(q), _attn_ready(k), _attn_ready(v)
+        for t in (q, k, v):
+            if S * t.stride(2) * 2 >= 2 ** 31:
+                raise NotImplementedError("flash attention: per-head extent must stay below 2 GiB")
+        o = torch.empty(B, S, Hq, D, dtype=q.dtype, device=q.device)
+        lse = torch.empty(B, Hq, S, dtype=torch.float32, device=q.device)
+        ov = o.transpose(1, 2)
+        shape = _hip.AttnShape(B, Hq, Hkv, S, float(scale), 0)
+        rc = _hip.load().smt_attn_fwd(ctypes.byref(_attn_tensor(q)), ctypes.byref(_attn_tensor(k)),
+                                      ctypes.byref(_attn_tensor(v)), ctypes.byref(_attn_tensor(ov)),
+                                      lse.data_ptr(), ctypes.byref(shape), _stream(q))
+        _hip._check(rc, "smt_attn_fwd")
+        ctx.save_for_backward(q, k, v, o, lse)
+        ctx.scale = float(scale)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse = ctx.saved_tensors
+        B, Hq, S, D = q.shape
+        Hkv = k.shape[1]
+        do = do if (do.stride(-1) == 1 and not any(s % 8 for s in do.stride()[:3]) and do.data_ptr() % 16 == 0) \
+            else do.contiguous()
+        dq = torch.empty_strided(q.shape, q.stride(), dtype=q.dtype, device=q.device)
+        dk = torch.empty_strided(k.shape, k.stride(), dtype=k.dtype, device=k.device)
+        dv = torch.empty_strided(v.shape, v.stride(), dtype=v.dtype, device=v.device)
+        delta = torch.empty(B, Hq, S, dtype=torch.float32, device=q.device)
+        shape = _hip.AttnShape(B, Hq, Hkv, S, ctx.scale, 0)
+        T = _attn_tensor
+        rc = _hip.load().smt_attn_bwd(ctypes.byref(T(q)), ctypes.byref(T(k)), ctypes.byref(T(v)),
+                                      ctypes.byref(T(o.transpose(1, 2))), ctypes.byref(T(do.transpose(1, 2))),
+                                      lse.data_ptr(), delta.data_ptr(), ctypes.byref(T(dq)), ctypes.byref(T(dk)),
+                                      ctypes.byref(T(dv)), ctypes.byref(shape), _stream(q))
+        _hip._check(rc, "smt_attn_bwd")
+        return dq, dk, dv, None
+
+
+def flash_attention(q, k, v, scale=None):
+    """Causal attention ``[B, Hq, S, 128]`` x ``[B, Hkv, S, 128]`` -> ``[B, S, Hq, 128]``."""
+    return FlashAttnFn.apply(q, k, v, scale if scale is not None else q.shape[-1] ** -0.5)
+
+
+def smt_flash_attention_forward(module, query, key, value, attention_mask, dropout=0.0, scaling=None,
+                                is_causal=None, **kwargs):
+    """transformers attention-function signature (``AttentionInterface``). Causal self-attention
+    without padding only: anything else raises rather than silently changing semantics."""
+    if attention_mask is not None:
+        raise NotImplementedError("smt_flash attention: padded / custom masks are not supported "
+                                  "(the bench and the reference's packed batches use none)")
+    if dropout:
+        raise NotImplementedError("smt_flash attention: dropout is not supported")
+    if is_causal is False or not getattr(module, "is_causal", True):
+        raise NotImplementedError("smt_flash attention: causal attention only")
+    return flash_attention(query, key, value, scaling), None
+
+
+ATTN_NAME = "smt_flash"
+
+
+def register_attention() -> str:
+    """Register ``smt_flash`` with transformers (attention function + the sdpa mask builder, which
+    returns no mask for plain causal batches)."""
+    from transformers import AttentionInterface
+    from transformers.masking_utils import ALL_MASK_ATTENTION_FUNCTIONS, sdpa_mask
+    AttentionInterface.register(ATTN_NAME, smt_flash_attention_forward)
+    ALL_MASK_ATTENTION_FUNCTIONS.register(ATTN_NAME, sdpa_mask)
+    return ATTN_NAME
+
+
+# ------------------------------------------------------------------------------------------------
 _EAGER = {}
 
 
@@ -201,12 +304,22 @@ def eager_apply_rotary_pos_emb(*a, **k):
     return _ml() and _EAGER["rope"](*a, **k)
 
 
-def patch_llama(model: nn.Module) -> dict:
-    """Route a transformers LLaMA model's RMSNorm / RoPE / SwiGLU through the fused kernels.
-    RoPE is patched at module level (``modeling_llama.apply_rotary_pos_emb``, looked up by
-    ``LlamaAttention.forward`` at call time). Returns counts of patched modules. Idempotent."""
+def patch_llama(model: nn.Module, attention: bool = True) -> dict:
+    """Route a transformers LLaMA model's RMSNorm / RoPE / SwiGLU (and, with ``attention``, its
+    attention) through the fused kernels. RoPE is patched at module level
+    (``modeling_llama.apply_rotary_pos_emb``, looked up by ``LlamaAttention.forward`` at call time);
+    attention by switching ``config._attn_implementation`` to the registered ``smt_flash``.
+    Returns counts of patched modules. Idempotent."""
     ml = _ml()
-    counts = {"rmsnorm": 0, "mlp": 0, "rope": 1}
+    counts = {"rmsnorm": 0, "mlp": 0, "rope": 1, "attention": 0}
+    if attention:
+        cfg = getattr(model, "config", None)
+        if cfg is None:
+            raise RuntimeError("patch_llama(attention=True) needs a transformers model with a config")
+        if "smt_prev_attn" not in _EAGER:
+            _EAGER["smt_prev_attn"] = cfg._attn_implementation
+        cfg._attn_implementation = register_attention()
+        counts["attention"] = sum(1 for m in model.modules() if isinstance(m, ml.LlamaAttention))
     for m in model.modules():
         if isinstance(m, ml.LlamaRMSNorm):
             m.forward = fused_rmsnorm_forward.__get__(m, type(m))
@@ -225,6 +338,8 @@ def unpatch_llama(model: nn.Module = None) -> None:
     """Undo :func:`patch_llama` (module-level RoPE; per-instance forwards of ``model`` if given)."""
     ml = _ml()
     ml.apply_rotary_pos_emb = _EAGER["rope"]
+    if model is not None and "smt_prev_attn" in _EAGER and getattr(model, "config", None) is not None:
+        model.config._attn_implementation = _EAGER.pop("smt_prev_attn")
     if model is not None:
         for m in model.modules():
             if isinstance(m, (ml.LlamaRMSNorm, ml.LlamaMLP)) and "forward" in m.__dict__:
