@@ -66,6 +66,8 @@ def parse():
     ap.add_argument("--calculate-strategy", default="abs_mean")
     ap.add_argument("--smt-lr", type=float, default=9.865e-6)
     ap.add_argument("--no-grad-ckpt", action="store_true")
+    ap.add_argument("--sdpa-attention", action="store_true",
+                    help="keep transformers' sdpa (aotriton) attention instead of the gfx950 flash attention")
     ap.add_argument("--eager-ops", action="store_true",
                     help="keep transformers' eager RMSNorm/RoPE/SwiGLU instead of the fused HIP kernels")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0, help="0 disables the CPU leg")
@@ -230,7 +232,7 @@ def main():
     model = build_model(args.model, device)
     if not args.eager_ops:
         from sparse_matrix_tuning_amd.fused_llama import patch_llama
-        patch_llama(model)
+        patch_llama(model, attention=not args.sdpa_attention)
     # warm-up (full fine-tuning: fp32 master/moments for all 8 B params) always checkpoints;
     # --no-grad-ckpt turns it off for the SMT phase only (keeps activations in the 288 GB HBM)
     model.gradient_checkpointing_enable()
@@ -346,7 +348,8 @@ def main():
                        "global_batch": B * world, "seq_len": S, "parallelism": f"dp{world}",
                        "tiles": n_tiles, "trainable_params": trainable,
                        "grad_ckpt": not args.no_grad_ckpt, "full_ft_steps": args.full_ft_steps,
-                       "fused_llama_ops": not args.eager_ops},
+                       "fused_llama_ops": not args.eager_ops,
+                       "attention": "sdpa" if (args.eager_ops or args.sdpa_attention) else "smt_flash"},
             "peak_hbm_gb": round(peak.item(), 2), "warmup_peak_hbm_gb": round(warm_peak, 2),
             "step_mfma_frac": round(per_gpu * F_ALG_GFLOP_PER_TOKEN * 1e9 / (PEAK_BF16_TFLOPS * 1e12), 4),
             "roofline": roofline, "cpu_baseline": cpu,

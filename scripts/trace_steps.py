@@ -15,6 +15,10 @@ def cat(name):
         return "smt_optimizer"
     if n.startswith("Cijk") or n.startswith("Custom_Cijk"):
         return "gemm(hipBLASLt)"
+    if "attn_fwd_kernel" in n or "attn_dq_kernel" in n or "attn_dkdv_kernel" in n or "attn_delta_kernel" in n:
+        return "attention(smt_flash)"
+    if any(k in n for k in ("rmsnorm", "rope_kernel", "swiglu")):
+        return "fused_llama_ops"
     if "attn_fwd" in n or "bwd_kernel" in n or "bwd_preprocess" in n:
         return "attention(aotriton)"
     if "SoftMax" in n or "nll_loss" in n or "log_softmax" in n:

@@ -19,6 +19,7 @@
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include "smt_attention.h"
 
@@ -175,20 +176,27 @@ struct FwdArgs {
     float sl2;                             // scale * log2(e)
 };
 
-__global__ __launch_bounds__(256, 2)
-void attn_fwd_kernel(FwdArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * 2 * kTileB];      // 64 KiB
-    const int nqb = (a.S + kFwdQB - 1) / kFwdQB;
-    const int G = a.Hq / a.Hkv;
-    const int total = nqb * a.Hq * a.B;
-    const int L = xcd_logical(blockIdx.x, total);
-    const int per_group = G * nqb;
+// Causal balance: a workgroup takes the query blocks qb and nqb-1-qb (equal total work per workgroup).
+struct PairTask {
+    int b, hk, hh, blk[2], n;
+};
+__device__ __forceinline__ PairTask pair_task(int L, int nblk, int G, int Hkv) {
+    const int npair = (nblk + 1) / 2;
+    const int per_group = G * npair;
     const int grp = L / per_group;
     const int rem = L - grp * per_group;
-    const int qb = nqb - 1 - rem / G;                  // heaviest (longest causal row) first
-    const int h = (grp % a.Hkv) * G + rem % G;
-    const int b = grp / a.Hkv, hk = grp % a.Hkv;
+    const int p = rem / G;
+    PairTask t;
+    t.b = grp / Hkv;
+    t.hk = grp % Hkv;
+    t.hh = rem % G;
+    t.blk[0] = nblk - 1 - p;
+    t.blk[1] = p;
+    t.n = (t.blk[1] == t.blk[0]) ? 1 : 2;
+    return t;
+}
 
+__device__ __forceinline__ void fwd_block(const FwdArgs& a, uint8_t* lds, int b, int h, int hk, int qb) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int hi = lane >> 5, l32 = lane & 31;
@@ -301,6 +309,22 @@ void attn_fwd_kernel(FwdArgs a) {
     }
 }
 
+__global__ __launch_bounds__(256, 2)
+void attn_fwd_kernel(FwdArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * 2 * kTileB];      // 64 KiB
+    const int nqb = (a.S + kFwdQB - 1) / kFwdQB;
+    const int G = a.Hq / a.Hkv;
+    const int total = nqb * a.Hq * a.B;
+    // consecutive ids: the G heads of one (b, kv head) at one q block, heaviest (longest causal row)
+    // q blocks first (pairing q blocks measured 1-2 % slower here than this order)
+    const int L = xcd_logical(blockIdx.x, total);
+    const int per_group = G * nqb;
+    const int grp = L / per_group;
+    const int rem = L - grp * per_group;
+    const int hk = grp % a.Hkv;
+    fwd_block(a, lds, grp / a.Hkv, hk * G + rem % G, hk, nqb - 1 - rem / G);
+}
+
 // ------------------------------------------------------------------------------------------------
 // Backward preprocess: delta[b, h, q] = sum_d dO * O (fp32 of the bf16 values). 16 lanes per row.
 // ------------------------------------------------------------------------------------------------
@@ -342,20 +366,7 @@ struct DqArgs {
     float sl2, scale;
 };
 
-__global__ __launch_bounds__(256, 2)
-void attn_dq_kernel(DqArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * 2 * kTileB];      // 64 KiB
-    const int nqb = (a.S + kFwdQB - 1) / kFwdQB;
-    const int G = a.Hq / a.Hkv;
-    const int total = nqb * a.Hq * a.B;
-    const int L = xcd_logical(blockIdx.x, total);
-    const int per_group = G * nqb;
-    const int grp = L / per_group;
-    const int rem = L - grp * per_group;
-    const int qb = nqb - 1 - rem / G;
-    const int h = (grp % a.Hkv) * G + rem % G;
-    const int b = grp / a.Hkv, hk = grp % a.Hkv;
-
+__device__ __forceinline__ void dq_block(const DqArgs& a, uint8_t* lds, int b, int h, int hk, int qb) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int hi = lane >> 5, l32 = lane & 31;
@@ -460,6 +471,22 @@ void attn_dq_kernel(DqArgs a) {
     }
 }
 
+__global__ __launch_bounds__(256, 2)
+void attn_dq_kernel(DqArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * 2 * kTileB];      // 64 KiB
+    const int nqb = (a.S + kFwdQB - 1) / kFwdQB;
+    const int G = a.Hq / a.Hkv;
+    const int total = nqb * a.Hq * a.B;
+    // consecutive ids: the G heads of one (b, kv head) at one q block, heaviest (longest causal row)
+    // q blocks first (pairing q blocks measured 1-2 % slower here than this order)
+    const int L = xcd_logical(blockIdx.x, total);
+    const int per_group = G * nqb;
+    const int grp = L / per_group;
+    const int rem = L - grp * per_group;
+    const int hk = grp % a.Hkv;
+    dq_block(a, lds, grp / a.Hkv, hk * G + rem % G, hk, nqb - 1 - rem / G);
+}
+
 // ------------------------------------------------------------------------------------------------
 // dK, dV: a workgroup = 8 waves x 32 keys (256 keys) of one (b, kv head); it sweeps the G query
 // heads x 32-row query slices from the block's first key to S, so the G heads' contributions are
@@ -485,17 +512,8 @@ struct DkvArgs {
     float sl2, scale;
 };
 
-__global__ __launch_bounds__(kDkvWaves * 64, 2)
-void attn_dkdv_kernel(DkvArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kVImg + 2 * kSliceBuf];
-    const int nkb = (a.S + kKB - 1) / kKB;
-    const int total = nkb * a.Hkv * a.B;
-    const int L = xcd_logical(blockIdx.x, total);
-    const int grp = L / nkb;
-    const int kb = L - grp * nkb;                      // kb = 0 (longest causal sweep) first
-    const int b = grp / a.Hkv, hk = grp % a.Hkv;
+__device__ __forceinline__ void dkdv_block(const DkvArgs& a, uint8_t* lds, int b, int hk, int kb) {
     const int G = a.Hq / a.Hkv;
-
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int hi = lane >> 5, l32 = lane & 31;
@@ -521,7 +539,7 @@ void attn_dkdv_kernel(DkvArgs a) {
     // Slice staging by DMA: waves 0-3 bring Q rows 8w..8w+7, waves 4-7 dO rows; waves 0 / 1 also
     // the slice's 32 lse / 32 delta values (8 lanes x 16 B).
     auto issue = [&](int it) {
-        const int hh = it / n_sl, sl = it - hh * n_sl;
+        const int hh = it / n_sl, sl = n_sl - 1 - (it - hh * n_sl);
         const int h = hk * G + hh;
         const int s0 = k0 + sl * kSlice;
         const uint32_t buf = lds0 + kVImg + (uint32_t)((it & 1) * kSliceBuf);
@@ -553,8 +571,8 @@ void attn_dkdv_kernel(DkvArgs a) {
         const uint8_t* Qs = lds + kVImg + (it & 1) * kSliceBuf;
         const uint8_t* Ds = Qs + kSliceB;
         const float* cst = reinterpret_cast<const float*>(Qs + 2 * kSliceB);     // lse[32], delta[32]
-        const int sl = it % n_sl;
-        const int s0 = k0 + sl * kSlice;
+        const int sl = n_sl - 1 - it % n_sl;               // descending q: the group's key blocks read
+        const int s0 = k0 + sl * kSlice;                   // the same slices at the same time (L2)
         if (s0 + kSlice - 1 >= kw) {                        // some q of the slice sees some key of the wave
             // row constants as initial accumulators: rows q = (i&3) + 8(i>>2) + 4hi
             f32x16_t s, dp;
@@ -572,7 +590,7 @@ void attn_dkdv_kernel(DkvArgs a) {
                 dp = mfma(row_frag(Ds, l32, 32 * ks + 16 * hi), row_frag(lds, wave * kKW + l32, 32 * ks + 16 * hi), dp);
             }
             const bool diag = s0 < kw + kKW - 1;
-            float p[16], ds[16];
+            float pr[16];
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 float pv = __builtin_amdgcn_exp2f(s[i] * a.sl2);
@@ -580,12 +598,13 @@ void attn_dkdv_kernel(DkvArgs a) {
                     const int q = s0 + (i & 3) + 8 * (i >> 2) + 4 * hi;
                     if (key > q) pv = 0.f;
                 }
-                p[i] = pv;
-                ds[i] = pv * dp[i];
+                pr[i] = pv;
             }
             bf16x8_t pf[2], sf[2];
-            pack_b_frags(p, pf[0], pf[1]);
-            pack_b_frags(ds, sf[0], sf[1]);
+            pack_b_frags(pr, pf[0], pf[1]);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) pr[i] *= dp[i];
+            pack_b_frags(pr, sf[0], sf[1]);
 #pragma unroll
             for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
@@ -615,6 +634,21 @@ void attn_dkdv_kernel(DkvArgs a) {
                 w.y = pk_bf16(dvt[dt][4 * g + 2], dvt[dt][4 * g + 3]);
                 *reinterpret_cast<uint2*>(dvr + d) = w;
             }
+    }
+}
+
+__global__ __launch_bounds__(kDkvWaves * 64, 2)
+void attn_dkdv_kernel(DkvArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kVImg + 2 * kSliceBuf];
+    const int nkb = (a.S + kKB - 1) / kKB;
+    const int total = ((nkb + 1) / 2) * a.Hkv * a.B;
+    // key blocks kb (long causal sweep) and nkb-1-kb (short) in one workgroup: equal work per
+    // workgroup (1594 vs 1946 us unpaired at B16 Hq32 Hkv8 S2048)
+    const PairTask t = pair_task(xcd_logical(blockIdx.x, total), nkb, 1, a.Hkv);
+#pragma nounroll
+    for (int i = 0; i < t.n; ++i) {
+        if (i) __syncthreads();
+        dkdv_block(a, lds, t.b, t.hk, t.blk[1 - i]);
     }
 }
 
@@ -700,7 +734,7 @@ int smt_attn_bwd(const smt_attn_tensor* q, const smt_attn_tensor* k, const smt_a
     ka.lse = lse; ka.delta = delta_ws;
     ka.B = B; ka.Hq = Hq; ka.Hkv = Hkv; ka.S = S; ka.sl2 = sl2; ka.scale = shape->scale;
     const int64_t nkb = (S + kKB - 1) / kKB;
-    hipLaunchKernelGGL(attn_dkdv_kernel, dim3((unsigned)(nkb * Hkv * B)), dim3(kDkvWaves * 64), 0, stream, ka);
+    hipLaunchKernelGGL(attn_dkdv_kernel, dim3((unsigned)(((nkb + 1) / 2) * Hkv * B)), dim3(kDkvWaves * 64), 0, stream, ka);
     return check_launch("attn_dkdv_kernel");
 }
 

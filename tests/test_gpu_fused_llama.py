@@ -108,11 +108,13 @@ def test_patched_mini_llama_matches_eager():
     model.zero_grad(set_to_none=True)
     try:
         counts = fl.patch_llama(model)
-        assert counts["rmsnorm"] == 9 and counts["mlp"] == 4
+        assert counts["rmsnorm"] == 9 and counts["mlp"] == 4 and counts["attention"] == 4
+        assert model.config._attn_implementation == "smt_flash"
         out_f = model(input_ids=ids, labels=ids, use_cache=False)
         out_f.loss.backward()
     finally:
         fl.unpatch_llama(model)
+    assert model.config._attn_implementation == "sdpa"
     rel = abs(out_f.loss.item() - out_e.loss.item()) / abs(out_e.loss.item())
     assert rel < 1e-3, (out_f.loss.item(), out_e.loss.item())
     worst = max(((p.grad.float() - ge[n].float()).norm() / ge[n].float().norm()).item()
