@@ -7,8 +7,11 @@
 
 One process per GPU (RCCL over xGMI for N > 1, weak scaling: B=16 x S=2048 per GPU). Per rank:
 
-1. LLaMA-3-8B architecture (HF ``LlamaForCausalLM``), random init (seed 1234), bf16, gradient
-   checkpointing on (fine_tune.py:192), synthetic uniform token batches, labels = input ids.
+1. LLaMA-3-8B architecture (HF ``LlamaForCausalLM``), random init (seed 1234), bf16, synthetic
+   uniform token batches, labels = input ids. Gradient checkpointing (fine_tune.py:192) is on for
+   the full-FT warm-up; in the SMT phase the activations stay resident in HBM (its peak is then
+   still below the warm-up's), and a short second measurement with checkpointing on (the
+   reference's memory policy) is reported under ``grad_ckpt_mode``.
 2. Warm-up: ``--full-ft-steps`` full fine-tuning steps through the engine (fp32-master AdamW over
    all 8.03 B params) with the gradient harvest of fine_tune.py:714-767 in HBM.
 3. Selection + conversion (fine_tune.py:257-384): 436 attention + 436 MLP tiles of 256x256
@@ -65,7 +68,14 @@ def parse():
     ap.add_argument("--mlp-ratio", type=float, default=None, help="default 0.00356 (8B), 0.03 (mini)")
     ap.add_argument("--calculate-strategy", default="abs_mean")
     ap.add_argument("--smt-lr", type=float, default=9.865e-6)
-    ap.add_argument("--no-grad-ckpt", action="store_true")
+    ap.add_argument("--grad-ckpt", action="store_true",
+                    help="recompute each decoder layer in the SMT phase's backward (the reference's "
+                         "fine_tune.py:192 memory policy) for the timed steps; default: activations stay "
+                         "resident in HBM (the SMT phase then peaks below the warm-up phase)")
+    ap.add_argument("--no-grad-ckpt", action="store_true", help=argparse.SUPPRESS)   # the default now
+    ap.add_argument("--ref-mode-steps", type=int, default=4,
+                    help="after the timed steps, also time this many steps with gradient checkpointing "
+                         "(reported under 'grad_ckpt_mode'; 0 disables)")
     ap.add_argument("--sdpa-attention", action="store_true",
                     help="keep transformers' sdpa (aotriton) attention instead of the gfx950 flash attention")
     ap.add_argument("--eager-ops", action="store_true",
@@ -285,7 +295,7 @@ def main():
         f"({100.0 * trainable / total_params:.3f}% of {total_params})")
 
     # ---- SMT phase ----
-    if args.no_grad_ckpt:
+    if not args.grad_ckpt:
         engine.module.gradient_checkpointing_disable()
     smt_batches = batches(args.warmup + args.steps, B, S, vocab, rank, device)
     torch.cuda.reset_peak_memory_stats(device)
@@ -320,6 +330,32 @@ def main():
     value = tokens / elapsed
     w = timer.summary()
 
+    # ---- the reference's memory policy (per-layer recompute), same engine and tiles ----
+    ckpt_mode = None
+    if args.ref_mode_steps > 0 and not args.grad_ckpt:
+        engine.module.gradient_checkpointing_enable()
+        ref_batches = batches(1 + args.ref_mode_steps, B, S, vocab, rank, device, offset=50000)
+        step(ref_batches[0])
+        torch.cuda.synchronize()
+        torch.cuda.reset_peak_memory_stats(device)
+        if world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+        for b in ref_batches[1:]:
+            step(b)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        r = torch.tensor([time.perf_counter() - t1, torch.cuda.max_memory_allocated(device) / 1e9],
+                         dtype=torch.float64, device=device)
+        if world > 1:
+            dist.all_reduce(r, op=dist.ReduceOp.MAX)
+        ckpt_mode = {"grad_ckpt": True, "steps": args.ref_mode_steps,
+                     "value": round(world * B * S * args.ref_mode_steps / r[0].item(), 1),
+                     "ms_per_step": round(r[0].item() / args.ref_mode_steps * 1e3, 2),
+                     "peak_hbm_gb": round(r[1].item(), 2)}
+        del ref_batches
+
     if rank == 0:
         per_gpu = value / world
         roofline = None
@@ -347,10 +383,12 @@ def main():
                                    "training step (fwd+bwd+sparse AdamW)",
                        "global_batch": B * world, "seq_len": S, "parallelism": f"dp{world}",
                        "tiles": n_tiles, "trainable_params": trainable,
-                       "grad_ckpt": not args.no_grad_ckpt, "full_ft_steps": args.full_ft_steps,
+                       "grad_ckpt": bool(args.grad_ckpt), "full_ft_steps": args.full_ft_steps,
                        "fused_llama_ops": not args.eager_ops,
-                       "attention": "sdpa" if (args.eager_ops or args.sdpa_attention) else "smt_flash"},
+                       "attention": "sdpa" if (args.eager_ops or args.sdpa_attention) else "smt_flash",
+                       "loss": "transformers" if args.eager_ops else "smt_ce"},
             "peak_hbm_gb": round(peak.item(), 2), "warmup_peak_hbm_gb": round(warm_peak, 2),
+            "grad_ckpt_mode": ckpt_mode,
             "step_mfma_frac": round(per_gpu * F_ALG_GFLOP_PER_TOKEN * 1e9 / (PEAK_BF16_TFLOPS * 1e12), 4),
             "roofline": roofline, "cpu_baseline": cpu,
             "final_loss": round(loss.item(), 5),

@@ -54,6 +54,18 @@ int smt_swiglu_fwd(const void* gate, const void* up, void* out, int64_t n, hipSt
 int smt_swiglu_bwd(const void* gate, const void* up, const void* grad_out, void* grad_gate, void* grad_up, int64_t n,
                    hipStream_t stream);
 
+/* Causal-LM cross entropy over bf16 logits [rows, vocab] (transformers ForCausalLMLoss:
+ * logits.float() -> log_softmax -> nll), without materialising fp32 logits.
+ * Forward:  lse[r] = logsumexp(float(logits[r, :]));  loss[r] = lse[r] - float(logits[r, label[r]]),
+ *           0 where label[r] == ignore_index, NaN where the label is outside [0, vocab).
+ * Backward: dlogits[r, j] = bf16((exp(logits[r, j] - lse[r]) - [j == label[r]]) * scale[0]),
+ *           0 on ignored rows. `scale` is a device float (d loss / normaliser), so no host sync.
+ * vocab % 8 == 0, 16-byte aligned rows. */
+int smt_ce_fwd(const void* logits, int64_t ld, const int64_t* labels, int64_t rows, int64_t vocab,
+               int64_t ignore_index, float* lse, float* loss, hipStream_t stream);
+int smt_ce_bwd(const void* logits, int64_t ld, const int64_t* labels, const float* lse, const float* scale,
+               int64_t rows, int64_t vocab, int64_t ignore_index, void* dlogits, int64_t ld_d, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,22 @@
+#!/bin/bash
+# One GPU call: GPU test suite, headline bench, and (optionally) a GEMM TunableOp tuning pass.
+#   STEPS="tests bench tune" bash scripts/gpu_session.sh
+set -o pipefail
+OUT=gpurun_out/${TAG:-s}
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+for s in ${STEPS:-tests bench}; do
+  case $s in
+    tests)
+      timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+        > $OUT/tests.log 2>&1 || { echo "tests failed"; tail -30 $OUT/tests.log; exit 11; } ;;
+    bench)
+      timeout -k 10 500 python3 bench.py --out $OUT/bench.json > $OUT/bench.log 2>&1 || { echo "bench failed"; tail -30 $OUT/bench.log; exit 12; } ;;
+    tune)
+      PYTORCH_TUNABLEOP_ENABLED=1 PYTORCH_TUNABLEOP_TUNING=1 PYTORCH_TUNABLEOP_VERBOSE=1 \
+      PYTORCH_TUNABLEOP_FILENAME=$OUT/tunableop_results%d.csv \
+        timeout -k 10 900 python3 -u scripts/gemm_bench.py > $OUT/gemm_tuned.jsonl 2> $OUT/gemm_tuned.log \
+        || { echo "tune failed"; tail -30 $OUT/gemm_tuned.log; exit 13; } ;;
+  esac
+done
+echo "session ok"

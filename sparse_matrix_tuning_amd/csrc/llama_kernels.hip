@@ -259,11 +259,150 @@ void swiglu_bwd_kernel(const uint16_t* __restrict__ g, const uint16_t* __restric
     st8(du + i * 8, ou);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Causal-LM cross entropy (transformers ForCausalLMLoss: logits.float() -> log_softmax -> nll with
+// ignore_index). The eager chain writes an fp32 copy of the [rows, vocab] logits (16.8 GB at
+// B16 x S2048 x V128256), a log_softmax output of the same size, and an fp32 gradient cast back to
+// bf16. Here the forward reads the bf16 logits once (per-row online max / sum of exp, one workgroup
+// per row) and the backward reads them once more and writes the bf16 gradient.
+// Softmax arithmetic in the log2 domain: y = x * log2(e), exp via v_exp_f32.
+// ------------------------------------------------------------------------------------------------
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+constexpr float kNegInf = -__builtin_huge_valf();
+constexpr int kCeThreads = 256;
+
+// (m, s): running max of the log2-scaled logits and sum of exp2(y - m)
+__device__ __forceinline__ void lse_merge(float& m, float& s, float m2, float s2) {
+    const float M = fmaxf(m, m2);
+    if (M == kNegInf) return;                           // both still empty
+    s = s * __builtin_amdgcn_exp2f(m - M) + s2 * __builtin_amdgcn_exp2f(m2 - M);
+    m = M;
+}
+
+__device__ __forceinline__ void lse_chunk(const F8& v, float& m, float& s) {
+    float y[8];
+    float cm = kNegInf;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        y[j] = v.v[j] * kLog2e;
+        cm = fmaxf(cm, y[j]);
+    }
+    if (cm > m) {
+        s *= __builtin_amdgcn_exp2f(m - cm);
+        m = cm;
+    }
+    if (m == kNegInf) return;                           // every logit so far is -inf
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += __builtin_amdgcn_exp2f(y[j] - m);
+}
+
+__global__ __launch_bounds__(kCeThreads)
+void ce_fwd_kernel(const uint16_t* __restrict__ logits, int64_t ld, const int64_t* __restrict__ labels, int64_t V,
+                   int64_t ignore_index, float* __restrict__ lse, float* __restrict__ loss) {
+    __shared__ float wm[kCeThreads / 64], wsum[kCeThreads / 64];
+    const int64_t row = blockIdx.x;
+    const uint16_t* xr = logits + row * ld;
+    const int tid = threadIdx.x;
+    const int64_t n8 = V >> 3;
+    float m = kNegInf, s = 0.f;
+    int64_t c = tid;
+    for (; c + 3 * kCeThreads < n8; c += 4 * kCeThreads) {     // 4 x 16 B in flight per lane
+        const F8 a = ld8(xr + c * 8), b = ld8(xr + (c + kCeThreads) * 8);
+        const F8 d = ld8(xr + (c + 2 * kCeThreads) * 8), e = ld8(xr + (c + 3 * kCeThreads) * 8);
+        lse_chunk(a, m, s);
+        lse_chunk(b, m, s);
+        lse_chunk(d, m, s);
+        lse_chunk(e, m, s);
+    }
+    for (; c < n8; c += kCeThreads) lse_chunk(ld8(xr + c * 8), m, s);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const float m2 = __shfl_xor(m, off, 64), s2 = __shfl_xor(s, off, 64);
+        lse_merge(m, s, m2, s2);
+    }
+    if ((tid & 63) == 0) {
+        wm[tid >> 6] = m;
+        wsum[tid >> 6] = s;
+    }
+    __syncthreads();
+    if (tid == 0) {
+#pragma unroll
+        for (int w = 1; w < kCeThreads / 64; ++w) lse_merge(m, s, wm[w], wsum[w]);
+        const float l = (m + log2f(s)) * kLn2;
+        lse[row] = l;
+        const int64_t lab = labels[row];
+        float out;
+        if (lab == ignore_index) out = 0.f;
+        else if (lab < 0 || lab >= V) out = __builtin_nanf("");
+        else out = l - bf((uint32_t)xr[lab]);
+        loss[row] = out;
+    }
+}
+
+__device__ __forceinline__ F8 ce_grad8(const F8& v, int64_t col0, int64_t lab, float l2, float w) {
+    F8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(v.v[j], kLog2e, -l2)) * w;
+        o.v[j] = (col0 + j == lab) ? p - w : p;
+    }
+    return o;
+}
+
+__global__ __launch_bounds__(kCeThreads)
+void ce_bwd_kernel(const uint16_t* __restrict__ logits, int64_t ld, const int64_t* __restrict__ labels,
+                   const float* __restrict__ lse, const float* __restrict__ scale, int64_t V, int64_t ignore_index,
+                   uint16_t* __restrict__ dlogits, int64_t ldd) {
+    const int64_t row = blockIdx.x;
+    const int64_t lab = labels[row];
+    const float w = (lab == ignore_index) ? 0.f : scale[0];
+    const float l2 = lse[row] * kLog2e;
+    const uint16_t* xr = logits + row * ld;
+    uint16_t* dr = dlogits + row * ldd;
+    const int64_t n8 = V >> 3;
+    int64_t c = threadIdx.x;
+    for (; c + kCeThreads < n8; c += 2 * kCeThreads) {
+        const F8 a = ld8(xr + c * 8), b = ld8(xr + (c + kCeThreads) * 8);
+        st8(dr + c * 8, ce_grad8(a, c * 8, lab, l2, w));
+        st8(dr + (c + kCeThreads) * 8, ce_grad8(b, (c + kCeThreads) * 8, lab, l2, w));
+    }
+    for (; c < n8; c += kCeThreads) st8(dr + c * 8, ce_grad8(ld8(xr + c * 8), c * 8, lab, l2, w));
+}
+
 }  // namespace
 
 extern "C" {
 
 const char* smt_model_ops_last_error(void) { return g_err; }
+
+int smt_ce_fwd(const void* logits, int64_t ld, const int64_t* labels, int64_t rows, int64_t vocab,
+               int64_t ignore_index, float* lse, float* loss, hipStream_t stream) {
+    if (rows < 0 || vocab <= 0 || (vocab & 7) || ld < vocab)
+        return fail(-1, "smt_ce_fwd: bad sizes rows=%lld vocab=%lld ld=%lld (vocab %% 8 == 0, ld >= vocab)",
+                    (long long)rows, (long long)vocab, (long long)ld);
+    if (rows == 0) return 0;
+    if (!logits || !labels || !lse || !loss) return fail(-1, "smt_ce_fwd: null pointer");
+    if (!aligned16(logits) || (ld & 7)) return fail(-2, "smt_ce_fwd: 16-byte aligned rows required");
+    if (rows > 0x7fffffffLL) return fail(-1, "smt_ce_fwd: too many rows");
+    hipLaunchKernelGGL(ce_fwd_kernel, dim3((unsigned)rows), dim3(kCeThreads), 0, stream, (const uint16_t*)logits, ld,
+                       labels, vocab, ignore_index, lse, loss);
+    return check_launch("ce_fwd_kernel");
+}
+
+int smt_ce_bwd(const void* logits, int64_t ld, const int64_t* labels, const float* lse, const float* scale,
+               int64_t rows, int64_t vocab, int64_t ignore_index, void* dlogits, int64_t ld_d, hipStream_t stream) {
+    if (rows < 0 || vocab <= 0 || (vocab & 7) || ld < vocab || ld_d < vocab)
+        return fail(-1, "smt_ce_bwd: bad sizes rows=%lld vocab=%lld", (long long)rows, (long long)vocab);
+    if (rows == 0) return 0;
+    if (!logits || !labels || !lse || !scale || !dlogits) return fail(-1, "smt_ce_bwd: null pointer");
+    if (!aligned16(logits) || !aligned16(dlogits) || (ld & 7) || (ld_d & 7))
+        return fail(-2, "smt_ce_bwd: 16-byte aligned rows required");
+    if (rows > 0x7fffffffLL) return fail(-1, "smt_ce_bwd: too many rows");
+    hipLaunchKernelGGL(ce_bwd_kernel, dim3((unsigned)rows), dim3(kCeThreads), 0, stream, (const uint16_t*)logits, ld,
+                       labels, lse, scale, vocab, ignore_index, (uint16_t*)dlogits, ld_d);
+    return check_launch("ce_bwd_kernel");
+}
 
 int smt_rmsnorm_fwd(const void* x, int64_t ld_x, const void* weight, void* y, int64_t ld_y, float* rstd,
                     int64_t rows, int32_t hidden, float eps, hipStream_t stream) {

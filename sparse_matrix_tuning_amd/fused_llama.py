@@ -13,6 +13,10 @@ It also routes the decoder's attention to a gfx950 causal flash attention (forwa
 ``AttentionInterface`` as ``"smt_flash"``; sdpa on this torch build runs aotriton at 25-27 % of the
 step. Tolerances vs an fp32 reference are in tests/test_gpu_attention.py.
 
+The causal-LM loss (transformers ``ForCausalLMLoss``: ``logits.float()`` then cross entropy) becomes
+two row kernels over the bf16 logits (``smt_ce_fwd`` / ``smt_ce_bwd``), so the 16.8 GB fp32 logits
+copy, its log-softmax and its fp32 gradient are never materialised (tests/test_gpu_cross_entropy.py).
+
 Only bf16 CUDA tensors take the fused path; anything else raises (no silent fallback).
 """
 from __future__ import annotations
@@ -191,6 +195,62 @@ def fused_mlp_forward(self, x):
 
 
 # ------------------------------------------------------------------------------------------------
+# causal-LM cross entropy
+# ------------------------------------------------------------------------------------------------
+class FusedCrossEntropyFn(torch.autograd.Function):
+    """``F.cross_entropy(logits.float(), labels, ignore_index, reduction=sum) / denom`` over bf16
+    logits ``[N, V]`` without the fp32 copy: one pass for the row log-sum-exp, one for the bf16
+    gradient. ``denom``: fp32 device scalar (valid-label count for the mean, or num_items_in_batch)."""
+
+    @staticmethod
+    def forward(ctx, logits2d, labels, ignore_index, denom):
+        _need(logits2d, "cross entropy logits")
+        if logits2d.stride(1) != 1 or logits2d.stride(0) % 8 or logits2d.data_ptr() % 16:
+            logits2d = logits2d.contiguous()
+        N, V = logits2d.shape
+        labels = labels.to(device=logits2d.device, dtype=torch.int64).contiguous()
+        if labels.numel() != N:
+            raise ValueError(f"cross entropy: {labels.numel()} labels for {N} logit rows")
+        lse = torch.empty(N, dtype=torch.float32, device=logits2d.device)
+        rows = torch.empty(N, dtype=torch.float32, device=logits2d.device)
+        rc = _hip.load().smt_ce_fwd(logits2d.data_ptr(), logits2d.stride(0), labels.data_ptr(), N, V,
+                                    int(ignore_index), lse.data_ptr(), rows.data_ptr(), _stream(logits2d))
+        _hip._check(rc, "smt_ce_fwd")
+        ctx.save_for_backward(logits2d, labels, lse, denom)
+        ctx.ignore_index = int(ignore_index)
+        return rows.sum() / denom
+
+    @staticmethod
+    def backward(ctx, dloss):
+        logits2d, labels, lse, denom = ctx.saved_tensors
+        N, V = logits2d.shape
+        scale = (dloss.float() / denom).reshape(1).contiguous()
+        dlogits = torch.empty_like(logits2d)
+        rc = _hip.load().smt_ce_bwd(logits2d.data_ptr(), logits2d.stride(0), labels.data_ptr(), lse.data_ptr(),
+                                    scale.data_ptr(), N, V, ctx.ignore_index, dlogits.data_ptr(), dlogits.stride(0),
+                                    _stream(logits2d))
+        _hip._check(rc, "smt_ce_bwd")
+        return dlogits, None, None, None
+
+
+def fused_causal_lm_loss(logits, labels, vocab_size, num_items_in_batch=None, ignore_index=-100,
+                         shift_labels=None, **kwargs):
+    """Drop-in for ``transformers.loss.loss_utils.ForCausalLMLoss`` (the loss of
+    ``LlamaForCausalLM.forward``): labels shifted left by one with ``ignore_index`` padding, mean over
+    non-ignored tokens, or sum / ``num_items_in_batch``."""
+    if shift_labels is None:
+        labels = nn.functional.pad(labels, (0, 1), value=ignore_index)
+        shift_labels = labels[..., 1:]
+    logits2d = logits.reshape(-1, vocab_size)
+    shift = shift_labels.reshape(-1).to(logits2d.device)
+    if num_items_in_batch is None:
+        denom = (shift != ignore_index).sum().to(torch.float32)
+    else:
+        denom = torch.as_tensor(num_items_in_batch, device=logits2d.device).to(torch.float32)
+    return FusedCrossEntropyFn.apply(logits2d, shift, ignore_index, denom)
+
+
+# ------------------------------------------------------------------------------------------------
 # causal flash attention
 # ------------------------------------------------------------------------------------------------
 def _attn_tensor(t: torch.Tensor) -> _hip.AttnTensor:
@@ -304,14 +364,18 @@ def eager_apply_rotary_pos_emb(*a, **k):
     return _ml() and _EAGER["rope"](*a, **k)
 
 
-def patch_llama(model: nn.Module, attention: bool = True) -> dict:
+def patch_llama(model: nn.Module, attention: bool = True, loss: bool = True) -> dict:
     """Route a transformers LLaMA model's RMSNorm / RoPE / SwiGLU (and, with ``attention``, its
-    attention) through the fused kernels. RoPE is patched at module level
-    (``modeling_llama.apply_rotary_pos_emb``, looked up by ``LlamaAttention.forward`` at call time);
-    attention by switching ``config._attn_implementation`` to the registered ``smt_flash``.
+    attention; with ``loss``, its causal-LM loss) through the fused kernels. RoPE is patched at
+    module level (``modeling_llama.apply_rotary_pos_emb``, looked up by ``LlamaAttention.forward`` at
+    call time); attention by switching ``config._attn_implementation`` to the registered
+    ``smt_flash``; the loss through the model's ``loss_function`` attribute.
     Returns counts of patched modules. Idempotent."""
     ml = _ml()
-    counts = {"rmsnorm": 0, "mlp": 0, "rope": 1, "attention": 0}
+    counts = {"rmsnorm": 0, "mlp": 0, "rope": 1, "attention": 0, "loss": 0}
+    if loss and hasattr(type(model), "loss_function"):
+        model.loss_function = fused_causal_lm_loss
+        counts["loss"] = 1
     if attention:
         cfg = getattr(model, "config", None)
         if cfg is None:
@@ -341,6 +405,8 @@ def unpatch_llama(model: nn.Module = None) -> None:
     if model is not None and "smt_prev_attn" in _EAGER and getattr(model, "config", None) is not None:
         model.config._attn_implementation = _EAGER.pop("smt_prev_attn")
     if model is not None:
+        if "_loss_function" in model.__dict__:
+            del model.__dict__["_loss_function"]
         for m in model.modules():
             if isinstance(m, (ml.LlamaRMSNorm, ml.LlamaMLP)) and "forward" in m.__dict__:
                 del m.__dict__["forward"]

@@ -113,8 +113,13 @@ def test_golden_linearz_fixture_reproduces():
     tiles = [tuple(t) for t in d["tiles"].tolist()]
     y = ref.linearz_forward(x, W)
     gi, gw = ref.linearz_backward(g, x, W, tiles)
-    assert torch.equal(y, as_bf16(d["y"]))
-    assert torch.equal(gi, as_bf16(d["grad_input"]))
+    # torch-CPU's bf16 GEMM (oneDNN) picks its fp32 blocking from the host ISA, so the final bf16
+    # rounding of the dense products can differ by one ulp between hosts (the fixture was made on an
+    # AMD EPYC host; 0.02 % of y / grad_input differ by one ulp on an Intel Xeon host).
+    for got, want in ((y, as_bf16(d["y"])), (gi, as_bf16(d["grad_input"]))):
+        diff = (got.float() - want.float()).abs()
+        assert (diff <= want.float().abs() * 2 ** -7).all()
+        assert (diff > 0).float().mean().item() < 1e-3
     assert torch.equal(gw, as_bf16(d["grad_tiles_ref"]))
 
 
@@ -180,7 +185,10 @@ def test_golden_channel_fixtures_reproduce():
     x, g, W, idx = bf(d["x"]), bf(d["g"]), bf(d["W"]), d["idx"].tolist()
     y, partial = ref.linearchannel_forward(x, W, idx)
     gi, gw = ref.linearchannel_backward(g, partial, W)
-    assert torch.equal(y, bf(d["y"])) and torch.equal(gi, bf(d["grad_input"])) and torch.equal(gw, bf(d["grad_weight_ref"]))
+    for got, want in ((y, bf(d["y"])), (gi, bf(d["grad_input"])), (gw, bf(d["grad_weight_ref"]))):
+        diff = (got.float() - want.float()).abs()      # host-ISA bf16 GEMM rounding, see above
+        assert (diff <= want.float().abs() * 2 ** -7).all()
+        assert (diff > 0).float().mean().item() < 1e-3
 
 
 def test_linearchannel_grad_is_the_column_gradient_fp64():
