@@ -12,6 +12,8 @@
  *   smt_tile_scatter      deepspeed/smt/smt.py:332-341   per-forward write-back tiles -> W
  *                         (also smt.py:429-439, the merge in convert_matrix_sparsity_to_linear_layer)
  *   smt_tile_wgrad        deepspeed/smt/smt.py:382-404   per-tile sum_b g[b,:,rows]^T x[b,:,cols]
+ *   smt_colblock_gather   deepspeed/smt/smt.py:351-358   ctx.list1: the input column slices linearZ keeps
+ *                         for its backward (packed copy of the distinct 256-column blocks)
  *   smt_grad_accumulate   deepspeed/fine_tune.py:724-741, 751-764   warm-up fp32 grad harvest
  *   smt_block_score       deepspeed/smt/smt_helper.py:67-78, 233-251   per-256x256-block scores
  *   smt_sq_norm           DeepSpeed bf16/ZeRO global grad-norm for gradient_clipping=1.0
@@ -122,6 +124,13 @@ int smt_tile_wgrad(const void* grad_out, int64_t ld_grad_out,
                    const int32_t* tile_rc_dev, const int32_t* order_dev, int32_t n_tiles,
                    void* grad_tiles, int32_t out_dtype, int32_t accumulate,
                    void* workspace, size_t workspace_bytes, hipStream_t stream);
+
+/*
+ * out[t, j*256 : j*256+256] = x[t, c_j*256 : c_j*256+256] for the n_cb column blocks c_j of
+ * col_blocks_dev (device int32); x [T, ld_x] and out [T, n_cb*256] row-major, 16-bit elements.
+ */
+int smt_colblock_gather(const void* x, int64_t ld_x, int64_t T, const int32_t* col_blocks_dev, int32_t n_cb,
+                        void* out, hipStream_t stream);
 
 /* tiles[i] = W[r_i*256:+256, c_i*256:+256]; elem_bytes 2 or 4. */
 int smt_tile_gather(const void* weight, int64_t ld_weight, int32_t elem_bytes,

@@ -29,7 +29,10 @@ def timed(fn, iters=10):
 
 def main():
     torch.manual_seed(0)
+    only = [n for n in os.environ.get("GEMM_SHAPES", "").split(",") if n]
     for name, (fin, fout) in SHAPES.items():
+        if only and name not in only:
+            continue
         x = torch.randn(T, fin, device="cuda", dtype=torch.bfloat16)
         W = torch.randn(fout, fin, device="cuda", dtype=torch.bfloat16) * 0.02
         g = torch.randn(T, fout, device="cuda", dtype=torch.bfloat16)

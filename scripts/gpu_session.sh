@@ -12,11 +12,17 @@ for s in ${STEPS:-tests bench}; do
         > $OUT/tests.log 2>&1 || { echo "tests failed"; tail -30 $OUT/tests.log; exit 11; } ;;
     bench)
       timeout -k 10 500 python3 bench.py --out $OUT/bench.json > $OUT/bench.log 2>&1 || { echo "bench failed"; tail -30 $OUT/bench.log; exit 12; } ;;
+    bench_notune)
+      timeout -k 10 500 python3 bench.py --tunableop off --cpu-baseline-seconds 0 --ref-mode-steps 0 --out $OUT/bench_notune.json \
+        > $OUT/bench_notune.log 2>&1 || { echo "bench_notune failed"; tail -30 $OUT/bench_notune.log; exit 14; } ;;
     tune)
-      PYTORCH_TUNABLEOP_ENABLED=1 PYTORCH_TUNABLEOP_TUNING=1 PYTORCH_TUNABLEOP_VERBOSE=1 \
+      # tuning one large shape can run for minutes without output: keep a heartbeat file growing
+      ( while sleep 30; do date >> $OUT/tune_heartbeat; done ) & HB=$!
+      GEMM_SHAPES=${GEMM_SHAPES:-} PYTORCH_TUNABLEOP_ENABLED=1 PYTORCH_TUNABLEOP_TUNING=1 PYTORCH_TUNABLEOP_VERBOSE=1 \
       PYTORCH_TUNABLEOP_FILENAME=$OUT/tunableop_results%d.csv \
         timeout -k 10 900 python3 -u scripts/gemm_bench.py > $OUT/gemm_tuned.jsonl 2> $OUT/gemm_tuned.log \
-        || { echo "tune failed"; tail -30 $OUT/gemm_tuned.log; exit 13; } ;;
+        || { kill $HB; echo "tune failed"; tail -30 $OUT/gemm_tuned.log; exit 13; }
+      kill $HB ;;
   esac
 done
 echo "session ok"

@@ -28,7 +28,7 @@ _DT = {torch.bfloat16: DTYPE_BF16, torch.float32: DTYPE_FP32, torch.float16: DTY
 # Every function the headers declare (include/smt_hip.h, smt_model_ops.h, smt_attention.h); tests check the
 # library exports each of them.
 ABI_FUNCTIONS = (
-    "smt_last_error", "smt_abi_version", "smt_wgrad_workspace_bytes", "smt_tile_wgrad",
+    "smt_last_error", "smt_abi_version", "smt_wgrad_workspace_bytes", "smt_tile_wgrad", "smt_colblock_gather",
     "smt_tile_gather", "smt_tile_scatter", "smt_grad_accumulate", "smt_block_score",
     "smt_sq_norm", "smt_adamw_step",
     "smt_row_gather", "smt_row_scatter", "smt_column_gather", "smt_act_accumulate", "smt_channel_score",
@@ -89,6 +89,7 @@ _SIGS = {
     "smt_abi_version": (ctypes.c_int, []),
     "smt_wgrad_workspace_bytes": (_SZ, [_I64, _I32]),
     "smt_tile_wgrad": (ctypes.c_int, [_P, _I64, _P, _I64, _I64, _P, _P, _I32, _P, _I32, _I32, _P, _SZ, _P]),
+    "smt_colblock_gather": (ctypes.c_int, [_P, _I64, _I64, _P, _I32, _P, _P]),
     "smt_tile_gather": (ctypes.c_int, [_P, _I64, _I32, _P, _I32, _P, _P]),
     "smt_tile_scatter": (ctypes.c_int, [_P, _I64, _I32, _P, _I32, _P, _P]),
     "smt_grad_accumulate": (ctypes.c_int, [_P, _I32, _I64, _P]),
@@ -240,6 +241,19 @@ def tile_wgrad(grad_out2d: torch.Tensor, x2d: torch.Tensor, tile_rc: torch.Tenso
                                _ptr(tile_rc), _ptr(order), n, _ptr(out), _DT[out.dtype], int(bool(accumulate)),
                                _ptr(ws), ws_bytes, _stream(dev))
     _check(rc, "smt_tile_wgrad")
+    return out
+
+
+def colblock_gather(x2d: torch.Tensor, col_blocks: torch.Tensor) -> torch.Tensor:
+    """[T, n_cb*256] packed copy of the 256-column blocks ``col_blocks`` (device int32) of x2d."""
+    dev = _require_device(x2d, col_blocks)
+    if x2d.dim() != 2 or x2d.stride(1) != 1 or x2d.element_size() != 2:
+        raise ValueError("colblock_gather: x must be a 2-D row-major 16-bit tensor")
+    n_cb = col_blocks.numel()
+    out = torch.empty(x2d.shape[0], n_cb * BLOCK, dtype=x2d.dtype, device=dev)
+    rc = load().smt_colblock_gather(_ptr(x2d), x2d.stride(0), x2d.shape[0], _ptr(col_blocks), n_cb, _ptr(out),
+                                    _stream(dev))
+    _check(rc, "smt_colblock_gather")
     return out
 
 

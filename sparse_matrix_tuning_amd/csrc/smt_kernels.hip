@@ -823,6 +823,23 @@ void column_gather_kernel(const uint16_t* __restrict__ x, int64_t ld_x, int64_t 
     *reinterpret_cast<uint4*>(out + t * ld_out + j0) = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// The 256-column blocks of x that a module's tiles read, packed side by side:
+// out[t, j*256 + k] = x[t, col_blocks[j]*256 + k]. linearZ saves this [T, n_cb*256] slab for its
+// backward instead of the whole input (the tile wgrad reads nothing else). 16 B per thread; one
+// wave covers two (row, block) pairs of 512 contiguous bytes on both sides.
+__global__ __launch_bounds__(256)
+void colblock_gather_kernel(const uint16_t* __restrict__ x, int64_t ld_x, int64_t T,
+                            const int32_t* __restrict__ col_blocks, int32_t n_cb, uint16_t* __restrict__ out) {
+    const int64_t per_row = (int64_t)n_cb * 32;                  // 16-B chunks per output row
+    const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t t = v / per_row;
+    if (t >= T) return;
+    const int r = (int)(v - t * per_row);
+    const int j = r >> 5, ch = r & 31;
+    const uint4 val = *reinterpret_cast<const uint4*>(x + t * ld_x + (int64_t)col_blocks[j] * kTile + ch * 8);
+    *reinterpret_cast<uint4*>(out + t * per_row * 8 + (int64_t)j * kTile + ch * 8) = val;
+}
+
 // Activation harvest (the forward hook of fine_tune.py:636-667 plus the batch sum of
 // smt_helper.py:170): acc[s, c] (+)= sum_{b < B} |x[b, s, c]| in fp64, b ascending, then added to acc.
 // One thread per (s, 8 columns): B 16-byte loads, 64 B read-modify-write of acc.
@@ -1128,6 +1145,20 @@ int smt_column_gather(const void* x, int64_t ld_x, int64_t T, const int32_t* col
     hipLaunchKernelGGL(column_gather_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, static_cast<const uint16_t*>(x),
                        ld_x, T, cols_dev, n_cols, static_cast<uint16_t*>(out), ld_out);
     return check_launch("column_gather_kernel");
+}
+
+int smt_colblock_gather(const void* x, int64_t ld_x, int64_t T, const int32_t* col_blocks_dev, int32_t n_cb,
+                        void* out, hipStream_t stream) {
+    if (T < 0 || n_cb < 0 || ld_x < 0) return fail(SMT_E_INVALID, "smt_colblock_gather: negative size");
+    if (T == 0 || n_cb == 0) return SMT_OK;
+    if (!x || !out || !col_blocks_dev) return fail(SMT_E_INVALID, "smt_colblock_gather: null pointer");
+    if (!aligned16(x) || !aligned16(out) || (ld_x & 7))
+        return fail(SMT_E_ALIGN, "smt_colblock_gather: 16-byte aligned rows required (ld_x %% 8 == 0)");
+    const int64_t blocks = (T * (int64_t)n_cb * 32 + 255) / 256;
+    if (blocks > 0x7fffffffLL) return fail(SMT_E_INVALID, "smt_colblock_gather: too large");
+    hipLaunchKernelGGL(colblock_gather_kernel, dim3((unsigned)blocks), dim3(256), 0, stream,
+                       static_cast<const uint16_t*>(x), ld_x, T, col_blocks_dev, n_cb, static_cast<uint16_t*>(out));
+    return check_launch("colblock_gather_kernel");
 }
 
 int smt_act_accumulate(const void* x, int32_t x_dtype, int64_t ld_x, int64_t batch_stride, int32_t B, int32_t S,

@@ -11,8 +11,11 @@ returns an engine with that surface, designed for the SMT phase on one GPU per p
   operating point: 0.92 GB).
 * ``linearZ.backward`` writes each module's tile gradients straight into that fp32 buffer through
   the module's gradient sink (no autograd accumulation, no bf16 rounding).
-* At the gradient-accumulation boundary the engine issues ONE RCCL all-reduce (sum) of the flat
-  gradient buffer (torch.distributed "nccl" = RCCL over xGMI); averaging (1/world) is folded into
+* With more than one rank, the flat gradient buffer is cut into buckets of whole modules
+  (``reduce_bucket_size`` elements, DeepSpeed's knob, default 4 M). Backward fills the buffer from
+  the end (it is packed in forward order); as soon as every module of a bucket has written its
+  tiles, that bucket's RCCL all-reduce (sum; torch.distributed "nccl" = RCCL over xGMI) is issued
+  asynchronously, so the exchange overlaps the rest of backward. Averaging (1/world) is folded into
   the optimizer kernels.
 * ``step()`` = one ``smt_sq_norm`` (global norm for ``gradient_clipping``) + one fused
   ``smt_adamw_step`` launch per parameter group that clips, updates fp32 master/moments, writes the
@@ -91,20 +94,84 @@ class SMTFusedAdam(torch.optim.Optimizer):
 class _GradSink:
     """Where ``linearZ.backward`` writes one module's fp32 tile gradients."""
 
-    __slots__ = ("buffer", "engine")
+    __slots__ = ("buffer", "engine", "buckets", "index")
 
-    def __init__(self, buffer: torch.Tensor, engine: "SMTEngine"):
+    def __init__(self, buffer: torch.Tensor, engine: "SMTEngine", buckets: "TileGradBuckets" = None, index: int = 0):
         self.buffer = buffer
         self.engine = engine
+        self.buckets = buckets
+        self.index = index
 
     def take_accumulate(self) -> bool:
         return self.engine._accumulate_tiles
+
+    def mark_ready(self) -> None:
+        """Called by ``linearZ.backward`` once this module's tile-gradient kernels are enqueued."""
+        if self.buckets is not None:
+            self.buckets.ready(self.index)
+
+
+class TileGradBuckets:
+    """Bucketed, backward-overlapped all-reduce of one packed fp32 tile-gradient buffer.
+
+    ``module_ranges``: ascending, contiguous ``(start, end)`` element ranges of the modules in the
+    buffer (forward order). Consecutive modules are grouped into buckets of at least
+    ``bucket_elems`` elements. After :meth:`arm`, every :meth:`ready` call counts one module of its
+    bucket; the last one issues ``all_reduce(buffer[bucket], async_op=True)``. The collective is
+    enqueued on the process group's stream behind the current stream's work (the tile-gradient
+    kernels), so it runs while backward continues. :meth:`finish` issues the buckets whose modules
+    did not report (not used in this forward) and makes the current stream wait for all of them."""
+
+    def __init__(self, buffer: torch.Tensor, module_ranges: List[tuple], bucket_elems: int):
+        self.buffer = buffer
+        self.buckets: List[list] = []          # [start, end, n_modules]
+        self.bucket_of: List[int] = []
+        for s, e in module_ranges:
+            if not self.buckets or self.buckets[-1][1] - self.buckets[-1][0] >= bucket_elems:
+                self.buckets.append([s, e, 0])
+            b = self.buckets[-1]
+            if s != b[1] and b[2]:
+                raise ValueError("module ranges must be contiguous and ascending")
+            b[1] = e
+            b[2] += 1
+            self.bucket_of.append(len(self.buckets) - 1)
+        self.pending: List[int] = []
+        self.works: list = []
+        self.armed = False
+
+    def arm(self) -> None:
+        self.pending = [b[2] for b in self.buckets]
+        self.works = [None] * len(self.buckets)
+        self.armed = True
+
+    def ready(self, module_index: int) -> None:
+        if not self.armed:
+            return
+        b = self.bucket_of[module_index]
+        self.pending[b] -= 1
+        if self.pending[b] == 0:
+            self._launch(b)
+
+    def _launch(self, b: int) -> None:
+        start, end, _ = self.buckets[b]
+        self.works[b] = dist.all_reduce(self.buffer[start:end], async_op=True)
+
+    def finish(self) -> None:
+        if not self.armed:
+            return
+        for b, w in enumerate(self.works):
+            if w is None:
+                self._launch(b)
+        for w in self.works:
+            w.wait()
+        self.armed = False
 
 
 class _TileGroup:
     """All SMT tiles of one optimizer parameter group, packed tile-major."""
 
-    def __init__(self, group: dict, modules: List[LinearLayer_MatrixSparsity], device, engine):
+    def __init__(self, group: dict, modules: List[LinearLayer_MatrixSparsity], device, engine,
+                 bucket_elems: int = 0):
         self.group = group
         self.modules = modules
         n_tiles = sum(len(m.tiles) for m in modules)
@@ -112,14 +179,19 @@ class _TileGroup:
         n = n_tiles * TILE_ELEMS
         self.param = torch.empty(n, dtype=torch.bfloat16, device=device)
         self.grad = torch.zeros(n, dtype=torch.float32, device=device)
-        descs, off = [], 0
+        ranges, off = [], 0
         for m in modules:
+            ranges.append((off * TILE_ELEMS, (off + len(m.tiles)) * TILE_ELEMS))
+            off += len(m.tiles)
+        self.buckets = TileGradBuckets(self.grad, ranges, bucket_elems) if bucket_elems > 0 else None
+        descs, off = [], 0
+        for idx, m in enumerate(modules):
             k = len(m.tiles)
             view = self.param[off * TILE_ELEMS:(off + k) * TILE_ELEMS].view(k * 256, 256)
             view.copy_(m.selected_weight.data)
             m.selected_weight.data = view                       # re-point the Parameter's storage
             m.selected_weight._smt_grad_sink = _GradSink(
-                self.grad[off * TILE_ELEMS:(off + k) * TILE_ELEMS].view(k * 256, 256), engine)
+                self.grad[off * TILE_ELEMS:(off + k) * TILE_ELEMS].view(k * 256, 256), engine, self.buckets, idx)
             m.writeback_on_forward = False                      # the AdamW epilogue scatters into W
             m.sync_weight()                                     # W consistent with the tiles now
             for i, (r, c) in enumerate(m.tiles):
@@ -156,6 +228,8 @@ class SMTEngine:
         self._accumulate_tiles = False
         self.device = next(model.parameters()).device
 
+        zero = cfg.get("zero_optimization") or {}
+        self.reduce_bucket_size = int(float(cfg.get("reduce_bucket_size", zero.get("reduce_bucket_size", 4e6))))
         self.tile_groups: List[_TileGroup] = []
         self.dense_groups: List[tuple] = []   # (group, [params])
         self._dense_state = {}
@@ -170,7 +244,8 @@ class SMTEngine:
                 if mods:
                     if any(m.weight.dtype != torch.bfloat16 for m in mods):
                         raise NotImplementedError("SMT engine: bf16 models only")
-                    self.tile_groups.append(_TileGroup(group, mods, self.device, self))
+                    self.tile_groups.append(_TileGroup(group, mods, self.device, self,
+                                                       self.reduce_bucket_size if self.world > 1 else 0))
                 if dense:
                     self.dense_groups.append((group, dense))
         self._norm_sq = torch.zeros(1, dtype=torch.float64, device=self.device)
@@ -201,10 +276,16 @@ class SMTEngine:
         self._accumulate_tiles = (self.micro_steps % self.gradient_accumulation_steps) != 0
         if self.gradient_accumulation_steps > 1:
             loss = loss / self.gradient_accumulation_steps
+        boundary = self.is_gradient_accumulation_boundary() and self.world > 1
+        if boundary:
+            for tg in self.tile_groups:
+                tg.buckets.arm()                # tile buckets all-reduce while backward runs
         loss.backward()
-        if self.is_gradient_accumulation_boundary() and self.world > 1:
+        if boundary:
+            for tg in self.tile_groups:
+                tg.buckets.finish()
             dense = [p.grad for _g, ps in self.dense_groups for p in ps if p.grad is not None]
-            allreduce_gradients([tg.grad for tg in self.tile_groups], dense, self.world)
+            allreduce_gradients([], dense, self.world)
         return loss
 
     def _grad_scale(self) -> float:

@@ -101,6 +101,26 @@ class TileIndex:
             self._dev[key] = t
         return t
 
+    def column_blocks(self) -> List[int]:
+        """Distinct column blocks of the tiles, in order of first use."""
+        seen = {}
+        for _r, c in self.index_list:
+            seen.setdefault(c, len(seen))
+        return list(seen)
+
+    def packed_tables(self, device: torch.device):
+        """Device tables for the packed-input backward: int32 [n_cb] column blocks and the int32
+        [n, 2] table of (row_block, position of the column block in the packed input)."""
+        key = ("packed", device.type, device.index)
+        t = self._dev.get(key)
+        if t is None:
+            cbs = self.column_blocks()
+            pos = {c: i for i, c in enumerate(cbs)}
+            t = (torch.tensor(cbs, dtype=torch.int32).to(device),
+                 _hip.tile_table([(r, pos[c]) for r, c in self.index_list], device))
+            self._dev[key] = t
+        return t
+
     def schedule(self, device: torch.device) -> torch.Tensor:
         """Device int32 schedule permutation for the wgrad kernel (L2 reuse; speed only)."""
         key = ("order", device.type, device.index)
@@ -165,6 +185,11 @@ class LinearLayer_MatrixSparsity(torch.nn.Module):
     def forward(self, x):
         if self.writeback_on_forward:
             self.sync_weight()
+        if not torch.is_grad_enabled():
+            # nothing to save for a backward: linearZ.forward's 3-D check and matmul only
+            if len(self.tiles) and x.dim() != 3:
+                raise IndexError(f"too many indices for tensor of dimension {x.dim()}")
+            return torch.matmul(x, self.weight.t())
         return self.fn(x, self.selected_weight, self.tiles, self.weight)
 
     def extra_repr(self) -> str:
@@ -174,9 +199,23 @@ class LinearLayer_MatrixSparsity(torch.nn.Module):
 SMTLinear = LinearLayer_MatrixSparsity
 
 
+def _rows_ready(t: torch.Tensor) -> torch.Tensor:
+    """2-D row-major with 16-byte aligned rows, else a contiguous copy."""
+    if t.stride(1) != 1 or t.stride(0) % 8 or t.data_ptr() % 16:
+        return t.contiguous()
+    return t
+
+
 class linearZ(torch.autograd.Function):
     """``y = x @ W^T`` (smt.py:350-373); backward returns ``(grad_input, grad_tiles, None, None)``
     (smt.py:376-413) with every tile's gradient from one grouped MFMA launch.
+
+    What the forward keeps for the backward: the reference keeps views of the input's column
+    slices (``ctx.list1``, smt.py:351-358), which hold the whole input alive. Here, when the tiles
+    touch at most half of the input's 256-column blocks, one ``smt_colblock_gather`` launch packs
+    exactly those blocks into a ``[T, n_cb*256]`` copy and the input itself is not saved (for a
+    down_proj with ~14 tiles that is 14 of its 56 blocks); otherwise the input is saved as is.
+    The tile gradients are bit-identical either way (same operands, same kernel, same order).
 
     If ``selected_weight`` carries an engine gradient sink (``_smt_grad_sink``), the fp32 tile
     gradients are written straight into the engine's packed buffer and ``None`` is returned for
@@ -190,34 +229,41 @@ class linearZ(torch.autograd.Function):
             raise IndexError(f"too many indices for tensor of dimension {input.dim()}")
         ctx.tiles = tiles
         ctx.sink = getattr(selected_weight, "_smt_grad_sink", None)
-        ctx.save_for_backward(input, weight)
+        ctx.packed = False
+        saved = input
+        in_blocks = weight.shape[1] // Block_dimension
+        if (ctx.needs_input_grad[1] and len(tiles) and input.device.type == "cuda"
+                and 2 * len(tiles.column_blocks()) <= in_blocks):
+            cb_dev, _ = tiles.packed_tables(input.device)
+            saved = _hip.colblock_gather(_rows_ready(input.reshape(-1, weight.shape[1])), cb_dev)
+            ctx.packed = True
+        ctx.save_for_backward(saved, weight)
         return torch.matmul(input, weight.t())
 
     @staticmethod
     def backward(ctx, grad_output):
-        input, weight = ctx.saved_tensors
+        saved, weight = ctx.saved_tensors
         tiles = ctx.tiles
         n = len(tiles)
         grad_input = grad_weight = None
         if ctx.needs_input_grad[1]:
             out_f = weight.shape[0]
-            in_f = weight.shape[1]
-            g2 = grad_output.reshape(-1, out_f)
-            x2 = input.reshape(-1, in_f)
-            if g2.stride(1) != 1 or g2.stride(0) % 8 or g2.data_ptr() % 16:
-                g2 = g2.contiguous()
-            if x2.stride(1) != 1 or x2.stride(0) % 8 or x2.data_ptr() % 16:
-                x2 = x2.contiguous()
-            sink = ctx.sink
+            g2 = _rows_ready(grad_output.reshape(-1, out_f))
             dev = g2.device
+            if ctx.packed:
+                x2, table = saved, tiles.packed_tables(dev)[1]
+            else:
+                x2, table = _rows_ready(saved.reshape(-1, weight.shape[1])), tiles.device_table(dev)
+            sink = ctx.sink
             if sink is not None:
-                _hip.tile_wgrad(g2, x2, tiles.device_table(dev), sink.buffer, accumulate=sink.take_accumulate(),
+                _hip.tile_wgrad(g2, x2, table, sink.buffer, accumulate=sink.take_accumulate(),
                                 order=tiles.schedule(dev))
+                sink.mark_ready()
             else:
                 grad_weight = torch.empty(n * Block_dimension, Block_dimension,
                                           dtype=grad_output.dtype, device=grad_output.device)
                 if n:
-                    _hip.tile_wgrad(g2, x2, tiles.device_table(dev), grad_weight, order=tiles.schedule(dev))
+                    _hip.tile_wgrad(g2, x2, table, grad_weight, order=tiles.schedule(dev))
         if ctx.needs_input_grad[0]:
             grad_input = torch.matmul(grad_output, weight)
         return grad_input, grad_weight, None, None

@@ -1,5 +1,6 @@
 """The N>1 path on CPU with gloo, world_size 2: the packed tile-gradient all-reduce + dense averaging
-of the engine, and the rank-0 selection broadcast."""
+of the engine, the bucketed backward-overlapped tile all-reduce, and the rank-0 selection broadcast
+(SURVEY §8(e))."""
 import os
 import socket
 from collections import defaultdict
@@ -48,6 +49,51 @@ def test_gloo_world2_tile_allreduce_and_selection_broadcast():
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: True, 1: True}
+
+
+def _bucket_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from sparse_matrix_tuning_amd.engine import TileGradBuckets
+    sizes = [3, 1, 4, 1, 5, 2]                         # tiles per module, forward order
+    ranges, off = [], 0
+    for k in sizes:
+        ranges.append((off * 16, (off + k) * 16))      # 16 "elements" per tile keeps it small
+        off += k
+    buf = torch.zeros(off * 16)
+    buckets = TileGradBuckets(buf, ranges, bucket_elems=5 * 16)
+    ok = [b[:2] for b in buckets.buckets] == [[0, 128], [128, 224], [224, 256]]
+    ok &= buckets.bucket_of == [0, 0, 0, 1, 1, 2]
+    for step in range(2):
+        buckets.arm()
+        for i in reversed(range(len(sizes))):         # backward order; module 2 never reports
+            s, e = ranges[i]
+            buf[s:e] = float(rank + 1) * (i + 1) + step
+            if i != 2:
+                buckets.ready(i)
+        ok &= buckets.works[2] is not None and buckets.works[1] is not None and buckets.works[0] is None
+        buckets.finish()
+        want = torch.cat([torch.full((e - s,), float(3 * (i + 1) + 2 * step)) for i, (s, e) in enumerate(ranges)])
+        ok &= torch.equal(buf, want)
+    buckets.ready(0)                                   # not armed: ignored
+    ok &= not buckets.armed
+    q.put((rank, bool(ok)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_bucketed_tile_allreduce():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bucket_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in range(world))

@@ -182,3 +182,35 @@ def test_adamw_matches_oracle(tiled):
     if tiled:
         tiles_now = ref.gather_tiles(W.cpu(), tile_list)
         assert torch.equal(tiles_now.reshape(-1), param.cpu())
+
+
+# ---------------------------------------------------------------- packed input column blocks (smt.py:351-358)
+@pytest.mark.parametrize("T,in_f,cbs", [(300, 1024, [3, 0]), (4096, 14336, [55, 7, 8, 30]), (1, 512, [1])])
+def test_colblock_gather_bit_exact(T, in_f, cbs):
+    x = torch.randn(T, in_f).bfloat16().to(DEV)
+    out = _hip.colblock_gather(x, torch.tensor(cbs, dtype=torch.int32, device=DEV))
+    want = torch.cat([x[:, c * 256:(c + 1) * 256] for c in cbs], dim=1)
+    assert out.shape == (T, 256 * len(cbs)) and torch.equal(out, want)
+
+
+def test_linearz_packed_input_grads_bit_identical():
+    """A module whose tiles touch few column blocks saves only those blocks; its tile gradients are
+    bit-identical to the grouped kernel over the full input, and to the unpacked path."""
+    from sparse_matrix_tuning_amd.smt import smt
+    B, S, out_f, in_f = 2, 160, 512, 2048              # 8 column blocks
+    tiles = [(1, 6), (0, 2), (1, 2)]                    # 2 distinct column blocks -> packed
+    W = torch.nn.Parameter((torch.randn(out_f, in_f) * 0.02).bfloat16().to(DEV))
+    mod = smt.LinearLayer_MatrixSparsity(W, index_list=tiles)
+    x = torch.randn(B, S, in_f).bfloat16().to(DEV).requires_grad_(True)
+    g = torch.randn(B, S, out_f).bfloat16().to(DEV)
+    y = mod(x)
+    assert y.grad_fn.packed
+    y.backward(g)
+    direct = torch.empty(len(tiles) * 256, 256, dtype=torch.bfloat16, device=DEV)
+    _hip.tile_wgrad(g.reshape(-1, out_f), x.detach().reshape(-1, in_f), _hip.tile_table(tiles, torch.device(DEV)), direct)
+    assert torch.equal(mod.selected_weight.grad, direct)
+    assert torch.equal(x.grad, torch.matmul(g, W.detach()))
+    wide = [(0, c) for c in range(5)]                   # 5 of 8 blocks -> the input itself is saved
+    mod2 = smt.LinearLayer_MatrixSparsity(W, index_list=wide)
+    y2 = mod2(x.detach())
+    assert not y2.grad_fn.packed

@@ -322,3 +322,9 @@ def test_activation_harvester_hook_keys_on_meta():
     assert len(h2._handles) == 2 * 3
     h2.release()
     assert not h2._handles and h2.attention_activation == {}
+
+
+def test_tile_index_column_blocks_first_use_order():
+    from sparse_matrix_tuning_amd.smt.smt import TileIndex
+    t = TileIndex([(1, 6), (0, 2), (1, 2), (3, 6), (2, 0)])
+    assert t.column_blocks() == [6, 2, 0]
