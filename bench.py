@@ -80,9 +80,6 @@ def parse():
                     help="keep transformers' sdpa (aotriton) attention instead of the gfx950 flash attention")
     ap.add_argument("--eager-ops", action="store_true",
                     help="keep transformers' eager RMSNorm/RoPE/SwiGLU instead of the fused HIP kernels")
-    ap.add_argument("--tunableop", default=os.path.join(ROOT, "profiles", "tunableop_gfx950.csv"),
-                    help="PyTorch TunableOp results (hipBLASLt / rocBLAS solution per GEMM shape, tuned on "
-                         "MI355X by scripts/gpu_session.sh 'tune'); 'off' keeps the default heuristics")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0, help="0 disables the CPU leg")
     ap.add_argument("--out", default=None, help="also write the JSON line here")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm) or gloo (functional tests)")
@@ -135,19 +132,6 @@ def install_wgrad_timer(timer: WgradTimer):
         return timer.hook(g2.shape[0], rc.shape[0], out.element_size(),
                           lambda: orig(g2, x2, rc, out, accumulate=accumulate, order=order))
     _hip.tile_wgrad = timed
-
-
-def use_tunableop(path: str) -> bool:
-    """Route torch GEMMs through TunableOp with a fixed, pre-tuned results file (no tuning at run
-    time; shapes absent from the file keep the default hipBLASLt heuristic)."""
-    if not path or path == "off" or not os.path.exists(path):
-        return False
-    import torch.cuda.tunable as tunable
-    tunable.enable(True)
-    tunable.tuning_enable(False)
-    tunable.record_untuned_enable(False)
-    tunable.set_filename(path)
-    return bool(tunable.read_file(path))
 
 
 def build_model(name, device):
@@ -248,8 +232,6 @@ def main():
 
     from sparse_matrix_tuning_amd import _hip
     _hip.load(build_if_missing=True)
-    tuned = use_tunableop(args.tunableop)
-    log(f"TunableOp GEMM results: {args.tunableop if tuned else 'off'}")
     from sparse_matrix_tuning_amd.engine import SMTFusedAdam, initialize, linear_lr_lambda
     from sparse_matrix_tuning_amd import trainer
 
@@ -316,6 +298,7 @@ def main():
     if not args.grad_ckpt:
         engine.module.gradient_checkpointing_disable()
     smt_batches = batches(args.warmup + args.steps, B, S, vocab, rank, device)
+    log(f"SMT phase starts with {torch.cuda.memory_allocated(device) / 1e9:.1f} GB allocated")
     torch.cuda.reset_peak_memory_stats(device)
 
     def step(b):
@@ -404,9 +387,7 @@ def main():
                        "grad_ckpt": bool(args.grad_ckpt), "full_ft_steps": args.full_ft_steps,
                        "fused_llama_ops": not args.eager_ops,
                        "attention": "sdpa" if (args.eager_ops or args.sdpa_attention) else "smt_flash",
-                       "loss": "transformers" if args.eager_ops else "smt_ce",
-                       "gemm": "hipBLASLt/rocBLAS (TunableOp: profiles/tunableop_gfx950.csv)" if tuned
-                               else "hipBLASLt (default heuristics)"},
+                       "loss": "transformers" if args.eager_ops else "smt_ce"},
             "peak_hbm_gb": round(peak.item(), 2), "warmup_peak_hbm_gb": round(warm_peak, 2),
             "grad_ckpt_mode": ckpt_mode,
             "step_mfma_frac": round(per_gpu * F_ALG_GFLOP_PER_TOKEN * 1e9 / (PEAK_BF16_TFLOPS * 1e12), 4),

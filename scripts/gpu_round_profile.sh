@@ -1,11 +1,13 @@
 #!/bin/bash
-# One GPU call: headline bench, kernel-trace stats, and the two PMC passes for the wgrad kernel.
+# One GPU call: headline bench, kernel-trace stats of a short bench, and the two PMC passes for the
+# wgrad kernel (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950).
 set -o pipefail
 OUT=gpurun_out/${PROFILE_TAG:-r01}
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 400 python3 bench.py --out $OUT/bench.json > $OUT/bench.log 2>&1 || exit 11
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o bench -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline-seconds 0 > $OUT/trace.log 2>&1 || exit 12
-timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex wgrad_ --output-format csv -d $OUT/pmc_fetch -o fetch -- python3 bench.py --steps 2 --warmup 1 --cpu-baseline-seconds 0 > $OUT/pmc_fetch.log 2>&1 || exit 13
-timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex wgrad_ --output-format csv -d $OUT/pmc_write -o write -- python3 bench.py --steps 2 --warmup 1 --cpu-baseline-seconds 0 > $OUT/pmc_write.log 2>&1 || exit 14
+SHORT="--steps 3 --warmup 1 --cpu-baseline-seconds 0 --ref-mode-steps 0"
+timeout -k 10 500 python3 bench.py --out $OUT/bench.json > $OUT/bench.log 2>&1 || exit 11
+timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o bench -- python3 bench.py $SHORT > $OUT/trace.log 2>&1 || exit 12
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex wgrad_ --output-format csv -d $OUT/pmc_fetch -o fetch -- python3 bench.py $SHORT > $OUT/pmc_fetch.log 2>&1 || exit 13
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex wgrad_ --output-format csv -d $OUT/pmc_write -o write -- python3 bench.py $SHORT > $OUT/pmc_write.log 2>&1 || exit 14
 echo done

@@ -12,9 +12,9 @@ for s in ${STEPS:-tests bench}; do
         > $OUT/tests.log 2>&1 || { echo "tests failed"; tail -30 $OUT/tests.log; exit 11; } ;;
     bench)
       timeout -k 10 500 python3 bench.py --out $OUT/bench.json > $OUT/bench.log 2>&1 || { echo "bench failed"; tail -30 $OUT/bench.log; exit 12; } ;;
-    bench_notune)
-      timeout -k 10 500 python3 bench.py --tunableop off --cpu-baseline-seconds 0 --ref-mode-steps 0 --out $OUT/bench_notune.json \
-        > $OUT/bench_notune.log 2>&1 || { echo "bench_notune failed"; tail -30 $OUT/bench_notune.log; exit 14; } ;;
+    bench_ckpt)
+      timeout -k 10 500 python3 bench.py --grad-ckpt --cpu-baseline-seconds 0 --ref-mode-steps 0 --out $OUT/bench_ckpt.json \
+        > $OUT/bench_ckpt.log 2>&1 || { echo "bench_ckpt failed"; tail -30 $OUT/bench_ckpt.log; exit 14; } ;;
     tune)
       # tuning one large shape can run for minutes without output: keep a heartbeat file growing
       ( while sleep 30; do date >> $OUT/tune_heartbeat; done ) & HB=$!

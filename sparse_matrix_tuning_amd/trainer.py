@@ -122,8 +122,10 @@ class GradHarvester:
         self.steps += 1
 
     def release(self) -> None:
-        self.warmup_grads = {}
-        self.attention_warmup_grads = {}
+        """Free the accumulators (the dicts are cleared in place: ``targets`` refers to them)."""
+        self.warmup_grads.clear()
+        self.attention_warmup_grads.clear()
+        self.targets = []
 
 
 def select_and_convert(engine, harvester: GradHarvester, targeted_module_dims: dict,
