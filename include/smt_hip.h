@@ -12,6 +12,8 @@
  *   smt_tile_scatter      deepspeed/smt/smt.py:332-341   per-forward write-back tiles -> W
  *                         (also smt.py:429-439, the merge in convert_matrix_sparsity_to_linear_layer)
  *   smt_tile_wgrad        deepspeed/smt/smt.py:382-404   per-tile sum_b g[b,:,rows]^T x[b,:,cols]
+ *   smt_tile_scatter_t    deepspeed/smt/smt.py:332-341 / 406   write-back into the transposed copy W^T
+ *                         that the data-gradient GEMM grad_input = g @ W reads (as g @ (W^T)^T)
  *   smt_colblock_gather   deepspeed/smt/smt.py:351-358   ctx.list1: the input column slices linearZ keeps
  *                         for its backward (packed copy of the distinct 256-column blocks)
  *   smt_grad_accumulate   deepspeed/fine_tune.py:724-741, 751-764   warm-up fp32 grad harvest
@@ -131,6 +133,12 @@ int smt_tile_wgrad(const void* grad_out, int64_t ld_grad_out,
  */
 int smt_colblock_gather(const void* x, int64_t ld_x, int64_t T, const int32_t* col_blocks_dev, int32_t n_cb,
                         void* out, hipStream_t stream);
+
+/*
+ * Wt[c*256 + j, r*256 + k] = tiles[flat_offset + k*256 + j] for each descriptor (weight = the bf16
+ * transposed copy W^T of a W, row_block / col_block = the tile's (r, c) in W); NULL weight: skipped.
+ */
+int smt_tile_scatter_t(const smt_tile_desc* descs_dev, int32_t n_tiles, const void* tiles, hipStream_t stream);
 
 /* tiles[i] = W[r_i*256:+256, c_i*256:+256]; elem_bytes 2 or 4. */
 int smt_tile_gather(const void* weight, int64_t ld_weight, int32_t elem_bytes,

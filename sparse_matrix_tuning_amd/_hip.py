@@ -28,7 +28,7 @@ _DT = {torch.bfloat16: DTYPE_BF16, torch.float32: DTYPE_FP32, torch.float16: DTY
 # Every function the headers declare (include/smt_hip.h, smt_model_ops.h, smt_attention.h); tests check the
 # library exports each of them.
 ABI_FUNCTIONS = (
-    "smt_last_error", "smt_abi_version", "smt_wgrad_workspace_bytes", "smt_tile_wgrad", "smt_colblock_gather",
+    "smt_last_error", "smt_abi_version", "smt_wgrad_workspace_bytes", "smt_tile_wgrad", "smt_colblock_gather", "smt_tile_scatter_t",
     "smt_tile_gather", "smt_tile_scatter", "smt_grad_accumulate", "smt_block_score",
     "smt_sq_norm", "smt_adamw_step",
     "smt_row_gather", "smt_row_scatter", "smt_column_gather", "smt_act_accumulate", "smt_channel_score",
@@ -90,6 +90,7 @@ _SIGS = {
     "smt_wgrad_workspace_bytes": (_SZ, [_I64, _I32]),
     "smt_tile_wgrad": (ctypes.c_int, [_P, _I64, _P, _I64, _I64, _P, _P, _I32, _P, _I32, _I32, _P, _SZ, _P]),
     "smt_colblock_gather": (ctypes.c_int, [_P, _I64, _I64, _P, _I32, _P, _P]),
+    "smt_tile_scatter_t": (ctypes.c_int, [_P, _I32, _P, _P]),
     "smt_tile_gather": (ctypes.c_int, [_P, _I64, _I32, _P, _I32, _P, _P]),
     "smt_tile_scatter": (ctypes.c_int, [_P, _I64, _I32, _P, _I32, _P, _P]),
     "smt_grad_accumulate": (ctypes.c_int, [_P, _I32, _I64, _P]),
@@ -358,6 +359,15 @@ def adamw_step(grad: torch.Tensor, master: torch.Tensor, exp_avg: torch.Tensor, 
     rc = load().smt_adamw_step(_ptr(grad), _ptr(master), _ptr(exp_avg), _ptr(exp_avg_sq), _ptr(param_bf16),
                                _ptr(tiles), int(n_tiles), n, _ptr(grad_sq_norm), ctypes.byref(args), _stream(dev))
     _check(rc, "smt_adamw_step")
+
+
+def tile_scatter_t(descs: torch.Tensor, n_tiles: int, tiles: torch.Tensor) -> None:
+    """Transposed write-back of bf16 tiles into the W^T copies the descriptors point at."""
+    dev = _require_device(descs, tiles)
+    if tiles.dtype != torch.bfloat16 or not tiles.is_contiguous():
+        raise ValueError("tile_scatter_t: tiles must be contiguous bf16")
+    rc = load().smt_tile_scatter_t(_ptr(descs), int(n_tiles), _ptr(tiles), _stream(dev))
+    _check(rc, "smt_tile_scatter_t")
 
 
 def tile_descs(entries: Sequence[tuple], device: torch.device) -> torch.Tensor:

@@ -823,6 +823,41 @@ void column_gather_kernel(const uint16_t* __restrict__ x, int64_t ld_x, int64_t 
     *reinterpret_cast<uint4*>(out + t * ld_out + j0) = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// Transposed tile scatter: Wt[c*256 + j, r*256 + k] = tile[k, j] for every descriptor (weight = the
+// transposed copy Wt = W^T of a frozen W, ld_weight its row stride, (row_block, col_block) = the
+// tile's (r, c) in W, flat_offset = the tile in the bf16 source). Keeps the transposed copies that
+// the data-gradient GEMMs read (g @ W as the TN product g @ Wt^T) in step with the tiles. One
+// workgroup per 64x64 sub-block, transposed through LDS.
+__global__ __launch_bounds__(256)
+void tile_scatter_t_kernel(const smt_tile_desc* __restrict__ descs, const uint16_t* __restrict__ src) {
+    __shared__ __attribute__((aligned(16))) uint16_t sub[64][72];      // 144-B rows
+    const int tile = blockIdx.x >> 4;
+    const int sb = blockIdx.x & 15;
+    const int k0 = (sb >> 2) * 64, j0 = (sb & 3) * 64;               // sub-block origin (tile row k, col j)
+    const smt_tile_desc d = descs[tile];
+    if (d.weight == nullptr) return;
+    const uint16_t* t = src + d.flat_offset;
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = tid; i < 512; i += 256) {
+        const int k = i >> 3, ch = i & 7;
+        *reinterpret_cast<uint4*>(&sub[k][ch * 8]) =
+            *reinterpret_cast<const uint4*>(t + (int64_t)(k0 + k) * kTile + j0 + ch * 8);
+    }
+    __syncthreads();
+    uint16_t* w = static_cast<uint16_t*>(d.weight);
+#pragma unroll
+    for (int i = tid; i < 512; i += 256) {
+        const int j = i >> 3, ch = i & 7;
+        uint32_t p[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            p[q] = (uint32_t)sub[ch * 8 + 2 * q][j] | ((uint32_t)sub[ch * 8 + 2 * q + 1][j] << 16);
+        *reinterpret_cast<uint4*>(w + ((int64_t)d.col_block * kTile + j0 + j) * d.ld_weight +
+                                  (int64_t)d.row_block * kTile + k0 + ch * 8) = make_uint4(p[0], p[1], p[2], p[3]);
+    }
+}
+
 // The 256-column blocks of x that a module's tiles read, packed side by side:
 // out[t, j*256 + k] = x[t, col_blocks[j]*256 + k]. linearZ saves this [T, n_cb*256] slab for its
 // backward instead of the whole input (the tile wgrad reads nothing else). 16 B per thread; one
@@ -1145,6 +1180,16 @@ int smt_column_gather(const void* x, int64_t ld_x, int64_t T, const int32_t* col
     hipLaunchKernelGGL(column_gather_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, static_cast<const uint16_t*>(x),
                        ld_x, T, cols_dev, n_cols, static_cast<uint16_t*>(out), ld_out);
     return check_launch("column_gather_kernel");
+}
+
+int smt_tile_scatter_t(const smt_tile_desc* descs_dev, int32_t n_tiles, const void* tiles, hipStream_t stream) {
+    if (n_tiles < 0) return fail(SMT_E_INVALID, "smt_tile_scatter_t: negative n_tiles");
+    if (n_tiles == 0) return SMT_OK;
+    if (!descs_dev || !tiles) return fail(SMT_E_INVALID, "smt_tile_scatter_t: null pointer");
+    if (!aligned16(tiles)) return fail(SMT_E_ALIGN, "smt_tile_scatter_t: tiles not 16-byte aligned");
+    hipLaunchKernelGGL(tile_scatter_t_kernel, dim3((unsigned)n_tiles * 16u), dim3(256), 0, stream, descs_dev,
+                       static_cast<const uint16_t*>(tiles));
+    return check_launch("tile_scatter_t_kernel");
 }
 
 int smt_colblock_gather(const void* x, int64_t ld_x, int64_t T, const int32_t* col_blocks_dev, int32_t n_cb,

@@ -121,6 +121,16 @@ class TileIndex:
             self._dev[key] = t
         return t
 
+    def transposed_descs(self, weight_t: torch.Tensor) -> torch.Tensor:
+        """Device smt_tile_desc[] for the transposed write-back of ``selected_weight`` into W^T."""
+        key = ("wt", weight_t.data_ptr(), weight_t.device.index)
+        t = self._dev.get(key)
+        if t is None:
+            t = _hip.tile_descs([(weight_t, r, c, i * _hip.TILE_ELEMS) for i, (r, c) in enumerate(self.index_list)],
+                                weight_t.device)
+            self._dev[key] = t
+        return t
+
     def schedule(self, device: torch.device) -> torch.Tensor:
         """Device int32 schedule permutation for the wgrad kernel (L2 reuse; speed only)."""
         key = ("order", device.type, device.index)
@@ -177,10 +187,15 @@ class LinearLayer_MatrixSparsity(torch.nn.Module):
         self.fn = linearZ.apply
 
     def sync_weight(self) -> None:
-        """Scatter the tiles into W (smt.py:332-341) with one launch."""
+        """Scatter the tiles into W (smt.py:332-341) with one launch, and into W's transposed copy
+        when the data-gradient GEMM uses one (:func:`..engine.attach_transposed_weights`)."""
         w = self.weight.data
         if len(self.tiles) and w.device.type == "cuda":
             _hip.tile_scatter(w, self.tiles.device_table(w.device), self.selected_weight.data)
+            wt = getattr(self.weight, "_smt_weight_t", None)
+            if wt is not None:
+                descs = self.tiles.transposed_descs(wt)
+                _hip.tile_scatter_t(descs, len(self.tiles), self.selected_weight.data)
 
     def forward(self, x):
         if self.writeback_on_forward:
@@ -265,7 +280,10 @@ class linearZ(torch.autograd.Function):
                 if n:
                     _hip.tile_wgrad(g2, x2, table, grad_weight, order=tiles.schedule(dev))
         if ctx.needs_input_grad[0]:
-            grad_input = torch.matmul(grad_output, weight)
+            wt = getattr(weight, "_smt_weight_t", None)
+            # g @ W (smt.py:406); with a transposed copy as the TN product g @ (W^T)^T, the layout
+            # hipBLASLt runs 13-19 % faster on these shapes (profiles/r01_gemm_layout.jsonl)
+            grad_input = torch.matmul(grad_output, weight) if wt is None else torch.matmul(grad_output, wt.t())
         return grad_input, grad_weight, None, None
 
 
@@ -321,6 +339,8 @@ def convert_matrix_sparsity_to_linear_layer(model, part_module_name=['.layers'])
     for name in replace_name:
         module = recursive_getattr(model, name)
         module.sync_weight()
+        if hasattr(module.weight, "_smt_weight_t"):
+            del module.weight._smt_weight_t
         weight_shape = module.weight.shape
         new_linear = nn.Linear(weight_shape[1], weight_shape[0], bias=False, device="meta")
         new_linear.weight = module.weight

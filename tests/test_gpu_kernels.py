@@ -116,6 +116,18 @@ def test_gather_scatter_bit_exact(dtype):
     assert torch.equal(Wd.cpu(), W2)
 
 
+def test_tile_scatter_transposed_bit_exact():
+    W = torch.randn(1024, 768).bfloat16()
+    tiles = [(3, 2), (0, 0), (1, 1)]
+    Wt = W.t().contiguous().to(DEV)
+    new = torch.randn(len(tiles) * 256, 256).bfloat16()
+    descs = _hip.tile_descs([(Wt, r, c, i * 65536) for i, (r, c) in enumerate(tiles)], torch.device(DEV))
+    _hip.tile_scatter_t(descs, len(tiles), new.to(DEV))
+    W2 = W.clone()
+    ref.writeback_tiles(W2, new, tiles)
+    assert torch.equal(Wt.cpu(), W2.t())
+
+
 # ---------------------------------------------------------------- warm-up accumulation (fine_tune.py:731-741)
 def test_grad_accumulate_bit_exact():
     shapes = [(512, 256), (256, 768), (33, 17), (4096,)]

@@ -203,6 +203,38 @@ def test_engine_sparse_adamw_step_matches_oracle():
     assert torch.equal(ref.gather_tiles(W2.detach().cpu(), [(2, 0)]), net.layers[1].selected_weight.detach().cpu())
     # untouched blocks of W unchanged
     assert torch.equal(W1.detach().cpu()[0:256, 256:512], W1_0[0:256, 256:512])
+    # the transposed copies the data-gradient GEMMs read follow every tile update
+    assert torch.equal(W1._smt_weight_t, W1.detach().t()) and torch.equal(W2._smt_weight_t, W2.detach().t())
+
+
+def test_transposed_dgrad_matches_plain_dgrad():
+    """The TN data gradient on W^T (SMT modules and frozen nn.Linear) vs g @ W."""
+    from sparse_matrix_tuning_amd.engine import attach_transposed_weights, detach_transposed_weights
+    torch.manual_seed(11)
+    W = nn.Parameter((torch.randn(768, 512) * 0.05).bfloat16().to(DEV), requires_grad=False)
+    net = nn.Module()
+    net.lin = nn.Linear(768, 256, bias=False).to(DEV).bfloat16().requires_grad_(False)
+    net.smt = smt.LinearLayer_MatrixSparsity(W, index_list=[(2, 1), (0, 0)])
+    x = torch.randn(2, 64, 512).bfloat16().to(DEV)
+    g = torch.randn(2, 64, 256).bfloat16().to(DEV)
+
+    def run():
+        xi = x.clone().requires_grad_(True)
+        net.lin(net.smt(xi)).backward(g)
+        return xi.grad, net.smt.selected_weight.grad
+    gi0, gw0 = run()
+    net.smt.selected_weight.grad = None
+    assert attach_transposed_weights(net) == (768 * 512 + 256 * 768) * 2
+    assert torch.equal(W._smt_weight_t, W.detach().t())
+    gi1, gw1 = run()
+    assert _rel(gi1, gi0) < 1e-2 and torch.equal(gw1, gw0)
+    # the module write-back keeps W^T in step
+    with torch.no_grad():
+        net.smt.selected_weight.add_(1.0)
+    net.smt.sync_weight()
+    assert torch.equal(W._smt_weight_t, W.detach().t())
+    detach_transposed_weights(net)
+    assert not hasattr(W, "_smt_weight_t") and "forward" not in net.lin.__dict__
 
 
 def test_engine_sink_grads_are_fp32_and_exact():
