@@ -9,10 +9,12 @@ import sys
 
 def cat(name):
     n = name
-    if "wgrad_" in n:
+    if "wgrad_" in n or "colblock_gather" in n:
         return "smt_wgrad"
-    if "adamw" in n or "sq_norm" in n or "tile_copy" in n:
+    if "adamw" in n or "sq_norm" in n or "tile_copy" in n or "tile_scatter_t" in n:
         return "smt_optimizer"
+    if "ce_fwd_kernel" in n or "ce_bwd_kernel" in n:
+        return "loss(smt_ce)"
     if n.startswith("Cijk") or n.startswith("Custom_Cijk"):
         return "gemm(hipBLASLt)"
     if "attn_fwd_kernel" in n or "attn_dq_kernel" in n or "attn_dkdv_kernel" in n or "attn_delta_kernel" in n:
