@@ -80,11 +80,14 @@ def parse():
                     help="keep transformers' sdpa (aotriton) attention instead of the gfx950 flash attention")
     ap.add_argument("--eager-ops", action="store_true",
                     help="keep transformers' eager RMSNorm/RoPE/SwiGLU instead of the fused HIP kernels")
+    ap.add_argument("--fp8", action="store_true",
+                    help="BASELINE config 5 (DeepSeek-R1-Distill-LLaMA-8B = the LLaMA-3-8B architecture, "
+                         "SMT(0.86%%)): the decoder layers' frozen linears run as rowwise-scaled e4m3 GEMMs")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0, help="0 disables the CPU leg")
     ap.add_argument("--out", default=None, help="also write the JSON line here")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm) or gloo (functional tests)")
     args = ap.parse_args()
-    default_ratio = 0.00356 if args.model == "llama3-8b" else 0.03
+    default_ratio = (0.0043 if args.fp8 else 0.00356) if args.model == "llama3-8b" else 0.03
     args.att_ratio = default_ratio if args.att_ratio is None else args.att_ratio
     args.mlp_ratio = default_ratio if args.mlp_ratio is None else args.mlp_ratio
     return args
@@ -258,6 +261,7 @@ def main():
 
     # ---- warm-up: full fine-tuning + gradient harvest (fine_tune.py:710-775) ----
     ds_config = {"gradient_clipping": 1.0, "train_micro_batch_size_per_gpu": B, "train_batch_size": B * world}
+    smt_config = dict(ds_config, fp8_linears=bool(args.fp8))
     from sparse_matrix_tuning_amd.smt.smt import _NO_DECAY
     groups = [{"params": [p for n, p in model.named_parameters() if not any(nd in n.lower() for nd in _NO_DECAY)],
                "weight_decay": 0.0},
@@ -284,7 +288,7 @@ def main():
     total_steps = args.full_ft_steps + args.warmup + args.steps
     engine, opt, sched, sel_mlp, sel_att = trainer.select_and_convert(
         engine, harvester, dims, n_att, n_mlp, calculate_strategy=args.calculate_strategy,
-        smt_lr=args.smt_lr, num_training_steps=total_steps, ds_config=ds_config)
+        smt_lr=args.smt_lr, num_training_steps=total_steps, ds_config=smt_config)
     del groups, opt
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
@@ -378,10 +382,13 @@ def main():
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "tokens/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "fp8-e4m3 (rowwise-scaled decoder GEMMs) + bf16" if args.fp8 else "bf16",
             "data": "synthetic (uniform token ids, labels=inputs; random-init weights)",
-            "config": {"workload": f"{'LLaMA-3-8B' if args.model == 'llama3-8b' else args.model} SMT(0.71%) "
-                                   "training step (fwd+bwd+sparse AdamW)",
+            "config": {"workload": (f"{'LLaMA-3-8B' if args.model == 'llama3-8b' else args.model} SMT(0.71%) "
+                                    "training step (fwd+bwd+sparse AdamW)") if not args.fp8 else
+                                   (f"{'DeepSeek-R1-Distill-LLaMA-8B (LLaMA-3-8B architecture)' if args.model == 'llama3-8b' else args.model}"
+                                    " SMT(0.86%) fp8 training step (fwd+bwd+sparse AdamW)"),
                        "global_batch": B * world, "seq_len": S, "parallelism": f"dp{world}",
                        "tiles": n_tiles, "trainable_params": trainable,
                        "grad_ckpt": bool(args.grad_ckpt), "full_ft_steps": args.full_ft_steps,

@@ -1,0 +1,49 @@
+/*
+ * smt_fp8.h — C-ABI of the fp8 (OCP e4m3) quantisation kernels of the SMT fp8 path
+ * (BASELINE.json config 5; csrc/fp8_kernels.hip, same library libsmt_hip.so).
+ *
+ * The reference has no fp8 anywhere (bf16/fp16/fp32 only, deepspeed/fine_tune.py:955-959), so this
+ * path has no reference counterpart: parity is stated against the build's own bf16 path.
+ * The frozen weights of the decoder layers are kept as e4m3 copies with one fp32 scale per row
+ * (forward, W [out, in]) and per column (data gradient, written transposed as W^T [in, out]), and the
+ * activations / output gradients are quantised per row (token) on the fly; the GEMMs then run as
+ * hipBLASLt rowwise-scaled fp8 GEMMs. After every optimizer step the rows / columns that the
+ * updated 256x256 tiles touch are re-quantised from the bf16 W (whose tiles the AdamW epilogue wrote).
+ *
+ * Quantisation (both kernels): scale = amax / 448 (1 when amax == 0), q = e4m3_rne(x / scale),
+ * with x / scale an IEEE fp32 division, so the bytes equal torch's
+ * (x.float() / scale).to(torch.float8_e4m3fn).
+ * Return 0 or a negative code; smt_fp8_last_error() holds the message.
+ */
+#ifndef SMT_FP8_H
+#define SMT_FP8_H
+
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+const char* smt_fp8_last_error(void);
+
+/*
+ * Row-wise: out[r, 0:cols] = e4m3(x[r, 0:cols] / scales[r]) for every row r of x (bf16 [rows, ld_x]),
+ * or, when row_blocks_dev != NULL, only for the rows of the listed 256-row blocks (device int32 [n]).
+ * out: fp8 bytes [rows, ld_out]; scales: fp32 [rows]. cols % 8 == 0; 16-byte aligned bf16 rows.
+ */
+int smt_quant_rows_e4m3(const void* x, int64_t ld_x, int64_t rows, int32_t cols, const int32_t* row_blocks_dev,
+                        int32_t n_row_blocks, void* out, int64_t ld_out, float* scales, hipStream_t stream);
+
+/*
+ * Column-wise, transposed: out_t[c, 0:rows] = e4m3(w[0:rows, c] / scales[c]) for every column c of
+ * w (bf16 [rows, ld_w], cols % 256 == 0), or only the columns of the listed 256-column blocks.
+ * out_t: fp8 bytes [cols, ld_out] (the transposed matrix); scales: fp32 [cols]. rows % 64 == 0.
+ */
+int smt_quant_cols_t_e4m3(const void* w, int64_t ld_w, int32_t rows, int32_t cols, const int32_t* col_blocks_dev,
+                          int32_t n_col_blocks, void* out_t, int64_t ld_out, float* scales, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SMT_FP8_H */

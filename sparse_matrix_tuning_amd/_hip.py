@@ -35,6 +35,7 @@ ABI_FUNCTIONS = (
     "smt_model_ops_last_error", "smt_rmsnorm_fwd", "smt_rmsnorm_bwd_waves", "smt_rmsnorm_bwd",
     "smt_rope_fwd", "smt_rope_bwd", "smt_swiglu_fwd", "smt_swiglu_bwd", "smt_ce_fwd", "smt_ce_bwd",
     "smt_attn_last_error", "smt_attn_fwd", "smt_attn_bwd",
+    "smt_fp8_last_error", "smt_quant_rows_e4m3", "smt_quant_cols_t_e4m3",
 )
 
 
@@ -116,6 +117,9 @@ _SIGS = {
     "smt_swiglu_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I64, _P]),
     "smt_ce_fwd": (ctypes.c_int, [_P, _I64, _P, _I64, _I64, _I64, _P, _P, _P]),
     "smt_ce_bwd": (ctypes.c_int, [_P, _I64, _P, _P, _P, _I64, _I64, _I64, _P, _I64, _P]),
+    "smt_fp8_last_error": (ctypes.c_char_p, []),
+    "smt_quant_rows_e4m3": (ctypes.c_int, [_P, _I64, _I64, _I32, _P, _I32, _P, _I64, _P, _P]),
+    "smt_quant_cols_t_e4m3": (ctypes.c_int, [_P, _I64, _I32, _I32, _P, _I32, _P, _I64, _P, _P]),
 }
 
 
@@ -153,6 +157,8 @@ def _check(rc: int, what: str) -> None:
             err = lib.smt_model_ops_last_error
         elif what.startswith("smt_attn"):
             err = lib.smt_attn_last_error
+        elif what.startswith("smt_quant"):
+            err = lib.smt_fp8_last_error
         else:
             err = lib.smt_last_error
         raise RuntimeError(f"{what} failed (status {rc}): {err().decode(errors='replace')}")

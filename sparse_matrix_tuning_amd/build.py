@@ -3,7 +3,8 @@
 The library is the only native product code: ``csrc/smt_kernels.hip`` (the SMT hot path, C ABI
 ``include/smt_hip.h``) and ``csrc/llama_kernels.hip`` (fused LLaMA elementwise ops, C ABI
 ``include/smt_model_ops.h``) and ``csrc/attn_kernels.hip`` (causal flash attention, C ABI
-``include/smt_attention.h``) compiled for ``--offload-arch=gfx950``. It is loaded with
+``include/smt_attention.h``) and ``csrc/fp8_kernels.hip`` (e4m3 quantisation of the fp8 path, C ABI
+``include/smt_fp8.h``) compiled for ``--offload-arch=gfx950``. It is loaded with
 ctypes by :mod:`sparse_matrix_tuning_amd._hip` (no torch types cross the boundary).
 """
 from __future__ import annotations
@@ -15,8 +16,10 @@ import sys
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
-SRCS = [os.path.join(PKG_DIR, "csrc", n) for n in ("smt_kernels.hip", "llama_kernels.hip", "attn_kernels.hip")]
-HEADERS = [os.path.join(REPO_DIR, "include", n) for n in ("smt_hip.h", "smt_model_ops.h", "smt_attention.h")]
+SRCS = [os.path.join(PKG_DIR, "csrc", n) for n in ("smt_kernels.hip", "llama_kernels.hip", "attn_kernels.hip",
+                                                   "fp8_kernels.hip")]
+HEADERS = [os.path.join(REPO_DIR, "include", n) for n in ("smt_hip.h", "smt_model_ops.h", "smt_attention.h",
+                                                          "smt_fp8.h")]
 LIB_DIR = os.path.join(PKG_DIR, "_lib")
 LIB_PATH = os.path.join(LIB_DIR, "libsmt_hip.so")
 ARCH = "gfx950"

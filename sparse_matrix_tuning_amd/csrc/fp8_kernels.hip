@@ -1,0 +1,195 @@
+// fp8_kernels.hip — gfx950 OCP e4m3 quantisation for the SMT fp8 path (BASELINE config 5,
+// SURVEY §8(f) row 2). C ABI: include/smt_fp8.h.
+//
+// The frozen linear weights of the decoder layers get e4m3 copies with one fp32 scale per row
+// (W [out, in], the forward operand) and per column (written transposed as W^T [in, out], the data-
+// gradient operand); activations and output gradients are quantised per row (token) before each
+// GEMM. hipBLASLt then runs the rowwise-scaled fp8 GEMMs (2.4-2.9 PF/s on the LLaMA-3-8B shapes
+// against 1.4-1.6 PF/s bf16, profiles/r01_fp8_probe.jsonl).
+//
+// scale = amax / 448 (1 when amax == 0); q = e4m3_rne(x / scale), IEEE fp32 division and
+// v_cvt_pk_fp8_f32 (round to nearest even, OCP e4m3 on gfx950), clamped to +-448 first, so the
+// bytes equal torch's (x.float() / scale).to(torch.float8_e4m3fn).
+
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "smt_fp8.h"
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+int check_launch(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(-4, "%s: %s", what, hipGetErrorString(e));
+    return 0;
+}
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+constexpr float kE4M3Max = 448.f;
+
+__device__ __forceinline__ float bf(uint32_t b16) { return __uint_as_float(b16 << 16); }
+
+struct F8 { float v[8]; };
+
+__device__ __forceinline__ F8 ld8(const uint16_t* p) {
+    const uint4 a = *reinterpret_cast<const uint4*>(p);
+    F8 r;
+    const uint32_t w[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { r.v[2 * j] = bf(w[j] & 0xffffu); r.v[2 * j + 1] = bf(w[j] >> 16); }
+    return r;
+}
+
+__device__ __forceinline__ float qv(float x, float scale) {
+    return __builtin_amdgcn_fmed3f(x / scale, kE4M3Max, -kE4M3Max);
+}
+
+// four values -> four e4m3 bytes (little endian: a is byte 0)
+__device__ __forceinline__ uint32_t pack4(float a, float b, float c, float d) {
+    int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+    return (uint32_t)w;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+    return v;
+}
+
+// One wave per row: pass 1 the row's amax, pass 2 (the row again, L2-served) the conversion.
+__global__ __launch_bounds__(256)
+void quant_rows_kernel(const uint16_t* __restrict__ x, int64_t ldx, int64_t rows, int cols,
+                       const int32_t* __restrict__ row_blocks, int64_t n_sel, uint8_t* __restrict__ out, int64_t ldo,
+                       float* __restrict__ scales) {
+    const int lane = threadIdx.x & 63;
+    const int64_t idx = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (idx >= n_sel) return;
+    const int64_t row = row_blocks ? (int64_t)row_blocks[idx >> 8] * 256 + (idx & 255) : idx;
+    if (row >= rows) return;
+    const uint16_t* xr = x + row * ldx;
+    const int nch = cols >> 3;
+    float amax = 0.f;
+    for (int c = lane; c < nch; c += 64) {
+        const F8 v = ld8(xr + c * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(v.v[j]));
+    }
+    amax = wave_max(amax);
+    const float scale = amax > 0.f ? amax / kE4M3Max : 1.f;
+    if (lane == 0) scales[row] = scale;
+    uint8_t* orow = out + row * ldo;
+    for (int c = lane; c < nch; c += 64) {
+        const F8 v = ld8(xr + c * 8);
+        uint2 w;
+        w.x = pack4(qv(v.v[0], scale), qv(v.v[1], scale), qv(v.v[2], scale), qv(v.v[3], scale));
+        w.y = pack4(qv(v.v[4], scale), qv(v.v[5], scale), qv(v.v[6], scale), qv(v.v[7], scale));
+        *reinterpret_cast<uint2*>(orow + c * 8) = w;
+    }
+}
+
+// One workgroup per 256-column block: pass 1 the 256 column maxima (8 row groups x 32 lanes of 8
+// columns, combined in LDS); pass 2 in 64-row slabs staged through LDS, each thread converting its
+// column's 64 values into 64 contiguous bytes of the transposed output row.
+constexpr int kSlabRows = 64;
+constexpr int kSlabLd = 256 + 8;             // 528-B LDS rows
+
+__global__ __launch_bounds__(256)
+void quant_cols_t_kernel(const uint16_t* __restrict__ w, int64_t ldw, int rows, const int32_t* __restrict__ col_blocks,
+                         uint8_t* __restrict__ out_t, int64_t ldo, float* __restrict__ scales) {
+    __shared__ float red[8][256];
+    __shared__ __attribute__((aligned(16))) uint16_t slab[kSlabRows][kSlabLd];
+    const int cb = col_blocks ? col_blocks[blockIdx.x] : (int)blockIdx.x;
+    const int tid = threadIdx.x;
+    const int chunk = tid & 31, rg = tid >> 5;
+    const uint16_t* base = w + (int64_t)cb * 256;
+    float m[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m[j] = 0.f;
+    for (int r = rg; r < rows; r += 8) {
+        const F8 v = ld8(base + (int64_t)r * ldw + chunk * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], fabsf(v.v[j]));
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[rg][chunk * 8 + j] = m[j];
+    __syncthreads();
+    float amax = 0.f;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) amax = fmaxf(amax, red[g][tid]);
+    const float scale = amax > 0.f ? amax / kE4M3Max : 1.f;
+    const int64_t col = (int64_t)cb * 256 + tid;
+    scales[col] = scale;
+    uint8_t* orow = out_t + col * ldo;
+    for (int r0 = 0; r0 < rows; r0 += kSlabRows) {
+        __syncthreads();                                     // the previous slab is consumed
+        for (int i = tid; i < kSlabRows * 32; i += 256) {
+            const int rr = i >> 5, ch = i & 31;
+            *reinterpret_cast<uint4*>(&slab[rr][ch * 8]) =
+                *reinterpret_cast<const uint4*>(base + (int64_t)(r0 + rr) * ldw + ch * 8);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < kSlabRows / 16; ++q) {
+            uint32_t wd[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int rr = q * 16 + k * 4;
+                wd[k] = pack4(qv(bf(slab[rr][tid]), scale), qv(bf(slab[rr + 1][tid]), scale),
+                              qv(bf(slab[rr + 2][tid]), scale), qv(bf(slab[rr + 3][tid]), scale));
+            }
+            *reinterpret_cast<uint4*>(orow + r0 + q * 16) = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* smt_fp8_last_error(void) { return g_err; }
+
+int smt_quant_rows_e4m3(const void* x, int64_t ld_x, int64_t rows, int32_t cols, const int32_t* row_blocks_dev,
+                        int32_t n_row_blocks, void* out, int64_t ld_out, float* scales, hipStream_t stream) {
+    if (rows < 0 || cols <= 0 || (cols & 7) || ld_x < cols || ld_out < cols || n_row_blocks < 0)
+        return fail(-1, "smt_quant_rows_e4m3: bad sizes rows=%lld cols=%d (cols %% 8 == 0)", (long long)rows, cols);
+    const int64_t n_sel = row_blocks_dev ? (int64_t)n_row_blocks * 256 : rows;
+    if (n_sel == 0) return 0;
+    if (!x || !out || !scales) return fail(-1, "smt_quant_rows_e4m3: null pointer");
+    if (!aligned16(x) || (ld_x & 7) || (reinterpret_cast<uintptr_t>(out) & 7) || (ld_out & 7))
+        return fail(-2, "smt_quant_rows_e4m3: 16-byte aligned bf16 rows and 8-byte aligned fp8 rows required");
+    const int64_t blocks = (n_sel + 3) / 4;
+    if (blocks > 0x7fffffffLL) return fail(-1, "smt_quant_rows_e4m3: too many rows");
+    hipLaunchKernelGGL(quant_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, static_cast<const uint16_t*>(x),
+                       ld_x, rows, cols, row_blocks_dev, n_sel, static_cast<uint8_t*>(out), ld_out, scales);
+    return check_launch("quant_rows_kernel");
+}
+
+int smt_quant_cols_t_e4m3(const void* w, int64_t ld_w, int32_t rows, int32_t cols, const int32_t* col_blocks_dev,
+                          int32_t n_col_blocks, void* out_t, int64_t ld_out, float* scales, hipStream_t stream) {
+    if (rows <= 0 || cols <= 0 || (cols % 256) || (rows % kSlabRows) || ld_w < cols || ld_out < rows || n_col_blocks < 0)
+        return fail(-1, "smt_quant_cols_t_e4m3: bad sizes rows=%d cols=%d (cols %% 256 == 0, rows %% 64 == 0)", rows, cols);
+    const int nb = col_blocks_dev ? n_col_blocks : cols / 256;
+    if (nb == 0) return 0;
+    if (!w || !out_t || !scales) return fail(-1, "smt_quant_cols_t_e4m3: null pointer");
+    if (!aligned16(w) || (ld_w & 7) || !aligned16(out_t) || (ld_out & 15))
+        return fail(-2, "smt_quant_cols_t_e4m3: 16-byte aligned rows required (ld_w %% 8 == 0, ld_out %% 16 == 0)");
+    hipLaunchKernelGGL(quant_cols_t_kernel, dim3((unsigned)nb), dim3(256), 0, stream, static_cast<const uint16_t*>(w),
+                       ld_w, rows, col_blocks_dev, static_cast<uint8_t*>(out_t), ld_out, scales);
+    return check_launch("quant_cols_t_kernel");
+}
+
+}  // extern "C"

@@ -114,8 +114,14 @@ class FrozenLinearFn(torch.autograd.Function):
 
 
 def _frozen_linear_forward(self, x):
+    if self.weight.requires_grad or (self.bias is not None and self.bias.requires_grad):
+        return torch.nn.functional.linear(x, self.weight, self.bias)
+    fw = getattr(self.weight, "_smt_fp8", None)
+    if fw is not None:
+        from .fp8 import Fp8LinearFn
+        return Fp8LinearFn.apply(x, self.weight, fw, self.bias)
     wt = getattr(self.weight, "_smt_weight_t", None)
-    if wt is None or self.weight.requires_grad or (self.bias is not None and self.bias.requires_grad):
+    if wt is None:
         return torch.nn.functional.linear(x, self.weight, self.bias)
     return FrozenLinearFn.apply(x, self.weight, wt, self.bias)
 
@@ -125,15 +131,37 @@ def _transposable(w: torch.Tensor) -> bool:
             and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0)
 
 
+def attach_fp8_weights(model: torch.nn.Module, part_module_name=(".layers",)) -> int:
+    """fp8 path (config 5): give every frozen bf16 linear weight under ``part_module_name`` (the
+    decoder layers; smt.py:86-88's default) its e4m3 copies (:class:`..fp8.Fp8Weight`) and route plain
+    frozen ``nn.Linear`` forwards through them. Returns the bytes added."""
+    from .fp8 import Fp8Weight
+    added = 0
+    for name, m in model.named_modules():
+        if not any(p in name for p in part_module_name):
+            continue
+        if isinstance(m, LinearLayer_MatrixSparsity) or type(m) is torch.nn.Linear:
+            w = m.weight
+            if not _transposable(w) or getattr(w, "_smt_fp8", None) is not None or w.shape[0] % 256 or w.shape[1] % 256:
+                continue
+            w._smt_fp8 = Fp8Weight(w)
+            added += w._smt_fp8.nbytes
+            if type(m) is torch.nn.Linear:
+                m.forward = _frozen_linear_forward.__get__(m, type(m))
+    return added
+
+
 def attach_transposed_weights(model: torch.nn.Module) -> int:
     """Give every frozen bf16 linear weight of ``model`` (SMT modules and plain ``nn.Linear``) a
     transposed contiguous copy ``weight._smt_weight_t`` for the TN data-gradient GEMM, and route
-    plain frozen ``nn.Linear`` forwards through :class:`FrozenLinearFn`. Returns the bytes added."""
+    plain frozen ``nn.Linear`` forwards through :class:`FrozenLinearFn`. Weights that carry fp8
+    copies are skipped. Returns the bytes added."""
     added = 0
     for m in model.modules():
         if isinstance(m, LinearLayer_MatrixSparsity) or type(m) is torch.nn.Linear:
             w = m.weight
-            if not _transposable(w) or getattr(w, "_smt_weight_t", None) is not None:
+            if (not _transposable(w) or getattr(w, "_smt_weight_t", None) is not None
+                    or getattr(w, "_smt_fp8", None) is not None):
                 continue
             w._smt_weight_t = w.detach().t().contiguous()
             added += w.numel() * w.element_size()
@@ -146,8 +174,9 @@ def detach_transposed_weights(model: torch.nn.Module) -> None:
     """Undo :func:`attach_transposed_weights`."""
     for m in model.modules():
         w = getattr(m, "weight", None)
-        if isinstance(w, torch.Tensor) and hasattr(w, "_smt_weight_t"):
-            del w._smt_weight_t
+        for attr in ("_smt_weight_t", "_smt_fp8"):
+            if isinstance(w, torch.Tensor) and hasattr(w, attr):
+                delattr(w, attr)
         if type(m) is torch.nn.Linear and "forward" in m.__dict__:
             del m.__dict__["forward"]
 
@@ -267,6 +296,7 @@ class _TileGroup:
         self.descs = _hip.tile_descs(descs, device) if descs else None
         self.n_tdescs = len(tdescs)
         self.tdescs = _hip.tile_descs(tdescs, device) if tdescs else None
+        self.fp8_modules = [(m, m.weight._smt_fp8) for m in modules if getattr(m.weight, "_smt_fp8", None) is not None]
         self.step = 0
 
 
@@ -300,11 +330,15 @@ class SMTEngine:
         self.dense_groups: List[tuple] = []   # (group, [params])
         self._dense_state = {}
         self.transposed_bytes = 0
+        self.fp8_bytes = 0
         if optimizer is not None:
             owner = {}
             for m in model.modules():
                 if isinstance(m, LinearLayer_MatrixSparsity) and m.selected_weight.requires_grad and len(m.tiles):
                     owner[id(m.selected_weight)] = m
+            if owner and cfg.get("fp8_linears", False):
+                # config 5: e4m3 copies of the decoder-layer weights (re-quantised after each step)
+                self.fp8_bytes = attach_fp8_weights(model)
             if owner and cfg.get("transposed_dgrad", True):
                 # SMT phase: every linear weight is frozen (tiles change only through the epilogue)
                 self.transposed_bytes = attach_transposed_weights(model)
@@ -385,6 +419,9 @@ class SMTEngine:
                             tiles=tg.descs, n_tiles=tg.n_tiles, grad_sq_norm=norm)
             if tg.tdescs is not None:
                 _hip.tile_scatter_t(tg.tdescs, tg.n_tdescs, tg.param)
+            for m, fw in tg.fp8_modules:
+                rb, cb = m.tiles.block_tables(self.device)
+                fw.refresh(m.weight, rb, cb)
         for group, params in self.dense_groups:
             for p in params:
                 if p.grad is None:

@@ -121,6 +121,17 @@ class TileIndex:
             self._dev[key] = t
         return t
 
+    def block_tables(self, device: torch.device):
+        """Device int32 tables of the distinct row blocks and column blocks the tiles touch."""
+        key = ("blocks", device.type, device.index)
+        t = self._dev.get(key)
+        if t is None:
+            rows = sorted({r for r, _c in self.index_list})
+            t = (torch.tensor(rows, dtype=torch.int32).to(device),
+                 torch.tensor(sorted(self.column_blocks()), dtype=torch.int32).to(device))
+            self._dev[key] = t
+        return t
+
     def transposed_descs(self, weight_t: torch.Tensor) -> torch.Tensor:
         """Device smt_tile_desc[] for the transposed write-back of ``selected_weight`` into W^T."""
         key = ("wt", weight_t.data_ptr(), weight_t.device.index)
@@ -196,6 +207,10 @@ class LinearLayer_MatrixSparsity(torch.nn.Module):
             if wt is not None:
                 descs = self.tiles.transposed_descs(wt)
                 _hip.tile_scatter_t(descs, len(self.tiles), self.selected_weight.data)
+            fw = getattr(self.weight, "_smt_fp8", None)
+            if fw is not None:
+                rb, cb = self.tiles.block_tables(w.device)
+                fw.refresh(w, rb, cb)
 
     def forward(self, x):
         if self.writeback_on_forward:
@@ -204,7 +219,7 @@ class LinearLayer_MatrixSparsity(torch.nn.Module):
             # nothing to save for a backward: linearZ.forward's 3-D check and matmul only
             if len(self.tiles) and x.dim() != 3:
                 raise IndexError(f"too many indices for tensor of dimension {x.dim()}")
-            return torch.matmul(x, self.weight.t())
+            return _dense_forward(x, self.weight)
         return self.fn(x, self.selected_weight, self.tiles, self.weight)
 
     def extra_repr(self) -> str:
@@ -212,6 +227,15 @@ class LinearLayer_MatrixSparsity(torch.nn.Module):
 
 
 SMTLinear = LinearLayer_MatrixSparsity
+
+
+def _dense_forward(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """``x @ W^T`` (smt.py:366): bf16 hipBLASLt, or the e4m3 copy when the fp8 path attached one."""
+    fw = getattr(weight, "_smt_fp8", None)
+    if fw is not None:
+        from ..fp8 import fp8_linear_forward
+        return fp8_linear_forward(x, fw)
+    return torch.matmul(x, weight.t())
 
 
 def _rows_ready(t: torch.Tensor) -> torch.Tensor:
@@ -253,7 +277,7 @@ class linearZ(torch.autograd.Function):
             saved = _hip.colblock_gather(_rows_ready(input.reshape(-1, weight.shape[1])), cb_dev)
             ctx.packed = True
         ctx.save_for_backward(saved, weight)
-        return torch.matmul(input, weight.t())
+        return _dense_forward(input, weight)
 
     @staticmethod
     def backward(ctx, grad_output):
@@ -281,9 +305,17 @@ class linearZ(torch.autograd.Function):
                     _hip.tile_wgrad(g2, x2, table, grad_weight, order=tiles.schedule(dev))
         if ctx.needs_input_grad[0]:
             wt = getattr(weight, "_smt_weight_t", None)
+            fw = getattr(weight, "_smt_fp8", None)
             # g @ W (smt.py:406); with a transposed copy as the TN product g @ (W^T)^T, the layout
-            # hipBLASLt runs 13-19 % faster on these shapes (profiles/r01_gemm_layout.jsonl)
-            grad_input = torch.matmul(grad_output, weight) if wt is None else torch.matmul(grad_output, wt.t())
+            # hipBLASLt runs 13-19 % faster on these shapes (profiles/r01_gemm_layout.jsonl); on the
+            # fp8 path through W's transposed e4m3 copy
+            if fw is not None:
+                from ..fp8 import fp8_linear_dgrad
+                grad_input = fp8_linear_dgrad(grad_output, fw)
+            elif wt is not None:
+                grad_input = torch.matmul(grad_output, wt.t())
+            else:
+                grad_input = torch.matmul(grad_output, weight)
         return grad_input, grad_weight, None, None
 
 
@@ -339,8 +371,9 @@ def convert_matrix_sparsity_to_linear_layer(model, part_module_name=['.layers'])
     for name in replace_name:
         module = recursive_getattr(model, name)
         module.sync_weight()
-        if hasattr(module.weight, "_smt_weight_t"):
-            del module.weight._smt_weight_t
+        for attr in ("_smt_weight_t", "_smt_fp8"):
+            if hasattr(module.weight, attr):
+                delattr(module.weight, attr)
         weight_shape = module.weight.shape
         new_linear = nn.Linear(weight_shape[1], weight_shape[0], bias=False, device="meta")
         new_linear.weight = module.weight
