@@ -10,7 +10,7 @@
  * hipBLASLt rowwise-scaled fp8 GEMMs. After every optimizer step the rows / columns that the
  * updated 256x256 tiles touch are re-quantised from the bf16 W (whose tiles the AdamW epilogue wrote).
  *
- * Quantisation (both kernels): scale = amax / 448 (1 when amax == 0), q = e4m3_rne(x / scale),
+ * Quantisation (both kernels): scale = amax * fp32(1/448) (1 when amax == 0), q = e4m3_rne(x / scale),
  * with x / scale an IEEE fp32 division, so the bytes equal torch's
  * (x.float() / scale).to(torch.float8_e4m3fn).
  * Return 0 or a negative code; smt_fp8_last_error() holds the message.

@@ -15,6 +15,9 @@ for s in ${STEPS:-tests bench}; do
     bench_ckpt)
       timeout -k 10 500 python3 bench.py --grad-ckpt --cpu-baseline-seconds 0 --ref-mode-steps 0 --out $OUT/bench_ckpt.json \
         > $OUT/bench_ckpt.log 2>&1 || { echo "bench_ckpt failed"; tail -30 $OUT/bench_ckpt.log; exit 14; } ;;
+    bench_fp8)
+      timeout -k 10 500 python3 bench.py --fp8 --cpu-baseline-seconds 0 --out $OUT/bench_fp8.json > $OUT/bench_fp8.log 2>&1 \
+        || { echo "bench_fp8 failed"; tail -30 $OUT/bench_fp8.log; exit 15; } ;;
     tune)
       # tuning one large shape can run for minutes without output: keep a heartbeat file growing
       ( while sleep 30; do date >> $OUT/tune_heartbeat; done ) & HB=$!

@@ -7,7 +7,7 @@
 // GEMM. hipBLASLt then runs the rowwise-scaled fp8 GEMMs (2.4-2.9 PF/s on the LLaMA-3-8B shapes
 // against 1.4-1.6 PF/s bf16, profiles/r01_fp8_probe.jsonl).
 //
-// scale = amax / 448 (1 when amax == 0); q = e4m3_rne(x / scale), IEEE fp32 division and
+// scale = amax * fp32(1/448) (1 when amax == 0); q = e4m3_rne(x / scale), IEEE fp32 division and
 // v_cvt_pk_fp8_f32 (round to nearest even, OCP e4m3 on gfx950), clamped to +-448 first, so the
 // bytes equal torch's (x.float() / scale).to(torch.float8_e4m3fn).
 
@@ -39,6 +39,7 @@ int check_launch(const char* what) {
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 constexpr float kE4M3Max = 448.f;
+constexpr float kInvE4M3Max = 1.f / 448.f;          // fp32-rounded reciprocal: scale = amax * (1/448)
 
 __device__ __forceinline__ float bf(uint32_t b16) { return __uint_as_float(b16 << 16); }
 
@@ -89,7 +90,7 @@ void quant_rows_kernel(const uint16_t* __restrict__ x, int64_t ldx, int64_t rows
         for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(v.v[j]));
     }
     amax = wave_max(amax);
-    const float scale = amax > 0.f ? amax / kE4M3Max : 1.f;
+    const float scale = amax > 0.f ? amax * kInvE4M3Max : 1.f;
     if (lane == 0) scales[row] = scale;
     uint8_t* orow = out + row * ldo;
     for (int c = lane; c < nch; c += 64) {
@@ -130,7 +131,7 @@ void quant_cols_t_kernel(const uint16_t* __restrict__ w, int64_t ldw, int rows, 
     float amax = 0.f;
 #pragma unroll
     for (int g = 0; g < 8; ++g) amax = fmaxf(amax, red[g][tid]);
-    const float scale = amax > 0.f ? amax / kE4M3Max : 1.f;
+    const float scale = amax > 0.f ? amax * kInvE4M3Max : 1.f;
     const int64_t col = (int64_t)cb * 256 + tid;
     scales[col] = scale;
     uint8_t* orow = out_t + col * ldo;

@@ -3,7 +3,7 @@ linears vs the bf16 path, and the engine keeping the fp8 copies in step with the
 
 The reference has no fp8, so parity is stated against the build's bf16 path (parity unpinned by the
 reference). Tolerances: the quantisation bytes and scales are bit-exact against
-``(x.float() / scale).to(float8_e4m3fn)``; an fp8 GEMM is within 2e-3 relative of the fp32 product
+``scale = amax * (1/448)``, ``(x.float() / scale).to(float8_e4m3fn)``; an fp8 GEMM is within 2e-3 relative of the fp32 product
 of its own quantised operands; against the bf16 GEMM it is within 8 % relative (two e4m3 roundings,
 3 mantissa bits, per element); a 2-layer model's loss is within 1 % of the bf16 path's."""
 import pytest
@@ -25,7 +25,7 @@ def _rel(a, b):
 
 def _ref_rows(x):
     amax = x.float().abs().amax(dim=1)
-    scale = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax))
+    scale = torch.where(amax > 0, amax * (1.0 / 448.0), torch.ones_like(amax))     # fp32 reciprocal, as ATen
     return (x.float() / scale[:, None]).to(torch.float8_e4m3fn), scale
 
 
