@@ -104,16 +104,28 @@ class Fp8Weight:
         return self.w8.numel() + self.wt8.numel() + 4 * (self.sw.numel() + self.swt.numel())
 
 
-def fp8_matmul(a2d: torch.Tensor, b8: torch.Tensor, b_scales_row: torch.Tensor) -> torch.Tensor:
-    """``a2d [M, K] (bf16, quantised per row here) @ b8 [N, K]^T`` with ``b8``'s per-row scales:
-    a hipBLASLt rowwise-scaled e4m3 GEMM, bf16 out."""
-    a8, sa = quant_rows(a2d)
+def quant_rows_cached(x: torch.Tensor):
+    """Per-row e4m3 copy of an activation ``[..., K]``, cached on the tensor (keyed by its version):
+    q/k/v (and gate/up) read the same normalised input, which is then quantised once, not 3 (2) times.
+    The copy lives exactly as long as the bf16 activation does."""
+    c = x.__dict__.get("_smt_q8")
+    if c is not None and c[0] == x._version:
+        return c[1], c[2]
+    x8, sx = quant_rows(x.reshape(-1, x.shape[-1]))
+    x._smt_q8 = (x._version, x8, sx)
+    return x8, sx
+
+
+def fp8_matmul(a2d: torch.Tensor, b8: torch.Tensor, b_scales_row: torch.Tensor, a_q=None) -> torch.Tensor:
+    """``a2d [M, K] (bf16, quantised per row here unless ``a_q`` = (a8, scales) is given) @ b8 [N, K]^T``
+    with ``b8``'s per-row scales: a hipBLASLt rowwise-scaled e4m3 GEMM, bf16 out."""
+    a8, sa = a_q if a_q is not None else quant_rows(a2d)
     return torch._scaled_mm(a8, b8.t(), scale_a=sa.view(-1, 1), scale_b=b_scales_row, out_dtype=torch.bfloat16)
 
 
 def fp8_linear_forward(x: torch.Tensor, fw: Fp8Weight) -> torch.Tensor:
     shape = x.shape
-    y = fp8_matmul(x.reshape(-1, shape[-1]), fw.w8, fw.sw_row)
+    y = fp8_matmul(None, fw.w8, fw.sw_row, a_q=quant_rows_cached(x))
     return y.view(*shape[:-1], y.shape[-1])
 
 

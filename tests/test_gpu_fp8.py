@@ -29,7 +29,7 @@ def _ref_rows(x):
     return (x.float() / scale[:, None]).to(torch.float8_e4m3fn), scale
 
 
-@pytest.mark.parametrize("rows,cols", [(64, 4096), (300, 1024), (17, 14336)])
+@pytest.mark.parametrize("rows,cols", [(64, 4096), (300, 1024), (17, 14336), (9, 16392)])   # register variants + two-pass
 def test_quant_rows_bit_exact(rows, cols):
     torch.manual_seed(rows)
     x = (torch.randn(rows, cols, device=DEV) * torch.logspace(-3, 2, rows, device=DEV)[:, None]).bfloat16()
