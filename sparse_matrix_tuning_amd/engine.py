@@ -40,7 +40,7 @@ from typing import List, Optional
 import torch
 import torch.distributed as dist
 
-from . import _hip
+from . import _hip, dgrad
 from .smt.smt import LinearLayer_MatrixSparsity
 
 TILE_ELEMS = _hip.TILE_ELEMS
@@ -104,12 +104,13 @@ class FrozenLinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, weight_t, bias):
         ctx.save_for_backward(weight_t)
+        ctx.acc = dgrad.register(x)
         return torch.nn.functional.linear(x, weight, bias)
 
     @staticmethod
     def backward(ctx, grad_output):
         (weight_t,) = ctx.saved_tensors
-        grad_input = torch.matmul(grad_output, weight_t.t()) if ctx.needs_input_grad[0] else None
+        grad_input = dgrad.input_grad(ctx.acc, grad_output, weight_t.t()) if ctx.needs_input_grad[0] else None
         return grad_input, None, None, None
 
 

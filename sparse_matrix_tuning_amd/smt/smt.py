@@ -31,7 +31,7 @@ from typing import Iterable, List, Optional, Sequence, Tuple
 import torch
 from torch import nn
 
-from .. import _hip
+from .. import _hip, dgrad
 
 Block_dimension = 256
 
@@ -277,6 +277,8 @@ class linearZ(torch.autograd.Function):
             saved = _hip.colblock_gather(_rows_ready(input.reshape(-1, weight.shape[1])), cb_dev)
             ctx.packed = True
         ctx.save_for_backward(saved, weight)
+        # q/k/v (gate/up) share their input: their data gradients accumulate in one buffer
+        ctx.acc = dgrad.register(input) if getattr(weight, "_smt_fp8", None) is None else None
         return _dense_forward(input, weight)
 
     @staticmethod
@@ -312,10 +314,8 @@ class linearZ(torch.autograd.Function):
             if fw is not None:
                 from ..fp8 import fp8_linear_dgrad
                 grad_input = fp8_linear_dgrad(grad_output, fw)
-            elif wt is not None:
-                grad_input = torch.matmul(grad_output, wt.t())
             else:
-                grad_input = torch.matmul(grad_output, weight)
+                grad_input = dgrad.input_grad(ctx.acc, grad_output, weight if wt is None else wt.t())
         return grad_input, grad_weight, None, None
 
 

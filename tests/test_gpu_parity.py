@@ -286,3 +286,25 @@ def test_end_to_end_mini_llama_loss_matches_reference_restatement():
     for n in gpu_mods:
         e = _rel(gpu_mods[n].selected_weight.grad, cpu_mods[n].selected_weight.grad)
         assert e < 3e-2, (n, e)      # whole-network bf16 pipelines on two devices
+
+
+def test_shared_input_data_gradients_accumulate_once():
+    """q/k/v-style consumers of one input (SMT modules and a frozen nn.Linear, with and without
+    transposed copies): the accumulated input gradient equals the fp64 sum of the three."""
+    from sparse_matrix_tuning_amd.engine import attach_transposed_weights
+    torch.manual_seed(12)
+    net = nn.Module()
+    Ws = [nn.Parameter((torch.randn(o, 512) * 0.05).bfloat16().to(DEV), requires_grad=False) for o in (512, 256, 256)]
+    net.q = smt.LinearLayer_MatrixSparsity(Ws[0], index_list=[(1, 1)])
+    net.k = smt.LinearLayer_MatrixSparsity(Ws[1], index_list=[(0, 0)])
+    net.v = nn.Linear(512, 256, bias=False).to(DEV).bfloat16().requires_grad_(False)
+    x = torch.randn(2, 96, 512).bfloat16().to(DEV)
+    gs = [torch.randn(2, 96, m.weight.shape[0]).bfloat16().to(DEV) for m in (net.q, net.k, net.v)]
+    truth = sum(g.double() @ m.weight.detach().double() for g, m in zip(gs, (net.q, net.k, net.v)))
+    for transposed in (False, True):
+        if transposed:
+            attach_transposed_weights(net)
+        xi = x.clone().requires_grad_(True)
+        outs = [net.q(xi), net.k(xi), net.v(xi)]
+        torch.autograd.backward(outs, gs)
+        assert _rel(xi.grad, truth) < 5e-3, transposed
