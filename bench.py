@@ -297,10 +297,14 @@ def main():
     total_params = sum(p.numel() for p in engine.module.parameters())
     log(f"selection+conversion {time.time() - t_s:.1f}s: {n_tiles} tiles, trainable {trainable} "
         f"({100.0 * trainable / total_params:.3f}% of {total_params})")
+    tile_layers = sorted({l for (_m, l) in list(sel_mlp) + list(sel_att) if l is not None})
+    log(f"tiles in {len(sel_mlp) + len(sel_att)} modules of layers {tile_layers}")
 
     # ---- SMT phase ----
     if not args.grad_ckpt:
         engine.module.gradient_checkpointing_disable()
+        if hasattr(engine.module, "disable_input_require_grads"):
+            engine.module.disable_input_require_grads()
     smt_batches = batches(args.warmup + args.steps, B, S, vocab, rank, device)
     log(f"SMT phase starts with {torch.cuda.memory_allocated(device) / 1e9:.1f} GB allocated")
     torch.cuda.reset_peak_memory_stats(device)

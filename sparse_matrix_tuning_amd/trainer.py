@@ -128,6 +128,29 @@ class GradHarvester:
         self.targets = []
 
 
+def uses_reentrant_checkpointing(model) -> bool:
+    """True when some module runs transformers' gradient checkpointing with the REENTRANT
+    ``torch.utils.checkpoint`` (the only variant that needs a grad-requiring input)."""
+    for m in model.modules():
+        if getattr(m, "gradient_checkpointing", False):
+            fn = getattr(m, "_gradient_checkpointing_func", None)
+            if (getattr(fn, "keywords", None) or {}).get("use_reentrant", True):
+                return True
+    return False
+
+
+def make_gradient_checkpointing_compatible(model) -> bool:
+    """fine_tune.py:345 -> deepspeed_helpers.py:151-161: make the embedding output require grad so
+    that reentrant activation checkpointing sees a grad-requiring input. Done only when the model
+    actually checkpoints reentrantly: otherwise the hook makes autograd run the data-gradient chain
+    through every layer down to the (frozen) embeddings, where without it the backward stops at the
+    lowest module that holds a trainable tile. Returns whether the hook was installed."""
+    if hasattr(model, "enable_input_require_grads") and uses_reentrant_checkpointing(model):
+        model.enable_input_require_grads()
+        return True
+    return False
+
+
 def select_and_convert(engine, harvester: GradHarvester, targeted_module_dims: dict,
                        num_attention_blocks: int, num_mlp_blocks: int, *, selection_strategy="no_restriction",
                        calculate_strategy="mean_abs", no_limit_mixture=False, w_decay=0.0, smt_lr=9.865e-6,
@@ -162,8 +185,7 @@ def select_and_convert(engine, harvester: GradHarvester, targeted_module_dims: d
     engine.release()
     harvester.release()
     model = convert_linear_layer_to_matrix_sparsity(model, selected_mlp, selected_att)
-    if hasattr(model, "enable_input_require_grads"):     # make_model_gradient_checkpointing_compatible
-        model.enable_input_require_grads()
+    make_gradient_checkpointing_compatible(model)
     groups = get_optimizer_sparse_grouped_parameters(model, w_decay, smt_lr)
     if not groups:
         raise RuntimeError("SMT selection produced no trainable tile (block budgets "
@@ -321,8 +343,7 @@ def select_and_convert_channels(model, harvester: ActivationHarvester, num_atten
         model = freeze_unselected_channel_layer(model, selected_mlp, selected_att)
     harvester.release()
     model = convert_linear_layer_to_channel_sparsity(model, selected_mlp, selected_att)
-    if hasattr(model, "enable_input_require_grads"):
-        model.enable_input_require_grads()
+    make_gradient_checkpointing_compatible(model)
     groups = get_optimizer_sparse_grouped_parameters(model, w_decay, smt_lr)
     if not groups:
         raise RuntimeError("channel selection produced no trainable row (channel budgets "
