@@ -401,7 +401,8 @@ def main():
                        "loss": "transformers" if args.eager_ops else "smt_ce"},
             "peak_hbm_gb": round(peak.item(), 2), "warmup_peak_hbm_gb": round(warm_peak, 2),
             "grad_ckpt_mode": ckpt_mode,
-            "step_mfma_frac": round(per_gpu * F_ALG_GFLOP_PER_TOKEN * 1e9 / (PEAK_BF16_TFLOPS * 1e12), 4),
+            "step_mfma_frac": (round(per_gpu * F_ALG_GFLOP_PER_TOKEN * 1e9 / (PEAK_BF16_TFLOPS * 1e12), 4)
+                               if args.model == "llama3-8b" else None),
             "roofline": roofline, "cpu_baseline": cpu,
             "final_loss": round(loss.item(), 5),
         }
