@@ -4,6 +4,8 @@
  * they replace eager op chains of the HF transformers LLaMA decoder that carries the SMT modules
  * (the reference trains that model through AutoModelForCausalLM, deepspeed/fine_tune.py:150-155):
  *   smt_rmsnorm_fwd/bwd   transformers LlamaRMSNorm.forward (+ autograd of its op chain)
+ *   smt_add_rmsnorm_fwd / smt_rmsnorm_bwd_add   LlamaDecoderLayer's residual add fused into the
+ *                         post-attention RMSNorm (forward) and its gradient sum (backward)
  *   smt_rope_fwd/bwd      transformers apply_rotary_pos_emb
  *   smt_swiglu_fwd/bwd    transformers LlamaMLP.forward: act_fn(gate_proj(x)) * up_proj(x), act = SiLU
  * bf16 tensors, 16-byte aligned rows; every intermediate bf16 rounding of the eager chain is kept.
@@ -34,6 +36,18 @@ const char* smt_model_ops_last_error(void);
 /* y = w * bf16(x * rsqrt(mean(x^2) + eps)); rstd[rows] (fp32) saved for the backward. */
 int smt_rmsnorm_fwd(const void* x, int64_t ld_x, const void* weight, void* y, int64_t ld_y, float* rstd,
                     int64_t rows, int32_t hidden, float eps, hipStream_t stream);
+
+/* LlamaDecoderLayer's `h = residual + attn_out; post_attention_layernorm(h)` in one pass:
+ * h = bf16(x + residual) is written to h and normalised into y (rstd saved). hidden % 512 == 0, <= 8192. */
+int smt_add_rmsnorm_fwd(const void* x, int64_t ld_x, const void* residual, int64_t ld_r, const void* weight, void* h,
+                        int64_t ld_h, void* y, int64_t ld_y, float* rstd, int64_t rows, int32_t hidden, float eps,
+                        hipStream_t stream);
+
+/* RMSNorm backward (no weight grad) plus the gradient reaching the same input by the residual path:
+ * dx = bf16(bf16(dx_norm) + dres), as autograd's sum of the two. hidden % 512 == 0, <= 8192. */
+int smt_rmsnorm_bwd_add(const void* dy, int64_t ld_dy, const void* x, int64_t ld_x, const void* weight, const float* rstd,
+                        const void* dres, int64_t ld_dres, void* dx, int64_t ld_dx, int64_t rows, int32_t hidden,
+                        hipStream_t stream);
 
 /* Number of waves (and rows of dw_partial) smt_rmsnorm_bwd uses for `rows` rows. */
 int smt_rmsnorm_bwd_waves(int64_t rows);

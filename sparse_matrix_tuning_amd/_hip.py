@@ -33,6 +33,7 @@ ABI_FUNCTIONS = (
     "smt_sq_norm", "smt_adamw_step",
     "smt_row_gather", "smt_row_scatter", "smt_column_gather", "smt_act_accumulate", "smt_channel_score",
     "smt_model_ops_last_error", "smt_rmsnorm_fwd", "smt_rmsnorm_bwd_waves", "smt_rmsnorm_bwd",
+    "smt_add_rmsnorm_fwd", "smt_rmsnorm_bwd_add",
     "smt_rope_fwd", "smt_rope_bwd", "smt_swiglu_fwd", "smt_swiglu_bwd", "smt_ce_fwd", "smt_ce_bwd",
     "smt_attn_last_error", "smt_attn_fwd", "smt_attn_bwd",
     "smt_fp8_last_error", "smt_quant_rows_e4m3", "smt_quant_cols_t_e4m3",
@@ -110,6 +111,8 @@ _SIGS = {
     "smt_model_ops_last_error": (ctypes.c_char_p, []),
     "smt_rmsnorm_fwd": (ctypes.c_int, [_P, _I64, _P, _P, _I64, _P, _I64, _I32, ctypes.c_float, _P]),
     "smt_rmsnorm_bwd_waves": (ctypes.c_int, [_I64]),
+    "smt_add_rmsnorm_fwd": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _P, _I64, _P, _I64, _P, _I64, _I32, ctypes.c_float, _P]),
+    "smt_rmsnorm_bwd_add": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _P, _P, _I64, _P, _I64, _I64, _I32, _P]),
     "smt_rmsnorm_bwd": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _P, _P, _I64, _P, _P, _I64, _I32, _P]),
     "smt_rope_fwd": (ctypes.c_int, [ctypes.POINTER(RopeTensor), ctypes.POINTER(RopeTensor), _P, _P, _I64, _I64, _I64, _I32, _I32, _P]),
     "smt_rope_bwd": (ctypes.c_int, [ctypes.POINTER(RopeTensor), ctypes.POINTER(RopeTensor), _P, _P, _I64, _I64, _I64, _I32, _I32, _P]),
@@ -153,7 +156,7 @@ def load(build_if_missing: bool = False) -> ctypes.CDLL:
 def _check(rc: int, what: str) -> None:
     if rc != 0:
         lib = load()
-        if what.startswith(("smt_rmsnorm", "smt_rope", "smt_swiglu", "smt_ce_")):
+        if what.startswith(("smt_rmsnorm", "smt_add_rmsnorm", "smt_rope", "smt_swiglu", "smt_ce_")):
             err = lib.smt_model_ops_last_error
         elif what.startswith("smt_attn"):
             err = lib.smt_attn_last_error

@@ -160,6 +160,93 @@ void rmsnorm_dw_kernel(const float* __restrict__ partial, int64_t n_waves, int H
     dw[col] = (uint16_t)tobf(s);
 }
 
+// Register-resident variants (hidden = 512 * CPL, CPL <= 16): one wave per row keeps its 8 * CPL
+// values in registers, so each input is read from HBM once (the generic kernels above read the row
+// twice). Same arithmetic and the same per-lane accumulation order, so the results are bit-identical
+// to them.
+//
+// Forward with an optional fused residual add (LlamaDecoderLayer: h = residual + attn_out, then
+// post_attention_layernorm(h)): h = bf16(x + res) is written out as well and normalised.
+template <int CPL, bool ADD>
+__global__ __launch_bounds__(256)
+void rmsnorm_fwd_reg_kernel(const uint16_t* __restrict__ x, int64_t ldx, const uint16_t* __restrict__ res, int64_t ldr,
+                            const uint16_t* __restrict__ w, uint16_t* __restrict__ h, int64_t ldh,
+                            uint16_t* __restrict__ y, int64_t ldy, float* __restrict__ rstd, int64_t rows, int H,
+                            float eps) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    F8 v[CPL];
+    float ss = 0.f;
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+        const int c = lane + 64 * k;
+        v[k] = ld8(x + row * ldx + c * 8);
+        if (ADD) {
+            const F8 rv = ld8(res + row * ldr + c * 8);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[k].v[j] = rbf(v[k].v[j] + rv.v[j]);
+            st8(h + row * ldh + c * 8, v[k]);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ss += v[k].v[j] * v[k].v[j];
+    }
+    ss = wave_sum_f(ss);
+    const float r = 1.0f / sqrtf(ss / (float)H + eps);
+    if (lane == 0) rstd[row] = r;
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+        const int c = lane + 64 * k;
+        const F8 wv = ld8(w + c * 8);
+        F8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o.v[j] = wv.v[j] * rbf(v[k].v[j] * r);
+        st8(y + row * ldy + c * 8, o);
+    }
+}
+
+// Backward without weight grad; with ADD the gradient reaching the norm's input by the residual path
+// is added as autograd would: dx = bf16(bf16(dx_norm) + dres).
+template <int CPL, bool ADD>
+__global__ __launch_bounds__(256)
+void rmsnorm_bwd_reg_kernel(const uint16_t* __restrict__ dy, int64_t lddy, const uint16_t* __restrict__ x, int64_t ldx,
+                            const uint16_t* __restrict__ w, const float* __restrict__ rstd,
+                            const uint16_t* __restrict__ dres, int64_t lddr, uint16_t* __restrict__ dx, int64_t lddx,
+                            int64_t rows, int H) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const float r = rstd[row];
+    F8 gw[CPL], xv[CPL];
+    float dot = 0.f;
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+        const int c = lane + 64 * k;
+        xv[k] = ld8(x + row * ldx + c * 8);
+        const F8 gv = ld8(dy + row * lddy + c * 8), wv = ld8(w + c * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            gw[k].v[j] = rbf(gv.v[j] * wv.v[j]);
+            dot += gw[k].v[j] * xv[k].v[j];
+        }
+    }
+    dot = wave_sum_f(dot);
+    const float coef = r * r * r * dot / (float)H;
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+        const int c = lane + 64 * k;
+        F8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o.v[j] = r * gw[k].v[j] - xv[k].v[j] * coef;
+        if (ADD) {
+            const F8 dr = ld8(dres + row * lddr + c * 8);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o.v[j] = rbf(o.v[j]) + dr.v[j];
+        }
+        st8(dx + row * lddx + c * 8, o);
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // RoPE (apply_rotary_pos_emb): per element pair (d, d+D/2) of one head row,
 //   lo' = bf16(bf16(lo*c_lo) + bf16(-hi*s_lo)),  hi' = bf16(bf16(hi*c_hi) + bf16(lo*s_hi))
@@ -370,6 +457,56 @@ void ce_bwd_kernel(const uint16_t* __restrict__ logits, int64_t ld, const int64_
     for (; c < n8; c += kCeThreads) st8(dr + c * 8, ce_grad8(ld8(xr + c * 8), c * 8, lab, l2, w));
 }
 
+template <bool ADD>
+int fwd_reg_dispatch(int cpl, dim3 grid, hipStream_t stream, const uint16_t* x, int64_t ldx, const uint16_t* r, int64_t ldr,
+                     const uint16_t* w, uint16_t* h, int64_t ldh, uint16_t* y, int64_t ldy, float* rstd, int64_t rows,
+                     int H, float eps) {
+#define FWD_REG(C) case C: hipLaunchKernelGGL((rmsnorm_fwd_reg_kernel<C, ADD>), grid, dim3(256), 0, stream, x, ldx, r, ldr, w, h, ldh, y, ldy, rstd, rows, H, eps); break;
+    switch (cpl) {
+        FWD_REG(1) FWD_REG(2) FWD_REG(3) FWD_REG(4) FWD_REG(5) FWD_REG(6) FWD_REG(7) FWD_REG(8)
+        FWD_REG(9) FWD_REG(10) FWD_REG(11) FWD_REG(12) FWD_REG(13) FWD_REG(14) FWD_REG(15) FWD_REG(16)
+        default: return fail(-1, "rmsnorm: hidden %d", H);
+    }
+#undef FWD_REG
+    return check_launch("rmsnorm_fwd_reg_kernel");
+}
+
+int launch_fwd_reg(bool add, const void* x, int64_t ldx, const void* r, int64_t ldr, const void* w, void* h, int64_t ldh,
+                   void* y, int64_t ldy, float* rstd, int64_t rows, int H, float eps, hipStream_t stream) {
+    const dim3 grid((unsigned)((rows + 3) / 4));
+    const int cpl = H / 512;
+    if (add)
+        return fwd_reg_dispatch<true>(cpl, grid, stream, (const uint16_t*)x, ldx, (const uint16_t*)r, ldr,
+                                      (const uint16_t*)w, (uint16_t*)h, ldh, (uint16_t*)y, ldy, rstd, rows, H, eps);
+    return fwd_reg_dispatch<false>(cpl, grid, stream, (const uint16_t*)x, ldx, nullptr, 0, (const uint16_t*)w, nullptr, 0,
+                                   (uint16_t*)y, ldy, rstd, rows, H, eps);
+}
+
+template <bool ADD>
+int bwd_reg_dispatch(int cpl, dim3 grid, hipStream_t stream, const uint16_t* dy, int64_t lddy, const uint16_t* x, int64_t ldx,
+                     const uint16_t* w, const float* rstd, const uint16_t* dres, int64_t lddr, uint16_t* dx, int64_t lddx,
+                     int64_t rows, int H) {
+#define BWD_REG(C) case C: hipLaunchKernelGGL((rmsnorm_bwd_reg_kernel<C, ADD>), grid, dim3(256), 0, stream, dy, lddy, x, ldx, w, rstd, dres, lddr, dx, lddx, rows, H); break;
+    switch (cpl) {
+        BWD_REG(1) BWD_REG(2) BWD_REG(3) BWD_REG(4) BWD_REG(5) BWD_REG(6) BWD_REG(7) BWD_REG(8)
+        BWD_REG(9) BWD_REG(10) BWD_REG(11) BWD_REG(12) BWD_REG(13) BWD_REG(14) BWD_REG(15) BWD_REG(16)
+        default: return fail(-1, "rmsnorm: hidden %d", H);
+    }
+#undef BWD_REG
+    return check_launch("rmsnorm_bwd_reg_kernel");
+}
+
+int launch_bwd_reg(bool add, const void* dy, int64_t lddy, const void* x, int64_t ldx, const void* w, const float* rstd,
+                   const void* dres, int64_t lddr, void* dx, int64_t lddx, int64_t rows, int H, hipStream_t stream) {
+    const dim3 grid((unsigned)((rows + 3) / 4));
+    const int cpl = H / 512;
+    if (add)
+        return bwd_reg_dispatch<true>(cpl, grid, stream, (const uint16_t*)dy, lddy, (const uint16_t*)x, ldx,
+                                      (const uint16_t*)w, rstd, (const uint16_t*)dres, lddr, (uint16_t*)dx, lddx, rows, H);
+    return bwd_reg_dispatch<false>(cpl, grid, stream, (const uint16_t*)dy, lddy, (const uint16_t*)x, ldx,
+                                   (const uint16_t*)w, rstd, nullptr, 0, (uint16_t*)dx, lddx, rows, H);
+}
+
 }  // namespace
 
 extern "C" {
@@ -412,9 +549,37 @@ int smt_rmsnorm_fwd(const void* x, int64_t ld_x, const void* weight, void* y, in
     if (!aligned16(x) || !aligned16(weight) || !aligned16(y) || (ld_x & 7) || (ld_y & 7))
         return fail(-2, "smt_rmsnorm_fwd: 16-byte aligned rows required");
     const int64_t blocks = (rows + 3) / 4;
+    if (hidden % 512 == 0 && hidden <= 8192)
+        return launch_fwd_reg(false, x, ld_x, nullptr, 0, weight, nullptr, 0, y, ld_y, rstd, rows, hidden, eps, stream);
     hipLaunchKernelGGL(rmsnorm_fwd_kernel, dim3((unsigned)blocks), dim3(256), 0, stream,
                        (const uint16_t*)x, ld_x, (const uint16_t*)weight, (uint16_t*)y, ld_y, rstd, rows, hidden, eps);
     return check_launch("rmsnorm_fwd_kernel");
+}
+
+int smt_add_rmsnorm_fwd(const void* x, int64_t ld_x, const void* residual, int64_t ld_r, const void* weight, void* h,
+                        int64_t ld_h, void* y, int64_t ld_y, float* rstd, int64_t rows, int32_t hidden, float eps,
+                        hipStream_t stream) {
+    if (rows < 0 || hidden <= 0 || hidden % 512 || hidden > 8192)
+        return fail(-1, "smt_add_rmsnorm_fwd: hidden %d must be a multiple of 512, <= 8192", hidden);
+    if (rows == 0) return 0;
+    if (!x || !residual || !weight || !h || !y || !rstd) return fail(-1, "smt_add_rmsnorm_fwd: null pointer");
+    if (!aligned16(x) || !aligned16(residual) || !aligned16(weight) || !aligned16(h) || !aligned16(y) ||
+        (ld_x & 7) || (ld_r & 7) || (ld_h & 7) || (ld_y & 7))
+        return fail(-2, "smt_add_rmsnorm_fwd: 16-byte aligned rows required");
+    return launch_fwd_reg(true, x, ld_x, residual, ld_r, weight, h, ld_h, y, ld_y, rstd, rows, hidden, eps, stream);
+}
+
+int smt_rmsnorm_bwd_add(const void* dy, int64_t ld_dy, const void* x, int64_t ld_x, const void* weight, const float* rstd,
+                        const void* dres, int64_t ld_dres, void* dx, int64_t ld_dx, int64_t rows, int32_t hidden,
+                        hipStream_t stream) {
+    if (rows < 0 || hidden <= 0 || hidden % 512 || hidden > 8192)
+        return fail(-1, "smt_rmsnorm_bwd_add: hidden %d must be a multiple of 512, <= 8192", hidden);
+    if (rows == 0) return 0;
+    if (!dy || !x || !weight || !rstd || !dres || !dx) return fail(-1, "smt_rmsnorm_bwd_add: null pointer");
+    if (!aligned16(dy) || !aligned16(x) || !aligned16(weight) || !aligned16(dres) || !aligned16(dx) || (ld_dy & 7) ||
+        (ld_x & 7) || (ld_dres & 7) || (ld_dx & 7))
+        return fail(-2, "smt_rmsnorm_bwd_add: 16-byte aligned rows required");
+    return launch_bwd_reg(true, dy, ld_dy, x, ld_x, weight, rstd, dres, ld_dres, dx, ld_dx, rows, hidden, stream);
 }
 
 int smt_rmsnorm_bwd_waves(int64_t rows) {
@@ -435,6 +600,8 @@ int smt_rmsnorm_bwd(const void* dy, int64_t ld_dy, const void* x, int64_t ld_x, 
     const uint16_t *pdy = (const uint16_t*)dy, *px = (const uint16_t*)x, *pw = (const uint16_t*)weight;
     uint16_t* pdx = (uint16_t*)dx;
     if (dw == nullptr) {
+        if (hidden % 512 == 0 && hidden <= 8192)
+            return launch_bwd_reg(false, dy, ld_dy, x, ld_x, weight, rstd, nullptr, 0, dx, ld_dx, rows, hidden, stream);
         hipLaunchKernelGGL((rmsnorm_bwd_kernel<false, 1>), grid, block, 0, stream, pdy, ld_dy, px, ld_x, pw, rstd, pdx, ld_dx,
                            nullptr, rows, hidden);
         return check_launch("rmsnorm_bwd_kernel");

@@ -90,6 +90,77 @@ def fused_rmsnorm_forward(self, hidden_states):
     return FusedRMSNormFn.apply(hidden_states, self.weight, self.variance_epsilon)
 
 
+class FusedAddRMSNormFn(torch.autograd.Function):
+    """``h = x + residual`` and ``y = RMSNorm(h)`` (LlamaDecoderLayer's attention residual feeding
+    ``post_attention_layernorm``) in one pass; the backward adds the gradient that reaches ``h`` by
+    the residual path inside the norm's backward. Returns ``(h, y)``."""
+
+    @staticmethod
+    def forward(ctx, x, residual, weight, eps):
+        for t, n in ((x, "x"), (residual, "residual"), (weight, "weight")):
+            _need(t, "add+rmsnorm " + n)
+        x2, r2 = _rows2d(x), _rows2d(residual)
+        rows, H = x2.shape
+        h = torch.empty((rows, H), dtype=x.dtype, device=x.device)
+        y = torch.empty((rows, H), dtype=x.dtype, device=x.device)
+        rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+        w = weight.contiguous()
+        rc = _hip.load().smt_add_rmsnorm_fwd(x2.data_ptr(), x2.stride(0), r2.data_ptr(), r2.stride(0), w.data_ptr(),
+                                             h.data_ptr(), H, y.data_ptr(), H, rstd.data_ptr(), rows, H, float(eps),
+                                             _stream(x))
+        _hip._check(rc, "smt_add_rmsnorm_fwd")
+        ctx.save_for_backward(h, w, rstd)
+        ctx.shape = x.shape
+        return h.view(x.shape), y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dh, dy):
+        h, w, rstd = ctx.saved_tensors
+        rows, H = h.shape
+        lib = _hip.load()
+        dw = None
+        if dy is None:
+            dx = dh
+        elif ctx.needs_input_grad[2] or dh is None:
+            # weight grad (full fine-tuning warm-up) or no residual gradient: the plain norm backward
+            dy2 = _rows2d(dy)
+            dx = torch.empty_like(h)
+            partial = None
+            if ctx.needs_input_grad[2]:
+                partial = torch.empty(lib.smt_rmsnorm_bwd_waves(rows), H, dtype=torch.float32, device=h.device)
+                dw = torch.empty(H, dtype=w.dtype, device=w.device)
+            rc = lib.smt_rmsnorm_bwd(dy2.data_ptr(), dy2.stride(0), h.data_ptr(), H, w.data_ptr(), rstd.data_ptr(),
+                                     dx.data_ptr(), H, None if partial is None else partial.data_ptr(),
+                                     None if dw is None else dw.data_ptr(), rows, H, _stream(h))
+            _hip._check(rc, "smt_rmsnorm_bwd")
+            dx = dx.view(ctx.shape)
+            if dh is not None:
+                dx = dx + dh
+        else:
+            dy2, dh2 = _rows2d(dy), _rows2d(dh)
+            dx = torch.empty_like(h)
+            rc = lib.smt_rmsnorm_bwd_add(dy2.data_ptr(), dy2.stride(0), h.data_ptr(), H, w.data_ptr(), rstd.data_ptr(),
+                                         dh2.data_ptr(), dh2.stride(0), dx.data_ptr(), H, rows, H, _stream(h))
+            _hip._check(rc, "smt_rmsnorm_bwd_add")
+            dx = dx.view(ctx.shape)
+        return dx, dx, dw, None
+
+
+def fused_decoder_layer_forward(self, hidden_states, attention_mask=None, position_ids=None, past_key_values=None,
+                                use_cache=False, position_embeddings=None, **kwargs):
+    """Drop-in for ``LlamaDecoderLayer.forward`` with the attention residual add fused into the
+    post-attention RMSNorm (:class:`FusedAddRMSNormFn`); the same ops in the same order otherwise."""
+    residual = hidden_states
+    hidden_states = self.input_layernorm(hidden_states)
+    hidden_states, _ = self.self_attn(hidden_states=hidden_states, attention_mask=attention_mask,
+                                      position_ids=position_ids, past_key_values=past_key_values, use_cache=use_cache,
+                                      position_embeddings=position_embeddings, **kwargs)
+    norm = self.post_attention_layernorm
+    residual, hidden_states = FusedAddRMSNormFn.apply(hidden_states, residual, norm.weight, norm.variance_epsilon)
+    hidden_states = self.mlp(hidden_states)
+    return residual + hidden_states
+
+
 # ------------------------------------------------------------------------------------------------
 # RoPE
 # ------------------------------------------------------------------------------------------------
@@ -365,14 +436,14 @@ def eager_apply_rotary_pos_emb(*a, **k):
 
 
 def patch_llama(model: nn.Module, attention: bool = True, loss: bool = True) -> dict:
-    """Route a transformers LLaMA model's RMSNorm / RoPE / SwiGLU (and, with ``attention``, its
+    """Route a transformers LLaMA model's RMSNorm / RoPE / SwiGLU / attention-residual add (and, with ``attention``, its
     attention; with ``loss``, its causal-LM loss) through the fused kernels. RoPE is patched at
     module level (``modeling_llama.apply_rotary_pos_emb``, looked up by ``LlamaAttention.forward`` at
     call time); attention by switching ``config._attn_implementation`` to the registered
     ``smt_flash``; the loss through the model's ``loss_function`` attribute.
     Returns counts of patched modules. Idempotent."""
     ml = _ml()
-    counts = {"rmsnorm": 0, "mlp": 0, "rope": 1, "attention": 0, "loss": 0}
+    counts = {"rmsnorm": 0, "mlp": 0, "rope": 1, "attention": 0, "loss": 0, "decoder": 0}
     if loss and hasattr(type(model), "loss_function"):
         model.loss_function = fused_causal_lm_loss
         counts["loss"] = 1
@@ -388,6 +459,9 @@ def patch_llama(model: nn.Module, attention: bool = True, loss: bool = True) -> 
         if isinstance(m, ml.LlamaRMSNorm):
             m.forward = fused_rmsnorm_forward.__get__(m, type(m))
             counts["rmsnorm"] += 1
+        elif isinstance(m, ml.LlamaDecoderLayer):
+            m.forward = fused_decoder_layer_forward.__get__(m, type(m))
+            counts["decoder"] += 1
         elif isinstance(m, ml.LlamaMLP):
             act = getattr(m, "act_fn", None)
             if act is None or "silu" not in type(act).__name__.lower():
@@ -408,5 +482,5 @@ def unpatch_llama(model: nn.Module = None) -> None:
         if "_loss_function" in model.__dict__:
             del model.__dict__["_loss_function"]
         for m in model.modules():
-            if isinstance(m, (ml.LlamaRMSNorm, ml.LlamaMLP)) and "forward" in m.__dict__:
+            if isinstance(m, (ml.LlamaRMSNorm, ml.LlamaMLP, ml.LlamaDecoderLayer)) and "forward" in m.__dict__:
                 del m.__dict__["forward"]

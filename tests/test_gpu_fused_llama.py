@@ -108,7 +108,7 @@ def test_patched_mini_llama_matches_eager():
     model.zero_grad(set_to_none=True)
     try:
         counts = fl.patch_llama(model)
-        assert counts["rmsnorm"] == 9 and counts["mlp"] == 4 and counts["attention"] == 4
+        assert counts["rmsnorm"] == 9 and counts["mlp"] == 4 and counts["attention"] == 4 and counts["decoder"] == 4
         assert model.config._attn_implementation == "smt_flash"
         out_f = model(input_ids=ids, labels=ids, use_cache=False)
         out_f.loss.backward()
@@ -120,3 +120,37 @@ def test_patched_mini_llama_matches_eager():
     worst = max(((p.grad.float() - ge[n].float()).norm() / ge[n].float().norm()).item()
                 for n, p in model.named_parameters() if p.grad is not None)
     assert worst < 5e-2, worst
+
+
+@pytest.mark.parametrize("H", [4096, 512])
+@pytest.mark.parametrize("weight_grad", [False, True])
+def test_fused_add_rmsnorm_vs_eager(H, weight_grad):
+    """h = x + residual, y = RMSNorm(h); grads of (x, residual, weight) with a residual-path gradient."""
+    from transformers.models.llama.modeling_llama import LlamaRMSNorm
+    torch.manual_seed(H)
+    norm = LlamaRMSNorm(H, eps=1e-5).to(DEV).bfloat16()
+    with torch.no_grad():
+        norm.weight.copy_(torch.randn(H) * 0.2 + 1.0)
+    norm.weight.requires_grad_(weight_grad)
+    x = (torch.randn(2, 133, H, device=DEV) * 2).bfloat16()
+    r = (torch.randn(2, 133, H, device=DEV) * 3).bfloat16()
+    dh = torch.randn(2, 133, H, device=DEV).bfloat16()
+    dy = torch.randn(2, 133, H, device=DEV).bfloat16()
+    xe, re_ = x.clone().requires_grad_(True), r.clone().requires_grad_(True)
+    he = re_ + xe
+    ye = norm(he)
+    torch.autograd.backward([he, ye], [dh, dy])
+    dw_e = norm.weight.grad.clone() if weight_grad else None
+    norm.weight.grad = None
+    xf, rf = x.clone().requires_grad_(True), r.clone().requires_grad_(True)
+    hf, yf = fl.FusedAddRMSNormFn.apply(xf, rf, norm.weight, norm.variance_epsilon)
+    torch.autograd.backward([hf, yf], [dh, dy])
+    assert torch.equal(hf, he)
+    ok, bad = _ulp_close(yf, ye)
+    assert ok, bad
+    for a, b in ((xf.grad, xe.grad), (rf.grad, re_.grad)):
+        rel = ((a.float() - b.float()).norm() / b.float().norm()).item()
+        assert rel < 5e-3, rel
+    if weight_grad:
+        relw = ((norm.weight.grad.float() - dw_e.float()).norm() / dw_e.float().norm()).item()
+        assert relw < 5e-3, relw
