@@ -149,6 +149,57 @@ void quant_rows_reg_kernel(const uint16_t* __restrict__ x, int64_t ldx, int64_t 
     }
 }
 
+// Wide rows (the 14336-wide MLP activations and gradients): one 256-thread workgroup per row, each
+// thread holding CPT 16-B chunks in registers (7 at 14336), the row maximum combined through LDS.
+// One wave per row with 28 chunks in flight ran latency-bound at 3.3 TB/s.
+template <int CPT>
+__global__ __launch_bounds__(256)
+void quant_rows_wg_kernel(const uint16_t* __restrict__ x, int64_t ldx, int64_t rows, int cols,
+                          const int32_t* __restrict__ row_blocks, int64_t n_sel, uint8_t* __restrict__ out,
+                          int64_t ldo, float* __restrict__ scales) {
+    __shared__ float wmax[4];
+    const int tid = threadIdx.x;
+    const int64_t idx = blockIdx.x;
+    const int64_t row = row_blocks ? (int64_t)row_blocks[idx >> 8] * 256 + (idx & 255) : idx;
+    if (row >= rows) return;                                  // uniform per workgroup
+    const uint16_t* xr = x + row * ldx;
+    const int nch = cols >> 3;
+    uint4 buf[CPT];
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+        const int c = tid + 256 * i;
+        buf[i] = c < nch ? *reinterpret_cast<const uint4*>(xr + c * 8) : make_uint4(0u, 0u, 0u, 0u);
+    }
+    float amax = 0.f;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+        const uint32_t w[4] = {buf[i].x, buf[i].y, buf[i].z, buf[i].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            amax = fmaxf(amax, fmaxf(fabsf(bf(w[j] & 0xffffu)), fabsf(bf(w[j] >> 16))));
+    }
+    amax = wave_max(amax);
+    if ((tid & 63) == 0) wmax[tid >> 6] = amax;
+    __syncthreads();
+    amax = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
+    const float scale = amax > 0.f ? amax * kInvE4M3Max : 1.f;
+    if (tid == 0) scales[row] = scale;
+    uint8_t* orow = out + row * ldo;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+        const int c = tid + 256 * i;
+        if (c < nch) {
+            const uint32_t w[4] = {buf[i].x, buf[i].y, buf[i].z, buf[i].w};
+            uint2 o;
+            o.x = pack4(qv(bf(w[0] & 0xffffu), scale), qv(bf(w[0] >> 16), scale),
+                        qv(bf(w[1] & 0xffffu), scale), qv(bf(w[1] >> 16), scale));
+            o.y = pack4(qv(bf(w[2] & 0xffffu), scale), qv(bf(w[2] >> 16), scale),
+                        qv(bf(w[3] & 0xffffu), scale), qv(bf(w[3] >> 16), scale));
+            *reinterpret_cast<uint2*>(orow + c * 8) = o;
+        }
+    }
+}
+
 // One workgroup per 256-column block: pass 1 the 256 column maxima (8 row groups x 32 lanes of 8
 // columns, combined in LDS); pass 2 in 64-row slabs staged through LDS, each thread converting its
 // column's 64 values into 64 contiguous bytes of the transposed output row.
@@ -220,7 +271,7 @@ int smt_quant_rows_e4m3(const void* x, int64_t ld_x, int64_t rows, int32_t cols,
     if (!aligned16(x) || (ld_x & 7) || (reinterpret_cast<uintptr_t>(out) & 7) || (ld_out & 7))
         return fail(-2, "smt_quant_rows_e4m3: 16-byte aligned bf16 rows and 8-byte aligned fp8 rows required");
     const int64_t blocks = (n_sel + 3) / 4;
-    if (blocks > 0x7fffffffLL) return fail(-1, "smt_quant_rows_e4m3: too many rows");
+    if (blocks > 0x7fffffffLL || n_sel > 0x7fffffffLL) return fail(-1, "smt_quant_rows_e4m3: too many rows");
     const uint16_t* px = static_cast<const uint16_t*>(x);
     uint8_t* po = static_cast<uint8_t*>(out);
     const int nch = cols >> 3;
@@ -230,8 +281,8 @@ int smt_quant_rows_e4m3(const void* x, int64_t ld_x, int64_t rows, int32_t cols,
     else if (nch <= 64 * 8)
         hipLaunchKernelGGL(quant_rows_reg_kernel<8>, dim3((unsigned)blocks), dim3(256), 0, stream, px, ld_x, rows, cols,
                            row_blocks_dev, n_sel, po, ld_out, scales);
-    else if (nch <= 64 * 28)
-        hipLaunchKernelGGL(quant_rows_reg_kernel<28>, dim3((unsigned)blocks), dim3(256), 0, stream, px, ld_x, rows, cols,
+    else if (nch <= 256 * 8)
+        hipLaunchKernelGGL(quant_rows_wg_kernel<8>, dim3((unsigned)n_sel), dim3(256), 0, stream, px, ld_x, rows, cols,
                            row_blocks_dev, n_sel, po, ld_out, scales);
     else
         hipLaunchKernelGGL(quant_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, px, ld_x, rows, cols,
