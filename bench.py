@@ -137,6 +137,51 @@ def install_wgrad_timer(timer: WgradTimer):
     _hip.tile_wgrad = timed
 
 
+class AttnTimer:
+    """HIP events around every smt_flash forward / backward launch (current stream), with the causal
+    attention FLOPs each one does: forward 2 GEMM-equivalents (QK^T, PV) over the causal half,
+    backward 5 (S and dP recomputed, dV, dK, dQ) plus the 2 recomputed ones of the separate dQ
+    kernel (S, dP): 7 in this implementation, 5 algorithmic."""
+
+    def __init__(self):
+        self.enabled = False
+        self.records = []      # (start, end, algorithmic flops)
+
+    def wrap(self, fn, flops_fn):
+        def timed(*a, **k):
+            if not self.enabled:
+                return fn(*a, **k)
+            fl = flops_fn(*a)
+            s = torch.cuda.current_stream()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            r = fn(*a, **k)
+            e1.record(s)
+            self.records.append((e0, e1, fl))
+            return r
+        return timed
+
+    def summary(self):
+        if not self.records:
+            return None
+        torch.cuda.synchronize()
+        t = sum(a.elapsed_time(b) for a, b, _ in self.records) * 1e-3
+        return dict(launches=len(self.records), seconds=t, flops=sum(r[2] for r in self.records))
+
+
+def install_attn_timer(timer: AttnTimer):
+    from sparse_matrix_tuning_amd import fused_llama as fl
+    fn_cls = fl.FlashAttnFn
+
+    def unit(q):                  # one causal QK^T-sized GEMM: 2 * B * Hq * S^2 / 2 * D
+        B, Hq, S, D = q.shape
+        return 2.0 * B * Hq * S * S / 2 * D
+
+    fwd, bwd = fn_cls.forward, fn_cls.backward
+    fn_cls.forward = staticmethod(timer.wrap(fwd, lambda ctx, q, *r: 2 * unit(q)))
+    fn_cls.backward = staticmethod(timer.wrap(bwd, lambda ctx, do: 5 * unit(ctx.saved_tensors[0])))
+
+
 def build_model(name, device):
     from transformers import LlamaConfig, LlamaForCausalLM
     cfg = LlamaConfig(**MODELS[name])
@@ -240,6 +285,9 @@ def main():
 
     timer = WgradTimer()
     install_wgrad_timer(timer)
+    atimer = AttnTimer()
+    if not (args.eager_ops or args.sdpa_attention):
+        install_attn_timer(atimer)
 
     t_setup = time.time()
     model = build_model(args.model, device)
@@ -321,6 +369,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     timer.enabled = True
+    atimer.enabled = True
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = step(smt_batches[args.warmup + i])
@@ -329,6 +378,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     timer.enabled = False
+    atimer.enabled = False
     t_max = torch.tensor([elapsed], dtype=torch.float64, device=device)
     peak = torch.tensor([torch.cuda.max_memory_allocated(device) / 1e9], dtype=torch.float64, device=device)
     if world > 1:
@@ -338,6 +388,7 @@ def main():
     tokens = world * B * S * args.steps
     value = tokens / elapsed
     w = timer.summary()
+    a_sum = atimer.summary()
 
     # ---- the reference's memory policy (per-layer recompute), same engine and tiles ----
     ckpt_mode = None
@@ -403,7 +454,14 @@ def main():
             "grad_ckpt_mode": ckpt_mode,
             "step_mfma_frac": (round(per_gpu * F_ALG_GFLOP_PER_TOKEN * 1e9 / (PEAK_BF16_TFLOPS * 1e12), 4)
                                if args.model == "llama3-8b" else None),
-            "roofline": roofline, "cpu_baseline": cpu,
+            "roofline": roofline,
+            "roofline_attention": None if not a_sum else {
+                "bound": "mfma", "kernel": "smt_flash causal GQA attention (attn_fwd / attn_delta + attn_dq + attn_dkdv)",
+                "achieved": round(a_sum["flops"] / a_sum["seconds"] / 1e12, 1), "peak": PEAK_BF16_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(a_sum["flops"] / a_sum["seconds"] / 1e12 / PEAK_BF16_TFLOPS, 4),
+                "launches": a_sum["launches"], "avg_launch_us": round(a_sum["seconds"] / a_sum["launches"] * 1e6, 1),
+                "flops_note": "algorithmic causal FLOPs: fwd 2, bwd 5 QK^T-sized GEMMs per launch"},
+            "cpu_baseline": cpu,
             "final_loss": round(loss.item(), 5),
         }
         line = json.dumps(out)
