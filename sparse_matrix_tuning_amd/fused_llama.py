@@ -90,6 +90,33 @@ def fused_rmsnorm_forward(self, hidden_states):
     return FusedRMSNormFn.apply(hidden_states, self.weight, self.variance_epsilon)
 
 
+class FusedRMSNormResFn(torch.autograd.Function):
+    """``LlamaDecoderLayer``'s ``residual = x; y = input_layernorm(x)`` as one node returning
+    ``(y, residual)`` (the residual an alias of ``x``), so that the backward receives both gradients
+    of ``x`` and sums them inside the norm's backward kernel (``smt_rmsnorm_bwd_add``) instead of an
+    autograd add."""
+
+    @staticmethod
+    def forward(ctx, x, weight, eps):
+        y = FusedRMSNormFn.forward(ctx, x, weight, eps)
+        return y, x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dy, dres):
+        x2, w, rstd = ctx.saved_tensors
+        if dres is None or ctx.needs_input_grad[1] or x2.shape[1] % 512 or x2.shape[1] > 8192:
+            dx, dw, _ = FusedRMSNormFn.backward(ctx, dy)
+            return (dx if dres is None else dx + dres), dw, None
+        rows, H = x2.shape
+        dy2, dr2 = _rows2d(dy), _rows2d(dres)
+        dx = torch.empty_like(x2)
+        rc = _hip.load().smt_rmsnorm_bwd_add(dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0), w.data_ptr(),
+                                             rstd.data_ptr(), dr2.data_ptr(), dr2.stride(0), dx.data_ptr(), H, rows, H,
+                                             _stream(x2))
+        _hip._check(rc, "smt_rmsnorm_bwd_add")
+        return dx.view(ctx.shape), None, None
+
+
 class FusedAddRMSNormFn(torch.autograd.Function):
     """``h = x + residual`` and ``y = RMSNorm(h)`` (LlamaDecoderLayer's attention residual feeding
     ``post_attention_layernorm``) in one pass; the backward adds the gradient that reaches ``h`` by
@@ -149,9 +176,10 @@ class FusedAddRMSNormFn(torch.autograd.Function):
 def fused_decoder_layer_forward(self, hidden_states, attention_mask=None, position_ids=None, past_key_values=None,
                                 use_cache=False, position_embeddings=None, **kwargs):
     """Drop-in for ``LlamaDecoderLayer.forward`` with the attention residual add fused into the
-    post-attention RMSNorm (:class:`FusedAddRMSNormFn`); the same ops in the same order otherwise."""
-    residual = hidden_states
-    hidden_states = self.input_layernorm(hidden_states)
+    post-attention RMSNorm (:class:`FusedAddRMSNormFn`) and the input norm's two gradients summed in
+    its backward (:class:`FusedRMSNormResFn`); the same ops in the same order otherwise."""
+    norm1 = self.input_layernorm
+    hidden_states, residual = FusedRMSNormResFn.apply(hidden_states, norm1.weight, norm1.variance_epsilon)
     hidden_states, _ = self.self_attn(hidden_states=hidden_states, attention_mask=attention_mask,
                                       position_ids=position_ids, past_key_values=past_key_values, use_cache=use_cache,
                                       position_embeddings=position_embeddings, **kwargs)
