@@ -68,21 +68,26 @@ class FusedRMSNormFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x2, w, rstd = ctx.saved_tensors
-        rows, H = x2.shape
-        dy2 = _rows2d(dy)
-        dx = torch.empty_like(x2)
-        lib = _hip.load()
-        dw = partial = None
-        if ctx.needs_input_grad[1]:
-            waves = lib.smt_rmsnorm_bwd_waves(rows)
-            partial = torch.empty(waves, H, dtype=torch.float32, device=x2.device)
-            dw = torch.empty(H, dtype=w.dtype, device=w.device)
-        rc = lib.smt_rmsnorm_bwd(dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0), w.data_ptr(),
-                                 rstd.data_ptr(), dx.data_ptr(), dx.stride(0),
-                                 None if partial is None else partial.data_ptr(),
-                                 None if dw is None else dw.data_ptr(), rows, H, _stream(x2))
-        _hip._check(rc, "smt_rmsnorm_bwd")
+        dx, dw = _rmsnorm_bwd(x2, w, rstd, dy, ctx.needs_input_grad[1])
         return dx.view(ctx.shape), dw, None
+
+
+def _rmsnorm_bwd(x2, w, rstd, dy, need_dw: bool):
+    rows, H = x2.shape
+    dy2 = _rows2d(dy)
+    dx = torch.empty_like(x2)
+    lib = _hip.load()
+    dw = partial = None
+    if need_dw:
+        waves = lib.smt_rmsnorm_bwd_waves(rows)
+        partial = torch.empty(waves, H, dtype=torch.float32, device=x2.device)
+        dw = torch.empty(H, dtype=w.dtype, device=w.device)
+    rc = lib.smt_rmsnorm_bwd(dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0), w.data_ptr(),
+                             rstd.data_ptr(), dx.data_ptr(), dx.stride(0),
+                             None if partial is None else partial.data_ptr(),
+                             None if dw is None else dw.data_ptr(), rows, H, _stream(x2))
+    _hip._check(rc, "smt_rmsnorm_bwd")
+    return dx, dw
 
 
 def fused_rmsnorm_forward(self, hidden_states):
@@ -103,9 +108,10 @@ class FusedRMSNormResFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy, dres):
-        x2, w, rstd = ctx.saved_tensors
+        x2, w, rstd = ctx.saved_tensors              # unpacked once (activation checkpointing)
         if dres is None or ctx.needs_input_grad[1] or x2.shape[1] % 512 or x2.shape[1] > 8192:
-            dx, dw, _ = FusedRMSNormFn.backward(ctx, dy)
+            dx, dw = _rmsnorm_bwd(x2, w, rstd, dy, ctx.needs_input_grad[1])
+            dx = dx.view(ctx.shape)
             return (dx if dres is None else dx + dres), dw, None
         rows, H = x2.shape
         dy2, dr2 = _rows2d(dy), _rows2d(dres)
