@@ -22,6 +22,7 @@ Only bf16 CUDA tensors take the fused path; anything else raises (no silent fall
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 from torch import nn
@@ -179,13 +180,20 @@ class FusedAddRMSNormFn(torch.autograd.Function):
         return dx, dx, dw, None
 
 
+_RESIDUAL_NORM = os.environ.get("SMT_FUSED_RESIDUAL_NORM", "1") != "0"
+
+
 def fused_decoder_layer_forward(self, hidden_states, attention_mask=None, position_ids=None, past_key_values=None,
                                 use_cache=False, position_embeddings=None, **kwargs):
     """Drop-in for ``LlamaDecoderLayer.forward`` with the attention residual add fused into the
     post-attention RMSNorm (:class:`FusedAddRMSNormFn`) and the input norm's two gradients summed in
     its backward (:class:`FusedRMSNormResFn`); the same ops in the same order otherwise."""
     norm1 = self.input_layernorm
-    hidden_states, residual = FusedRMSNormResFn.apply(hidden_states, norm1.weight, norm1.variance_epsilon)
+    if _RESIDUAL_NORM:
+        hidden_states, residual = FusedRMSNormResFn.apply(hidden_states, norm1.weight, norm1.variance_epsilon)
+    else:
+        residual = hidden_states
+        hidden_states = norm1(hidden_states)
     hidden_states, _ = self.self_attn(hidden_states=hidden_states, attention_mask=attention_mask,
                                       position_ids=position_ids, past_key_values=past_key_values, use_cache=use_cache,
                                       position_embeddings=position_embeddings, **kwargs)
