@@ -35,6 +35,23 @@ const char* smt_fp8_last_error(void);
 int smt_quant_rows_e4m3(const void* x, int64_t ld_x, int64_t rows, int32_t cols, const int32_t* row_blocks_dev,
                         int32_t n_row_blocks, void* out, int64_t ld_out, float* scales, hipStream_t stream);
 
+/* One bf16 source of a row-wise concatenation. */
+typedef struct smt_quant_src {
+    const void* ptr;                /* bf16 [rows, ld], 16-byte aligned rows */
+    int64_t ld;
+    int32_t cols;                   /* % 8 == 0 */
+    int32_t pad_;
+} smt_quant_src;
+
+/*
+ * Row-wise over the concatenation [src_0 | ... | src_{n-1}] (1 <= n <= 4, <= 32768 columns in all):
+ * one scale per row over all sources; out: fp8 [rows, ld_out] holding the concatenated row.
+ * (The output gradients of linears that share one input -- q/k/v, gate/up -- for ONE joint
+ * data-gradient GEMM.)
+ */
+int smt_quant_rows_cat_e4m3(const smt_quant_src* srcs, int32_t n_src, int64_t rows, void* out, int64_t ld_out,
+                            float* scales, hipStream_t stream);
+
 /*
  * Column-wise, transposed: out_t[c, 0:rows] = e4m3(w[0:rows, c] / scales[c]) for every column c of
  * w (bf16 [rows, ld_w], cols % 256 == 0), or only the columns of the listed 256-column blocks.

@@ -36,7 +36,7 @@ ABI_FUNCTIONS = (
     "smt_add_rmsnorm_fwd", "smt_rmsnorm_bwd_add",
     "smt_rope_fwd", "smt_rope_bwd", "smt_swiglu_fwd", "smt_swiglu_bwd", "smt_ce_fwd", "smt_ce_bwd",
     "smt_attn_last_error", "smt_attn_fwd", "smt_attn_bwd",
-    "smt_fp8_last_error", "smt_quant_rows_e4m3", "smt_quant_cols_t_e4m3",
+    "smt_fp8_last_error", "smt_quant_rows_e4m3", "smt_quant_cols_t_e4m3", "smt_quant_rows_cat_e4m3",
 )
 
 
@@ -70,6 +70,10 @@ class RopeTensor(ctypes.Structure):
                 ("in_sb", ctypes.c_int64), ("in_sh", ctypes.c_int64), ("in_ss", ctypes.c_int64),
                 ("out_sb", ctypes.c_int64), ("out_sh", ctypes.c_int64), ("out_ss", ctypes.c_int64),
                 ("heads", ctypes.c_int32), ("pad_", ctypes.c_int32)]
+
+
+class QuantSrc(ctypes.Structure):
+    _fields_ = [("ptr", ctypes.c_void_p), ("ld", ctypes.c_int64), ("cols", ctypes.c_int32), ("pad_", ctypes.c_int32)]
 
 
 class AttnTensor(ctypes.Structure):
@@ -123,6 +127,7 @@ _SIGS = {
     "smt_fp8_last_error": (ctypes.c_char_p, []),
     "smt_quant_rows_e4m3": (ctypes.c_int, [_P, _I64, _I64, _I32, _P, _I32, _P, _I64, _P, _P]),
     "smt_quant_cols_t_e4m3": (ctypes.c_int, [_P, _I64, _I32, _I32, _P, _I32, _P, _I64, _P, _P]),
+    "smt_quant_rows_cat_e4m3": (ctypes.c_int, [ctypes.POINTER(QuantSrc), _I32, _I64, _P, _I64, _P, _P]),
 }
 
 

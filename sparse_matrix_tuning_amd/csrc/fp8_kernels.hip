@@ -200,6 +200,66 @@ void quant_rows_wg_kernel(const uint16_t* __restrict__ x, int64_t ldx, int64_t r
     }
 }
 
+// Row-wise over a concatenation of up to 4 bf16 sources [src0 | src1 | ...] (the output gradients
+// of the linears that share one input: q/k/v or gate/up), one scale per row over all of them; the
+// fp8 rows are written concatenated, ready for ONE data-gradient GEMM against the jointly quantised
+// transposed weights. One 256-thread workgroup per row, up to 16 chunks of 8 per thread in registers.
+struct CatSrcs {
+    const uint16_t* p[4];
+    int64_t ld[4];
+    int off[5];                        // chunk offsets (8 elements per chunk), off[n] = total
+    int n;
+};
+
+__global__ __launch_bounds__(256)
+void quant_rows_cat_kernel(CatSrcs src, int64_t rows, uint8_t* __restrict__ out, int64_t ldo, float* __restrict__ scales) {
+    constexpr int CPT = 16;
+    __shared__ float wmax[4];
+    const int tid = threadIdx.x;
+    const int64_t row = blockIdx.x;
+    if (row >= rows) return;
+    const int nch = src.off[src.n];
+    uint4 buf[CPT];
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+        const int c = tid + 256 * i;
+        if (c < nch) {
+            const int k = (c >= src.off[1]) + (c >= src.off[2]) + (c >= src.off[3]);
+            buf[i] = *reinterpret_cast<const uint4*>(src.p[k] + row * src.ld[k] + (int64_t)(c - src.off[k]) * 8);
+        } else {
+            buf[i] = make_uint4(0u, 0u, 0u, 0u);
+        }
+    }
+    float amax = 0.f;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+        const uint32_t w[4] = {buf[i].x, buf[i].y, buf[i].z, buf[i].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            amax = fmaxf(amax, fmaxf(fabsf(bf(w[j] & 0xffffu)), fabsf(bf(w[j] >> 16))));
+    }
+    amax = wave_max(amax);
+    if ((tid & 63) == 0) wmax[tid >> 6] = amax;
+    __syncthreads();
+    amax = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
+    const float scale = amax > 0.f ? amax * kInvE4M3Max : 1.f;
+    if (tid == 0) scales[row] = scale;
+    uint8_t* orow = out + row * ldo;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+        const int c = tid + 256 * i;
+        if (c < nch) {
+            const uint32_t w[4] = {buf[i].x, buf[i].y, buf[i].z, buf[i].w};
+            uint2 o;
+            o.x = pack4(qv(bf(w[0] & 0xffffu), scale), qv(bf(w[0] >> 16), scale),
+                        qv(bf(w[1] & 0xffffu), scale), qv(bf(w[1] >> 16), scale));
+            o.y = pack4(qv(bf(w[2] & 0xffffu), scale), qv(bf(w[2] >> 16), scale),
+                        qv(bf(w[3] & 0xffffu), scale), qv(bf(w[3] >> 16), scale));
+            *reinterpret_cast<uint2*>(orow + c * 8) = o;
+        }
+    }
+}
+
 // One workgroup per 256-column block: pass 1 the 256 column maxima (8 row groups x 32 lanes of 8
 // columns, combined in LDS); pass 2 in 64-row slabs staged through LDS, each thread converting its
 // column's 64 values into 64 contiguous bytes of the transposed output row.
@@ -288,6 +348,39 @@ int smt_quant_rows_e4m3(const void* x, int64_t ld_x, int64_t rows, int32_t cols,
         hipLaunchKernelGGL(quant_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, px, ld_x, rows, cols,
                            row_blocks_dev, n_sel, po, ld_out, scales);
     return check_launch("quant_rows_kernel");
+}
+
+int smt_quant_rows_cat_e4m3(const smt_quant_src* srcs, int32_t n_src, int64_t rows, void* out, int64_t ld_out,
+                            float* scales, hipStream_t stream) {
+    if (n_src < 1 || n_src > 4 || rows < 0) return fail(-1, "smt_quant_rows_cat_e4m3: 1..4 sources, rows >= 0");
+    if (rows == 0) return 0;
+    if (!srcs || !out || !scales) return fail(-1, "smt_quant_rows_cat_e4m3: null pointer");
+    CatSrcs c{};
+    c.n = n_src;
+    int total = 0;
+    for (int k = 0; k < 4; ++k) {
+        c.off[k] = total;
+        if (k < n_src) {
+            const smt_quant_src& s = srcs[k];
+            if (!s.ptr || s.cols <= 0 || (s.cols & 7) || s.ld < s.cols || (s.ld & 7) || !aligned16(s.ptr))
+                return fail(-2, "smt_quant_rows_cat_e4m3: source %d needs 16-byte aligned bf16 rows, cols %% 8 == 0", k);
+            c.p[k] = static_cast<const uint16_t*>(s.ptr);
+            c.ld[k] = s.ld;
+            total += s.cols / 8;
+        } else {
+            c.p[k] = nullptr;
+            c.ld[k] = 0;
+        }
+    }
+    c.off[4] = total;
+    for (int k = n_src; k < 4; ++k) c.off[k] = total;
+    if (total > 256 * 16) return fail(-1, "smt_quant_rows_cat_e4m3: %d columns > 32768", total * 8);
+    if (ld_out < (int64_t)total * 8 || (ld_out & 7) || (reinterpret_cast<uintptr_t>(out) & 7))
+        return fail(-2, "smt_quant_rows_cat_e4m3: ld_out must cover the concatenation, 8-byte aligned");
+    if (rows > 0x7fffffffLL) return fail(-1, "smt_quant_rows_cat_e4m3: too many rows");
+    hipLaunchKernelGGL(quant_rows_cat_kernel, dim3((unsigned)rows), dim3(256), 0, stream, c, rows,
+                       static_cast<uint8_t*>(out), ld_out, scales);
+    return check_launch("quant_rows_cat_kernel");
 }
 
 int smt_quant_cols_t_e4m3(const void* w, int64_t ld_w, int32_t rows, int32_t cols, const int32_t* col_blocks_dev,

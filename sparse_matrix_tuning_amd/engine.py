@@ -136,17 +136,35 @@ def attach_fp8_weights(model: torch.nn.Module, part_module_name=(".layers",)) ->
     """fp8 path (config 5): give every frozen bf16 linear weight under ``part_module_name`` (the
     decoder layers; smt.py:86-88's default) its e4m3 copies (:class:`..fp8.Fp8Weight`) and route plain
     frozen ``nn.Linear`` forwards through them. Returns the bytes added."""
-    from .fp8 import Fp8Weight
+    from .fp8 import Fp8Group, Fp8Weight
+
+    def ok(m):
+        return ((isinstance(m, LinearLayer_MatrixSparsity) or type(m) is torch.nn.Linear) and _transposable(m.weight)
+                and getattr(m.weight, "_smt_fp8", None) is None and m.weight.shape[0] % 256 == 0
+                and m.weight.shape[1] % 256 == 0)
+
+    groups = {"q_proj": ("q_proj", "k_proj", "v_proj"), "k_proj": ("q_proj", "k_proj", "v_proj"),
+              "v_proj": ("q_proj", "k_proj", "v_proj"), "gate_proj": ("gate_proj", "up_proj"),
+              "up_proj": ("gate_proj", "up_proj")}
     added = 0
-    for name, m in model.named_modules():
-        if not any(p in name for p in part_module_name):
+    linears = [(n, m) for n, m in model.named_modules() if any(p in n for p in part_module_name) and ok(m)]
+    by_name = dict(linears)
+    for name, m in linears:
+        if getattr(m.weight, "_smt_fp8", None) is not None:
             continue
-        if isinstance(m, LinearLayer_MatrixSparsity) or type(m) is torch.nn.Linear:
-            w = m.weight
-            if not _transposable(w) or getattr(w, "_smt_fp8", None) is not None or w.shape[0] % 256 or w.shape[1] % 256:
-                continue
-            w._smt_fp8 = Fp8Weight(w)
-            added += w._smt_fp8.nbytes
+        parent, _, leaf = name.rpartition(".")
+        names = [f"{parent}.{x}" for x in groups.get(leaf, ())]
+        if names and all(n in by_name for n in names) and len({by_name[n].weight.shape[1] for n in names}) == 1:
+            group = Fp8Group([by_name[n].weight for n in names])
+            added += group.nbytes
+            for i, n in enumerate(names):
+                by_name[n].weight._smt_fp8 = Fp8Weight(by_name[n].weight, group, i)
+        else:
+            m.weight._smt_fp8 = Fp8Weight(m.weight)
+    for _name, m in linears:
+        fw = getattr(m.weight, "_smt_fp8", None)
+        if fw is not None:
+            added += fw.nbytes
             if type(m) is torch.nn.Linear:
                 m.forward = _frozen_linear_forward.__get__(m, type(m))
     return added

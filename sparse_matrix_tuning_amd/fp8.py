@@ -15,6 +15,9 @@ MI355X extension whose parity is stated against the build's own bf16 path
   AdamW epilogue, and their weight gradient is the bf16 MFMA tile GEMM on the bf16 activations. After
   each step the rows (for ``w8``) and columns (for ``wt8``) that the tiles touch are re-quantised
   from the bf16 W, so the fp8 copies always describe the current tiles.
+* The linears that read one input (q/k/v, gate/up) form an :class:`Fp8Group`: their data gradients
+  are ONE fp8 GEMM of the concatenated output gradients against the jointly quantised transposed
+  weight, so neither a per-member GEMM nor autograd's gradient adds remain.
 * The LM head, embeddings, norms and attention stay bf16.
 
 No CPU path: every entry point raises without a ROCm device.
@@ -83,25 +86,84 @@ def quant_cols_t(w: torch.Tensor, col_blocks: Optional[torch.Tensor] = None, out
     return raw.view(F8), scales
 
 
-class Fp8Weight:
-    """The two e4m3 copies of one frozen bf16 ``W [out, in]``."""
+def quant_rows_cat(parts):
+    """Per-row e4m3 quantisation of the concatenation ``[p_0 | p_1 | ...]`` of bf16 ``[rows, cols_i]``
+    matrices (one scale per row over all of them), without materialising the bf16 concatenation."""
+    dev = _hip._require_device(*parts)
+    parts = [_bf16_rows(p, "quant_rows_cat") for p in parts]
+    rows = parts[0].shape[0]
+    if any(p.shape[0] != rows for p in parts) or not 1 <= len(parts) <= 4:
+        raise ValueError("quant_rows_cat: 1-4 sources with the same number of rows")
+    cols = sum(p.shape[1] for p in parts)
+    out = torch.empty(rows, cols, dtype=torch.uint8, device=dev)
+    scales = torch.empty(rows, dtype=torch.float32, device=dev)
+    srcs = (_hip.QuantSrc * len(parts))(*[_hip.QuantSrc(p.data_ptr(), p.stride(0), p.shape[1], 0) for p in parts])
+    rc = _hip.load().smt_quant_rows_cat_e4m3(srcs, len(parts), rows, out.data_ptr(), out.stride(0), scales.data_ptr(),
+                                             _stream(dev))
+    _hip._check(rc, "smt_quant_rows_cat_e4m3")
+    return out.view(F8), scales
 
-    def __init__(self, weight: torch.Tensor):
+
+class Fp8Group:
+    """Frozen linears that read the same input (q/k/v of a LlamaAttention, gate/up of a LlamaMLP).
+    Their data gradients run as ONE fp8 GEMM: the concatenated output gradients (quantised per row
+    over all of them by ``smt_quant_rows_cat_e4m3``) against the jointly quantised transposed weight
+    ``[W_0; W_1; ...]^T`` (one scale per input column over all members). That replaces one GEMM per
+    member plus the adds autograd would use to sum their input gradients."""
+
+    def __init__(self, weights):
+        self.weights = list(weights)
+        self.outs = [w.shape[0] for w in self.weights]
+        self.offsets = [sum(self.outs[:i]) for i in range(len(self.outs))]
+        self.wt8, self.swt = quant_cols_t(self._cat())           # [in, sum(out)]
+        self.swt_row = self.swt.view(1, -1)
+
+    def _cat(self) -> torch.Tensor:
+        return torch.cat([w.detach() for w in self.weights], 0)
+
+    def refresh(self, col_blocks: torch.Tensor) -> None:
+        """Re-quantise the joint copy's rows for the given 256-column blocks of the members' W."""
+        quant_cols_t(self._cat(), col_blocks, out_t=self.wt8, scales=self.swt)
+
+    def member_wt8(self, i: int) -> torch.Tensor:
+        """Member i's transposed copy as a column slice ``[in, out_i]`` of the joint one (same scales)."""
+        return self.wt8[:, self.offsets[i]:self.offsets[i] + self.outs[i]]
+
+    @property
+    def nbytes(self) -> int:
+        return self.wt8.numel() + 4 * self.swt.numel()
+
+
+class Fp8Weight:
+    """The e4m3 copies of one frozen bf16 ``W [out, in]``: ``w8`` (per output row) for the forward,
+    and for the data gradient either its own ``wt8 [in, out]`` (per input column) or, as a member of
+    an :class:`Fp8Group`, a slice of the group's joint transposed copy."""
+
+    def __init__(self, weight: torch.Tensor, group: "Fp8Group" = None, group_index: int = 0):
         w = weight.detach()
         self.w8, self.sw = quant_rows(w)                  # [out, in], per output row
-        self.wt8, self.swt = quant_cols_t(w)              # [in, out], per input column
         self.sw_row = self.sw.view(1, -1)
+        self.group = group
+        self.group_index = group_index
+        if group is None:
+            self.wt8, self.swt = quant_cols_t(w)          # [in, out], per input column
+        else:
+            self.wt8, self.swt = group.member_wt8(group_index), group.swt
         self.swt_row = self.swt.view(1, -1)
 
     def refresh(self, weight: torch.Tensor, row_blocks: torch.Tensor, col_blocks: torch.Tensor) -> None:
         """Re-quantise the rows / columns of the given 256-blocks from the current bf16 W."""
         w = weight.detach()
         quant_rows(w, row_blocks, out=self.w8, scales=self.sw)
-        quant_cols_t(w, col_blocks, out_t=self.wt8, scales=self.swt)
+        if self.group is None:
+            quant_cols_t(w, col_blocks, out_t=self.wt8, scales=self.swt)
+        else:
+            self.group.refresh(col_blocks)
 
     @property
     def nbytes(self) -> int:
-        return self.w8.numel() + self.wt8.numel() + 4 * (self.sw.numel() + self.swt.numel())
+        own = self.wt8.numel() + 4 * self.swt.numel() if self.group is None else 0
+        return self.w8.numel() + 4 * self.sw.numel() + own
 
 
 def quant_rows_cached(x: torch.Tensor):
@@ -135,16 +197,74 @@ def fp8_linear_dgrad(grad_output: torch.Tensor, fw: Fp8Weight) -> torch.Tensor:
     return gi.view(*shape[:-1], gi.shape[-1])
 
 
+class GroupGrad:
+    """The output gradients of one forward's group members, collected until the last one arrives."""
+
+    __slots__ = ("version", "group", "registered", "parts", "pending")
+
+    def __init__(self, version: int, group: Fp8Group):
+        self.version = version
+        self.group = group
+        self.registered = 0
+        self.parts = {}
+        self.pending = 0
+
+
+def register_group(x: torch.Tensor, fw: Fp8Weight):
+    """Count one more group member reading ``x`` (call from the member's forward); None when the
+    weight is not grouped or ``x`` needs no gradient."""
+    if fw.group is None or not x.requires_grad:
+        return None
+    acc = x.__dict__.get("_smt_gacc8")
+    if acc is None or acc.version != x._version or acc.group is not fw.group:
+        acc = GroupGrad(x._version, fw.group)
+        x._smt_gacc8 = acc
+    acc.registered += 1
+    return acc
+
+
+def group_input_grad(acc: GroupGrad, fw: Fp8Weight, grad_output: torch.Tensor):
+    """The summed input gradient of all group members from the last one to run (one joint fp8 GEMM
+    when every member of the group took part), None from the others."""
+    if not acc.parts:
+        acc.pending = acc.registered
+    acc.parts[fw.group_index] = grad_output
+    acc.pending -= 1
+    if acc.pending > 0:
+        return None
+    parts, acc.parts = acc.parts, {}
+    g = acc.group
+    lead = grad_output.shape[:-1]
+    if sorted(parts) == list(range(len(g.outs))):
+        q, sq = quant_rows_cat([parts[i].reshape(-1, g.outs[i]) for i in range(len(g.outs))])
+        gi = torch._scaled_mm(q, g.wt8.t(), scale_a=sq.view(-1, 1), scale_b=g.swt_row, out_dtype=torch.bfloat16)
+    else:                                   # a subset of the members: per-member GEMMs on the slices
+        gi = None
+        for i, go in parts.items():
+            part = fp8_matmul(go.reshape(-1, g.outs[i]), g.member_wt8(i), g.swt_row)
+            gi = part if gi is None else gi.add_(part)
+    return gi.view(*lead, gi.shape[-1])
+
+
+def fp8_input_grad(ctx_acc, fw: Fp8Weight, grad_output: torch.Tensor):
+    """Data gradient of one fp8 linear: through its group when it registered with one."""
+    if ctx_acc is not None:
+        return group_input_grad(ctx_acc, fw, grad_output)
+    return fp8_linear_dgrad(grad_output, fw)
+
+
 class Fp8LinearFn(torch.autograd.Function):
-    """``x @ W^T (+ b)`` of a frozen W through its e4m3 copies; the data gradient through ``wt8``."""
+    """``x @ W^T (+ b)`` of a frozen W through its e4m3 copies; the data gradient through ``wt8``
+    (jointly with the other members of its group when it has one)."""
 
     @staticmethod
     def forward(ctx, x, weight, fw, bias):
         ctx.fw = fw
+        ctx.gacc = register_group(x, fw)
         y = fp8_linear_forward(x, fw)
         return y if bias is None else y + bias
 
     @staticmethod
     def backward(ctx, grad_output):
-        gi = fp8_linear_dgrad(grad_output, ctx.fw) if ctx.needs_input_grad[0] else None
+        gi = fp8_input_grad(ctx.gacc, ctx.fw, grad_output) if ctx.needs_input_grad[0] else None
         return gi, None, None, None

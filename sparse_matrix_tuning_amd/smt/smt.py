@@ -277,8 +277,14 @@ class linearZ(torch.autograd.Function):
             saved = _hip.colblock_gather(_rows_ready(input.reshape(-1, weight.shape[1])), cb_dev)
             ctx.packed = True
         ctx.save_for_backward(saved, weight)
-        # q/k/v (gate/up) share their input: their data gradients accumulate in one buffer
-        ctx.acc = dgrad.register(input) if getattr(weight, "_smt_fp8", None) is None else None
+        # q/k/v (gate/up) share their input: their data gradients accumulate in one buffer (bf16)
+        # or run as one joint GEMM (fp8 group)
+        fw = getattr(weight, "_smt_fp8", None)
+        if fw is None:
+            ctx.acc = dgrad.register(input)
+        else:
+            from ..fp8 import register_group
+            ctx.acc = register_group(input, fw)
         return _dense_forward(input, weight)
 
     @staticmethod
@@ -312,8 +318,8 @@ class linearZ(torch.autograd.Function):
             # hipBLASLt runs 13-19 % faster on these shapes (profiles/r01_gemm_layout.jsonl); on the
             # fp8 path through W's transposed e4m3 copy
             if fw is not None:
-                from ..fp8 import fp8_linear_dgrad
-                grad_input = fp8_linear_dgrad(grad_output, fw)
+                from ..fp8 import fp8_input_grad
+                grad_input = fp8_input_grad(ctx.acc, fw, grad_output)
             else:
                 grad_input = dgrad.input_grad(ctx.acc, grad_output, weight if wt is None else wt.t())
         return grad_input, grad_weight, None, None

@@ -136,19 +136,59 @@ def test_engine_fp8_keeps_copies_in_step_and_loss_close_to_bf16():
     for a, b in zip(l8, lb):
         assert abs(a - b) / abs(b) < 1e-2, (l8, lb)
     # after the steps every fp8 copy equals a fresh quantisation of the (tile-updated) bf16 W
-    n = 0
+    n, groups = 0, set()
     for mod in m8.modules():
         w = getattr(mod, "weight", None)
         fw = getattr(w, "_smt_fp8", None)
         if fw is None:
             continue
         rq, rs = _ref_rows(w.detach())
-        tq, ts = _ref_rows(w.detach().t().contiguous())
         assert torch.equal(fw.sw, rs) and torch.equal(fw.w8.view(torch.uint8), rq.view(torch.uint8))
-        assert torch.equal(fw.swt, ts) and torch.equal(fw.wt8.view(torch.uint8), tq.view(torch.uint8))
+        if fw.group is None:
+            tq, ts = _ref_rows(w.detach().t().contiguous())
+            assert torch.equal(fw.swt, ts) and torch.equal(fw.wt8.view(torch.uint8), tq.view(torch.uint8))
+        else:                                   # joint transposed copy of [W_q; W_k; W_v] / [W_gate; W_up]
+            g = fw.group
+            tq, ts = _ref_rows(torch.cat([x.detach() for x in g.weights], 0).t().contiguous())
+            assert torch.equal(g.swt, ts) and torch.equal(g.wt8.view(torch.uint8), tq.view(torch.uint8))
+            groups.add(id(g))
         n += 1
     assert n == 2 * 7                                                  # every decoder-layer linear
+    assert len(groups) == 2 * 2                                        # q/k/v and gate/up per layer
     assert getattr(m8.lm_head.weight, "_smt_fp8", None) is None        # the head stays bf16
+
+
+def test_quant_rows_cat_matches_quant_of_concatenation():
+    torch.manual_seed(5)
+    parts = [torch.randn(300, c, device=DEV).bfloat16() * s for c, s in ((4096, 1.0), (1024, 30.0), (1024, 0.01))]
+    q, s = f8.quant_rows_cat(parts)
+    rq, rs = _ref_rows(torch.cat(parts, 1))
+    assert torch.equal(s, rs) and torch.equal(q.view(torch.uint8), rq.view(torch.uint8))
+    big = [torch.randn(7, 14336, device=DEV).bfloat16(), torch.randn(7, 20000, device=DEV).bfloat16()[:, :14336]]
+    q, s = f8.quant_rows_cat(big)
+    rq, rs = _ref_rows(torch.cat(big, 1))
+    assert torch.equal(s, rs) and torch.equal(q.view(torch.uint8), rq.view(torch.uint8))
+
+
+def test_fp8_group_joint_input_grad():
+    """q/k/v sharing one input: the joint fp8 data gradient is close to the bf16 sum of the three."""
+    torch.manual_seed(6)
+    ws = [(torch.randn(o, 512, device=DEV) * 0.02).bfloat16() for o in (512, 256, 256)]
+    g = f8.Fp8Group(ws)
+    fws = [f8.Fp8Weight(w, g, i) for i, w in enumerate(ws)]
+    x = torch.randn(2, 128, 512, device=DEV).bfloat16().requires_grad_()
+    ys = [f8.Fp8LinearFn.apply(x, w, fw, None) for w, fw in zip(ws, fws)]
+    dys = [torch.randn_like(y) for y in ys]
+    torch.autograd.backward(ys, dys)
+    ref = sum(dy.float() @ w.float() for dy, w in zip(dys, ws))
+    assert _rel(x.grad, ref) < 8e-2
+    # a subset of the members (only q and v take part) falls back to per-member GEMMs on the slices
+    x2 = x.detach().clone().requires_grad_()
+    y0 = f8.Fp8LinearFn.apply(x2, ws[0], fws[0], None)
+    y2 = f8.Fp8LinearFn.apply(x2, ws[2], fws[2], None)
+    torch.autograd.backward([y0, y2], [dys[0], dys[2]])
+    ref2 = dys[0].float() @ ws[0].float() + dys[2].float() @ ws[2].float()
+    assert _rel(x2.grad, ref2) < 8e-2
 
 
 def test_fp8_rejects_cpu_and_fp32():
