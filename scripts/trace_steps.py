@@ -52,6 +52,18 @@ def main(path):
         print(f"step: wall {wall:.1f} ms, kernel-busy {busy:.1f} ms, dispatches {len(seg)}")
         for k, v in by.most_common():
             print(f"   {k:22s} {v:8.1f} ms  {100 * v / wall:5.1f}%  n={cnt[k]}")
+    # the last step's non-GEMM kernels by name
+    seg = rows[idx[-2] + 1:idx[-1] + 1]
+    per = collections.defaultdict(lambda: [0, 0.0])
+    for r in seg:
+        n = r["Kernel_Name"]
+        if cat(n) == "gemm(hipBLASLt)":
+            continue
+        per[n][0] += 1
+        per[n][1] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+    print("last step, non-GEMM kernels:")
+    for n, (c, t) in sorted(per.items(), key=lambda kv: -kv[1][1])[:25]:
+        print(f"   {t:8.2f} ms  n={c:4d}  {n[:140]}")
 
 
 if __name__ == "__main__":

@@ -203,7 +203,9 @@ void quant_rows_wg_kernel(const uint16_t* __restrict__ x, int64_t ldx, int64_t r
 // Row-wise over a concatenation of up to 4 bf16 sources [src0 | src1 | ...] (the output gradients
 // of the linears that share one input: q/k/v or gate/up), one scale per row over all of them; the
 // fp8 rows are written concatenated, ready for ONE data-gradient GEMM against the jointly quantised
-// transposed weights. One 256-thread workgroup per row, up to 16 chunks of 8 per thread in registers.
+// transposed weights. One NT-thread workgroup per row, CPT chunks of 8 per thread held in registers.
+// UNIFORM: every source is a whole number of 64-chunk wave spans (cols % 512 == 0), so the source of
+// a wave's chunks is wave-uniform and its pointer / stride come from scalar registers.
 struct CatSrcs {
     const uint16_t* p[4];
     int64_t ld[4];
@@ -211,10 +213,11 @@ struct CatSrcs {
     int n;
 };
 
-__global__ __launch_bounds__(256)
+template <int CPT, int NT, bool UNIFORM>
+__global__ __launch_bounds__(NT)
 void quant_rows_cat_kernel(CatSrcs src, int64_t rows, uint8_t* __restrict__ out, int64_t ldo, float* __restrict__ scales) {
-    constexpr int CPT = 16;
-    __shared__ float wmax[4];
+    constexpr int NW = NT / 64;
+    __shared__ float wmax[NW];
     const int tid = threadIdx.x;
     const int64_t row = blockIdx.x;
     if (row >= rows) return;
@@ -222,13 +225,13 @@ void quant_rows_cat_kernel(CatSrcs src, int64_t rows, uint8_t* __restrict__ out,
     uint4 buf[CPT];
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
-        const int c = tid + 256 * i;
-        if (c < nch) {
-            const int k = (c >= src.off[1]) + (c >= src.off[2]) + (c >= src.off[3]);
+        const int c = tid + NT * i;
+        int k = (c >= src.off[1]) + (c >= src.off[2]) + (c >= src.off[3]);
+        if (UNIFORM) k = __builtin_amdgcn_readfirstlane(k);
+        if (c < nch)
             buf[i] = *reinterpret_cast<const uint4*>(src.p[k] + row * src.ld[k] + (int64_t)(c - src.off[k]) * 8);
-        } else {
+        else
             buf[i] = make_uint4(0u, 0u, 0u, 0u);
-        }
     }
     float amax = 0.f;
 #pragma unroll
@@ -241,13 +244,15 @@ void quant_rows_cat_kernel(CatSrcs src, int64_t rows, uint8_t* __restrict__ out,
     amax = wave_max(amax);
     if ((tid & 63) == 0) wmax[tid >> 6] = amax;
     __syncthreads();
-    amax = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
+    amax = wmax[0];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) amax = fmaxf(amax, wmax[w]);
     const float scale = amax > 0.f ? amax * kInvE4M3Max : 1.f;
     if (tid == 0) scales[row] = scale;
     uint8_t* orow = out + row * ldo;
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
-        const int c = tid + 256 * i;
+        const int c = tid + NT * i;
         if (c < nch) {
             const uint32_t w[4] = {buf[i].x, buf[i].y, buf[i].z, buf[i].w};
             uint2 o;
@@ -260,26 +265,37 @@ void quant_rows_cat_kernel(CatSrcs src, int64_t rows, uint8_t* __restrict__ out,
     }
 }
 
-// One workgroup per 256-column block: pass 1 the 256 column maxima (8 row groups x 32 lanes of 8
-// columns, combined in LDS); pass 2 in 64-row slabs staged through LDS, each thread converting its
-// column's 64 values into 64 contiguous bytes of the transposed output row.
 constexpr int kSlabRows = 64;
 constexpr int kSlabLd = 256 + 8;             // 528-B LDS rows
+constexpr int kSegRows = 256;                // rows of W one workgroup covers (4 slabs)
+
+// Per-input-column quantisation of W [rows, cols] into out_t = W^T [cols, rows] (one scale per column
+// of W), over the 256-column blocks listed in col_blocks (all when null). Grid: (column block,
+// 256-row segment), so a 14336-row W spreads over 56 x n_blocks workgroups instead of n_blocks.
+// Three passes that need no scratch: the column amaxes are reduced into `scales` itself (atomicMax
+// on the bits of non-negative floats) after zeroing it, the quantise pass reads them, and a last
+// pass turns each amax into the scale in place.
+__device__ __forceinline__ int col_block_of(const int32_t* col_blocks, int i) { return col_blocks ? col_blocks[i] : i; }
 
 __global__ __launch_bounds__(256)
-void quant_cols_t_kernel(const uint16_t* __restrict__ w, int64_t ldw, int rows, const int32_t* __restrict__ col_blocks,
-                         uint8_t* __restrict__ out_t, int64_t ldo, float* __restrict__ scales) {
+void cols_t_zero_kernel(const int32_t* __restrict__ col_blocks, float* __restrict__ scales) {
+    scales[(int64_t)col_block_of(col_blocks, blockIdx.x) * 256 + threadIdx.x] = 0.f;
+}
+
+__global__ __launch_bounds__(256)
+void cols_t_amax_kernel(const uint16_t* __restrict__ w, int64_t ldw, int rows, const int32_t* __restrict__ col_blocks,
+                        float* __restrict__ scales) {
     __shared__ float red[8][256];
-    __shared__ __attribute__((aligned(16))) uint16_t slab[kSlabRows][kSlabLd];
-    const int cb = col_blocks ? col_blocks[blockIdx.x] : (int)blockIdx.x;
-    const int tid = threadIdx.x;
-    const int chunk = tid & 31, rg = tid >> 5;
-    const uint16_t* base = w + (int64_t)cb * 256;
+    const int cb = col_block_of(col_blocks, blockIdx.x);
+    const int tid = threadIdx.x, chunk = tid & 31, rg = tid >> 5;
+    const int r0 = blockIdx.y * kSegRows, r1 = min(rows, r0 + kSegRows);
+    const uint16_t* base = w + (int64_t)cb * 256 + chunk * 8;
     float m[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) m[j] = 0.f;
-    for (int r = rg; r < rows; r += 8) {
-        const F8 v = ld8(base + (int64_t)r * ldw + chunk * 8);
+#pragma unroll 4
+    for (int r = r0 + rg; r < r1; r += 8) {
+        const F8 v = ld8(base + (int64_t)r * ldw);
 #pragma unroll
         for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], fabsf(v.v[j]));
     }
@@ -289,12 +305,25 @@ void quant_cols_t_kernel(const uint16_t* __restrict__ w, int64_t ldw, int rows, 
     float amax = 0.f;
 #pragma unroll
     for (int g = 0; g < 8; ++g) amax = fmaxf(amax, red[g][tid]);
-    const float scale = amax > 0.f ? amax * kInvE4M3Max : 1.f;
+    atomicMax(reinterpret_cast<unsigned int*>(scales) + (int64_t)cb * 256 + tid, __float_as_uint(amax));
+}
+
+__device__ __forceinline__ float scale_of_amax(float amax) { return amax > 0.f ? amax * kInvE4M3Max : 1.f; }
+
+__global__ __launch_bounds__(256)
+void cols_t_quant_kernel(const uint16_t* __restrict__ w, int64_t ldw, int rows, const int32_t* __restrict__ col_blocks,
+                         const float* __restrict__ amaxes, uint8_t* __restrict__ out_t, int64_t ldo) {
+    __shared__ __attribute__((aligned(16))) uint16_t slab[kSlabRows][kSlabLd];
+    const int cb = col_block_of(col_blocks, blockIdx.x);
+    const int tid = threadIdx.x;
     const int64_t col = (int64_t)cb * 256 + tid;
-    scales[col] = scale;
+    const float scale = scale_of_amax(amaxes[col]);
+    const uint16_t* base = w + (int64_t)cb * 256;
     uint8_t* orow = out_t + col * ldo;
-    for (int r0 = 0; r0 < rows; r0 += kSlabRows) {
+    const int seg0 = blockIdx.y * kSegRows, seg1 = min(rows, seg0 + kSegRows);
+    for (int r0 = seg0; r0 < seg1; r0 += kSlabRows) {
         __syncthreads();                                     // the previous slab is consumed
+#pragma unroll
         for (int i = tid; i < kSlabRows * 32; i += 256) {
             const int rr = i >> 5, ch = i & 31;
             *reinterpret_cast<uint4*>(&slab[rr][ch * 8]) =
@@ -313,6 +342,12 @@ void quant_cols_t_kernel(const uint16_t* __restrict__ w, int64_t ldw, int rows, 
             *reinterpret_cast<uint4*>(orow + r0 + q * 16) = make_uint4(wd[0], wd[1], wd[2], wd[3]);
         }
     }
+}
+
+__global__ __launch_bounds__(256)
+void cols_t_finalize_kernel(const int32_t* __restrict__ col_blocks, float* __restrict__ scales) {
+    float* s = scales + (int64_t)col_block_of(col_blocks, blockIdx.x) * 256 + threadIdx.x;
+    *s = scale_of_amax(*s);
 }
 
 }  // namespace
@@ -374,12 +409,27 @@ int smt_quant_rows_cat_e4m3(const smt_quant_src* srcs, int32_t n_src, int64_t ro
     }
     c.off[4] = total;
     for (int k = n_src; k < 4; ++k) c.off[k] = total;
-    if (total > 256 * 16) return fail(-1, "smt_quant_rows_cat_e4m3: %d columns > 32768", total * 8);
+    if (total > 512 * 8) return fail(-1, "smt_quant_rows_cat_e4m3: %d columns > 32768", total * 8);
     if (ld_out < (int64_t)total * 8 || (ld_out & 7) || (reinterpret_cast<uintptr_t>(out) & 7))
         return fail(-2, "smt_quant_rows_cat_e4m3: ld_out must cover the concatenation, 8-byte aligned");
     if (rows > 0x7fffffffLL) return fail(-1, "smt_quant_rows_cat_e4m3: too many rows");
-    hipLaunchKernelGGL(quant_rows_cat_kernel, dim3((unsigned)rows), dim3(256), 0, stream, c, rows,
-                       static_cast<uint8_t*>(out), ld_out, scales);
+    bool uniform = true;
+    for (int k = 0; k < n_src; ++k) uniform = uniform && (c.off[k + 1] - c.off[k]) % 64 == 0;
+    const dim3 grid((unsigned)rows);
+    uint8_t* po = static_cast<uint8_t*>(out);
+#define SMT_CAT(CPT, NT)                                                                                         \
+    do {                                                                                                         \
+        if (uniform)                                                                                             \
+            hipLaunchKernelGGL((quant_rows_cat_kernel<CPT, NT, true>), grid, dim3(NT), 0, stream, c, rows, po,    \
+                               ld_out, scales);                                                                  \
+        else                                                                                                     \
+            hipLaunchKernelGGL((quant_rows_cat_kernel<CPT, NT, false>), grid, dim3(NT), 0, stream, c, rows, po,   \
+                               ld_out, scales);                                                                  \
+    } while (0)
+    if (total <= 4 * 256) SMT_CAT(4, 256);
+    else if (total <= 8 * 256) SMT_CAT(8, 256);
+    else SMT_CAT(8, 512);
+#undef SMT_CAT
     return check_launch("quant_rows_cat_kernel");
 }
 
@@ -392,9 +442,14 @@ int smt_quant_cols_t_e4m3(const void* w, int64_t ld_w, int32_t rows, int32_t col
     if (!w || !out_t || !scales) return fail(-1, "smt_quant_cols_t_e4m3: null pointer");
     if (!aligned16(w) || (ld_w & 7) || !aligned16(out_t) || (ld_out & 15))
         return fail(-2, "smt_quant_cols_t_e4m3: 16-byte aligned rows required (ld_w %% 8 == 0, ld_out %% 16 == 0)");
-    hipLaunchKernelGGL(quant_cols_t_kernel, dim3((unsigned)nb), dim3(256), 0, stream, static_cast<const uint16_t*>(w),
-                       ld_w, rows, col_blocks_dev, static_cast<uint8_t*>(out_t), ld_out, scales);
-    return check_launch("quant_cols_t_kernel");
+    const uint16_t* pw = static_cast<const uint16_t*>(w);
+    const dim3 grid2((unsigned)nb, (unsigned)((rows + kSegRows - 1) / kSegRows));
+    hipLaunchKernelGGL(cols_t_zero_kernel, dim3((unsigned)nb), dim3(256), 0, stream, col_blocks_dev, scales);
+    hipLaunchKernelGGL(cols_t_amax_kernel, grid2, dim3(256), 0, stream, pw, ld_w, rows, col_blocks_dev, scales);
+    hipLaunchKernelGGL(cols_t_quant_kernel, grid2, dim3(256), 0, stream, pw, ld_w, rows, col_blocks_dev, scales,
+                       static_cast<uint8_t*>(out_t), ld_out);
+    hipLaunchKernelGGL(cols_t_finalize_kernel, dim3((unsigned)nb), dim3(256), 0, stream, col_blocks_dev, scales);
+    return check_launch("quant_cols_t kernels");
 }
 
 }  // extern "C"

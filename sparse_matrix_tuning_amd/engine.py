@@ -316,6 +316,13 @@ class _TileGroup:
         self.n_tdescs = len(tdescs)
         self.tdescs = _hip.tile_descs(tdescs, device) if tdescs else None
         self.fp8_modules = [(m, m.weight._smt_fp8) for m in modules if getattr(m.weight, "_smt_fp8", None) is not None]
+        # grouped fp8 copies: the joint transposed copy is re-quantised once per step over the union of
+        # the column blocks its tile-carrying members touch
+        union = {}
+        for m, fw in self.fp8_modules:
+            if fw.group is not None:
+                union.setdefault(id(fw.group), (fw.group, set()))[1].update(m.tiles.column_blocks())
+        self.fp8_groups = [(g, torch.tensor(sorted(cbs), dtype=torch.int32).to(device)) for g, cbs in union.values()]
         self.step = 0
 
 
@@ -440,7 +447,9 @@ class SMTEngine:
                 _hip.tile_scatter_t(tg.tdescs, tg.n_tdescs, tg.param)
             for m, fw in tg.fp8_modules:
                 rb, cb = m.tiles.block_tables(self.device)
-                fw.refresh(m.weight, rb, cb)
+                fw.refresh(m.weight, rb, cb, group=False)
+            for g, cb in tg.fp8_groups:
+                g.refresh(cb)
         for group, params in self.dense_groups:
             for p in params:
                 if p.grad is None:

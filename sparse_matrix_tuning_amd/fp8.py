@@ -151,13 +151,15 @@ class Fp8Weight:
             self.wt8, self.swt = group.member_wt8(group_index), group.swt
         self.swt_row = self.swt.view(1, -1)
 
-    def refresh(self, weight: torch.Tensor, row_blocks: torch.Tensor, col_blocks: torch.Tensor) -> None:
-        """Re-quantise the rows / columns of the given 256-blocks from the current bf16 W."""
+    def refresh(self, weight: torch.Tensor, row_blocks: torch.Tensor, col_blocks: torch.Tensor,
+                group: bool = True) -> None:
+        """Re-quantise the rows / columns of the given 256-blocks from the current bf16 W (the
+        columns of a grouped copy only with ``group``: the engine refreshes each group once)."""
         w = weight.detach()
         quant_rows(w, row_blocks, out=self.w8, scales=self.sw)
         if self.group is None:
             quant_cols_t(w, col_blocks, out_t=self.wt8, scales=self.swt)
-        else:
+        elif group:
             self.group.refresh(col_blocks)
 
     @property

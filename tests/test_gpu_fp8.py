@@ -52,7 +52,7 @@ def test_quant_rows_selected_blocks_only():
     assert torch.equal(s, rs) and torch.equal(q.view(torch.uint8), rq.view(torch.uint8))
 
 
-@pytest.mark.parametrize("rows,cols", [(1024, 4096), (4096, 1024), (192, 512)])
+@pytest.mark.parametrize("rows,cols", [(1024, 4096), (4096, 1024), (192, 512), (14400, 768)])   # 256-row segments, ragged last
 def test_quant_cols_t_bit_exact(rows, cols):
     torch.manual_seed(cols)
     w = (torch.randn(rows, cols, device=DEV) * torch.logspace(-2, 1, cols, device=DEV)[None, :]).bfloat16()
