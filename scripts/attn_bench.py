@@ -48,6 +48,7 @@ def main():
         o = f()
         fwd = timed(f, a.iters)
         def fb():
+            q.grad = k.grad = v.grad = None          # no gradient-accumulation adds in the timing
             out = f()
             out.backward(g)
         tot = timed(fb, a.iters)

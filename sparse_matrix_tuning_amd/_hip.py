@@ -144,7 +144,9 @@ def load(build_if_missing: bool = False) -> ctypes.CDLL:
         if _lib is None:
             if build_if_missing and _build.is_stale():
                 _build.build()
-            path = _build.LIB_PATH
+            # SMT_HIP_LIB: load a kernel-variant build of the same sources instead (A/B runs,
+            # scripts/diag/build_variant.py); the in-tree library otherwise
+            path = os.environ.get("SMT_HIP_LIB") or _build.LIB_PATH
             if not os.path.exists(path):
                 raise RuntimeError(
                     f"SMT HIP library not built ({path}); run `python -c 'import __graft_entry__ as g; g.build()'`"

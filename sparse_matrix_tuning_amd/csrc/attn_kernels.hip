@@ -145,6 +145,25 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base,
     return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
 }
 __device__ __forceinline__ void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// The same wait as a builtin the compiler's waitcnt pass understands: after it, the pass knows that
+// the register loads issued before the loop (Q / dO / K fragments) have landed. Without it the pass
+// still counts them as pending at the loop header and puts a vmcnt(0) in front of their first use
+// INSIDE the loop, which also waits for the next tile's LDS-DMA issued just before it (the prefetch
+// then never overlaps compute). gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15.
+__device__ __forceinline__ void vm_wait_all_known() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+#ifndef SMT_ATTN_KNOWN_WAIT
+#define SMT_ATTN_KNOWN_WAIT 1
+#endif
+// Wait until at most n (wave-uniform) of this wave's vector-memory operations are outstanding,
+// rounded down to an encodable immediate (waiting for more than needed is always safe).
+__device__ __forceinline__ void vm_wait_upto(int n) {
+    if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (n >= 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else if (n >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
 
 // One wave copies `pieces` x 4 rows [row0, row0 + 4*pieces) of a [rows][128] bf16 operand (row stride
 // ss elements, rows counted from the rsrc base) into a swizzled LDS image at img (image row = row - img_row0).
@@ -234,6 +253,7 @@ __device__ __forceinline__ void fwd_block(const FwdArgs& a, uint8_t* lds, int b,
 
     if (nt > 0) issue(0);
     vm_wait_all();
+    if (SMT_ATTN_KNOWN_WAIT) vm_wait_all_known();
     __syncthreads();
     for (int t = 0; t < nt; ++t) {
         if (t + 1 < nt) issue(t + 1);
@@ -413,6 +433,7 @@ __device__ __forceinline__ void dq_block(const DqArgs& a, uint8_t* lds, int b, i
 
     if (nt > 0) issue(0);
     vm_wait_all();
+    if (SMT_ATTN_KNOWN_WAIT) vm_wait_all_known();
     __syncthreads();
     for (int t = 0; t < nt; ++t) {
         if (t + 1 < nt) issue(t + 1);
@@ -491,14 +512,23 @@ void attn_dq_kernel(DqArgs a) {
 // dK, dV: a workgroup = 8 waves x 32 keys (256 keys) of one (b, kv head); it sweeps the G query
 // heads x 32-row query slices from the block's first key to S, so the G heads' contributions are
 // summed in registers (no atomics). K fragments live in registers, V rows in LDS (64 KiB); the
-// Q / dO slices (+ their lse / delta) arrive by LDS-DMA into a double-buffered ring.
+// Q / dO slices (+ their lse / delta) arrive by LDS-DMA into a kDkvRing-deep ring (slices it+1 ..
+// it+kDkvRing-1 in flight while slice it is computed; the end-of-slice wait is a counted vmcnt).
 // Per slice and wave: S = Q K^T and dP = dO V^T with the row constants (-lse/c, -delta) as the
 // initial accumulators, P = exp2(c S'), dS = P dP', dV^T += dO^T P, dK^T += Q^T dS.
+// Measured alternatives (profiles/r01_attn_variants.jsonl): V fragments in registers instead of the
+// LDS image, and one wave per SIMD with 64 keys per wave (AGPR accumulators), both ran slower: at
+// 256 VGPRs the kernel already spills ~30 registers, and every extra live value adds scratch reloads
+// (each one a vmcnt wait) to the loop.
 // ------------------------------------------------------------------------------------------------
 constexpr int kKB = 256, kKW = 32, kDkvWaves = kKB / kKW, kSlice = 32;
 constexpr int kSliceB = kSlice * kRowB;            // 8 KiB per operand slice
 constexpr int kSliceBuf = 2 * kSliceB + 256;       // Q, dO, 32 lse + 32 delta
 constexpr int kVImg = kKB * kRowB;                 // 64 KiB
+#ifndef SMT_DKV_RING
+#define SMT_DKV_RING 2
+#endif
+constexpr int kDkvRing = SMT_DKV_RING;             // 2; a 4-deep ring measured no faster (the loop is not DMA-bound)
 
 struct DkvArgs {
     Tns q, k, v, dout;
@@ -542,7 +572,7 @@ __device__ __forceinline__ void dkdv_block(const DkvArgs& a, uint8_t* lds, int b
         const int hh = it / n_sl, sl = n_sl - 1 - (it - hh * n_sl);
         const int h = hk * G + hh;
         const int s0 = k0 + sl * kSlice;
-        const uint32_t buf = lds0 + kVImg + (uint32_t)((it & 1) * kSliceBuf);
+        const uint32_t buf = lds0 + kVImg + (uint32_t)((it % kDkvRing) * kSliceBuf);
         const bool is_q = wave < 4;
         const Tns& src = is_q ? a.q : a.dout;
         const uint16_t* base = src.p + b * src.sb + h * src.sh;
@@ -563,12 +593,17 @@ __device__ __forceinline__ void dkdv_block(const DkvArgs& a, uint8_t* lds, int b
         for (int i = 0; i < 16; ++i) { dvt[dt][i] = 0.f; dkt[dt][i] = 0.f; }
     const float inv_sl2 = 1.f / a.sl2;
 
-    if (n_it > 0) issue(0);
-    vm_wait_all();
+    // DMA instructions one wave issues per slice (Q or dO rows: 2; waves 0 / 1 also lse / delta)
+    const int per_slice = wave < 2 ? 3 : 2;
+#pragma unroll
+    for (int i = 0; i < kDkvRing - 1; ++i)
+        if (i < n_it) issue(i);
+    vm_wait_upto(per_slice * min(kDkvRing - 2, n_it - 1));     // slice 0 (and V, K) landed
+    if (SMT_ATTN_KNOWN_WAIT) vm_wait_all_known();               // K fragments: see vm_wait_all_known
     __syncthreads();
     for (int it = 0; it < n_it; ++it) {
-        if (it + 1 < n_it) issue(it + 1);
-        const uint8_t* Qs = lds + kVImg + (it & 1) * kSliceBuf;
+        if (it + kDkvRing - 1 < n_it) issue(it + kDkvRing - 1);   // into the buffer slice it-1 used
+        const uint8_t* Qs = lds + kVImg + (it % kDkvRing) * kSliceBuf;
         const uint8_t* Ds = Qs + kSliceB;
         const float* cst = reinterpret_cast<const float*>(Qs + 2 * kSliceB);     // lse[32], delta[32]
         const int sl = n_sl - 1 - it % n_sl;               // descending q: the group's key blocks read
@@ -613,7 +648,8 @@ __device__ __forceinline__ void dkdv_block(const DkvArgs& a, uint8_t* lds, int b
                     dkt[dt] = mfma(tr_frag(Qs, tl, 16 * kq, 32 * dt), sf[kq], dkt[dt]);
                 }
         }
-        vm_wait_all();
+        // slice it+1 must have landed; it+2 .. it+kDkvRing-1 (those issued) may stay in flight
+        vm_wait_upto(per_slice * max(0, min(kDkvRing - 2, n_it - 2 - it)));
         __syncthreads();
     }
 
@@ -639,7 +675,7 @@ __device__ __forceinline__ void dkdv_block(const DkvArgs& a, uint8_t* lds, int b
 
 __global__ __launch_bounds__(kDkvWaves * 64, 2)
 void attn_dkdv_kernel(DkvArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kVImg + 2 * kSliceBuf];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kVImg + kDkvRing * kSliceBuf];
     const int nkb = (a.S + kKB - 1) / kKB;
     const int total = ((nkb + 1) / 2) * a.Hkv * a.B;
     // key blocks kb (long causal sweep) and nkb-1-kb (short) in one workgroup: equal work per
@@ -734,7 +770,8 @@ int smt_attn_bwd(const smt_attn_tensor* q, const smt_attn_tensor* k, const smt_a
     ka.lse = lse; ka.delta = delta_ws;
     ka.B = B; ka.Hq = Hq; ka.Hkv = Hkv; ka.S = S; ka.sl2 = sl2; ka.scale = shape->scale;
     const int64_t nkb = (S + kKB - 1) / kKB;
-    hipLaunchKernelGGL(attn_dkdv_kernel, dim3((unsigned)(((nkb + 1) / 2) * Hkv * B)), dim3(kDkvWaves * 64), 0, stream, ka);
+    const dim3 grid((unsigned)(((nkb + 1) / 2) * Hkv * B));
+    hipLaunchKernelGGL(attn_dkdv_kernel, grid, dim3(kDkvWaves * 64), 0, stream, ka);
     return check_launch("attn_dkdv_kernel");
 }
 
