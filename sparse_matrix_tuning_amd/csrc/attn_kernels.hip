@@ -215,6 +215,18 @@ __device__ __forceinline__ PairTask pair_task(int L, int nblk, int G, int Hkv) {
     return t;
 }
 
+// Forward K/V staging: tiles of SMT_FWD_KV keys (64 or 32) in a SMT_FWD_RING-deep LDS ring;
+// 64 x 2 = 32 x 4 = 64 KiB per workgroup (two workgroups per CU). 32-key tiles in a 3- or 4-deep
+// ring measured 8-12 % slower than 64 x 2 (profiles/r01_attn_variants.jsonl): the forward is not
+// bound by the K/V DMA latency once the prologue wait is compiler-visible.
+#ifndef SMT_FWD_KV
+#define SMT_FWD_KV 64
+#endif
+#ifndef SMT_FWD_RING
+#define SMT_FWD_RING 2
+#endif
+constexpr int kFKV = SMT_FWD_KV, kFRing = SMT_FWD_RING, kFTileB = kFKV * kRowB, kFS = kFKV / 32;
+
 __device__ __forceinline__ void fwd_block(const FwdArgs& a, uint8_t* lds, int b, int h, int hk, int qb) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -233,14 +245,16 @@ __device__ __forceinline__ void fwd_block(const FwdArgs& a, uint8_t* lds, int b,
     }
 
     const int kv_end = min(a.S, q0 + kFwdQB);
-    const int nt = (kv_end + kKV - 1) / kKV;
+    const int nt = (kv_end + kFKV - 1) / kFKV;
     const __amdgpu_buffer_rsrc_t rk = uniform_rsrc(kp, (int64_t)a.S * a.k.ss * 2);
     const __amdgpu_buffer_rsrc_t rv = uniform_rsrc(vp, (int64_t)a.S * a.v.ss * 2);
     const uint32_t lds0 = lds_addr(lds);
-    auto issue = [&](int t) {            // wave w: rows [16w, 16w+16) of the K and V tiles
-        const uint32_t slot = lds0 + (uint32_t)((t & 1) * 2 * kTileB);
-        dma_rows(rk, a.k.ss, slot, t * kKV, t * kKV + 16 * wave, 4, lane);
-        dma_rows(rv, a.v.ss, slot + kTileB, t * kKV, t * kKV + 16 * wave, 4, lane);
+    constexpr int kRowsW = kFKV / kFwdWaves;             // rows of each operand tile one wave brings
+    constexpr int per_tile = 2 * (kRowsW / 4);           // its DMA instructions per tile (K + V)
+    auto issue = [&](int t) {
+        const uint32_t slot = lds0 + (uint32_t)((t % kFRing) * 2 * kFTileB);
+        dma_rows(rk, a.k.ss, slot, t * kFKV, t * kFKV + kRowsW * wave, kRowsW / 4, lane);
+        dma_rows(rv, a.v.ss, slot + kFTileB, t * kFKV, t * kFKV + kRowsW * wave, kRowsW / 4, lane);
     };
 
     const TrLane tl = tr_lane(lane);
@@ -251,45 +265,49 @@ __device__ __forceinline__ void fwd_block(const FwdArgs& a, uint8_t* lds, int b,
         for (int i = 0; i < 16; ++i) o[dt][i] = 0.f;
     float m_run = kNegInf, l_run = 0.f;
 
-    if (nt > 0) issue(0);
-    vm_wait_all();
-    if (SMT_ATTN_KNOWN_WAIT) vm_wait_all_known();
+    if (kFRing > 2 && SMT_ATTN_KNOWN_WAIT) vm_wait_all_known();    // Q fragments landed (compiler-visible)
+#pragma unroll
+    for (int i = 0; i < kFRing - 1; ++i)
+        if (i < nt) issue(i);
+    vm_wait_upto(per_tile * min(kFRing - 2, nt - 1));                // tile 0 landed
+    if (kFRing == 2 && SMT_ATTN_KNOWN_WAIT) vm_wait_all_known();
     __syncthreads();
     for (int t = 0; t < nt; ++t) {
-        if (t + 1 < nt) issue(t + 1);
-        const uint8_t* K = lds + (t & 1) * 2 * kTileB;
-        const uint8_t* V = K + kTileB;
-        const int k0 = t * kKV;
+        if (t + kFRing - 1 < nt) issue(t + kFRing - 1);               // into the buffer tile t-1 used
+        const uint8_t* K = lds + (t % kFRing) * 2 * kFTileB;
+        const uint8_t* V = K + kFTileB;
+        const int k0 = t * kFKV;
         if (k0 <= qw + kFwdQW - 1) {
-            f32x16_t s0, s1;
+            f32x16_t sc[kFS];
 #pragma unroll
-            for (int i = 0; i < 16; ++i) { s0[i] = 0.f; s1[i] = 0.f; }
+            for (int j = 0; j < kFS; ++j)
 #pragma unroll
-            for (int ks = 0; ks < 8; ++ks) {
-                const bf16x8_t a0 = row_frag(K, l32, 32 * ks + 16 * hi);
-                const bf16x8_t a1 = row_frag(K, 32 + l32, 32 * ks + 16 * hi);
-                s0 = mfma(a0, qf[ks], s0);
-                s1 = mfma(a1, qf[ks], s1);
-            }
-            float x[32];
+                for (int i = 0; i < 16; ++i) sc[j][i] = 0.f;
 #pragma unroll
-            for (int i = 0; i < 16; ++i) { x[i] = s0[i] * a.sl2; x[16 + i] = s1[i] * a.sl2; }
-            if (k0 + kKV - 1 > qw) {                               // tile crosses this wave's diagonal
+            for (int ks = 0; ks < 8; ++ks)
 #pragma unroll
-                for (int i = 0; i < 32; ++i) {
+                for (int j = 0; j < kFS; ++j) sc[j] = mfma(row_frag(K, 32 * j + l32, 32 * ks + 16 * hi), qf[ks], sc[j]);
+            float x[16 * kFS];
+#pragma unroll
+            for (int j = 0; j < kFS; ++j)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) x[16 * j + i] = sc[j][i] * a.sl2;
+            if (k0 + kFKV - 1 > qw) {                              // tile crosses this wave's diagonal
+#pragma unroll
+                for (int i = 0; i < 16 * kFS; ++i) {
                     const int key = k0 + 32 * (i >> 4) + (i & 3) + 8 * ((i & 15) >> 2) + 4 * hi;
                     if (key > qrow) x[i] = kNegInf;
                 }
             }
             float mloc = x[0];
 #pragma unroll
-            for (int i = 1; i < 32; ++i) mloc = fmaxf(mloc, x[i]);
+            for (int i = 1; i < 16 * kFS; ++i) mloc = fmaxf(mloc, x[i]);
             const float m_new = fmaxf(m_run, other_half_max(mloc));
             const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-            float p[32];
+            float p[16 * kFS];
             float sum = 0.f;
 #pragma unroll
-            for (int i = 0; i < 32; ++i) {
+            for (int i = 0; i < 16 * kFS; ++i) {
                 p[i] = __builtin_amdgcn_exp2f(x[i] - m_new);
                 sum += p[i];
             }
@@ -299,15 +317,16 @@ __device__ __forceinline__ void fwd_block(const FwdArgs& a, uint8_t* lds, int b,
             for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
                 for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
-            bf16x8_t pf[4];
-            pack_b_frags(*reinterpret_cast<const float(*)[16]>(&p[0]), pf[0], pf[1]);
-            pack_b_frags(*reinterpret_cast<const float(*)[16]>(&p[16]), pf[2], pf[3]);
+            bf16x8_t pf[2 * kFS];
+#pragma unroll
+            for (int j = 0; j < kFS; ++j)
+                pack_b_frags(*reinterpret_cast<const float(*)[16]>(&p[16 * j]), pf[2 * j], pf[2 * j + 1]);
 #pragma unroll
             for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-                for (int kst = 0; kst < 4; ++kst) o[dt] = mfma(tr_frag(V, tl, 16 * kst, 32 * dt), pf[kst], o[dt]);
+                for (int kst = 0; kst < 2 * kFS; ++kst) o[dt] = mfma(tr_frag(V, tl, 16 * kst, 32 * dt), pf[kst], o[dt]);
         }
-        vm_wait_all();
+        vm_wait_upto(per_tile * max(0, min(kFRing - 2, nt - 2 - t)));   // tile t+1 landed
         __syncthreads();
     }
 
@@ -331,7 +350,7 @@ __device__ __forceinline__ void fwd_block(const FwdArgs& a, uint8_t* lds, int b,
 
 __global__ __launch_bounds__(256, 2)
 void attn_fwd_kernel(FwdArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * 2 * kTileB];      // 64 KiB
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kFRing * 2 * kFTileB];      // 64 KiB
     const int nqb = (a.S + kFwdQB - 1) / kFwdQB;
     const int G = a.Hq / a.Hkv;
     const int total = nqb * a.Hq * a.B;
