@@ -60,6 +60,15 @@ int smt_quant_rows_cat_e4m3(const smt_quant_src* srcs, int32_t n_src, int64_t ro
 int smt_quant_cols_t_e4m3(const void* w, int64_t ld_w, int32_t rows, int32_t cols, const int32_t* col_blocks_dev,
                           int32_t n_col_blocks, void* out_t, int64_t ld_out, float* scales, hipStream_t stream);
 
+/* SwiGLU backward (transformers LlamaMLP, act = SiLU; the formula and bf16 roundings of
+ * smt_swiglu_bwd in smt_model_ops.h) fused with the per-row quantisation of [grad_gate | grad_up]:
+ * out[rows, 2*cols] e4m3 (ld_out >= 2*cols) with one scale per row over both, bit-identical to
+ * smt_swiglu_bwd + smt_quant_rows_cat_e4m3. gate / up / grad_out are contiguous [rows, cols] bf16;
+ * grad_gate / grad_up (same layout) are written only when non-NULL. cols % 8 == 0, <= 16384. */
+int smt_swiglu_bwd_quant_e4m3(const void* gate, const void* up, const void* grad_out, int64_t rows, int32_t cols,
+                              void* out, int64_t ld_out, float* scales, void* grad_gate, void* grad_up,
+                              hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

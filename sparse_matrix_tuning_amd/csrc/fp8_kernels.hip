@@ -265,6 +265,81 @@ void quant_rows_cat_kernel(CatSrcs src, int64_t rows, uint8_t* __restrict__ out,
     }
 }
 
+// SwiGLU backward fused with the per-row quantisation of its two outputs for the gate/up group's
+// joint data-gradient GEMM (fp8.Fp8Group): per token row, dgate and dup are computed exactly as
+// llama_kernels.hip swiglu_bwd_kernel does (same fp32 formula, same bf16 roundings), the row's amax
+// is taken over the bf16 values of BOTH, and they are written as one e4m3 row [dgate | dup] with one
+// scale -- bit-identical to smt_swiglu_bwd followed by smt_quant_rows_cat_e4m3, without writing
+// and re-reading the bf16 gradients (written too only when grad_gate / grad_up are non-null: an SMT
+// gate/up module needs them for its tile weight gradient). One 512-thread workgroup per row.
+__device__ __forceinline__ uint32_t tobf16(float f) { return (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)f); }
+__device__ __forceinline__ float rbf16(float f) { return bf(tobf16(f)); }
+
+template <int CPT>
+__global__ __launch_bounds__(512)
+void swiglu_bwd_quant_kernel(const uint16_t* __restrict__ g, const uint16_t* __restrict__ u,
+                             const uint16_t* __restrict__ dh, int64_t ld, int cols, uint8_t* __restrict__ out,
+                             int64_t ldo, float* __restrict__ scales, uint16_t* __restrict__ dg_out,
+                             uint16_t* __restrict__ du_out) {
+    __shared__ float wmax[8];
+    const int tid = threadIdx.x;
+    const int64_t row = blockIdx.x;
+    const int nch = cols >> 3;
+    uint4 dgv[CPT], duv[CPT];                           // the row's bf16 dgate / dup, 8 per chunk
+    float amax = 0.f;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+        const int c = tid + 512 * i;
+        uint32_t og[4] = {0u, 0u, 0u, 0u}, ou[4] = {0u, 0u, 0u, 0u};
+        if (c < nch) {
+            const int64_t off = row * ld + (int64_t)c * 8;
+            const F8 gv = ld8(g + off), uv = ld8(u + off), hv = ld8(dh + off);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float x = gv.v[j];
+                const float sig = 1.0f / (1.0f + expf(-x));
+                const float sl = rbf16(x / (1.0f + expf(-x)));
+                const float ds = rbf16(hv.v[j] * uv.v[j]);
+                const float vu = rbf16(hv.v[j] * sl);
+                const float vg = rbf16(ds * sig * (1.0f + x * (1.0f - sig)));
+                amax = fmaxf(amax, fmaxf(fabsf(vg), fabsf(vu)));
+                og[j >> 1] |= tobf16(vg) << (16 * (j & 1));
+                ou[j >> 1] |= tobf16(vu) << (16 * (j & 1));
+            }
+        }
+        dgv[i] = make_uint4(og[0], og[1], og[2], og[3]);
+        duv[i] = make_uint4(ou[0], ou[1], ou[2], ou[3]);
+    }
+    amax = wave_max(amax);
+    if ((tid & 63) == 0) wmax[tid >> 6] = amax;
+    __syncthreads();
+    amax = wmax[0];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) amax = fmaxf(amax, wmax[w]);
+    const float scale = amax > 0.f ? amax * kInvE4M3Max : 1.f;
+    if (tid == 0) scales[row] = scale;
+    uint8_t* orow = out + row * ldo;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+        const int c = tid + 512 * i;
+        if (c < nch) {
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+                const uint4 v = half ? duv[i] : dgv[i];
+                const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+                uint2 o;
+                o.x = pack4(qv(bf(w[0] & 0xffffu), scale), qv(bf(w[0] >> 16), scale),
+                            qv(bf(w[1] & 0xffffu), scale), qv(bf(w[1] >> 16), scale));
+                o.y = pack4(qv(bf(w[2] & 0xffffu), scale), qv(bf(w[2] >> 16), scale),
+                            qv(bf(w[3] & 0xffffu), scale), qv(bf(w[3] >> 16), scale));
+                *reinterpret_cast<uint2*>(orow + (int64_t)half * cols + c * 8) = o;
+            }
+            if (dg_out) *reinterpret_cast<uint4*>(dg_out + row * ld + (int64_t)c * 8) = dgv[i];
+            if (du_out) *reinterpret_cast<uint4*>(du_out + row * ld + (int64_t)c * 8) = duv[i];
+        }
+    }
+}
+
 constexpr int kSlabRows = 64;
 constexpr int kSlabLd = 256 + 8;             // 528-B LDS rows
 constexpr int kSegRows = 256;                // rows of W one workgroup covers (4 slabs)
@@ -431,6 +506,33 @@ int smt_quant_rows_cat_e4m3(const smt_quant_src* srcs, int32_t n_src, int64_t ro
     else SMT_CAT(8, 512);
 #undef SMT_CAT
     return check_launch("quant_rows_cat_kernel");
+}
+
+int smt_swiglu_bwd_quant_e4m3(const void* gate, const void* up, const void* grad_out, int64_t rows, int32_t cols,
+                              void* out, int64_t ld_out, float* scales, void* grad_gate, void* grad_up,
+                              hipStream_t stream) {
+    if (rows < 0 || cols <= 0 || (cols & 7) || cols > 512 * 4 * 8)
+        return fail(-1, "smt_swiglu_bwd_quant_e4m3: bad sizes rows=%lld cols=%d (cols %% 8 == 0, <= 16384)",
+                    (long long)rows, cols);
+    if (rows == 0) return 0;
+    if (!gate || !up || !grad_out || !out || !scales) return fail(-1, "smt_swiglu_bwd_quant_e4m3: null pointer");
+    if (!aligned16(gate) || !aligned16(up) || !aligned16(grad_out) || (grad_gate && !aligned16(grad_gate)) ||
+        (grad_up && !aligned16(grad_up)) || (reinterpret_cast<uintptr_t>(out) & 7) || (ld_out & 7) ||
+        ld_out < 2LL * cols)
+        return fail(-2, "smt_swiglu_bwd_quant_e4m3: 16-byte aligned bf16 rows, 8-byte aligned fp8 rows of >= 2*cols");
+    if (rows > 0x7fffffffLL) return fail(-1, "smt_swiglu_bwd_quant_e4m3: too many rows");
+    const uint16_t *pg = static_cast<const uint16_t*>(gate), *pu = static_cast<const uint16_t*>(up),
+                   *ph = static_cast<const uint16_t*>(grad_out);
+    uint8_t* po = static_cast<uint8_t*>(out);
+    uint16_t *dg = static_cast<uint16_t*>(grad_gate), *du = static_cast<uint16_t*>(grad_up);
+    const int nch = cols >> 3;
+    if (nch <= 512 * 2)
+        hipLaunchKernelGGL(swiglu_bwd_quant_kernel<2>, dim3((unsigned)rows), dim3(512), 0, stream, pg, pu, ph,
+                           (int64_t)cols, cols, po, ld_out, scales, dg, du);
+    else
+        hipLaunchKernelGGL(swiglu_bwd_quant_kernel<4>, dim3((unsigned)rows), dim3(512), 0, stream, pg, pu, ph,
+                           (int64_t)cols, cols, po, ld_out, scales, dg, du);
+    return check_launch("swiglu_bwd_quant_kernel");
 }
 
 int smt_quant_cols_t_e4m3(const void* w, int64_t ld_w, int32_t rows, int32_t cols, const int32_t* col_blocks_dev,

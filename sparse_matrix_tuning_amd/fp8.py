@@ -26,6 +26,8 @@ from __future__ import annotations
 
 from typing import Optional
 
+import os
+
 import torch
 
 from . import _hip
@@ -200,9 +202,11 @@ def fp8_linear_dgrad(grad_output: torch.Tensor, fw: Fp8Weight) -> torch.Tensor:
 
 
 class GroupGrad:
-    """The output gradients of one forward's group members, collected until the last one arrives."""
+    """The output gradients of one forward's group members, collected until the last one arrives.
+    ``prequant``: the members' output gradients already quantised as one row by their producer
+    (:func:`swiglu_bwd_quant` for gate/up), used instead of quantising the collected parts."""
 
-    __slots__ = ("version", "group", "registered", "parts", "pending")
+    __slots__ = ("version", "group", "registered", "parts", "pending", "prequant")
 
     def __init__(self, version: int, group: Fp8Group):
         self.version = version
@@ -210,6 +214,50 @@ class GroupGrad:
         self.registered = 0
         self.parts = {}
         self.pending = 0
+        self.prequant = None
+
+
+# SMT_FP8_FUSED_SWIGLU=0 turns the SwiGLU-backward + quantisation fusion off (A/B, parity tests)
+FUSED_SWIGLU_QUANT = os.environ.get("SMT_FP8_FUSED_SWIGLU", "1") != "0"
+
+
+def tag_group_output(y: torch.Tensor, acc, fw: "Fp8Weight", needs_bf16_grad: bool) -> torch.Tensor:
+    """Mark a group member's output so that its consumer can hand the member's gradient over
+    pre-quantised (``needs_bf16_grad``: the member also needs the bf16 gradient itself, e.g. an SMT
+    module's tile weight gradient)."""
+    if acc is not None:
+        y._smt_gout = (acc, fw.group_index, needs_bf16_grad)
+    return y
+
+
+def swiglu_group(gate: torch.Tensor, up: torch.Tensor):
+    """``(acc, needs_bf16_gate, needs_bf16_up)`` when gate and up are the two members of one fp8
+    group (gate first), else None: their SwiGLU backward can then emit the joint fp8 rows."""
+    if not FUSED_SWIGLU_QUANT:
+        return None
+    tg, tu = gate.__dict__.get("_smt_gout"), up.__dict__.get("_smt_gout")
+    if tg is None or tu is None or tg[0] is not tu[0] or (tg[1], tu[1]) != (0, 1) or len(tg[0].group.outs) != 2:
+        return None
+    if gate.shape != up.shape or gate.shape[-1] > 16384:
+        return None
+    return tg[0], tg[2], tu[2]
+
+
+def swiglu_bwd_quant(g: torch.Tensor, u: torch.Tensor, dh: torch.Tensor, need_dg: bool, need_du: bool):
+    """SwiGLU backward fused with the per-row e4m3 quantisation of ``[dgate | dup]``
+    (``smt_swiglu_bwd_quant_e4m3``): returns ``(q [T, 2n], scales [T], dgate or None, dup or None)``."""
+    dev = _hip._require_device(g, u, dh)
+    n = g.shape[-1]
+    rows = g.numel() // n
+    q = torch.empty(rows, 2 * n, dtype=torch.uint8, device=dev)
+    sq = torch.empty(rows, dtype=torch.float32, device=dev)
+    dg = torch.empty_like(g) if need_dg else None
+    du = torch.empty_like(u) if need_du else None
+    rc = _hip.load().smt_swiglu_bwd_quant_e4m3(g.data_ptr(), u.data_ptr(), dh.data_ptr(), rows, n, q.data_ptr(),
+                                               q.stride(0), sq.data_ptr(), dg.data_ptr() if need_dg else None,
+                                               du.data_ptr() if need_du else None, _stream(dev))
+    _hip._check(rc, "smt_swiglu_bwd_quant_e4m3")
+    return q.view(F8), sq, dg, du
 
 
 def register_group(x: torch.Tensor, fw: Fp8Weight):
@@ -237,8 +285,12 @@ def group_input_grad(acc: GroupGrad, fw: Fp8Weight, grad_output: torch.Tensor):
     parts, acc.parts = acc.parts, {}
     g = acc.group
     lead = grad_output.shape[:-1]
+    pre, acc.prequant = acc.prequant, None
     if sorted(parts) == list(range(len(g.outs))):
-        q, sq = quant_rows_cat([parts[i].reshape(-1, g.outs[i]) for i in range(len(g.outs))])
+        if pre is not None:                 # quantised by the producer of the parts
+            q, sq = pre
+        else:
+            q, sq = quant_rows_cat([parts[i].reshape(-1, g.outs[i]) for i in range(len(g.outs))])
         gi = torch._scaled_mm(q, g.wt8.t(), scale_a=sq.view(-1, 1), scale_b=g.swt_row, out_dtype=torch.bfloat16)
     else:                                   # a subset of the members: per-member GEMMs on the slices
         gi = None
@@ -264,7 +316,7 @@ class Fp8LinearFn(torch.autograd.Function):
         ctx.fw = fw
         ctx.gacc = register_group(x, fw)
         y = fp8_linear_forward(x, fw)
-        return y if bias is None else y + bias
+        return tag_group_output(y if bias is None else y + bias, ctx.gacc, fw, False)
 
     @staticmethod
     def backward(ctx, grad_output):

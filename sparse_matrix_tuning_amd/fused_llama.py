@@ -278,10 +278,17 @@ def fused_apply_rotary_pos_emb(q, k, cos, sin, unsqueeze_dim=1):
 # SwiGLU
 # ------------------------------------------------------------------------------------------------
 class FusedSwiGLUFn(torch.autograd.Function):
+    """When gate and up are the two members of one fp8 group (``fp8_linears``), the backward also
+    emits their joint e4m3 gradient rows (``fp8.swiglu_bwd_quant``) for the group's single data-
+    gradient GEMM, and the bf16 gradients only for a member that needs them (an SMT module's tile
+    weight gradient); the others get a zero-stride placeholder that nothing reads."""
+
     @staticmethod
     def forward(ctx, gate, up):
         _need(gate, "swiglu")
         _need(up, "swiglu")
+        from .fp8 import swiglu_group
+        ctx.fp8 = swiglu_group(gate, up)
         g = gate.contiguous()
         u = up.contiguous()
         h = torch.empty_like(g)
@@ -294,6 +301,13 @@ class FusedSwiGLUFn(torch.autograd.Function):
     def backward(ctx, dh):
         g, u = ctx.saved_tensors
         dh = dh.contiguous()
+        if ctx.fp8 is not None and not ctx.fp8[0].parts and ctx.fp8[0].prequant is None:
+            from .fp8 import swiglu_bwd_quant
+            acc, need_dg, need_du = ctx.fp8
+            q, sq, dg, du = swiglu_bwd_quant(g, u, dh, need_dg, need_du)
+            acc.prequant = (q, sq)
+            zero = g.new_zeros(()).expand_as(g)
+            return (dg if need_dg else zero), (du if need_du else zero)
         dg = torch.empty_like(g)
         du = torch.empty_like(u)
         rc = _hip.load().smt_swiglu_bwd(g.data_ptr(), u.data_ptr(), dh.data_ptr(), dg.data_ptr(), du.data_ptr(),

@@ -283,8 +283,10 @@ class linearZ(torch.autograd.Function):
         if fw is None:
             ctx.acc = dgrad.register(input)
         else:
-            from ..fp8 import register_group
+            from ..fp8 import register_group, tag_group_output
             ctx.acc = register_group(input, fw)
+            # the tile weight gradient reads the bf16 output gradient: ask the consumer for it
+            return tag_group_output(_dense_forward(input, weight), ctx.acc, fw, True)
         return _dense_forward(input, weight)
 
     @staticmethod

@@ -197,3 +197,47 @@ def test_fp8_rejects_cpu_and_fp32():
     with pytest.raises(RuntimeError):
         f8.quant_rows(torch.randn(4, 16, device=DEV))
     assert "smt_quant_rows_e4m3" in _hip.ABI_FUNCTIONS
+
+
+@pytest.mark.parametrize("rows,cols", [(300, 14336), (64, 1024), (5, 4104)])
+def test_swiglu_bwd_quant_matches_swiglu_bwd_then_cat_quant(rows, cols):
+    torch.manual_seed(cols)
+    g = (torch.randn(rows, cols, device=DEV) * 3).bfloat16()
+    u = torch.randn(rows, cols, device=DEV).bfloat16()
+    dh = (torch.randn(rows, cols, device=DEV) * 1e-3).bfloat16()
+    dg_ref, du_ref = torch.empty_like(g), torch.empty_like(u)
+    rc = _hip.load().smt_swiglu_bwd(g.data_ptr(), u.data_ptr(), dh.data_ptr(), dg_ref.data_ptr(), du_ref.data_ptr(),
+                                    g.numel(), torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    q_ref, s_ref = f8.quant_rows_cat([dg_ref, du_ref])
+    q, s, dg, du = f8.swiglu_bwd_quant(g, u, dh, True, True)
+    assert torch.equal(s, s_ref) and torch.equal(q.view(torch.uint8), q_ref.view(torch.uint8))
+    assert torch.equal(dg, dg_ref) and torch.equal(du, du_ref)
+    q2, s2, n1, n2 = f8.swiglu_bwd_quant(g, u, dh, False, False)
+    assert n1 is None and n2 is None and torch.equal(q2.view(torch.uint8), q_ref.view(torch.uint8))
+
+
+def test_fused_swiglu_group_grad_bit_identical_to_unfused():
+    from sparse_matrix_tuning_amd.fused_llama import FusedSwiGLUFn
+    torch.manual_seed(7)
+    ws = [(torch.randn(1024, 512, device=DEV) * 0.02).bfloat16() for _ in range(2)]
+    g = f8.Fp8Group(ws)
+    fws = [f8.Fp8Weight(w, g, i) for i, w in enumerate(ws)]
+    x0 = torch.randn(2, 128, 512, device=DEV).bfloat16()
+    dh = torch.randn(2, 128, 1024, device=DEV).bfloat16()
+
+    def run(fused):
+        old = f8.FUSED_SWIGLU_QUANT
+        f8.FUSED_SWIGLU_QUANT = fused
+        try:
+            x = x0.clone().requires_grad_()
+            gate = f8.Fp8LinearFn.apply(x, ws[0], fws[0], None)
+            up = f8.Fp8LinearFn.apply(x, ws[1], fws[1], None)
+            h = FusedSwiGLUFn.apply(gate, up)
+            h.backward(dh)
+            return x.grad
+        finally:
+            f8.FUSED_SWIGLU_QUANT = old
+
+    fused, plain = run(True), run(False)
+    assert torch.equal(fused, plain)
