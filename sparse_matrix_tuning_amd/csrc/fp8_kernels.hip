@@ -17,6 +17,7 @@
 #include <stdio.h>
 
 #include "smt_fp8.h"
+#include "silu_math.h"
 
 namespace {
 
@@ -45,6 +46,14 @@ __device__ __forceinline__ float bf(uint32_t b16) { return __uint_as_float(b16 <
 
 struct F8 { float v[8]; };
 
+__device__ __forceinline__ F8 unpack8(const uint4 a) {
+    F8 r;
+    const uint32_t w[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { r.v[2 * j] = bf(w[j] & 0xffffu); r.v[2 * j + 1] = bf(w[j] >> 16); }
+    return r;
+}
+
 __device__ __forceinline__ F8 ld8(const uint16_t* p) {
     const uint4 a = *reinterpret_cast<const uint4*>(p);
     F8 r;
@@ -54,8 +63,16 @@ __device__ __forceinline__ F8 ld8(const uint16_t* p) {
     return r;
 }
 
+// x / scale, correctly rounded (so bit-identical to torch's IEEE division) without a per-element
+// division: with rs = RN(1/scale), q0 = RN(x * rs) is within an ulp of the quotient, the residual
+// x - q0 * scale is exact in one FMA, and RN(q0 + residual * rs) is the correctly rounded quotient
+// (Markstein). 1/scale is loop-invariant per row / column, so the one real division is hoisted.
+// The quotient stays within +-448 (|x| <= amax = 448 * scale), far from overflow and underflow.
 __device__ __forceinline__ float qv(float x, float scale) {
-    return __builtin_amdgcn_fmed3f(x / scale, kE4M3Max, -kE4M3Max);
+    const float rs = 1.f / scale;
+    const float q0 = x * rs;
+    const float r = __builtin_fmaf(-q0, scale, x);
+    return __builtin_amdgcn_fmed3f(__builtin_fmaf(r, rs, q0), kE4M3Max, -kE4M3Max);
 }
 
 // four values -> four e4m3 bytes (little endian: a is byte 0)
@@ -286,19 +303,28 @@ void swiglu_bwd_quant_kernel(const uint16_t* __restrict__ g, const uint16_t* __r
     const int64_t row = blockIdx.x;
     const int nch = cols >> 3;
     uint4 dgv[CPT], duv[CPT];                           // the row's bf16 dgate / dup, 8 per chunk
+    uint4 graw[CPT], uraw[CPT], hraw[CPT];              // every load of the row issued before any math
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+        const int c = tid + 512 * i;
+        const int64_t off = row * ld + (int64_t)c * 8;
+        const bool in = c < nch;
+        graw[i] = in ? *reinterpret_cast<const uint4*>(g + off) : make_uint4(0u, 0u, 0u, 0u);
+        uraw[i] = in ? *reinterpret_cast<const uint4*>(u + off) : make_uint4(0u, 0u, 0u, 0u);
+        hraw[i] = in ? *reinterpret_cast<const uint4*>(dh + off) : make_uint4(0u, 0u, 0u, 0u);
+    }
     float amax = 0.f;
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
         const int c = tid + 512 * i;
         uint32_t og[4] = {0u, 0u, 0u, 0u}, ou[4] = {0u, 0u, 0u, 0u};
         if (c < nch) {
-            const int64_t off = row * ld + (int64_t)c * 8;
-            const F8 gv = ld8(g + off), uv = ld8(u + off), hv = ld8(dh + off);
+            const F8 gv = unpack8(graw[i]), uv = unpack8(uraw[i]), hv = unpack8(hraw[i]);
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const float x = gv.v[j];
-                const float sig = 1.0f / (1.0f + expf(-x));
-                const float sl = rbf16(x / (1.0f + expf(-x)));
+                const float sig = smt_sigmoid(x);
+                const float sl = rbf16(x * sig);
                 const float ds = rbf16(hv.v[j] * uv.v[j]);
                 const float vu = rbf16(hv.v[j] * sl);
                 const float vg = rbf16(ds * sig * (1.0f + x * (1.0f - sig)));
@@ -336,6 +362,72 @@ void swiglu_bwd_quant_kernel(const uint16_t* __restrict__ g, const uint16_t* __r
             }
             if (dg_out) *reinterpret_cast<uint4*>(dg_out + row * ld + (int64_t)c * 8) = dgv[i];
             if (du_out) *reinterpret_cast<uint4*>(du_out + row * ld + (int64_t)c * 8) = duv[i];
+        }
+    }
+}
+
+// SwiGLU forward fused with the per-row quantisation of its output (the down_proj input of the fp8
+// path): h = bf16(bf16(silu(gate)) * up) exactly as llama_kernels.hip swiglu_fwd_kernel, then one
+// e4m3 row + scale per token -- bit-identical to smt_swiglu_fwd + smt_quant_rows_e4m3. The bf16 h is
+// written only when h_out is non-null (an SMT down_proj reads its input columns for the tile weight
+// gradient; a frozen one reads only the fp8 copy). One 512-thread workgroup per row.
+template <int CPT>
+__global__ __launch_bounds__(512)
+void swiglu_fwd_quant_kernel(const uint16_t* __restrict__ g, const uint16_t* __restrict__ u, int64_t ld, int cols,
+                             uint8_t* __restrict__ out, int64_t ldo, float* __restrict__ scales,
+                             uint16_t* __restrict__ h_out) {
+    __shared__ float wmax[8];
+    const int tid = threadIdx.x;
+    const int64_t row = blockIdx.x;
+    const int nch = cols >> 3;
+    uint4 hv[CPT];
+    uint4 graw[CPT], uraw[CPT];                         // every load of the row issued before any math
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+        const int c = tid + 512 * i;
+        const int64_t off = row * ld + (int64_t)c * 8;
+        const bool in = c < nch;
+        graw[i] = in ? *reinterpret_cast<const uint4*>(g + off) : make_uint4(0u, 0u, 0u, 0u);
+        uraw[i] = in ? *reinterpret_cast<const uint4*>(u + off) : make_uint4(0u, 0u, 0u, 0u);
+    }
+    float amax = 0.f;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+        const int c = tid + 512 * i;
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+        if (c < nch) {
+            const F8 gv = unpack8(graw[i]), uv = unpack8(uraw[i]);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float sl = rbf16(gv.v[j] * smt_sigmoid(gv.v[j]));
+                const float hh = rbf16(sl * uv.v[j]);
+                amax = fmaxf(amax, fabsf(hh));
+                w[j >> 1] |= tobf16(hh) << (16 * (j & 1));
+            }
+        }
+        hv[i] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    amax = wave_max(amax);
+    if ((tid & 63) == 0) wmax[tid >> 6] = amax;
+    __syncthreads();
+    amax = wmax[0];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) amax = fmaxf(amax, wmax[w]);
+    const float scale = amax > 0.f ? amax * kInvE4M3Max : 1.f;
+    if (tid == 0) scales[row] = scale;
+    uint8_t* orow = out + row * ldo;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+        const int c = tid + 512 * i;
+        if (c < nch) {
+            const uint32_t w[4] = {hv[i].x, hv[i].y, hv[i].z, hv[i].w};
+            uint2 o;
+            o.x = pack4(qv(bf(w[0] & 0xffffu), scale), qv(bf(w[0] >> 16), scale),
+                        qv(bf(w[1] & 0xffffu), scale), qv(bf(w[1] >> 16), scale));
+            o.y = pack4(qv(bf(w[2] & 0xffffu), scale), qv(bf(w[2] >> 16), scale),
+                        qv(bf(w[3] & 0xffffu), scale), qv(bf(w[3] >> 16), scale));
+            *reinterpret_cast<uint2*>(orow + c * 8) = o;
+            if (h_out) *reinterpret_cast<uint4*>(h_out + row * ld + (int64_t)c * 8) = hv[i];
         }
     }
 }
@@ -506,6 +598,29 @@ int smt_quant_rows_cat_e4m3(const smt_quant_src* srcs, int32_t n_src, int64_t ro
     else SMT_CAT(8, 512);
 #undef SMT_CAT
     return check_launch("quant_rows_cat_kernel");
+}
+
+int smt_swiglu_fwd_quant_e4m3(const void* gate, const void* up, int64_t rows, int32_t cols, void* out, int64_t ld_out,
+                              float* scales, void* h_out, hipStream_t stream) {
+    if (rows < 0 || cols <= 0 || (cols & 7) || cols > 512 * 4 * 8)
+        return fail(-1, "smt_swiglu_fwd_quant_e4m3: bad sizes rows=%lld cols=%d (cols %% 8 == 0, <= 16384)",
+                    (long long)rows, cols);
+    if (rows == 0) return 0;
+    if (!gate || !up || !out || !scales) return fail(-1, "smt_swiglu_fwd_quant_e4m3: null pointer");
+    if (!aligned16(gate) || !aligned16(up) || (h_out && !aligned16(h_out)) ||
+        (reinterpret_cast<uintptr_t>(out) & 7) || (ld_out & 7) || ld_out < cols)
+        return fail(-2, "smt_swiglu_fwd_quant_e4m3: 16-byte aligned bf16 rows, 8-byte aligned fp8 rows");
+    if (rows > 0x7fffffffLL) return fail(-1, "smt_swiglu_fwd_quant_e4m3: too many rows");
+    const uint16_t *pg = static_cast<const uint16_t*>(gate), *pu = static_cast<const uint16_t*>(up);
+    uint8_t* po = static_cast<uint8_t*>(out);
+    uint16_t* ph = static_cast<uint16_t*>(h_out);
+    if ((cols >> 3) <= 512 * 2)
+        hipLaunchKernelGGL(swiglu_fwd_quant_kernel<2>, dim3((unsigned)rows), dim3(512), 0, stream, pg, pu,
+                           (int64_t)cols, cols, po, ld_out, scales, ph);
+    else
+        hipLaunchKernelGGL(swiglu_fwd_quant_kernel<4>, dim3((unsigned)rows), dim3(512), 0, stream, pg, pu,
+                           (int64_t)cols, cols, po, ld_out, scales, ph);
+    return check_launch("swiglu_fwd_quant_kernel");
 }
 
 int smt_swiglu_bwd_quant_e4m3(const void* gate, const void* up, const void* grad_out, int64_t rows, int32_t cols,

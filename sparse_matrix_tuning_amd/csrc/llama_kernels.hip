@@ -14,6 +14,7 @@
 #include <stdio.h>
 
 #include "smt_model_ops.h"
+#include "silu_math.h"
 
 namespace {
 
@@ -320,7 +321,7 @@ void swiglu_fwd_kernel(const uint16_t* __restrict__ g, const uint16_t* __restric
     F8 o;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        const float s = rbf(gv.v[j] / (1.0f + expf(-gv.v[j])));
+        const float s = rbf(gv.v[j] * smt_sigmoid(gv.v[j]));
         o.v[j] = s * uv.v[j];
     }
     st8(h + i * 8, o);
@@ -336,8 +337,8 @@ void swiglu_bwd_kernel(const uint16_t* __restrict__ g, const uint16_t* __restric
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const float x = gv.v[j];
-        const float sig = 1.0f / (1.0f + expf(-x));
-        const float s = rbf(x / (1.0f + expf(-x)));
+        const float sig = smt_sigmoid(x);
+        const float s = rbf(x * sig);
         const float ds = rbf(hv.v[j] * uv.v[j]);
         ou.v[j] = hv.v[j] * s;
         og.v[j] = ds * sig * (1.0f + x * (1.0f - sig));

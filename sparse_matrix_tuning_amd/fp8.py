@@ -219,6 +219,8 @@ class GroupGrad:
 
 # SMT_FP8_FUSED_SWIGLU=0 turns the SwiGLU-backward + quantisation fusion off (A/B, parity tests)
 FUSED_SWIGLU_QUANT = os.environ.get("SMT_FP8_FUSED_SWIGLU", "1") != "0"
+# SMT_FP8_FUSED_SWIGLU_FWD=0: only the forward half (down_proj input quantised by the SwiGLU) off
+FUSED_SWIGLU_FWD_QUANT = os.environ.get("SMT_FP8_FUSED_SWIGLU_FWD", "1") != "0"
 
 
 def tag_group_output(y: torch.Tensor, acc, fw: "Fp8Weight", needs_bf16_grad: bool) -> torch.Tensor:
@@ -241,6 +243,21 @@ def swiglu_group(gate: torch.Tensor, up: torch.Tensor):
     if gate.shape != up.shape or gate.shape[-1] > 16384:
         return None
     return tg[0], tg[2], tu[2]
+
+
+def swiglu_fwd_quant(g: torch.Tensor, u: torch.Tensor, need_h: bool):
+    """SwiGLU forward fused with the per-row e4m3 quantisation of its output
+    (``smt_swiglu_fwd_quant_e4m3``): returns ``(q [T, n], scales [T], h bf16 or None)``."""
+    dev = _hip._require_device(g, u)
+    n = g.shape[-1]
+    rows = g.numel() // n
+    q = torch.empty(rows, n, dtype=torch.uint8, device=dev)
+    sq = torch.empty(rows, dtype=torch.float32, device=dev)
+    h = torch.empty_like(g) if need_h else None
+    rc = _hip.load().smt_swiglu_fwd_quant_e4m3(g.data_ptr(), u.data_ptr(), rows, n, q.data_ptr(), q.stride(0),
+                                               sq.data_ptr(), h.data_ptr() if need_h else None, _stream(dev))
+    _hip._check(rc, "smt_swiglu_fwd_quant_e4m3")
+    return q.view(F8), sq, h
 
 
 def swiglu_bwd_quant(g: torch.Tensor, u: torch.Tensor, dh: torch.Tensor, need_dg: bool, need_du: bool):

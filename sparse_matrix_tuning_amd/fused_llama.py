@@ -284,17 +284,26 @@ class FusedSwiGLUFn(torch.autograd.Function):
     weight gradient); the others get a zero-stride placeholder that nothing reads."""
 
     @staticmethod
-    def forward(ctx, gate, up):
+    def forward(ctx, gate, up, quant_out=False, need_bf16_out=True):
         _need(gate, "swiglu")
         _need(up, "swiglu")
         from .fp8 import swiglu_group
         ctx.fp8 = swiglu_group(gate, up)
         g = gate.contiguous()
         u = up.contiguous()
+        ctx.save_for_backward(g, u)
+        if quant_out:
+            # fp8 down_proj: emit its per-row e4m3 input directly (cached on the output, where
+            # fp8.quant_rows_cached finds it); the bf16 output only if the consumer reads it
+            from .fp8 import swiglu_fwd_quant
+            q, sq, h = swiglu_fwd_quant(g, u, need_bf16_out)
+            if h is None:
+                h = g.new_zeros(()).expand(g.shape)
+            h._smt_q8 = (h._version, q, sq)
+            return h
         h = torch.empty_like(g)
         rc = _hip.load().smt_swiglu_fwd(g.data_ptr(), u.data_ptr(), h.data_ptr(), g.numel(), _stream(g))
         _hip._check(rc, "smt_swiglu_fwd")
-        ctx.save_for_backward(g, u)
         return h
 
     @staticmethod
@@ -307,18 +316,26 @@ class FusedSwiGLUFn(torch.autograd.Function):
             q, sq, dg, du = swiglu_bwd_quant(g, u, dh, need_dg, need_du)
             acc.prequant = (q, sq)
             zero = g.new_zeros(()).expand_as(g)
-            return (dg if need_dg else zero), (du if need_du else zero)
+            return (dg if need_dg else zero), (du if need_du else zero), None, None
         dg = torch.empty_like(g)
         du = torch.empty_like(u)
         rc = _hip.load().smt_swiglu_bwd(g.data_ptr(), u.data_ptr(), dh.data_ptr(), dg.data_ptr(), du.data_ptr(),
                                         g.numel(), _stream(g))
         _hip._check(rc, "smt_swiglu_bwd")
-        return dg, du
+        return dg, du, None, None
 
 
 def fused_mlp_forward(self, x):
-    """Drop-in for ``LlamaMLP.forward`` (SiLU activation)."""
-    return self.down_proj(FusedSwiGLUFn.apply(self.gate_proj(x), self.up_proj(x)))
+    """Drop-in for ``LlamaMLP.forward`` (SiLU activation). With an fp8 down_proj the SwiGLU also emits
+    down_proj's quantised input; a frozen plain down_proj then never reads the bf16 activation."""
+    gate, up = self.gate_proj(x), self.up_proj(x)
+    d = self.down_proj
+    if getattr(d.weight, "_smt_fp8", None) is not None and gate.shape[-1] <= 16384:
+        from . import fp8
+        if fp8.FUSED_SWIGLU_QUANT and fp8.FUSED_SWIGLU_FWD_QUANT:
+            frozen_plain = type(d) is torch.nn.Linear and not d.weight.requires_grad
+            return d(FusedSwiGLUFn.apply(gate, up, True, not frozen_plain))
+    return d(FusedSwiGLUFn.apply(gate, up))
 
 
 # ------------------------------------------------------------------------------------------------

@@ -241,3 +241,38 @@ def test_fused_swiglu_group_grad_bit_identical_to_unfused():
 
     fused, plain = run(True), run(False)
     assert torch.equal(fused, plain)
+
+
+@pytest.mark.parametrize("rows,cols", [(300, 14336), (17, 1024)])
+def test_swiglu_fwd_quant_matches_swiglu_then_quant(rows, cols):
+    torch.manual_seed(cols + 1)
+    g = (torch.randn(rows, cols, device=DEV) * 3).bfloat16()
+    u = torch.randn(rows, cols, device=DEV).bfloat16()
+    h_ref = torch.empty_like(g)
+    assert _hip.load().smt_swiglu_fwd(g.data_ptr(), u.data_ptr(), h_ref.data_ptr(), g.numel(),
+                                      torch.cuda.current_stream().cuda_stream) == 0
+    q_ref, s_ref = f8.quant_rows(h_ref)
+    q, s, h = f8.swiglu_fwd_quant(g, u, True)
+    assert torch.equal(h, h_ref)
+    assert torch.equal(s, s_ref) and torch.equal(q.view(torch.uint8), q_ref.view(torch.uint8))
+    q2, s2, none = f8.swiglu_fwd_quant(g, u, False)
+    assert none is None and torch.equal(q2.view(torch.uint8), q_ref.view(torch.uint8))
+
+
+def test_fused_swiglu_into_fp8_down_proj_bit_identical():
+    from sparse_matrix_tuning_amd.fused_llama import FusedSwiGLUFn
+    torch.manual_seed(8)
+    Wd = (torch.randn(512, 1024, device=DEV) * 0.02).bfloat16()
+    fwd = f8.Fp8Weight(Wd)
+    g0 = torch.randn(2, 64, 1024, device=DEV).bfloat16()
+    u0 = torch.randn(2, 64, 1024, device=DEV).bfloat16()
+    dy = torch.randn(2, 64, 512, device=DEV).bfloat16()
+    outs = []
+    for fused in (True, False):
+        g, u = g0.clone().requires_grad_(), u0.clone().requires_grad_()
+        h = FusedSwiGLUFn.apply(g, u, True, False) if fused else FusedSwiGLUFn.apply(g, u)
+        y = f8.Fp8LinearFn.apply(h, Wd, fwd, None)
+        y.backward(dy)
+        outs.append((y.detach(), g.grad, u.grad))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
