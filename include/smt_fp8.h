@@ -60,6 +60,13 @@ int smt_quant_rows_cat_e4m3(const smt_quant_src* srcs, int32_t n_src, int64_t ro
 int smt_quant_cols_t_e4m3(const void* w, int64_t ld_w, int32_t rows, int32_t cols, const int32_t* col_blocks_dev,
                           int32_t n_col_blocks, void* out_t, int64_t ld_out, float* scales, hipStream_t stream);
 
+/* SwiGLU forward (smt_swiglu_fwd's formula and roundings) fused with the per-row quantisation of
+ * its output: out[rows, cols] e4m3 + scales[rows], bit-identical to smt_swiglu_fwd followed by
+ * smt_quant_rows_e4m3; the bf16 output is written to h_out only when it is non-NULL.
+ * gate / up / h_out contiguous [rows, cols] bf16, cols % 8 == 0, <= 16384. */
+int smt_swiglu_fwd_quant_e4m3(const void* gate, const void* up, int64_t rows, int32_t cols, void* out, int64_t ld_out,
+                              float* scales, void* h_out, hipStream_t stream);
+
 /* SwiGLU backward (transformers LlamaMLP, act = SiLU; the formula and bf16 roundings of
  * smt_swiglu_bwd in smt_model_ops.h) fused with the per-row quantisation of [grad_gate | grad_up]:
  * out[rows, 2*cols] e4m3 (ld_out >= 2*cols) with one scale per row over both, bit-identical to
