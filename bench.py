@@ -433,7 +433,8 @@ def main():
             tiles_by_module.setdefault(m, [])
             tiles_by_module[m].extend(v)
         per_layer = {m: v[: max(1, round(len(v) / MODELS[args.model]["num_hidden_layers"]))] for m, v in tiles_by_module.items()}
-        cpu = cpu_baseline(args.cpu_baseline_seconds, per_layer, args.model)
+        # the CPU baseline is a property of the N = 1 line; a multi-GPU run does not repeat it
+        cpu = cpu_baseline(args.cpu_baseline_seconds, per_layer, args.model) if world == 1 else None
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "tokens/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2),
