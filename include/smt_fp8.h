@@ -60,6 +60,15 @@ int smt_quant_rows_cat_e4m3(const smt_quant_src* srcs, int32_t n_src, int64_t ro
 int smt_quant_cols_t_e4m3(const void* w, int64_t ld_w, int32_t rows, int32_t cols, const int32_t* col_blocks_dev,
                           int32_t n_col_blocks, void* out_t, int64_t ld_out, float* scales, hipStream_t stream);
 
+/* RMSNorm forward (smt_rmsnorm_fwd; with residual != NULL smt_add_rmsnorm_fwd, h = bf16(x + residual))
+ * that also writes its bf16 output y as one e4m3 row per token: out[rows, hidden] + scales[rows],
+ * bit-identical to the bf16 kernel followed by smt_quant_rows_e4m3. y may be NULL when no consumer
+ * reads the bf16 output (a frozen fp8 q/k/v or gate/up group). hidden in {1024, 2048, 4096, 8192}.
+ * (Defined in llama_kernels.hip next to the RMSNorm kernels.) */
+int smt_rmsnorm_fwd_quant_e4m3(const void* x, int64_t ld_x, const void* residual, int64_t ld_r, const void* weight,
+                               void* h, int64_t ld_h, void* y, int64_t ld_y, float* rstd, void* out, int64_t ld_out,
+                               float* scales, int64_t rows, int32_t hidden, float eps, hipStream_t stream);
+
 /* SwiGLU forward (smt_swiglu_fwd's formula and roundings) fused with the per-row quantisation of
  * its output: out[rows, cols] e4m3 + scales[rows], bit-identical to smt_swiglu_fwd followed by
  * smt_quant_rows_e4m3; the bf16 output is written to h_out only when it is non-NULL.

@@ -37,7 +37,7 @@ ABI_FUNCTIONS = (
     "smt_rope_fwd", "smt_rope_bwd", "smt_swiglu_fwd", "smt_swiglu_bwd", "smt_ce_fwd", "smt_ce_bwd",
     "smt_attn_last_error", "smt_attn_fwd", "smt_attn_bwd",
     "smt_fp8_last_error", "smt_quant_rows_e4m3", "smt_quant_cols_t_e4m3", "smt_quant_rows_cat_e4m3",
-    "smt_swiglu_fwd_quant_e4m3", "smt_swiglu_bwd_quant_e4m3",
+    "smt_swiglu_fwd_quant_e4m3", "smt_swiglu_bwd_quant_e4m3", "smt_rmsnorm_fwd_quant_e4m3",
 )
 
 
@@ -129,6 +129,8 @@ _SIGS = {
     "smt_quant_rows_e4m3": (ctypes.c_int, [_P, _I64, _I64, _I32, _P, _I32, _P, _I64, _P, _P]),
     "smt_quant_cols_t_e4m3": (ctypes.c_int, [_P, _I64, _I32, _I32, _P, _I32, _P, _I64, _P, _P]),
     "smt_quant_rows_cat_e4m3": (ctypes.c_int, [ctypes.POINTER(QuantSrc), _I32, _I64, _P, _I64, _P, _P]),
+    "smt_rmsnorm_fwd_quant_e4m3": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _P, _I64, _P, _I64, _P, _P, _I64, _P,
+                                                   _I64, _I32, ctypes.c_float, _P]),
     "smt_swiglu_fwd_quant_e4m3": (ctypes.c_int, [_P, _P, _I64, _I32, _P, _I64, _P, _P, _P]),
     "smt_swiglu_bwd_quant_e4m3": (ctypes.c_int, [_P, _P, _P, _I64, _I32, _P, _I64, _P, _P, _P, _P]),
 }
@@ -166,12 +168,12 @@ def load(build_if_missing: bool = False) -> ctypes.CDLL:
 def _check(rc: int, what: str) -> None:
     if rc != 0:
         lib = load()
-        if what.startswith(("smt_rmsnorm", "smt_add_rmsnorm", "smt_rope", "smt_swiglu", "smt_ce_")):
-            err = lib.smt_model_ops_last_error
+        if what.startswith(("smt_quant", "smt_swiglu_fwd_quant", "smt_swiglu_bwd_quant")):
+            err = lib.smt_fp8_last_error                 # fp8_kernels.hip
+        elif what.startswith(("smt_rmsnorm", "smt_add_rmsnorm", "smt_rope", "smt_swiglu", "smt_ce_")):
+            err = lib.smt_model_ops_last_error           # llama_kernels.hip (incl. smt_rmsnorm_fwd_quant_e4m3)
         elif what.startswith("smt_attn"):
             err = lib.smt_attn_last_error
-        elif what.startswith("smt_quant"):
-            err = lib.smt_fp8_last_error
         else:
             err = lib.smt_last_error
         raise RuntimeError(f"{what} failed (status {rc}): {err().decode(errors='replace')}")

@@ -20,7 +20,7 @@ SRCS = [os.path.join(PKG_DIR, "csrc", n) for n in ("smt_kernels.hip", "llama_ker
                                                    "fp8_kernels.hip")]
 HEADERS = [os.path.join(REPO_DIR, "include", n) for n in ("smt_hip.h", "smt_model_ops.h", "smt_attention.h",
                                                           "smt_fp8.h")]
-HEADERS.append(os.path.join(PKG_DIR, "csrc", "silu_math.h"))
+HEADERS += [os.path.join(PKG_DIR, "csrc", n) for n in ("silu_math.h", "fp8_math.h")]
 LIB_DIR = os.path.join(PKG_DIR, "_lib")
 LIB_PATH = os.path.join(LIB_DIR, "libsmt_hip.so")
 ARCH = "gfx950"

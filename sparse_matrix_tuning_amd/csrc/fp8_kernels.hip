@@ -18,6 +18,7 @@
 
 #include "smt_fp8.h"
 #include "silu_math.h"
+#include "fp8_math.h"
 
 namespace {
 
@@ -39,9 +40,6 @@ int check_launch(const char* what) {
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-constexpr float kE4M3Max = 448.f;
-constexpr float kInvE4M3Max = 1.f / 448.f;          // fp32-rounded reciprocal: scale = amax * (1/448)
-
 __device__ __forceinline__ float bf(uint32_t b16) { return __uint_as_float(b16 << 16); }
 
 struct F8 { float v[8]; };
@@ -61,25 +59,6 @@ __device__ __forceinline__ F8 ld8(const uint16_t* p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) { r.v[2 * j] = bf(w[j] & 0xffffu); r.v[2 * j + 1] = bf(w[j] >> 16); }
     return r;
-}
-
-// x / scale, correctly rounded (so bit-identical to torch's IEEE division) without a per-element
-// division: with rs = RN(1/scale), q0 = RN(x * rs) is within an ulp of the quotient, the residual
-// x - q0 * scale is exact in one FMA, and RN(q0 + residual * rs) is the correctly rounded quotient
-// (Markstein). 1/scale is loop-invariant per row / column, so the one real division is hoisted.
-// The quotient stays within +-448 (|x| <= amax = 448 * scale), far from overflow and underflow.
-__device__ __forceinline__ float qv(float x, float scale) {
-    const float rs = 1.f / scale;
-    const float q0 = x * rs;
-    const float r = __builtin_fmaf(-q0, scale, x);
-    return __builtin_amdgcn_fmed3f(__builtin_fmaf(r, rs, q0), kE4M3Max, -kE4M3Max);
-}
-
-// four values -> four e4m3 bytes (little endian: a is byte 0)
-__device__ __forceinline__ uint32_t pack4(float a, float b, float c, float d) {
-    int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
-    w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
-    return (uint32_t)w;
 }
 
 __device__ __forceinline__ float wave_max(float v) {

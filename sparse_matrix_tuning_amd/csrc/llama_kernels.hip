@@ -15,6 +15,8 @@
 
 #include "smt_model_ops.h"
 #include "silu_math.h"
+#include "fp8_math.h"
+#include "smt_fp8.h"
 
 namespace {
 
@@ -56,6 +58,12 @@ __device__ __forceinline__ void st8(uint16_t* p, const F8& r) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) w[j] = tobf(r.v[2 * j]) | (tobf(r.v[2 * j + 1]) << 16);
     *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__device__ __forceinline__ float wave_max_f(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+    return v;
 }
 
 __device__ __forceinline__ float wave_sum_f(float v) {
@@ -168,12 +176,12 @@ void rmsnorm_dw_kernel(const float* __restrict__ partial, int64_t n_waves, int H
 //
 // Forward with an optional fused residual add (LlamaDecoderLayer: h = residual + attn_out, then
 // post_attention_layernorm(h)): h = bf16(x + res) is written out as well and normalised.
-template <int CPL, bool ADD>
+template <int CPL, bool ADD, bool QUANT = false>
 __global__ __launch_bounds__(256)
 void rmsnorm_fwd_reg_kernel(const uint16_t* __restrict__ x, int64_t ldx, const uint16_t* __restrict__ res, int64_t ldr,
                             const uint16_t* __restrict__ w, uint16_t* __restrict__ h, int64_t ldh,
                             uint16_t* __restrict__ y, int64_t ldy, float* __restrict__ rstd, int64_t rows, int H,
-                            float eps) {
+                            float eps, uint8_t* __restrict__ q8, int64_t ldq, float* __restrict__ qscale) {
     const int lane = threadIdx.x & 63;
     const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= rows) return;
@@ -195,14 +203,42 @@ void rmsnorm_fwd_reg_kernel(const uint16_t* __restrict__ x, int64_t ldx, const u
     ss = wave_sum_f(ss);
     const float r = 1.0f / sqrtf(ss / (float)H + eps);
     if (lane == 0) rstd[row] = r;
+    if (!QUANT) {
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            const int c = lane + 64 * k;
+            const F8 wv = ld8(w + c * 8);
+            F8 o;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o.v[j] = wv.v[j] * rbf(v[k].v[j] * r);
+            st8(y + row * ldy + c * 8, o);
+        }
+        return;
+    }
+    // QUANT: the bf16 output (kept in registers) also as one e4m3 row + scale, exactly as
+    // smt_quant_rows_e4m3 would quantise it; the bf16 row is stored only when y is non-null
+    float amax = 0.f;
 #pragma unroll
     for (int k = 0; k < CPL; ++k) {
         const int c = lane + 64 * k;
         const F8 wv = ld8(w + c * 8);
-        F8 o;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o.v[j] = wv.v[j] * rbf(v[k].v[j] * r);
-        st8(y + row * ldy + c * 8, o);
+        for (int j = 0; j < 8; ++j) {
+            v[k].v[j] = rbf(wv.v[j] * rbf(v[k].v[j] * r));
+            amax = fmaxf(amax, fabsf(v[k].v[j]));
+        }
+        if (y) st8(y + row * ldy + c * 8, v[k]);
+    }
+    amax = wave_max_f(amax);
+    const float scale = e4m3_scale(amax);
+    if (lane == 0) qscale[row] = scale;
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+        const int c = lane + 64 * k;
+        uint2 o;
+        o.x = pack4(qv(v[k].v[0], scale), qv(v[k].v[1], scale), qv(v[k].v[2], scale), qv(v[k].v[3], scale));
+        o.y = pack4(qv(v[k].v[4], scale), qv(v[k].v[5], scale), qv(v[k].v[6], scale), qv(v[k].v[7], scale));
+        *reinterpret_cast<uint2*>(q8 + row * ldq + c * 8) = o;
     }
 }
 
@@ -462,7 +498,7 @@ template <bool ADD>
 int fwd_reg_dispatch(int cpl, dim3 grid, hipStream_t stream, const uint16_t* x, int64_t ldx, const uint16_t* r, int64_t ldr,
                      const uint16_t* w, uint16_t* h, int64_t ldh, uint16_t* y, int64_t ldy, float* rstd, int64_t rows,
                      int H, float eps) {
-#define FWD_REG(C) case C: hipLaunchKernelGGL((rmsnorm_fwd_reg_kernel<C, ADD>), grid, dim3(256), 0, stream, x, ldx, r, ldr, w, h, ldh, y, ldy, rstd, rows, H, eps); break;
+#define FWD_REG(C) case C: hipLaunchKernelGGL((rmsnorm_fwd_reg_kernel<C, ADD>), grid, dim3(256), 0, stream, x, ldx, r, ldr, w, h, ldh, y, ldy, rstd, rows, H, eps, nullptr, 0, nullptr); break;
     switch (cpl) {
         FWD_REG(1) FWD_REG(2) FWD_REG(3) FWD_REG(4) FWD_REG(5) FWD_REG(6) FWD_REG(7) FWD_REG(8)
         FWD_REG(9) FWD_REG(10) FWD_REG(11) FWD_REG(12) FWD_REG(13) FWD_REG(14) FWD_REG(15) FWD_REG(16)
@@ -555,6 +591,38 @@ int smt_rmsnorm_fwd(const void* x, int64_t ld_x, const void* weight, void* y, in
     hipLaunchKernelGGL(rmsnorm_fwd_kernel, dim3((unsigned)blocks), dim3(256), 0, stream,
                        (const uint16_t*)x, ld_x, (const uint16_t*)weight, (uint16_t*)y, ld_y, rstd, rows, hidden, eps);
     return check_launch("rmsnorm_fwd_kernel");
+}
+
+int smt_rmsnorm_fwd_quant_e4m3(const void* x, int64_t ld_x, const void* residual, int64_t ld_r, const void* weight,
+                               void* h, int64_t ld_h, void* y, int64_t ld_y, float* rstd, void* out, int64_t ld_out,
+                               float* scales, int64_t rows, int32_t hidden, float eps, hipStream_t stream) {
+    const int cpl = hidden / 512;
+    if (rows < 0 || hidden <= 0 || hidden % 512 || (cpl != 2 && cpl != 4 && cpl != 8 && cpl != 16))
+        return fail(-1, "smt_rmsnorm_fwd_quant_e4m3: hidden %d must be 1024, 2048, 4096 or 8192", hidden);
+    if (rows == 0) return 0;
+    if (!x || !weight || !rstd || !out || !scales || (residual && !h))
+        return fail(-1, "smt_rmsnorm_fwd_quant_e4m3: null pointer");
+    if (!aligned16(x) || (ld_x & 7) || !aligned16(weight) || (residual && (!aligned16(residual) || (ld_r & 7))) ||
+        (h && (!aligned16(h) || (ld_h & 7))) || (y && (!aligned16(y) || (ld_y & 7))) ||
+        (reinterpret_cast<uintptr_t>(out) & 7) || (ld_out & 7) || ld_out < hidden)
+        return fail(-2, "smt_rmsnorm_fwd_quant_e4m3: 16-byte aligned bf16 rows, 8-byte aligned fp8 rows");
+    const dim3 grid((unsigned)((rows + 3) / 4));
+    const uint16_t *px = (const uint16_t*)x, *pr = (const uint16_t*)residual, *pw = (const uint16_t*)weight;
+    uint16_t *ph = (uint16_t*)h, *py = (uint16_t*)y;
+    uint8_t* po = (uint8_t*)out;
+#define FWDQ(C)                                                                                                        \
+    case C:                                                                                                            \
+        if (residual)                                                                                                  \
+            hipLaunchKernelGGL((rmsnorm_fwd_reg_kernel<C, true, true>), grid, dim3(256), 0, stream, px, ld_x, pr, ld_r,  \
+                               pw, ph, ld_h, py, ld_y, rstd, rows, hidden, eps, po, ld_out, scales);                   \
+        else                                                                                                           \
+            hipLaunchKernelGGL((rmsnorm_fwd_reg_kernel<C, false, true>), grid, dim3(256), 0, stream, px, ld_x, nullptr,  \
+                               (int64_t)0, pw, nullptr, (int64_t)0, py, ld_y, rstd, rows, hidden, eps, po, ld_out,      \
+                               scales);                                                                                \
+        break;
+    switch (cpl) { FWDQ(2) FWDQ(4) FWDQ(8) FWDQ(16) }
+#undef FWDQ
+    return check_launch("rmsnorm_fwd_reg_kernel<quant>");
 }
 
 int smt_add_rmsnorm_fwd(const void* x, int64_t ld_x, const void* residual, int64_t ld_r, const void* weight, void* h,

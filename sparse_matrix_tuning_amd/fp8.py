@@ -245,6 +245,37 @@ def swiglu_group(gate: torch.Tensor, up: torch.Tensor):
     return tg[0], tg[2], tu[2]
 
 
+# SMT_FP8_FUSED_NORM=0: the decoder's RMSNorms stop emitting the e4m3 input of their fp8 consumers
+FUSED_NORM_QUANT = os.environ.get("SMT_FP8_FUSED_NORM", "1") != "0"
+
+
+def norm_consumers(*linears):
+    """``(quant, need_bf16)`` for an RMSNorm output read by these linears: quantise it in the norm
+    when every consumer runs in fp8; keep the bf16 output only if some consumer reads it (an SMT
+    module's tile weight gradient, or a trainable weight)."""
+    if not FUSED_NORM_QUANT or any(getattr(m.weight, "_smt_fp8", None) is None for m in linears):
+        return False, True
+    return True, any(not (type(m) is torch.nn.Linear and not m.weight.requires_grad) for m in linears)
+
+
+def rmsnorm_quant(x2: torch.Tensor, r2, w: torch.Tensor, eps: float, need_y: bool):
+    """RMSNorm (of ``x2 + r2`` when ``r2`` is given) that also emits its output as e4m3 rows
+    (``smt_rmsnorm_fwd_quant_e4m3``): returns ``(h or None, y or None, rstd, q, scales)``."""
+    dev = _hip._require_device(x2, w)
+    rows, H = x2.shape
+    h = torch.empty_like(x2) if r2 is not None else None
+    y = torch.empty_like(x2) if need_y else None
+    rstd = torch.empty(rows, dtype=torch.float32, device=dev)
+    q = torch.empty(rows, H, dtype=torch.uint8, device=dev)
+    sq = torch.empty(rows, dtype=torch.float32, device=dev)
+    rc = _hip.load().smt_rmsnorm_fwd_quant_e4m3(
+        x2.data_ptr(), x2.stride(0), None if r2 is None else r2.data_ptr(), 0 if r2 is None else r2.stride(0),
+        w.data_ptr(), None if h is None else h.data_ptr(), H, None if y is None else y.data_ptr(), H,
+        rstd.data_ptr(), q.data_ptr(), q.stride(0), sq.data_ptr(), rows, H, float(eps), _stream(dev))
+    _hip._check(rc, "smt_rmsnorm_fwd_quant_e4m3")
+    return h, y, rstd, q.view(F8), sq
+
+
 def swiglu_fwd_quant(g: torch.Tensor, u: torch.Tensor, need_h: bool):
     """SwiGLU forward fused with the per-row e4m3 quantisation of its output
     (``smt_swiglu_fwd_quant_e4m3``): returns ``(q [T, n], scales [T], h bf16 or None)``."""

@@ -103,8 +103,19 @@ class FusedRMSNormResFn(torch.autograd.Function):
     autograd add."""
 
     @staticmethod
-    def forward(ctx, x, weight, eps):
-        y = FusedRMSNormFn.forward(ctx, x, weight, eps)
+    def forward(ctx, x, weight, eps, quant=False, need_y=True):
+        if not quant:
+            y = FusedRMSNormFn.forward(ctx, x, weight, eps)
+            return y, x.view_as(x)
+        # fp8 consumers (q/k/v): the norm also emits their e4m3 input (fp8.quant_rows_cached finds it)
+        from .fp8 import rmsnorm_quant
+        _need(x, "rmsnorm")
+        x2, w = _rows2d(x), weight.contiguous()
+        _h, y, rstd, q, sq = rmsnorm_quant(x2, None, w, eps, need_y)
+        ctx.save_for_backward(x2, w, rstd)
+        ctx.shape = x.shape
+        y = y.view(x.shape) if y is not None else x.new_zeros(()).expand(x.shape)
+        y._smt_q8 = (y._version, q, sq)
         return y, x.view_as(x)
 
     @staticmethod
@@ -113,7 +124,7 @@ class FusedRMSNormResFn(torch.autograd.Function):
         if dres is None or ctx.needs_input_grad[1] or x2.shape[1] % 512 or x2.shape[1] > 8192:
             dx, dw = _rmsnorm_bwd(x2, w, rstd, dy, ctx.needs_input_grad[1])
             dx = dx.view(ctx.shape)
-            return (dx if dres is None else dx + dres), dw, None
+            return (dx if dres is None else dx + dres), dw, None, None, None
         rows, H = x2.shape
         dy2, dr2 = _rows2d(dy), _rows2d(dres)
         dx = torch.empty_like(x2)
@@ -121,7 +132,7 @@ class FusedRMSNormResFn(torch.autograd.Function):
                                              rstd.data_ptr(), dr2.data_ptr(), dr2.stride(0), dx.data_ptr(), H, rows, H,
                                              _stream(x2))
         _hip._check(rc, "smt_rmsnorm_bwd_add")
-        return dx.view(ctx.shape), None, None
+        return dx.view(ctx.shape), None, None, None, None
 
 
 class FusedAddRMSNormFn(torch.autograd.Function):
@@ -130,11 +141,21 @@ class FusedAddRMSNormFn(torch.autograd.Function):
     the residual path inside the norm's backward. Returns ``(h, y)``."""
 
     @staticmethod
-    def forward(ctx, x, residual, weight, eps):
+    def forward(ctx, x, residual, weight, eps, quant=False, need_y=True):
         for t, n in ((x, "x"), (residual, "residual"), (weight, "weight")):
             _need(t, "add+rmsnorm " + n)
         x2, r2 = _rows2d(x), _rows2d(residual)
         rows, H = x2.shape
+        if quant:
+            # fp8 consumers (gate/up): the norm also emits their e4m3 input
+            from .fp8 import rmsnorm_quant
+            w = weight.contiguous()
+            h, y, rstd, q, sq = rmsnorm_quant(x2, r2, w, eps, need_y)
+            ctx.save_for_backward(h, w, rstd)
+            ctx.shape = x.shape
+            y = y.view(x.shape) if y is not None else x.new_zeros(()).expand(x.shape)
+            y._smt_q8 = (y._version, q, sq)
+            return h.view(x.shape), y
         h = torch.empty((rows, H), dtype=x.dtype, device=x.device)
         y = torch.empty((rows, H), dtype=x.dtype, device=x.device)
         rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
@@ -177,7 +198,7 @@ class FusedAddRMSNormFn(torch.autograd.Function):
                                          dh2.data_ptr(), dh2.stride(0), dx.data_ptr(), H, rows, H, _stream(h))
             _hip._check(rc, "smt_rmsnorm_bwd_add")
             dx = dx.view(ctx.shape)
-        return dx, dx, dw, None
+        return dx, dx, dw, None, None, None
 
 
 _RESIDUAL_NORM = os.environ.get("SMT_FUSED_RESIDUAL_NORM", "1") != "0"
@@ -189,8 +210,16 @@ def fused_decoder_layer_forward(self, hidden_states, attention_mask=None, positi
     post-attention RMSNorm (:class:`FusedAddRMSNormFn`) and the input norm's two gradients summed in
     its backward (:class:`FusedRMSNormResFn`); the same ops in the same order otherwise."""
     norm1 = self.input_layernorm
+    attn, mlp = self.self_attn, self.mlp
+    H = hidden_states.shape[-1]
+    q1 = q2 = (False, True)
+    if H in (1024, 2048, 4096, 8192) and all(hasattr(attn, n) for n in ("q_proj", "k_proj", "v_proj")):
+        from .fp8 import norm_consumers
+        q1 = norm_consumers(attn.q_proj, attn.k_proj, attn.v_proj)
+        if hasattr(mlp, "gate_proj") and hasattr(mlp, "up_proj"):
+            q2 = norm_consumers(mlp.gate_proj, mlp.up_proj)
     if _RESIDUAL_NORM:
-        hidden_states, residual = FusedRMSNormResFn.apply(hidden_states, norm1.weight, norm1.variance_epsilon)
+        hidden_states, residual = FusedRMSNormResFn.apply(hidden_states, norm1.weight, norm1.variance_epsilon, *q1)
     else:
         residual = hidden_states
         hidden_states = norm1(hidden_states)
@@ -198,7 +227,7 @@ def fused_decoder_layer_forward(self, hidden_states, attention_mask=None, positi
                                       position_ids=position_ids, past_key_values=past_key_values, use_cache=use_cache,
                                       position_embeddings=position_embeddings, **kwargs)
     norm = self.post_attention_layernorm
-    residual, hidden_states = FusedAddRMSNormFn.apply(hidden_states, residual, norm.weight, norm.variance_epsilon)
+    residual, hidden_states = FusedAddRMSNormFn.apply(hidden_states, residual, norm.weight, norm.variance_epsilon, *q2)
     hidden_states = self.mlp(hidden_states)
     return residual + hidden_states
 

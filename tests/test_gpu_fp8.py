@@ -276,3 +276,68 @@ def test_fused_swiglu_into_fp8_down_proj_bit_identical():
         outs.append((y.detach(), g.grad, u.grad))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("H,residual,need_y", [(4096, False, True), (4096, True, False), (1024, True, True)])
+def test_rmsnorm_quant_matches_rmsnorm_then_quant(H, residual, need_y):
+    torch.manual_seed(H)
+    rows = 300
+    x = (torch.randn(rows, H, device=DEV) * 2).bfloat16()
+    r = torch.randn(rows, H, device=DEV).bfloat16() if residual else None
+    w = (1 + 0.1 * torch.randn(H, device=DEV)).bfloat16()
+    st = torch.cuda.current_stream().cuda_stream
+    y_ref = torch.empty_like(x)
+    rstd_ref = torch.empty(rows, device=DEV)
+    lib = _hip.load()
+    if residual:
+        h_ref = torch.empty_like(x)
+        assert lib.smt_add_rmsnorm_fwd(x.data_ptr(), H, r.data_ptr(), H, w.data_ptr(), h_ref.data_ptr(), H,
+                                       y_ref.data_ptr(), H, rstd_ref.data_ptr(), rows, H, 1e-5, st) == 0
+    else:
+        assert lib.smt_rmsnorm_fwd(x.data_ptr(), H, w.data_ptr(), y_ref.data_ptr(), H, rstd_ref.data_ptr(), rows, H,
+                                   1e-5, st) == 0
+    q_ref, s_ref = f8.quant_rows(y_ref)
+    h, y, rstd, q, s = f8.rmsnorm_quant(x, r, w, 1e-5, need_y)
+    assert torch.equal(rstd, rstd_ref)
+    assert torch.equal(s, s_ref) and torch.equal(q.view(torch.uint8), q_ref.view(torch.uint8))
+    if need_y:
+        assert torch.equal(y, y_ref)
+    else:
+        assert y is None
+    if residual:
+        assert torch.equal(h, h_ref)
+
+
+def test_decoder_with_norm_quant_matches_unfused():
+    """A patched 2-layer LLaMA (hidden 1024) on the fp8 path: the RMSNorms emitting their consumers'
+    e4m3 input change nothing beyond GEMM run-to-run noise (the kernels themselves are bit-exact, above)."""
+    import bench
+    from sparse_matrix_tuning_amd.engine import attach_fp8_weights
+    from sparse_matrix_tuning_amd.fused_llama import patch_llama
+    cfg = dict(bench.MODELS["mini"], hidden_size=1024, intermediate_size=2048, num_attention_heads=8,
+               num_key_value_heads=2, num_hidden_layers=2)
+    bench.MODELS["_n"] = cfg
+    try:
+        model = bench.build_model("_n", DEV)
+    finally:
+        del bench.MODELS["_n"]
+    patch_llama(model)
+    for p in model.parameters():
+        p.requires_grad_(False)
+    model.model.embed_tokens.weight.requires_grad_(True)
+    assert attach_fp8_weights(model) > 0
+    ids = torch.randint(0, 4096, (2, 256), generator=torch.Generator().manual_seed(3)).to(DEV)
+    out = []
+    for fused in (True, False):
+        old = f8.FUSED_NORM_QUANT
+        f8.FUSED_NORM_QUANT = fused
+        try:
+            model.model.embed_tokens.weight.grad = None
+            loss = model(input_ids=ids, labels=ids, use_cache=False).loss
+            loss.backward()
+            out.append((loss.item(), model.model.embed_tokens.weight.grad.clone()))
+        finally:
+            f8.FUSED_NORM_QUANT = old
+    (l1, g1), (l2, g2) = out
+    assert abs(l1 - l2) <= 1e-4 * abs(l2), (l1, l2)
+    assert _rel(g1, g2) < 1e-3
