@@ -69,6 +69,15 @@ int smt_rmsnorm_fwd_quant_e4m3(const void* x, int64_t ld_x, const void* residual
                                void* h, int64_t ld_h, void* y, int64_t ld_y, float* rstd, void* out, int64_t ld_out,
                                float* scales, int64_t rows, int32_t hidden, float eps, hipStream_t stream);
 
+/* smt_rmsnorm_bwd_add (RMSNorm backward plus the residual gradient, dx = bf16(bf16(dx_norm) + dres))
+ * that also writes dx as one e4m3 row per token (out[rows, hidden] + scales[rows]) for the fp8
+ * linear consuming that gradient (o_proj, down_proj), bit-identical to smt_quant_rows_e4m3 of dx.
+ * hidden in {1024, 2048, 4096, 8192}. (Defined in llama_kernels.hip.) */
+int smt_rmsnorm_bwd_add_quant_e4m3(const void* dy, int64_t ld_dy, const void* x, int64_t ld_x, const void* weight,
+                                   const float* rstd, const void* dres, int64_t ld_dres, void* dx, int64_t ld_dx,
+                                   void* out, int64_t ld_out, float* scales, int64_t rows, int32_t hidden,
+                                   hipStream_t stream);
+
 /* SwiGLU forward (smt_swiglu_fwd's formula and roundings) fused with the per-row quantisation of
  * its output: out[rows, cols] e4m3 + scales[rows], bit-identical to smt_swiglu_fwd followed by
  * smt_quant_rows_e4m3; the bf16 output is written to h_out only when it is non-NULL.

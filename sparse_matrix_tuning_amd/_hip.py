@@ -38,6 +38,7 @@ ABI_FUNCTIONS = (
     "smt_attn_last_error", "smt_attn_fwd", "smt_attn_bwd",
     "smt_fp8_last_error", "smt_quant_rows_e4m3", "smt_quant_cols_t_e4m3", "smt_quant_rows_cat_e4m3",
     "smt_swiglu_fwd_quant_e4m3", "smt_swiglu_bwd_quant_e4m3", "smt_rmsnorm_fwd_quant_e4m3",
+    "smt_rmsnorm_bwd_add_quant_e4m3",
 )
 
 
@@ -131,6 +132,8 @@ _SIGS = {
     "smt_quant_rows_cat_e4m3": (ctypes.c_int, [ctypes.POINTER(QuantSrc), _I32, _I64, _P, _I64, _P, _P]),
     "smt_rmsnorm_fwd_quant_e4m3": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _P, _I64, _P, _I64, _P, _P, _I64, _P,
                                                    _I64, _I32, ctypes.c_float, _P]),
+    "smt_rmsnorm_bwd_add_quant_e4m3": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _P, _P, _I64, _P, _I64, _P, _I64, _P,
+                                                       _I64, _I32, _P]),
     "smt_swiglu_fwd_quant_e4m3": (ctypes.c_int, [_P, _P, _I64, _I32, _P, _I64, _P, _P, _P]),
     "smt_swiglu_bwd_quant_e4m3": (ctypes.c_int, [_P, _P, _P, _I64, _I32, _P, _I64, _P, _P, _P, _P]),
 }

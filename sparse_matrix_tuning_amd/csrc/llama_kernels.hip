@@ -244,12 +244,13 @@ void rmsnorm_fwd_reg_kernel(const uint16_t* __restrict__ x, int64_t ldx, const u
 
 // Backward without weight grad; with ADD the gradient reaching the norm's input by the residual path
 // is added as autograd would: dx = bf16(bf16(dx_norm) + dres).
-template <int CPL, bool ADD>
+template <int CPL, bool ADD, bool QUANT = false>
 __global__ __launch_bounds__(256)
 void rmsnorm_bwd_reg_kernel(const uint16_t* __restrict__ dy, int64_t lddy, const uint16_t* __restrict__ x, int64_t ldx,
                             const uint16_t* __restrict__ w, const float* __restrict__ rstd,
                             const uint16_t* __restrict__ dres, int64_t lddr, uint16_t* __restrict__ dx, int64_t lddx,
-                            int64_t rows, int H) {
+                            int64_t rows, int H, uint8_t* __restrict__ q8 = nullptr, int64_t ldq = 0,
+                            float* __restrict__ qscale = nullptr) {
     const int lane = threadIdx.x & 63;
     const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= rows) return;
@@ -281,6 +282,30 @@ void rmsnorm_bwd_reg_kernel(const uint16_t* __restrict__ dy, int64_t lddy, const
             for (int j = 0; j < 8; ++j) o.v[j] = rbf(o.v[j]) + dr.v[j];
         }
         st8(dx + row * lddx + c * 8, o);
+        if (QUANT) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) gw[k].v[j] = rbf(o.v[j]);     // the stored bf16 dx, kept for the e4m3 pass
+        }
+    }
+    if (QUANT) {
+        // dx also as one e4m3 row + scale (the data-gradient GEMM operand of the fp8 linear that
+        // consumes this gradient), exactly as smt_quant_rows_e4m3 would quantise the stored dx
+        float amax = 0.f;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(gw[k].v[j]));
+        amax = wave_max_f(amax);
+        const float scale = e4m3_scale(amax);
+        if (lane == 0) qscale[row] = scale;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            const int c = lane + 64 * k;
+            uint2 q;
+            q.x = pack4(qv(gw[k].v[0], scale), qv(gw[k].v[1], scale), qv(gw[k].v[2], scale), qv(gw[k].v[3], scale));
+            q.y = pack4(qv(gw[k].v[4], scale), qv(gw[k].v[5], scale), qv(gw[k].v[6], scale), qv(gw[k].v[7], scale));
+            *reinterpret_cast<uint2*>(q8 + row * ldq + c * 8) = q;
+        }
     }
 }
 
@@ -649,6 +674,35 @@ int smt_rmsnorm_bwd_add(const void* dy, int64_t ld_dy, const void* x, int64_t ld
         (ld_x & 7) || (ld_dres & 7) || (ld_dx & 7))
         return fail(-2, "smt_rmsnorm_bwd_add: 16-byte aligned rows required");
     return launch_bwd_reg(true, dy, ld_dy, x, ld_x, weight, rstd, dres, ld_dres, dx, ld_dx, rows, hidden, stream);
+}
+
+int smt_rmsnorm_bwd_add_quant_e4m3(const void* dy, int64_t ld_dy, const void* x, int64_t ld_x, const void* weight,
+                                   const float* rstd, const void* dres, int64_t ld_dres, void* dx, int64_t ld_dx,
+                                   void* out, int64_t ld_out, float* scales, int64_t rows, int32_t hidden,
+                                   hipStream_t stream) {
+    const int cpl = hidden / 512;
+    if (rows < 0 || hidden <= 0 || hidden % 512 || (cpl != 2 && cpl != 4 && cpl != 8 && cpl != 16))
+        return fail(-1, "smt_rmsnorm_bwd_add_quant_e4m3: hidden %d must be 1024, 2048, 4096 or 8192", hidden);
+    if (rows == 0) return 0;
+    if (!dy || !x || !weight || !rstd || !dres || !dx || !out || !scales)
+        return fail(-1, "smt_rmsnorm_bwd_add_quant_e4m3: null pointer");
+    if (!aligned16(dy) || !aligned16(x) || !aligned16(weight) || !aligned16(dres) || !aligned16(dx) || (ld_dy & 7) ||
+        (ld_x & 7) || (ld_dres & 7) || (ld_dx & 7) || (reinterpret_cast<uintptr_t>(out) & 7) || (ld_out & 7) ||
+        ld_out < hidden)
+        return fail(-2, "smt_rmsnorm_bwd_add_quant_e4m3: 16-byte aligned bf16 rows, 8-byte aligned fp8 rows");
+    const dim3 grid((unsigned)((rows + 3) / 4));
+    const uint16_t *pdy = (const uint16_t*)dy, *px = (const uint16_t*)x, *pw = (const uint16_t*)weight,
+                   *pr = (const uint16_t*)dres;
+    uint16_t* pdx = (uint16_t*)dx;
+    uint8_t* po = (uint8_t*)out;
+#define BWDQ(C)                                                                                                       \
+    case C:                                                                                                           \
+        hipLaunchKernelGGL((rmsnorm_bwd_reg_kernel<C, true, true>), grid, dim3(256), 0, stream, pdy, ld_dy, px, ld_x, \
+                           pw, rstd, pr, ld_dres, pdx, ld_dx, rows, hidden, po, ld_out, scales);                      \
+        break;
+    switch (cpl) { BWDQ(2) BWDQ(4) BWDQ(8) BWDQ(16) }
+#undef BWDQ
+    return check_launch("rmsnorm_bwd_reg_kernel<quant>");
 }
 
 int smt_rmsnorm_bwd_waves(int64_t rows) {

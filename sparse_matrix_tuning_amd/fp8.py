@@ -197,7 +197,8 @@ def fp8_linear_forward(x: torch.Tensor, fw: Fp8Weight) -> torch.Tensor:
 
 def fp8_linear_dgrad(grad_output: torch.Tensor, fw: Fp8Weight) -> torch.Tensor:
     shape = grad_output.shape
-    gi = fp8_matmul(grad_output.reshape(-1, shape[-1]), fw.wt8, fw.swt_row)
+    # cached: the RMSNorm backward that produced a residual-stream gradient may have quantised it
+    gi = fp8_matmul(None, fw.wt8, fw.swt_row, a_q=quant_rows_cached(grad_output))
     return gi.view(*shape[:-1], gi.shape[-1])
 
 
@@ -274,6 +275,20 @@ def rmsnorm_quant(x2: torch.Tensor, r2, w: torch.Tensor, eps: float, need_y: boo
         rstd.data_ptr(), q.data_ptr(), q.stride(0), sq.data_ptr(), rows, H, float(eps), _stream(dev))
     _hip._check(rc, "smt_rmsnorm_fwd_quant_e4m3")
     return h, y, rstd, q.view(F8), sq
+
+
+def rmsnorm_bwd_add_quant(dy2, x2, w, rstd, dr2):
+    """``smt_rmsnorm_bwd_add`` that also emits dx as e4m3 rows: returns ``(dx, q, scales)``."""
+    dev = _hip._require_device(dy2, x2, w, rstd, dr2)
+    rows, H = x2.shape
+    dx = torch.empty_like(x2)
+    q = torch.empty(rows, H, dtype=torch.uint8, device=dev)
+    sq = torch.empty(rows, dtype=torch.float32, device=dev)
+    rc = _hip.load().smt_rmsnorm_bwd_add_quant_e4m3(
+        dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0), w.data_ptr(), rstd.data_ptr(), dr2.data_ptr(),
+        dr2.stride(0), dx.data_ptr(), dx.stride(0), q.data_ptr(), q.stride(0), sq.data_ptr(), rows, H, _stream(dev))
+    _hip._check(rc, "smt_rmsnorm_bwd_add_quant_e4m3")
+    return dx, q.view(F8), sq
 
 
 def swiglu_fwd_quant(g: torch.Tensor, u: torch.Tensor, need_h: bool):

@@ -114,6 +114,7 @@ class FusedRMSNormResFn(torch.autograd.Function):
         _h, y, rstd, q, sq = rmsnorm_quant(x2, None, w, eps, need_y)
         ctx.save_for_backward(x2, w, rstd)
         ctx.shape = x.shape
+        ctx.quant_grad = True             # fp8 model: the input gradient feeds the previous down_proj
         y = y.view(x.shape) if y is not None else x.new_zeros(()).expand(x.shape)
         y._smt_q8 = (y._version, q, sq)
         return y, x.view_as(x)
@@ -127,6 +128,12 @@ class FusedRMSNormResFn(torch.autograd.Function):
             return (dx if dres is None else dx + dres), dw, None, None, None
         rows, H = x2.shape
         dy2, dr2 = _rows2d(dy), _rows2d(dres)
+        if getattr(ctx, "quant_grad", False):
+            from .fp8 import rmsnorm_bwd_add_quant
+            dx, q, sq = rmsnorm_bwd_add_quant(dy2, x2, w, rstd, dr2)
+            dx = dx.view(ctx.shape)
+            dx._smt_q8 = (dx._version, q, sq)
+            return dx, None, None, None, None
         dx = torch.empty_like(x2)
         rc = _hip.load().smt_rmsnorm_bwd_add(dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0), w.data_ptr(),
                                              rstd.data_ptr(), dr2.data_ptr(), dr2.stride(0), dx.data_ptr(), H, rows, H,
@@ -153,6 +160,7 @@ class FusedAddRMSNormFn(torch.autograd.Function):
             h, y, rstd, q, sq = rmsnorm_quant(x2, r2, w, eps, need_y)
             ctx.save_for_backward(h, w, rstd)
             ctx.shape = x.shape
+            ctx.quant_grad = True         # fp8 model: the gradient of h feeds o_proj
             y = y.view(x.shape) if y is not None else x.new_zeros(()).expand(x.shape)
             y._smt_q8 = (y._version, q, sq)
             return h.view(x.shape), y
@@ -191,6 +199,11 @@ class FusedAddRMSNormFn(torch.autograd.Function):
             dx = dx.view(ctx.shape)
             if dh is not None:
                 dx = dx + dh
+        elif getattr(ctx, "quant_grad", False):
+            from .fp8 import rmsnorm_bwd_add_quant
+            dx, q, sq = rmsnorm_bwd_add_quant(_rows2d(dy), h, w, rstd, _rows2d(dh))
+            dx = dx.view(ctx.shape)
+            dx._smt_q8 = (dx._version, q, sq)
         else:
             dy2, dh2 = _rows2d(dy), _rows2d(dh)
             dx = torch.empty_like(h)

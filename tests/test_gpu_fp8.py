@@ -341,3 +341,22 @@ def test_decoder_with_norm_quant_matches_unfused():
     (l1, g1), (l2, g2) = out
     assert abs(l1 - l2) <= 1e-4 * abs(l2), (l1, l2)
     assert _rel(g1, g2) < 1e-3
+
+
+@pytest.mark.parametrize("H", [4096, 1024])
+def test_rmsnorm_bwd_add_quant_matches_bwd_then_quant(H):
+    torch.manual_seed(H + 1)
+    rows = 260
+    x = (torch.randn(rows, H, device=DEV) * 2).bfloat16()
+    w = (1 + 0.1 * torch.randn(H, device=DEV)).bfloat16()
+    dy = torch.randn(rows, H, device=DEV).bfloat16()
+    dres = torch.randn(rows, H, device=DEV).bfloat16()
+    rstd = (torch.rand(rows, device=DEV) + 0.5)
+    dx_ref = torch.empty_like(x)
+    assert _hip.load().smt_rmsnorm_bwd_add(dy.data_ptr(), H, x.data_ptr(), H, w.data_ptr(), rstd.data_ptr(),
+                                           dres.data_ptr(), H, dx_ref.data_ptr(), H, rows, H,
+                                           torch.cuda.current_stream().cuda_stream) == 0
+    q_ref, s_ref = f8.quant_rows(dx_ref)
+    dx, q, s = f8.rmsnorm_bwd_add_quant(dy, x, w, rstd, dres)
+    assert torch.equal(dx, dx_ref)
+    assert torch.equal(s, s_ref) and torch.equal(q.view(torch.uint8), q_ref.view(torch.uint8))
