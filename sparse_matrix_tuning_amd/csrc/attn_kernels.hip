@@ -395,12 +395,18 @@ void attn_delta_kernel(Tns o, Tns dout, float* __restrict__ delta, int Hq, int S
 // diagonal (staged as in the forward). Per tile: S^T = K Q^T, dP^T = V dO^T, P = exp2(S*c - lse),
 // dS = P (dP - delta), dQ^T += K^T dS^T.
 // ------------------------------------------------------------------------------------------------
+// SMT_DQ_DELTA: the dQ kernel computes delta = rowsum(dO * O) of its own rows from the dO fragments
+// it holds anyway (one O read) and writes it for the dK/dV kernel, instead of a separate pass
+#ifndef SMT_DQ_DELTA
+#define SMT_DQ_DELTA 1
+#endif
+
 struct DqArgs {
-    Tns q, k, v, dout;
+    Tns q, k, v, dout, o;
     uint16_t* dq;
     int64_t dq_sb, dq_sh, dq_ss;
     const float* lse;
-    const float* delta;
+    float* delta;
     int B, Hq, Hkv, S;
     float sl2, scale;
 };
@@ -430,7 +436,27 @@ __device__ __forceinline__ void dq_block(const DqArgs& a, uint8_t* lds, int b, i
     }
     const int64_t srow = ((int64_t)b * a.Hq + h) * a.S + (qvalid ? qrow : 0);
     const float lse = qvalid ? a.lse[srow] : 0.f;
-    const float dlt = qvalid ? a.delta[srow] : 0.f;
+    float dlt;
+    if (SMT_DQ_DELTA) {
+        // delta of this row: the lane pair (l, l^32) holds all 128 d of dO; O read at the same places
+        const uint16_t* op = a.o.p + b * a.o.sb + h * a.o.sh;
+        float part = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+            const u32x4_t ov = qvalid ? *reinterpret_cast<const u32x4_t*>(op + qrow * a.o.ss + 16 * ks + 8 * hi)
+                                      : u32x4_t{0u, 0u, 0u, 0u};
+            const u32x4_t dv = __builtin_bit_cast(u32x4_t, df[ks]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                part += __uint_as_float(ov[j] << 16) * __uint_as_float(dv[j] << 16);
+                part += __uint_as_float(ov[j] & 0xffff0000u) * __uint_as_float(dv[j] & 0xffff0000u);
+            }
+        }
+        dlt = halves_sum(part);
+        if (qvalid && hi == 0) a.delta[srow] = dlt;
+    } else {
+        dlt = qvalid ? a.delta[srow] : 0.f;
+    }
 
     const int kv_end = min(a.S, q0 + kFwdQB);
     const int nt = (kv_end + kKV - 1) / kKV;
@@ -768,13 +794,15 @@ int smt_attn_bwd(const smt_attn_tensor* q, const smt_attn_tensor* k, const smt_a
     const int B = shape->B, Hq = shape->Hq, Hkv = shape->Hkv, S = shape->S;
     const float sl2 = shape->scale * 1.4426950408889634f;
 
-    const int64_t rows = (int64_t)B * Hq * S;
-    hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((rows * 16 + 255) / 256)), dim3(256), 0, stream,
-                       tns(o), tns(d_o), delta_ws, Hq, S, rows);
-    if ((rc = check_launch("attn_delta_kernel"))) return rc;
+    if (!SMT_DQ_DELTA) {
+        const int64_t rows = (int64_t)B * Hq * S;
+        hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((rows * 16 + 255) / 256)), dim3(256), 0, stream,
+                           tns(o), tns(d_o), delta_ws, Hq, S, rows);
+        if ((rc = check_launch("attn_delta_kernel"))) return rc;
+    }
 
     DqArgs qa;
-    qa.q = tns(q); qa.k = tns(k); qa.v = tns(v); qa.dout = tns(d_o);
+    qa.q = tns(q); qa.k = tns(k); qa.v = tns(v); qa.dout = tns(d_o); qa.o = tns(o);
     qa.dq = static_cast<uint16_t*>(dq->ptr); qa.dq_sb = dq->sb; qa.dq_sh = dq->sh; qa.dq_ss = dq->ss;
     qa.lse = lse; qa.delta = delta_ws;
     qa.B = B; qa.Hq = Hq; qa.Hkv = Hkv; qa.S = S; qa.sl2 = sl2; qa.scale = shape->scale;
