@@ -151,6 +151,11 @@ __device__ __forceinline__ void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)
 // INSIDE the loop, which also waits for the next tile's LDS-DMA issued just before it (the prefetch
 // then never overlaps compute). gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15.
 __device__ __forceinline__ void vm_wait_all_known() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+// SMT_ATTN_FASTSM: forward softmax with the scale folded into the exponent's FMA and the O / l
+// rescale skipped when no row's running max changed in the tile (exact: alpha = 1 then)
+#ifndef SMT_ATTN_FASTSM
+#define SMT_ATTN_FASTSM 1
+#endif
 #ifndef SMT_ATTN_KNOWN_WAIT
 #define SMT_ATTN_KNOWN_WAIT 1
 #endif
@@ -287,11 +292,21 @@ __device__ __forceinline__ void fwd_block(const FwdArgs& a, uint8_t* lds, int b,
             for (int ks = 0; ks < 8; ++ks)
 #pragma unroll
                 for (int j = 0; j < kFS; ++j) sc[j] = mfma(row_frag(K, 32 * j + l32, 32 * ks + 16 * hi), qf[ks], sc[j]);
+#if SMT_ATTN_FASTSM
+            // raw scores; the log2-domain scale is folded into the exponent's FMA, and the row max is
+            // taken on the raw scores (scale > 0: max commutes with the monotone rounding of s * c)
+            float x[16 * kFS];
+#pragma unroll
+            for (int j = 0; j < kFS; ++j)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) x[16 * j + i] = sc[j][i];
+#else
             float x[16 * kFS];
 #pragma unroll
             for (int j = 0; j < kFS; ++j)
 #pragma unroll
                 for (int i = 0; i < 16; ++i) x[16 * j + i] = sc[j][i] * a.sl2;
+#endif
             if (k0 + kFKV - 1 > qw) {                              // tile crosses this wave's diagonal
 #pragma unroll
                 for (int i = 0; i < 16 * kFS; ++i) {
@@ -302,21 +317,33 @@ __device__ __forceinline__ void fwd_block(const FwdArgs& a, uint8_t* lds, int b,
             float mloc = x[0];
 #pragma unroll
             for (int i = 1; i < 16 * kFS; ++i) mloc = fmaxf(mloc, x[i]);
+#if SMT_ATTN_FASTSM
+            const float m_new = fmaxf(m_run, other_half_max(mloc) * a.sl2);
+#else
             const float m_new = fmaxf(m_run, other_half_max(mloc));
-            const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+#endif
             float p[16 * kFS];
             float sum = 0.f;
 #pragma unroll
             for (int i = 0; i < 16 * kFS; ++i) {
+#if SMT_ATTN_FASTSM
+                p[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(x[i], a.sl2, -m_new));
+#else
                 p[i] = __builtin_amdgcn_exp2f(x[i] - m_new);
+#endif
                 sum += p[i];
             }
-            l_run = l_run * alpha + sum;
+            // rescale only when some row's max grew (alpha = 1 exactly otherwise: skipping is exact)
+            if (!SMT_ATTN_FASTSM || __builtin_amdgcn_ballot_w64(m_new != m_run) != 0) {   // wave-uniform
+                const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+                l_run *= alpha;
+#pragma unroll
+                for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+            }
+            l_run += sum;
             m_run = m_new;
-#pragma unroll
-            for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
             bf16x8_t pf[2 * kFS];
 #pragma unroll
             for (int j = 0; j < kFS; ++j)
@@ -503,7 +530,7 @@ __device__ __forceinline__ void dq_block(const DqArgs& a, uint8_t* lds, int b, i
 #pragma unroll
             for (int i = 0; i < 32; ++i) {
                 const int j = i >> 4, ii = i & 15;
-                float pv = __builtin_amdgcn_exp2f(s[j][ii] * a.sl2 - lse);
+                float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(s[j][ii], a.sl2, -lse));
                 if (diag) {
                     const int key = k0 + 32 * j + (ii & 3) + 8 * (ii >> 2) + 4 * hi;
                     if (key > qrow) pv = 0.f;
