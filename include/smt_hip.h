@@ -18,6 +18,7 @@
  *                         for its backward (packed copy of the distinct 256-column blocks)
  *   smt_grad_accumulate   deepspeed/fine_tune.py:724-741, 751-764   warm-up fp32 grad harvest
  *   smt_block_score       deepspeed/smt/smt_helper.py:67-78, 233-251   per-256x256-block scores
+ *                         (fp64 sum + magnitude sum: the host bounds ATen's fp32 value with them)
  *   smt_sq_norm           DeepSpeed bf16/ZeRO global grad-norm for gradient_clipping=1.0
  *                         (deepspeed/helpers/deepspeed_helpers.py:87; DeepSpeed 0.16.5, external)
  *   smt_adamw_step        DeepSpeed FusedAdam(adam_w_mode=True) step over the tiles
@@ -27,9 +28,10 @@
  *   smt_row_gather        deepspeed/smt/smt.py:200-204   selected_weight[i, :] = W[index_list[i], :]
  *   smt_row_scatter       deepspeed/smt/smt.py:211-213   per-forward write-back rows -> W
  *   smt_column_gather     deepspeed/smt/smt.py:225-233   partial_input[:, :, i] = input[:, :, index_list[i]]
- *   smt_act_accumulate    deepspeed/fine_tune.py:636-667 (cache_input_hook: |x| summed over steps)
- *                         + deepspeed/smt/smt_helper.py:170 (sum over the batch dimension)
- *   smt_channel_score     deepspeed/smt/smt_helper.py:171-184   per-channel statistic over the sequence
+ *   smt_act_accumulate    deepspeed/fine_tune.py:636-667 (cache_input_hook: the fp32 [B, S, in]
+ *                         accumulator `feat[key] (+)= |x|` over steps)
+ *   smt_channel_score     deepspeed/smt/smt_helper.py:167-184   per-channel statistic (batch sum of
+ *                         smt_helper.py:170, then the sequence reduction) in fp64
  */
 #ifndef SMT_HIP_H
 #define SMT_HIP_H
@@ -56,11 +58,11 @@ extern "C" {
 #define SMT_DTYPE_FP32 1
 #define SMT_DTYPE_FP16 2
 
-/* block-score strategies, smt_helper.py:71-78 */
-#define SMT_SCORE_MEAN_ABS 0        /* mean(dim=(1,3)).abs()  -> raw sum of g      */
-#define SMT_SCORE_ABS_MEAN 1        /* abs().mean(dim=(1,3))  -> raw sum of |g|    */
-#define SMT_SCORE_L1 2              /* abs().sum(dim=(1,3))   -> raw sum of |g|    */
-#define SMT_SCORE_L2 3              /* sqrt(sum(abs()**2))    -> raw sum of g*g    */
+/* block-score strategies, smt_helper.py:71-78 (term = what the reference's fp32 reduction adds) */
+#define SMT_SCORE_MEAN_ABS 0        /* mean(dim=(1,3)).abs()  -> term g                   */
+#define SMT_SCORE_ABS_MEAN 1        /* abs().mean(dim=(1,3))  -> term |g|                 */
+#define SMT_SCORE_L1 2              /* abs().sum(dim=(1,3))   -> term |g|                 */
+#define SMT_SCORE_L2 3              /* sqrt(sum(abs()**2))    -> term fp32(g*g)           */
 
 /* AdamW update formulas */
 #define SMT_ADAM_DEEPSPEED 0        /* DeepSpeed FusedAdam ADAM_MODE_1 (decoupled decay inside update) */
@@ -91,7 +93,7 @@ typedef struct smt_score_entry {
     int64_t ld;
     int32_t d1, d2;                 /* block grid, smt_helper.py:57-58            */
     int64_t block_begin;            /* exclusive prefix of d1*d2                  */
-    double* out;                    /* d1*d2 raw fp64 block sums, row-major       */
+    double* out;                    /* d1*d2 pairs {sum of terms, sum of |terms|}, row-major (ABI v4) */
     int32_t strategy;               /* SMT_SCORE_*                                */
     int32_t pad_;
 } smt_score_entry;
@@ -154,7 +156,10 @@ int smt_tile_scatter(void* weight, int64_t ld_weight, int32_t elem_bytes,
 int smt_grad_accumulate(const smt_accum_entry* entries_dev, int32_t n_entries,
                         int64_t total_chunks, hipStream_t stream);
 
-/* Multi-tensor block scoring; one fp64 raw sum per 256x256 block. */
+/*
+ * Multi-tensor block scoring. Per 256x256 block, out[2k] = fp64 sum of the strategy's terms and
+ * out[2k+1] = fp64 sum of their magnitudes (equal unless MEAN_ABS). Deterministic order.
+ */
 int smt_block_score(const smt_score_entry* entries_dev, int32_t n_entries,
                     int64_t total_blocks, hipStream_t stream);
 
@@ -191,19 +196,20 @@ int smt_column_gather(const void* x, int64_t ld_x, int64_t T, const int32_t* col
                       void* out, int64_t ld_out, hipStream_t stream);
 
 /*
- * acc[s, c] = (assign ? 0 : acc[s, c]) + sum_{b<B} |x[b, s, c]|, in fp64 with b ascending.
- * x: element (b, s, c) at x + b*batch_stride + s*ld_x + c (dtype x_dtype); acc: fp64 [S, n_cols]
- * row-major; n_cols % 8 == 0.
+ * acc[b, s, c] = (assign ? 0 : acc[b, s, c]) + float(|x[b, s, c]|), one fp32 add per element (the
+ * reference's CPU `+=`, bit for bit). x: element (b, s, c) at x + b*batch_stride + s*ld_x + c (dtype
+ * x_dtype); acc: contiguous fp32 [B, S, n_cols]; n_cols % 8 == 0. (ABI v4: was an fp64 [S, n_cols]
+ * batch sum.)
  */
 int smt_act_accumulate(const void* x, int32_t x_dtype, int64_t ld_x, int64_t batch_stride, int32_t B, int32_t S,
-                       int32_t n_cols, double* acc, int32_t assign, hipStream_t stream);
+                       int32_t n_cols, float* acc, int32_t assign, hipStream_t stream);
 
 /*
- * out[c] = sum_{s<S} acc[s, c] (strategy MEAN_ABS, ABS_MEAN, L1) or sum_{s<S} acc[s, c]^2 (L2),
- * fp64, s ascending, unfused multiply-add. The caller divides by S (means) or takes the square root
- * (L2) and rounds to fp32 once.
+ * out[c] = sum_{s<S} A_s (strategy MEAN_ABS, ABS_MEAN, L1) or sum_{s<S} A_s^2 (L2) in fp64, with
+ * A_s = sum_{b<B} |acc[b, s, c]| and acc a contiguous fp32 [B, S, n_cols] accumulator. The caller
+ * divides by S (means) or takes the square root (L2) and rounds to fp32 once.
  */
-int smt_channel_score(const double* acc, int32_t S, int32_t n_cols, int32_t strategy, double* out,
+int smt_channel_score(const float* acc, int32_t B, int32_t S, int32_t n_cols, int32_t strategy, double* out,
                       hipStream_t stream);
 
 #ifdef __cplusplus

@@ -89,19 +89,36 @@ def block_stat(grad: torch.Tensor, d1: int, d2: int, strategy: str) -> torch.Ten
     return None
 
 
+def block_raw_fp64(grad: torch.Tensor, d1: int, d2: int, strategy: str) -> torch.Tensor:
+    """What ``smt_block_score`` computes, restated: per block ``[sum of terms, sum of |terms|]`` in
+    fp64, with the reference's terms (g, |g|, or the fp32-rounded ``g.abs()**2``)."""
+    g = grad.float().reshape(d1, Block_dimension, d2, Block_dimension)
+    if strategy == 'mean_abs':
+        t = g.double()
+    elif strategy in ('abs_mean', 'L1'):
+        t = g.abs().double()
+    elif strategy == 'L2':
+        t = (g * g).double()
+    else:
+        return None
+    return torch.stack([t.sum(dim=(1, 3)), t.abs().sum(dim=(1, 3))], dim=-1).reshape(-1, 2)
+
+
 def block_stat_fp64(grad: torch.Tensor, d1: int, d2: int, strategy: str) -> torch.Tensor:
-    """The same statistic with fp64 sums, rounded once to fp32 (what the GPU kernel computes)."""
-    g = grad.double().reshape(d1, Block_dimension, d2, Block_dimension)
+    """The same statistic from fp64 sums of the reference's terms, rounded once to fp32 (the
+    nominal value the GPU scan reports)."""
+    raw = block_raw_fp64(grad, d1, d2, strategy)
+    if raw is None:
+        return None
+    s = raw[:, 0].reshape(d1, d2)
     n = float(Block_dimension * Block_dimension)
     if strategy == 'mean_abs':
-        return (g.sum(dim=(1, 3)) / n).float().abs()
+        return (s / n).float().abs()
     if strategy == 'abs_mean':
-        return (g.abs().sum(dim=(1, 3)) / n).float()
+        return (s / n).float()
     if strategy == 'L1':
-        return g.abs().sum(dim=(1, 3)).float()
-    if strategy == 'L2':
-        return torch.sqrt((g * g).sum(dim=(1, 3))).float()
-    return None
+        return s.float()
+    return torch.sqrt(s).float()
 
 
 def select_submatrix(grads: Dict[Hashable, torch.Tensor], targeted_module_dims, n=660,
@@ -188,29 +205,25 @@ def channel_hook_accumulate(feat: dict, key, x: torch.Tensor) -> None:
         feat[key] += a
 
 
-def channel_acc_fp64(steps: Sequence[torch.Tensor]) -> torch.Tensor:
-    """The build's exact-arithmetic definition of the harvested statistic before scoring:
-    ``acc[s, c] = sum over steps (in order) of sum over b (ascending) of |x[b, s, c]|`` in fp64.
-    Written with the same operation order as ``smt_act_accumulate`` so the two agree bit for bit."""
-    acc = None
-    for x in steps:
-        xs = x.detach().cpu().to(torch.float64).abs()
-        part = torch.zeros(xs.shape[1], xs.shape[2], dtype=torch.float64)
-        for b in range(xs.shape[0]):
-            part = part + xs[b]
-        acc = part if acc is None else acc + part
-    return acc
+def channel_raw_fp64(act: torch.Tensor, strategy: str) -> torch.Tensor:
+    """What ``smt_channel_score`` computes, restated with its operation order: per channel
+    ``sum_s A_s`` (``sum_s A_s^2`` for L2) in fp64, ``A_s = sum_b |act[b, s, c]|`` with b ascending
+    from 0, s ascending."""
+    a = act.detach().cpu().to(torch.float32).abs().double()
+    tot = torch.zeros(a.shape[2], dtype=torch.float64)
+    for s in range(a.shape[1]):
+        col = torch.zeros(a.shape[2], dtype=torch.float64)
+        for b in range(a.shape[0]):
+            col = col + a[b, s]
+        tot = tot + (col * col if strategy == 'L2' else col)
+    return tot
 
 
-def channel_stat_fp64(acc: torch.Tensor, strategy: str) -> torch.Tensor:
-    """smt_helper.py:171-184 on an fp64 ``[S, C]`` accumulator: the sequence reduction in fp64
-    (s ascending, as ``smt_channel_score``), one division / sqrt, one rounding to fp32."""
-    tot = torch.zeros(acc.shape[1], dtype=torch.float64)
-    for s in range(acc.shape[0]):
-        v = acc[s]
-        tot = tot + (v * v if strategy == 'L2' else v)
+def channel_stat_fp64(act: torch.Tensor, strategy: str) -> torch.Tensor:
+    """The channel statistic from those fp64 sums, rounded once to fp32 (the GPU's nominal value)."""
+    tot = channel_raw_fp64(act, strategy)
     if strategy in ('mean_abs', 'abs_mean'):
-        return (tot / acc.shape[0]).abs().to(torch.float32)
+        return (tot / act.shape[1]).abs().to(torch.float32)
     if strategy == 'L1':
         return tot.to(torch.float32)
     if strategy == 'L2':

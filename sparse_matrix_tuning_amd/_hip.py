@@ -109,7 +109,7 @@ _SIGS = {
     "smt_row_scatter": (ctypes.c_int, [_P, _I64, _I32, _I64, _P, _I32, _P, _I64, _P]),
     "smt_column_gather": (ctypes.c_int, [_P, _I64, _I64, _P, _I32, _P, _I64, _P]),
     "smt_act_accumulate": (ctypes.c_int, [_P, _I32, _I64, _I64, _I32, _I32, _I32, _P, _I32, _P]),
-    "smt_channel_score": (ctypes.c_int, [_P, _I32, _I32, _I32, _P, _P]),
+    "smt_channel_score": (ctypes.c_int, [_P, _I32, _I32, _I32, _I32, _P, _P]),
     "smt_attn_last_error": (ctypes.c_char_p, []),
     "smt_attn_fwd": (ctypes.c_int, [ctypes.POINTER(AttnTensor)] * 4 + [_P, ctypes.POINTER(AttnShape), _P]),
     "smt_attn_bwd": (ctypes.c_int, [ctypes.POINTER(AttnTensor)] * 5 + [_P, _P] + [ctypes.POINTER(AttnTensor)] * 3
@@ -333,7 +333,8 @@ def grad_accumulate(pairs: Sequence[tuple], assign: bool = False) -> None:
 
 
 def block_scores(grads: Sequence[torch.Tensor], dims: Sequence[tuple], strategy: int) -> list:
-    """Raw fp64 per-256x256-block sums for each fp32 gradient; one launch for all of them."""
+    """Per fp32 gradient, an fp64 ``[d1*d2, 2]`` tensor: per 256x256 block (row-major) the sum of the
+    strategy's terms and the sum of their magnitudes; one launch for all of them."""
     entries, outs, blk = [], [], 0
     dev = None
     for g, (d1, d2) in zip(grads, dims):
@@ -343,7 +344,7 @@ def block_scores(grads: Sequence[torch.Tensor], dims: Sequence[tuple], strategy:
         g2 = g.reshape(d1 * BLOCK, d2 * BLOCK)
         if g2.stride(1) != 1 or (g2.stride(0) % 4) or (g2.data_ptr() % 16):
             g2 = g2.contiguous()
-        out = torch.empty(d1 * d2, dtype=torch.float64, device=dev)
+        out = torch.empty(d1 * d2, 2, dtype=torch.float64, device=dev)
         outs.append((out, g2))
         entries.append(ScoreEntry(g2.data_ptr(), g2.stride(0), d1, d2, blk, out.data_ptr(), strategy, 0))
         blk += d1 * d2
@@ -450,24 +451,27 @@ def column_gather(x2d: torch.Tensor, cols_dev: torch.Tensor, n_cols: int, ld_out
 
 
 def act_accumulate(x3d: torch.Tensor, acc: torch.Tensor, assign: bool) -> None:
-    """acc[s, c] (+)= sum_b |x3d[b, s, c]| in fp64 (fine_tune.py:636-667, smt_helper.py:170)."""
+    """acc[b, s, c] = |x3d[b, s, c]| (assign) or acc += |x3d| in fp32, elementwise: the reference's
+    ``feat[key] = x.abs().float()`` / ``feat[key] += ...`` (fine_tune.py:636-667)."""
     dev = _require_device(x3d, acc)
     if x3d.dim() != 3 or x3d.stride(2) != 1:
         raise ValueError("act_accumulate: x must be [B, S, C] with unit channel stride")
     B, S, C = x3d.shape
-    if acc.dtype != torch.float64 or not acc.is_contiguous() or tuple(acc.shape) != (S, C):
-        raise ValueError(f"act_accumulate: acc must be contiguous fp64 [{S}, {C}]")
+    if acc.dtype != torch.float32 or not acc.is_contiguous() or tuple(acc.shape) != (B, S, C):
+        raise ValueError(f"act_accumulate: acc must be contiguous fp32 [{B}, {S}, {C}]")
     rc = load().smt_act_accumulate(_ptr(x3d), _DT[x3d.dtype], x3d.stride(1), x3d.stride(0), B, S, C, _ptr(acc),
                                    int(bool(assign)), _stream(dev))
     _check(rc, "smt_act_accumulate")
 
 
 def channel_scores(acc: torch.Tensor, strategy: int) -> torch.Tensor:
-    """Raw fp64 per-channel sums over the sequence dim of an fp64 [S, C] accumulator."""
+    """fp64 per-channel sums over (batch, sequence) of an fp32 [B, S, C] accumulator: sum_s A_s, or
+    sum_s A_s^2 for L2, with A_s = sum_b |acc[b, s, c]|."""
     dev = _require_device(acc)
-    if acc.dtype != torch.float64 or not acc.is_contiguous() or acc.dim() != 2:
-        raise ValueError("channel_scores: contiguous fp64 [S, C] accumulator expected")
-    out = torch.empty(acc.shape[1], dtype=torch.float64, device=dev)
-    rc = load().smt_channel_score(_ptr(acc), acc.shape[0], acc.shape[1], int(strategy), _ptr(out), _stream(dev))
+    if acc.dtype != torch.float32 or not acc.is_contiguous() or acc.dim() != 3:
+        raise ValueError("channel_scores: contiguous fp32 [B, S, C] accumulator expected")
+    out = torch.empty(acc.shape[2], dtype=torch.float64, device=dev)
+    rc = load().smt_channel_score(_ptr(acc), acc.shape[0], acc.shape[1], acc.shape[2], int(strategy), _ptr(out),
+                                  _stream(dev))
     _check(rc, "smt_channel_score")
     return out

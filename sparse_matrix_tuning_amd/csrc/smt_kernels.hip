@@ -580,8 +580,10 @@ void grad_accumulate_kernel(const smt_accum_entry* __restrict__ entries, int n_e
 // ------------------------------------------------------------------------------------------------
 // Block scores (smt_helper.py:67-78, 233-251): one 256-thread workgroup per 256x256 block of an
 // fp32 gradient; float4 row loads (a wave covers one 1 KiB row), fp64 accumulation, wave shuffle
-// then LDS reduction in a fixed order. Writes the raw fp64 sum of g / |g| / g^2; the host turns it
-// into mean / abs / sqrt and rounds to fp32, the dtype the reference compares in.
+// then LDS reduction in a fixed order. Writes, per block, the fp64 sum of the reference's terms
+// (g for mean_abs, |g| for abs_mean / L1, the fp32-rounded g*g of `g.abs()**2` for L2) and the fp64
+// sum of their magnitudes. The host turns the first into mean / abs / sqrt and rounds to fp32; the
+// second bounds how far ATen's fp32 reduction of the same terms can be from it (smt_helper.py).
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ int find_score_entry(const smt_score_entry* e, int n, int64_t blk) {
     int lo = 0, hi = n - 1;
@@ -598,46 +600,60 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
+// contract(off): the L2 term is the fp32-rounded square, never fused into the fp64 add
+#pragma clang fp contract(off)
 template <int STRAT>
 __device__ __forceinline__ double score_term(float f) {
     if (STRAT == SMT_SCORE_MEAN_ABS) return (double)f;
-    if (STRAT == SMT_SCORE_L2) return (double)f * (double)f;      // exact: 24-bit x 24-bit < 53 bits
+    if (STRAT == SMT_SCORE_L2) return (double)(f * f);             // the fp32 square of `g.abs()**2`
     return (double)fabsf(f);
 }
 
+// acc.x = sum of terms, acc.y = sum of |terms| (only differs from acc.x for mean_abs)
 template <int STRAT>
-__device__ double block_partial(const float* __restrict__ src, int64_t ld) {
+__device__ double2 block_partial(const float* __restrict__ src, int64_t ld) {
     const int col = (threadIdx.x & 63) * 4;
     const int row0 = threadIdx.x >> 6;
-    double acc = 0.0;
+    double s = 0.0, m = 0.0;
 #pragma unroll 4
     for (int it = 0; it < kTile / 4; ++it) {
         const float4 v = *reinterpret_cast<const float4*>(src + (int64_t)(row0 + 4 * it) * ld + col);
-        acc += score_term<STRAT>(v.x) + score_term<STRAT>(v.y) + score_term<STRAT>(v.z) + score_term<STRAT>(v.w);
+        s += score_term<STRAT>(v.x) + score_term<STRAT>(v.y) + score_term<STRAT>(v.z) + score_term<STRAT>(v.w);
+        if (STRAT == SMT_SCORE_MEAN_ABS)
+            m += (double)fabsf(v.x) + (double)fabsf(v.y) + (double)fabsf(v.z) + (double)fabsf(v.w);
     }
-    return acc;
+    return make_double2(s, STRAT == SMT_SCORE_MEAN_ABS ? m : s);
 }
 
 __global__ __launch_bounds__(256)
 void block_score_kernel(const smt_score_entry* __restrict__ entries, int n_entries) {
-    __shared__ double part[4];
+    __shared__ double part[2][4];
     const int64_t blk = blockIdx.x;
     const smt_score_entry ent = entries[find_score_entry(entries, n_entries, blk)];
     const int64_t local = blk - ent.block_begin;
     const int bi = (int)(local / ent.d2);
     const int bj = (int)(local - (int64_t)bi * ent.d2);
     const float* src = ent.src + (int64_t)bi * kTile * ent.ld + (int64_t)bj * kTile;
-    double acc;
+    double2 acc;
     switch (ent.strategy) {
         case SMT_SCORE_MEAN_ABS: acc = block_partial<SMT_SCORE_MEAN_ABS>(src, ent.ld); break;
         case SMT_SCORE_L2: acc = block_partial<SMT_SCORE_L2>(src, ent.ld); break;
         default: acc = block_partial<SMT_SCORE_ABS_MEAN>(src, ent.ld); break;
     }
-    acc = wave_sum(acc);
-    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+    acc.x = wave_sum(acc.x);
+    acc.y = wave_sum(acc.y);
+    if ((threadIdx.x & 63) == 0) {
+        part[0][threadIdx.x >> 6] = acc.x;
+        part[1][threadIdx.x >> 6] = acc.y;
+    }
     __syncthreads();
-    if (threadIdx.x == 0) ent.out[local] = (part[0] + part[1]) + (part[2] + part[3]);
+    if (threadIdx.x == 0) {
+        reinterpret_cast<double2*>(ent.out)[local] =
+            make_double2((part[0][0] + part[0][1]) + (part[0][2] + part[0][3]),
+                         (part[1][0] + part[1][1]) + (part[1][2] + part[1][3]));
+    }
 }
+#pragma clang fp contract(fast)
 
 // ------------------------------------------------------------------------------------------------
 // Global squared L2 norm of the flat fp32 gradient (deterministic two-pass, fp64).
@@ -875,56 +891,55 @@ void colblock_gather_kernel(const uint16_t* __restrict__ x, int64_t ld_x, int64_
     *reinterpret_cast<uint4*>(out + t * per_row * 8 + (int64_t)j * kTile + ch * 8) = val;
 }
 
-// Activation harvest (the forward hook of fine_tune.py:636-667 plus the batch sum of
-// smt_helper.py:170): acc[s, c] (+)= sum_{b < B} |x[b, s, c]| in fp64, b ascending, then added to acc.
-// One thread per (s, 8 columns): B 16-byte loads, 64 B read-modify-write of acc.
+// Activation harvest, the forward hook of fine_tune.py:636-667: the reference keeps, per key, the
+// fp32 [B, S, in] tensor `feat[key] = |x|` (first step) / `feat[key] += |x|` (later steps). Same
+// state here, elementwise in HBM: acc[b, s, c] = (assign ? 0 : acc[b, s, c]) + float(|x[b, s, c]|),
+// one fp32 add per element exactly as the CPU `+=` (|x| of a bf16/fp16 value is exact in fp32).
+// One thread per 8 contiguous channels: one 16-B (bf16) or 32-B (fp32) load, 32 B read-modify-write.
 template <int DT>
 __global__ __launch_bounds__(256)
-void act_accumulate_kernel(const void* __restrict__ x, int64_t ld_x, int64_t sb, int32_t B, int32_t S,
-                           int32_t n_cols, double* __restrict__ acc, int32_t assign) {
+void act_accumulate_kernel(const void* __restrict__ x, int64_t ld_x, int64_t sb, int32_t S,
+                           int32_t n_cols, int64_t rows, float* __restrict__ acc, int32_t assign) {
     const int64_t groups = n_cols >> 3;
     const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int64_t s = v / groups;
-    if (s >= S) return;
-    const int64_t c0 = (v - s * groups) * 8;
-    double sum[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) sum[q] = 0.0;
-    for (int b = 0; b < B; ++b) {
-        float e[8];
-        load8<DT>(x, (int64_t)b * sb + s * ld_x + c0, e);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) sum[q] += (double)fabsf(e[q]);
-    }
-    double2* a = reinterpret_cast<double2*>(acc + s * n_cols + c0);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        double2 cur = assign ? make_double2(0.0, 0.0) : a[q];
-        cur.x = assign ? sum[2 * q] : cur.x + sum[2 * q];
-        cur.y = assign ? sum[2 * q + 1] : cur.y + sum[2 * q + 1];
-        a[q] = cur;
-    }
+    const int64_t row = v / groups;                       // row = b * S + s
+    if (row >= rows) return;
+    const int64_t c0 = (v - row * groups) * 8;
+    const int64_t b = row / S, s = row - b * S;
+    float e[8];
+    load8<DT>(x, b * sb + s * ld_x + c0, e);
+    float4* a = reinterpret_cast<float4*>(acc + row * n_cols + c0);
+    float4 lo = assign ? make_float4(0.f, 0.f, 0.f, 0.f) : a[0];
+    float4 hi = assign ? make_float4(0.f, 0.f, 0.f, 0.f) : a[1];
+    lo.x += fabsf(e[0]); lo.y += fabsf(e[1]); lo.z += fabsf(e[2]); lo.w += fabsf(e[3]);
+    hi.x += fabsf(e[4]); hi.y += fabsf(e[5]); hi.z += fabsf(e[6]); hi.w += fabsf(e[7]);
+    a[0] = lo;
+    a[1] = hi;
 }
 
-// Column statistic of the harvested activations (smt_helper.py:170-184): out[c] = sum_s acc[s, c]
-// (mean_abs / abs_mean / L1) or sum_s acc[s, c]^2 (L2), fp64, s ascending, no contraction (the
-// oracle restates this exact order; the host divides / takes sqrt and rounds to fp32 once).
+// Column statistic of the harvested activations (smt_helper.py:167-184): the reference sums |acc|
+// over the batch (`torch.sum(act.abs(), dim=0)`, fp32) and reduces the [S, in] result over the
+// sequence. Here, in fp64 (nearly exact): out[c] = sum_s A_s (mean_abs / abs_mean / L1) or
+// sum_s A_s^2 (L2) with A_s = sum_b |acc[b, s, c]|. The host divides by S / takes the square root,
+// rounds to fp32 once, and bounds the reference's fp32 value around it (smt_helper.py). One thread per
+// column; a wave reads 256 contiguous bytes of a row per (b, s).
 #pragma clang fp contract(off)
 __global__ __launch_bounds__(256)
-void channel_score_kernel(const double* __restrict__ acc, int32_t S, int32_t n_cols, int32_t square,
+void channel_score_kernel(const float* __restrict__ acc, int32_t B, int32_t S, int32_t n_cols, int32_t square,
                           double* __restrict__ out) {
     const int c = blockIdx.x * 256 + threadIdx.x;
     if (c >= n_cols) return;
+    const int64_t bstride = (int64_t)S * n_cols;
     double tot = 0.0;
-    const double* p = acc + c;
-    if (square) {
-        for (int s = 0; s < S; ++s) { const double v = p[(int64_t)s * n_cols]; tot = tot + v * v; }
-    } else {
-        for (int s = 0; s < S; ++s) tot = tot + p[(int64_t)s * n_cols];
+    for (int s = 0; s < S; ++s) {
+        const float* p = acc + (int64_t)s * n_cols + c;
+        double a = 0.0;
+        for (int b = 0; b < B; ++b) a += (double)fabsf(p[b * bstride]);
+        tot += square ? a * a : a;
     }
     out[c] = tot;
 }
-#pragma clang fp contract(on)
+#pragma clang fp contract(fast)
 
 // Split of T over workgroups for one tile set. One 512-thread workgroup fits per CU (128 KiB LDS),
 // so the launch runs in rounds of 256 workgroups; pick S in [1, 64] (chunks >= 512 rows, multiple of
@@ -967,7 +982,7 @@ extern "C" {
 
 const char* smt_last_error(void) { return g_err; }
 
-int smt_abi_version(void) { return 3; }
+int smt_abi_version(void) { return 4; }
 
 size_t smt_wgrad_workspace_bytes(int64_t T, int32_t n_tiles) {
     if (T <= 0 || n_tiles <= 0) return 0;
@@ -1207,32 +1222,35 @@ int smt_colblock_gather(const void* x, int64_t ld_x, int64_t T, const int32_t* c
 }
 
 int smt_act_accumulate(const void* x, int32_t x_dtype, int64_t ld_x, int64_t batch_stride, int32_t B, int32_t S,
-                       int32_t n_cols, double* acc, int32_t assign, hipStream_t stream) {
+                       int32_t n_cols, float* acc, int32_t assign, hipStream_t stream) {
     if (B < 0 || S < 0 || n_cols < 0) return fail(SMT_E_INVALID, "smt_act_accumulate: negative size");
-    if (S == 0 || n_cols == 0) return SMT_OK;
-    if (!acc || (B > 0 && !x)) return fail(SMT_E_INVALID, "smt_act_accumulate: null pointer");
+    if (B == 0 || S == 0 || n_cols == 0) return SMT_OK;
+    if (!acc || !x) return fail(SMT_E_INVALID, "smt_act_accumulate: null pointer");
     if (x_dtype != SMT_DTYPE_BF16 && x_dtype != SMT_DTYPE_FP16 && x_dtype != SMT_DTYPE_FP32)
         return fail(SMT_E_INVALID, "smt_act_accumulate: x_dtype %d", x_dtype);
     const int64_t vec = x_dtype == SMT_DTYPE_FP32 ? 4 : 8;
-    if ((n_cols & 7) || !aligned16(acc) || (B > 0 && (!aligned16(x) || (ld_x % vec) || (batch_stride % vec))))
+    if ((n_cols & 7) || !aligned16(acc) || !aligned16(x) || (ld_x % vec) || (batch_stride % vec))
         return fail(SMT_E_ALIGN, "smt_act_accumulate: needs n_cols %% 8 == 0 and 16-byte aligned rows");
-    const int64_t blocks = ((int64_t)S * (n_cols >> 3) + 255) / 256;
+    const int64_t rows = (int64_t)B * S;
+    const int64_t blocks = (rows * (n_cols >> 3) + 255) / 256;
+    if (blocks > 0x7fffffffLL) return fail(SMT_E_INVALID, "smt_act_accumulate: too large");
     const dim3 grid((unsigned)blocks), block(256);
     if (x_dtype == SMT_DTYPE_BF16)
-        hipLaunchKernelGGL(act_accumulate_kernel<SMT_DTYPE_BF16>, grid, block, 0, stream, x, ld_x, batch_stride, B, S, n_cols, acc, assign);
+        hipLaunchKernelGGL(act_accumulate_kernel<SMT_DTYPE_BF16>, grid, block, 0, stream, x, ld_x, batch_stride, S, n_cols, rows, acc, assign);
     else if (x_dtype == SMT_DTYPE_FP16)
-        hipLaunchKernelGGL(act_accumulate_kernel<SMT_DTYPE_FP16>, grid, block, 0, stream, x, ld_x, batch_stride, B, S, n_cols, acc, assign);
+        hipLaunchKernelGGL(act_accumulate_kernel<SMT_DTYPE_FP16>, grid, block, 0, stream, x, ld_x, batch_stride, S, n_cols, rows, acc, assign);
     else
-        hipLaunchKernelGGL(act_accumulate_kernel<SMT_DTYPE_FP32>, grid, block, 0, stream, x, ld_x, batch_stride, B, S, n_cols, acc, assign);
+        hipLaunchKernelGGL(act_accumulate_kernel<SMT_DTYPE_FP32>, grid, block, 0, stream, x, ld_x, batch_stride, S, n_cols, rows, acc, assign);
     return check_launch("act_accumulate_kernel");
 }
 
-int smt_channel_score(const double* acc, int32_t S, int32_t n_cols, int32_t strategy, double* out, hipStream_t stream) {
-    if (S < 0 || n_cols < 0) return fail(SMT_E_INVALID, "smt_channel_score: negative size");
+int smt_channel_score(const float* acc, int32_t B, int32_t S, int32_t n_cols, int32_t strategy, double* out,
+                      hipStream_t stream) {
+    if (B < 0 || S < 0 || n_cols < 0) return fail(SMT_E_INVALID, "smt_channel_score: negative size");
     if (strategy < SMT_SCORE_MEAN_ABS || strategy > SMT_SCORE_L2) return fail(SMT_E_INVALID, "smt_channel_score: strategy %d", strategy);
     if (n_cols == 0) return SMT_OK;
-    if (!out || (S > 0 && !acc)) return fail(SMT_E_INVALID, "smt_channel_score: null pointer");
-    hipLaunchKernelGGL(channel_score_kernel, dim3((n_cols + 255) / 256), dim3(256), 0, stream, acc, S, n_cols,
+    if (!out || (B > 0 && S > 0 && !acc)) return fail(SMT_E_INVALID, "smt_channel_score: null pointer");
+    hipLaunchKernelGGL(channel_score_kernel, dim3((n_cols + 255) / 256), dim3(256), 0, stream, acc, B, S, n_cols,
                        (int32_t)(strategy == SMT_SCORE_L2), out);
     return check_launch("channel_score_kernel");
 }

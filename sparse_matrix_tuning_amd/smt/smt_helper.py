@@ -1,31 +1,35 @@
 """MI355X drop-in for ``deepspeed/smt/smt_helper.py`` (block scoring and top-n selection).
 
 Scoring (smt_helper.py:54-78, 233-251) runs on the GPU: one multi-tensor launch of the
-``block_score`` kernel reads every fp32 gradient once and returns an fp64 raw sum per 256x256
-block; the host turns it into the reference's statistic and rounds to fp32, the dtype the
-reference compares in (``block_mean[i, j].item()`` of an fp32 tensor, smt_helper.py:114).
+``block_score`` kernel reads every fp32 gradient once and returns, per 256x256 block, the fp64 sum
+of the reference's terms and of their magnitudes. The host turns that into the reference's
+statistic rounded to fp32 (the dtype the reference compares in, ``block_mean[i, j].item()``,
+smt_helper.py:114) and into an interval that provably contains the value ATen's fp32 CPU reduction
+gives (:mod:`.ranking`).
 
-Ranking (smt_helper.py:102-146) is host integer/tuple work: the reference keeps the ``n``
-largest ``(score, (key, i, j))`` tuples with ``heapq`` and sorts them descending, which is the
-first ``n`` of all candidate tuples in descending tuple order (ties fall to the larger module
-name, then layer, then i, then j). That order is reproduced exactly; a numpy partition only
-pre-filters candidates strictly below the n-th score.
+Ranking (smt_helper.py:102-146) is host integer/tuple work: the first ``n`` of all
+``(score, (key, i, j))`` tuples in descending order (ties to the larger module name, then layer,
+then i, then j). Where two scores the ranking depends on are too close for the fp64 estimate to
+decide, the keys involved are re-scored with the reference's own expression on the host CPU
+(``grad.reshape(d1, 256, d2, 256)`` reduced as in smt_helper.py:233-251, over the whole key so
+ATen's reduction order per block is the reference's), which makes the selection identical to the
+reference's, bit for bit. ``ranking.LAST_REPORT`` says how many blocks that took.
 
 Gradient dicts may live on the CPU (as the reference's warm-up harvest does, fine_tune.py:731);
 they are copied to the current ROCm device for scoring. Without a ROCm device the call raises:
-there is no CPU scoring path outside ``oracle/``.
+the GPU scan has no CPU substitute (the host re-score only decides near-ties).
 """
 from __future__ import annotations
 
-import heapq
 import os
 from collections import defaultdict
-from typing import Dict, Hashable, Optional, Tuple
+from typing import Dict, Hashable, List, Optional, Tuple
 
 import numpy as np
 import torch
 
 from .. import _hip
+from . import ranking
 
 Block_dimension = 256
 
@@ -39,7 +43,8 @@ _STRATEGY = {
 
 # ------------------------------------------------------------------------------------------------
 # statistic helpers with the reference's names (smt_helper.py:233-251); each takes the
-# [d1, 256, d2, 256] view and returns the fp32 [d1, d2] block statistic, computed on the GPU.
+# [d1, 256, d2, 256] view and returns the fp32 [d1, d2] block statistic computed on the GPU (the
+# fp64 sum rounded once: within the interval of ranking.block_intervals of the reference's value).
 # ------------------------------------------------------------------------------------------------
 def _stat(grad_tensor: torch.Tensor, strategy: str) -> torch.Tensor:
     if grad_tensor.dim() != 4 or grad_tensor.shape[1] != Block_dimension or grad_tensor.shape[3] != Block_dimension:
@@ -71,7 +76,11 @@ def L2_norm(grad_tensor):
 
 
 def finalize_scores(raw: np.ndarray, strategy: str) -> np.ndarray:
-    """fp64 raw block sums -> the reference's fp32 statistic (rounded once)."""
+    """fp64 block sums (``[n, 2]`` from the kernel, or ``[n]`` sums of terms) -> the reference's
+    fp32 statistic, rounded once."""
+    raw = np.asarray(raw, dtype=np.float64)
+    if raw.ndim == 2:
+        raw = raw[:, 0]
     n = float(Block_dimension * Block_dimension)
     if strategy == "mean_abs":
         return np.abs((raw / n).astype(np.float32))
@@ -84,6 +93,27 @@ def finalize_scores(raw: np.ndarray, strategy: str) -> np.ndarray:
     raise ValueError(strategy)
 
 
+def reference_block_stat(grad: torch.Tensor, d1: int, d2: int, strategy: str) -> np.ndarray:
+    """The reference's own expression (smt_helper.py:67-78, 233-251) on the host CPU in fp32: the
+    exact values the reference ranks. Used by the ranking for the few keys whose order the GPU
+    estimate cannot decide."""
+    g = grad.detach()
+    if g.device.type != "cpu":
+        g = g.cpu()
+    g = g.to(torch.float32).reshape(d1, Block_dimension, d2, Block_dimension)
+    if strategy == "mean_abs":
+        s = g.mean(dim=(1, 3)).abs()
+    elif strategy == "abs_mean":
+        s = g.abs().mean(dim=(1, 3))
+    elif strategy == "L1":
+        s = g.abs().sum(dim=(1, 3))
+    elif strategy == "L2":
+        s = torch.sqrt(torch.sum(g.abs() ** 2, dim=(1, 3)))
+    else:
+        raise ValueError(strategy)
+    return s.numpy().reshape(-1)
+
+
 def _to_device(t: torch.Tensor) -> torch.Tensor:
     if t.device.type == "cuda":
         return t if t.dtype == torch.float32 else t.float()
@@ -93,13 +123,14 @@ def _to_device(t: torch.Tensor) -> torch.Tensor:
     return t.to(device=torch.device("cuda", torch.cuda.current_device()), dtype=torch.float32)
 
 
-def score_blocks(grads: Dict[Hashable, torch.Tensor], targeted_module_dims: Dict[str, list],
-                 calculate_strategy: str = "mean_abs") -> Dict[Hashable, np.ndarray]:
-    """smt_helper.py:54-78: per key, the fp32 ``[d1, d2]`` block statistic. Keys with an unknown
-    strategy are skipped exactly as in the reference (no branch assigns them)."""
+def score_block_entries(grads: Dict[Hashable, torch.Tensor], targeted_module_dims: Dict[str, list],
+                        calculate_strategy: str = "mean_abs") -> List[ranking.KeyScores]:
+    """smt_helper.py:54-78 on the GPU: per key, the block statistics as :class:`ranking.KeyScores`
+    (nominal fp32 values, intervals holding the reference's values, the host re-score). Keys with an
+    unknown strategy are skipped exactly as in the reference (no branch assigns them)."""
     if calculate_strategy not in _STRATEGY:
-        return {}
-    keys, tensors, dims = [], [], []
+        return []
+    keys, sources, tensors, dims = [], [], [], []
     for key, grad in grads.items():
         name = key[0]
         d1 = int(targeted_module_dims[name][0] / Block_dimension)
@@ -109,59 +140,67 @@ def score_blocks(grads: Dict[Hashable, torch.Tensor], targeted_module_dims: Dict
             raise RuntimeError(f"shape '[{d1}, {Block_dimension}, {d2}, {Block_dimension}]' is invalid "
                                f"for input of size {numel}")
         keys.append(key)
+        sources.append(grad)
         tensors.append(_to_device(grad).reshape(d1 * Block_dimension, d2 * Block_dimension))
         dims.append((d1, d2))
     if not keys:
-        return {}
+        return []
     raws = _hip.block_scores(tensors, dims, _STRATEGY[calculate_strategy])
-    host = torch.cat([r for r in raws]).cpu().numpy()
-    out, off = {}, 0
-    for key, (d1, d2) in zip(keys, dims):
-        out[key] = finalize_scores(host[off:off + d1 * d2], calculate_strategy).reshape(d1, d2)
+    del tensors
+    host = torch.cat(raws).cpu().numpy()
+    entries, off = [], 0
+    for key, src, (d1, d2) in zip(keys, sources, dims):
+        raw = host[off:off + d1 * d2]
         off += d1 * d2
+        nominal, lo, hi = ranking.block_intervals(raw, calculate_strategy)
+        entries.append(ranking.KeyScores(
+            key, (d1, d2), nominal, lo, hi,
+            rescore=lambda src=src, d1=d1, d2=d2: reference_block_stat(src, d1, d2, calculate_strategy),
+            bounds=lambda worst, raw=raw: ranking.block_intervals(raw, calculate_strategy, worst)[1:]))
+    return entries
+
+
+def score_blocks(grads: Dict[Hashable, torch.Tensor], targeted_module_dims: Dict[str, list],
+                 calculate_strategy: str = "mean_abs") -> Dict[Hashable, np.ndarray]:
+    """Per key, the nominal fp32 ``[d1, d2]`` block statistic (GPU, fp64 rounded once)."""
+    return {e.key: e.nominal.reshape(e.shape)
+            for e in score_block_entries(grads, targeted_module_dims, calculate_strategy)}
+
+
+def _exact_entries(values: Dict[Hashable, np.ndarray]) -> List[ranking.KeyScores]:
+    out = []
+    for key, v in values.items():
+        a = np.asarray(v, dtype=np.float32)
+        shape = a.shape if a.ndim else (1,)
+        a64 = a.reshape(-1).astype(np.float64)
+        e = ranking.KeyScores(key, shape, a, a64, a64, rescore=lambda a=a: a)
+        e.exact = True
+        out.append(e)
     return out
+
+
+def _rank_block_entries(entries: List[ranking.KeyScores], n: int, selection_strategy: str) -> defaultdict:
+    if not entries:
+        # the reference reaches `del indices` / `del mean` with nothing bound
+        raise UnboundLocalError("cannot access local variable 'mean' where it is not associated with a value "
+                                "(no candidate blocks: empty gradients or unknown calculate_strategy)")
+    to_ij = lambda e, f: (int(f // e.shape[1]), int(f % e.shape[1]))
+    if selection_strategy == "norm_dist":
+        ranked = defaultdict(list)
+        for e, flats in zip(entries, ranking.top_n_per_key(entries, n)):
+            for f in flats:                     # a key is only created by an append, as in smt_helper.py:96
+                ranked[e.key].append(to_ij(e, f))
+        return ranked
+    if n <= 0:
+        raise UnboundLocalError("cannot access local variable 'mean' where it is not associated with a value "
+                                "(n <= 0 selects no block)")
+    return ranking.group(entries, ranking.top_n(entries, n), to_ij)
 
 
 def rank_blocks(block_means: Dict[Hashable, np.ndarray], n: int,
                 selection_strategy: str = "no_restriction") -> defaultdict:
-    """smt_helper.py:81-146 on precomputed fp32 block statistics (host logic)."""
-    if not block_means:
-        # the reference reaches `del indices` / `del mean` with nothing bound
-        raise UnboundLocalError("cannot access local variable 'mean' where it is not associated with a value "
-                                "(no candidate blocks: empty gradients or unknown calculate_strategy)")
-    ranked_blocks = defaultdict(list)
-    if selection_strategy == "norm_dist":
-        # per key: the n best blocks by descending score; ties in index order (the reference's
-        # unstable torch.argsort leaves tie order unspecified)
-        for key, bm in block_means.items():
-            flat = np.asarray(bm, dtype=np.float32).reshape(-1)
-            order = np.argsort(-flat.astype(np.float64), kind="stable")[:max(n, 0)]
-            d2 = bm.shape[1]
-            for idx in order:
-                ranked_blocks[key].append((int(idx // d2), int(idx % d2)))
-        return ranked_blocks
-
-    if n <= 0:
-        raise UnboundLocalError("cannot access local variable 'mean' where it is not associated with a value "
-                                "(n <= 0 selects no block)")
-    # Pre-filter: keep only candidates whose score is >= the n-th largest score (all ties kept),
-    # then order them exactly as the reference's tuples.
-    all_scores = np.concatenate([np.asarray(v, dtype=np.float32).reshape(-1) for v in block_means.values()])
-    if n < all_scores.size:
-        thresh = np.partition(all_scores, all_scores.size - n)[all_scores.size - n]
-    else:
-        thresh = -np.inf
-    cands = []
-    for key, bm in block_means.items():
-        bm = np.asarray(bm, dtype=np.float32)
-        d2 = bm.shape[1]
-        flat = bm.reshape(-1)
-        for idx in np.nonzero(flat >= thresh)[0]:
-            cands.append((float(flat[idx]), (key, int(idx // d2), int(idx % d2))))
-    top_blocks = heapq.nlargest(n, cands)       # == sorted(cands, reverse=True)[:n]
-    for _mean, (info, row, col) in top_blocks:
-        ranked_blocks[info].append((row, col))
-    return ranked_blocks
+    """smt_helper.py:81-146 on given exact fp32 block statistics ``{key: [d1, d2]}`` (host logic)."""
+    return _rank_block_entries(_exact_entries(block_means), n, selection_strategy)
 
 
 def analyze_gradient_distribution(gradients_per_key, key_string, output_dir):
@@ -196,22 +235,24 @@ def select_submatrix_based_on_grads(grads,
                                     output_dir=""):
     """smt_helper.py:40-146. ``grads``: ``{(module_name, layer): fp32 [out, in]}``; returns
     ``defaultdict(list)`` ``{(module_name, layer): [(row_block, col_block), ...]}`` with each
-    key's list in descending tuple order (the tile order of LinearLayer_MatrixSparsity)."""
-    block_means = score_blocks(grads, targeted_module_dims, calculate_strategy)
-    if do_gradient_distribution_analysis and selection_strategy != "norm_dist" and block_means:
+    key's list in descending tuple order (the tile order of LinearLayer_MatrixSparsity), identical
+    to the reference's."""
+    entries = score_block_entries(grads, targeted_module_dims, calculate_strategy)
+    if do_gradient_distribution_analysis and selection_strategy != "norm_dist" and entries:
         per_key = {}
-        for key in block_means:
-            per_key.setdefault(key[0], [])
-        for key, bm in block_means.items():
-            per_key[key[0]].extend(float(v) for v in np.asarray(bm).reshape(-1))
+        for e in entries:
+            per_key.setdefault(e.key[0], [])
+        for e in entries:
+            per_key[e.key[0]].extend(float(v) for v in e.nominal)
         analyze_gradient_distribution(per_key, "_".join(str(k) for k in per_key), output_dir)
-    return rank_blocks(block_means, n, selection_strategy)
+    return _rank_block_entries(entries, n, selection_strategy)
 
 
 class ChannelActivation:
-    """Device-resident harvested activations of one ``(module, layer)`` key: fp64
-    ``acc[s, c] = sum over steps, ranks and batch of |x[b, s, c]|`` (what the reference's CPU
-    ``[B, S, in]`` fp32 dict entry holds after ``torch.sum(act.abs(), dim=0)``, smt_helper.py:170)."""
+    """Device-resident harvested activations of one ``(module, layer)`` key: the fp32
+    ``[B, S, in]`` tensor the reference keeps on the CPU (``feat[key] = |x|`` then ``+= |x|`` over
+    steps, fine_tune.py:636-667), here in HBM and updated elementwise by ``smt_act_accumulate``.
+    Keys whose linears read the same input (q/k/v, gate/up) share one object."""
 
     __slots__ = ("acc", "steps")
 
@@ -220,9 +261,10 @@ class ChannelActivation:
         self.steps = steps
 
 
-def _channel_acc(act) -> torch.Tensor:
+def _channel_sources(act) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(fp32 [B, S, in] on the device for the GPU scan, the tensor the host re-score reads)."""
     if isinstance(act, ChannelActivation):
-        return act.acc
+        return act.acc, act.acc
     if act.dim() != 3:
         raise IndexError(f"activation must be [batch, seq, channels] (the hook input), got {tuple(act.shape)}")
     x = act
@@ -231,15 +273,17 @@ def _channel_acc(act) -> torch.Tensor:
             raise RuntimeError("SMT channel scoring runs on a ROCm device; none is available "
                                "(the CPU restatement is oracle/, test-only)")
         x = x.to(torch.device("cuda", torch.cuda.current_device()))
-    if x.stride(2) != 1 or x.data_ptr() % 16 or x.stride(1) % 8 or x.stride(0) % 8:
+    x = x.to(torch.float32)
+    if not x.is_contiguous() or x.data_ptr() % 16 or x.shape[2] % 8:
+        if x.shape[2] % 8:
+            pad = torch.zeros(x.shape[0], x.shape[1], (-x.shape[2]) % 8, dtype=x.dtype, device=x.device)
+            x = torch.cat([x, pad], dim=2)
         x = x.contiguous()
-    acc = torch.empty(x.shape[1], x.shape[2], dtype=torch.float64, device=x.device)
-    _hip.act_accumulate(x, acc, assign=True)
-    return acc
+    return x, act
 
 
 def finalize_channel_scores(raw: np.ndarray, seq_len: int, strategy: str) -> np.ndarray:
-    """fp64 raw column sums over the sequence -> the reference's fp32 statistic (smt_helper.py:171-184;
+    """fp64 column sums over (batch, sequence) -> the reference's fp32 statistic (smt_helper.py:171-184;
     the harvested values are non-negative, so mean_abs == abs_mean)."""
     if strategy in ("mean_abs", "abs_mean"):
         return np.abs(raw / float(seq_len)).astype(np.float32)
@@ -250,57 +294,81 @@ def finalize_channel_scores(raw: np.ndarray, seq_len: int, strategy: str) -> np.
     raise ValueError(strategy)
 
 
-def score_channels(activation: Dict[Hashable, object], calculate_strategy: str = "mean_abs") -> Dict[Hashable, np.ndarray]:
-    """smt_helper.py:167-184 on the GPU: per key, the fp32 per-channel statistic. Keys with an
-    unknown strategy are skipped as in the reference (no branch assigns them)."""
+def reference_channel_stat(act: torch.Tensor, strategy: str) -> np.ndarray:
+    """The reference's own expression (smt_helper.py:167-184) on the host CPU: the exact fp32 values
+    it ranks, for the keys whose order the GPU estimate cannot decide."""
+    a = act.detach()
+    if a.device.type != "cpu":
+        a = a.cpu()
+    a = torch.sum(a.to(torch.float32).abs(), dim=0)
+    if strategy == "mean_abs":
+        s = torch.mean(a.abs(), dim=0)
+    elif strategy == "abs_mean":
+        s = torch.abs(torch.mean(a, dim=0))
+    elif strategy == "L1":
+        s = torch.norm(a, p=1, dim=0)
+    elif strategy == "L2":
+        s = torch.norm(a, p=2, dim=0)
+    else:
+        raise ValueError(strategy)
+    return s.numpy().reshape(-1)
+
+
+def score_channel_entries(activation: Dict[Hashable, object], calculate_strategy: str = "mean_abs") -> List[ranking.KeyScores]:
+    """smt_helper.py:167-184 on the GPU: per key, the channel statistics as :class:`ranking.KeyScores`.
+    Keys with an unknown strategy are skipped as in the reference (no branch assigns them)."""
     if calculate_strategy not in _STRATEGY:
-        return {}
-    out = {}
+        return []
+    entries = []
     for key, act in activation.items():
-        acc = _channel_acc(act)
-        raw = _hip.channel_scores(acc, _STRATEGY[calculate_strategy])
-        out[key] = finalize_channel_scores(raw.cpu().numpy(), acc.shape[0], calculate_strategy)
-    return out
+        dev_acc, src = _channel_sources(act)
+        B, S, C = src.shape
+        raw = _hip.channel_scores(dev_acc, _STRATEGY[calculate_strategy]).cpu().numpy()[:C]
+        nominal, lo, hi = ranking.channel_intervals(raw, B, S, calculate_strategy)
+        entries.append(ranking.KeyScores(
+            key, (C,), nominal, lo, hi,
+            rescore=lambda src=src: reference_channel_stat(src, calculate_strategy),
+            bounds=lambda worst, raw=raw, B=B, S=S: ranking.channel_intervals(raw, B, S, calculate_strategy,
+                                                                               worst)[1:]))
+    return entries
 
 
-def rank_channels(column_means: Dict[Hashable, np.ndarray], n: int,
-                  selection_strategy: str = "no_restriction") -> defaultdict:
-    """smt_helper.py:186-230 on precomputed fp32 channel statistics (host logic). ``no_restriction``:
-    the first ``n`` of all ``(score, (key, idx))`` tuples in descending order, grouped per key in that
-    order; ``norm_dist``: the ``n`` best channels of every key."""
-    if not column_means:
+def score_channels(activation: Dict[Hashable, object], calculate_strategy: str = "mean_abs") -> Dict[Hashable, np.ndarray]:
+    """Per key, the nominal fp32 per-channel statistic (GPU, fp64 rounded once)."""
+    return {e.key: e.nominal for e in score_channel_entries(activation, calculate_strategy)}
+
+
+def _rank_channel_entries(entries: List[ranking.KeyScores], n: int, selection_strategy: str) -> defaultdict:
+    if not entries:
         raise UnboundLocalError("cannot access local variable 'value' where it is not associated with a value "
                                 "(no candidate channels: empty activations or unknown calculate_strategy)")
-    ranked = defaultdict(list)
     if selection_strategy == "norm_dist":
-        for key, cm in column_means.items():
-            flat = np.asarray(cm, dtype=np.float32).reshape(-1)
-            # ties in index order (the reference's unstable torch.argsort leaves them unspecified)
-            ranked[key] = [int(i) for i in np.argsort(-flat.astype(np.float64), kind="stable")[:max(n, 0)]]
+        ranked = defaultdict(list)
+        for e, flats in zip(entries, ranking.top_n_per_key(entries, n)):
+            ranked[e.key] = [int(f) for f in flats]        # smt_helper.py:195-197 assigns every key
         return ranked
     if n <= 0:
         raise UnboundLocalError("cannot access local variable 'value' where it is not associated with a value "
                                 "(n <= 0 selects no channel)")
-    all_scores = np.concatenate([np.asarray(v, dtype=np.float32).reshape(-1) for v in column_means.values()])
-    thresh = np.partition(all_scores, all_scores.size - n)[all_scores.size - n] if n < all_scores.size else -np.inf
-    cands = []
-    for key, cm in column_means.items():
-        flat = np.asarray(cm, dtype=np.float32).reshape(-1)
-        for idx in np.nonzero(flat >= thresh)[0]:
-            cands.append((float(flat[idx]), (key, int(idx))))
-    for _value, (key, idx) in heapq.nlargest(n, cands):
-        ranked[key].append(idx)
-    return ranked
+    return ranking.group(entries, ranking.top_n(entries, n), lambda e, f: int(f))
+
+
+def rank_channels(column_means: Dict[Hashable, np.ndarray], n: int,
+                  selection_strategy: str = "no_restriction") -> defaultdict:
+    """smt_helper.py:186-230 on given exact fp32 channel statistics (host logic). ``no_restriction``:
+    the first ``n`` of all ``(score, (key, idx))`` tuples in descending order, grouped per key in that
+    order; ``norm_dist``: the ``n`` best channels of every key."""
+    return _rank_channel_entries(_exact_entries(column_means), n, selection_strategy)
 
 
 def select_channel_based_on_activation(activation, n=660, selection_strategy="no_restriction",
                                        calculate_strategy="mean_abs", model="yahma/llama-13b-hf"):
     """smt_helper.py:149-230. ``activation``: ``{(module_name, layer): act}`` where ``act`` is the
-    reference's ``[B, S, in]`` tensor of summed ``|x|`` (any device) or a :class:`ChannelActivation`
-    from :class:`sparse_matrix_tuning_amd.trainer.ActivationHarvester`. Returns
-    ``defaultdict(list)`` ``{key: [channel, ...]}`` with each list in descending tuple order (the row
-    order of LinearLayer_ChannelSparsity)."""
-    return rank_channels(score_channels(activation, calculate_strategy), n, selection_strategy)
+    reference's fp32 ``[B, S, in]`` tensor of accumulated ``|x|`` (any device) or a
+    :class:`ChannelActivation` from :class:`sparse_matrix_tuning_amd.trainer.ActivationHarvester`.
+    Returns ``defaultdict(list)`` ``{key: [channel, ...]}`` with each list in descending tuple order
+    (the row order of LinearLayer_ChannelSparsity), identical to the reference's."""
+    return _rank_channel_entries(score_channel_entries(activation, calculate_strategy), n, selection_strategy)
 
 
 def get_blocks(model):

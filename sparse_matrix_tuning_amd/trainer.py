@@ -224,9 +224,12 @@ class ActivationHarvester:
     position in ``model.model.layers``.
 
     Here the hooks stay registered on those linears and one ordinary ``no_grad`` forward of the
-    model feeds them the same inputs. Each hook is one ``smt_act_accumulate`` launch into an fp64
-    ``[S, in]`` accumulator (the batch sum the reference does at selection, smt_helper.py:170, is
-    folded in); ranks are summed once, in :meth:`finalize`, with one all-reduce of all accumulators."""
+    model feeds them the same inputs. Each hook is one ``smt_act_accumulate`` launch that keeps the
+    reference's own state, the fp32 ``[B, S, in]`` sum of ``|x|`` over steps, in HBM (bit for bit the
+    CPU ``+=``). Linears that read the same input tensor in one forward (q/k/v, gate/up) share one
+    accumulator instead of holding identical copies. Ranks are summed once, in :meth:`finalize`,
+    with one fp32 all-reduce of all accumulators (the reference all-reduces every hook's bf16 ``|x|``;
+    at world size 1 both are the identity)."""
 
     def __init__(self, model, num_mlp_channel: int, num_attention_channel: int):
         self.model = model
@@ -234,6 +237,7 @@ class ActivationHarvester:
         self.attention_activation: Dict[tuple, ChannelActivation] = {}
         self._handles = []
         self._reduced = False
+        self._last = None                   # (input tensor object, accumulator) of the latest hook
         layers = model.model.layers
         for i, layer in enumerate(layers):
             for name, lin in get_named_linears(layer).items():
@@ -248,22 +252,29 @@ class ActivationHarvester:
                 if store is not None:
                     self._handles.append(lin.register_forward_hook(self._hook(store, key)))
 
-    @staticmethod
-    def _hook(store: dict, key: tuple):
+    def _hook(self, store: dict, key: tuple):
         def hook(_module, inputs, _output):
-            x = inputs[0].detach()
+            x_obj = inputs[0]
+            last = self._last
+            ent = store.get(key)
+            if last is not None and last[0] is x_obj and (ent is None or ent is last[1]):
+                # same input tensor as the previous linear (q/k/v, gate/up): same accumulator, already
+                # updated for this forward
+                store[key] = last[1]
+                return
+            x = x_obj.detach()
             if x.stride(-1) != 1 or x.data_ptr() % 16 or any(st % 8 for st in x.stride()[:-1]):
                 x = x.contiguous()
-            ent = store.get(key)
             if ent is None:
                 ent = store[key] = ChannelActivation(
-                    torch.empty(x.shape[1], x.shape[2], dtype=torch.float64, device=x.device))
-            elif tuple(ent.acc.shape) != (x.shape[1], x.shape[2]):
+                    torch.empty(x.shape, dtype=torch.float32, device=x.device))
+            elif tuple(ent.acc.shape) != tuple(x.shape):
                 # the reference's `feat_dict[key] += x` needs equal shapes across steps too
                 raise RuntimeError(f"activation shape {tuple(x.shape)} differs from earlier steps "
                                    f"({tuple(ent.acc.shape)}) for {key}")
             _hip.act_accumulate(x, ent.acc, assign=ent.steps == 0)
             ent.steps += 1
+            self._last = (x_obj, ent)
         return hook
 
     @torch.no_grad()
@@ -274,6 +285,7 @@ class ActivationHarvester:
         try:
             self.model(**batch, use_cache=False)
         finally:
+            self._last = None
             self.model.train(was_training)
 
     def finalize(self) -> None:
@@ -284,7 +296,12 @@ class ActivationHarvester:
         self._reduced = True
         if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
             return
-        accs = [e.acc for d in (self.activation, self.attention_activation) for e in d.values()]
+        seen, accs = set(), []
+        for d in (self.activation, self.attention_activation):
+            for e in d.values():
+                if id(e) not in seen:
+                    seen.add(id(e))
+                    accs.append(e.acc)
         if not accs:
             return
         flat = torch.cat([a.reshape(-1) for a in accs])
@@ -303,6 +320,7 @@ class ActivationHarvester:
         self.remove()
         self.activation = {}
         self.attention_activation = {}
+        self._last = None
 
 
 def select_and_convert_channels(model, harvester: ActivationHarvester, num_attention_channel: int,

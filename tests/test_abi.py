@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
     out = subprocess.run(["nm", "-D", "--defined-only", _hip.lib_path()], capture_output=True, text=True).stdout
     for name in declared_functions():
         assert re.search(rf"\bT {name}$", out, re.M), name
-    assert lib.smt_abi_version() == 3
+    assert lib.smt_abi_version() == 4
 
 
 def test_library_carries_gfx950_code_object():
@@ -68,8 +68,9 @@ def test_validation_errors_without_gpu():
     assert lib.smt_row_scatter(None, 256, 8, 256, None, 4, None, 256, None) == -1
     assert lib.smt_column_gather(None, 256, 16, None, 300, None, 256, None) == -1      # ld_out < n_cols
     assert lib.smt_act_accumulate(None, 0, 256, 0, 1, 4, 256, None, 1, None) == -1
-    assert lib.smt_act_accumulate(None, 7, 256, 0, 0, 4, 256, None, 1, None) == -1     # bad dtype / null acc
-    assert lib.smt_channel_score(None, 4, 256, 9, None, None) == -1
+    assert lib.smt_act_accumulate(None, 7, 256, 0, 1, 4, 256, None, 1, None) == -1     # bad dtype / null acc
+    assert lib.smt_act_accumulate(None, 0, 256, 0, 0, 4, 256, None, 1, None) == 0      # empty batch: no-op
+    assert lib.smt_channel_score(None, 1, 4, 256, 9, None, None) == -1
     assert b"strategy" in lib.smt_last_error()
 
 

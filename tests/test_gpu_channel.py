@@ -2,10 +2,11 @@
 fine_tune.py:406-709) against the oracle.
 
 Tolerances:
-* row / column copies, harvested fp64 accumulators and per-channel fp64 sums: bit-exact vs the
-  oracle's operation-order restatement (oracle.channel_acc_fp64 / channel_stat_fp64);
-* channel selection: bit-exact (same keys, same order, same channel order) vs the golden fixture,
-  which the ATen fp32 restatement of the reference produced;
+* row / column copies and the harvested fp32 [B, S, in] accumulators: bit-exact vs the reference's
+  hook arithmetic (oracle.channel_hook_accumulate); per-channel fp64 sums: bit-exact vs the oracle's
+  operation-order restatement (oracle.channel_raw_fp64);
+* channel selection: bit-exact (same keys, same order, same channel order) vs the golden fixtures,
+  which the ATen fp32 restatement of the reference produced, including the near-tie fixture;
 * channel gradient (bf16): relative Frobenius error vs fp64 truth from identical bf16 inputs
   <= max(1e-3, 1.1 x the reference restatement's own error);
 * whole-model loss: relative <= 1e-3 vs the reference restatement on the same weights / inputs.
@@ -66,16 +67,34 @@ def test_column_gather_bit_exact_and_zero_pad(T, k):
 def test_act_accumulate_and_channel_scores_bit_exact(strategy, dtype):
     torch.manual_seed(2)
     steps = [(torch.randn(3, 24, 520) * torch.exp(2 * torch.randn(520))).to(dtype) for _ in range(3)]
-    acc = torch.empty(24, 520, dtype=torch.float64, device=DEV)
+    acc = torch.empty(3, 24, 520, dtype=torch.float32, device=DEV)
+    feat = {}
     for i, x in enumerate(steps):
         big = torch.zeros(3, 24, 528, dtype=dtype, device=DEV)     # strided input: row stride 528
         big[:, :, :520] = x.to(DEV)
         _hip.act_accumulate(big[:, :, :520], acc, assign=i == 0)
-    truth = ref.channel_acc_fp64(steps)
-    assert torch.equal(acc.cpu(), truth)
+        ref.channel_hook_accumulate(feat, "k", x)                 # fine_tune.py:636-667 at world size 1
+    assert torch.equal(acc.cpu(), feat["k"])
     raw = _hip.channel_scores(acc, smt_helper._STRATEGY[strategy])
+    assert torch.equal(raw.cpu(), ref.channel_raw_fp64(feat["k"], strategy))
     got = smt_helper.finalize_channel_scores(raw.cpu().numpy(), 24, strategy)
-    assert np.array_equal(got, ref.channel_stat_fp64(truth, strategy).numpy())
+    assert np.array_equal(got, ref.channel_stat_fp64(feat["k"], strategy).numpy())
+
+
+def test_channel_near_tie_selection_bit_identical():
+    """Near-tie fixture: channels holding the same values in another order; the fp64-rounded ranking
+    gets some cases wrong (``nominal_ranking_differs``), the product must not."""
+    from tests.golden.make_golden import near_tie_channel_inputs
+    spec = json.load(open(os.path.join(GOLDEN, "near_tie_expected.json")))["channel"]
+    act = near_tie_channel_inputs()
+    dev_act = {k: smt_helper.ChannelActivation(v.to(DEV).contiguous(), 1) for k, v in act.items()}
+    for case in spec["cases"]:
+        st, n, sel = case["strategy"], case["n"], case["selection_strategy"]
+        live = ref.select_channel(act, n, selection_strategy=sel, calculate_strategy=st)   # this host's ATen
+        for src in (act, dev_act):
+            out = smt_helper.select_channel_based_on_activation(src, n, selection_strategy=sel, calculate_strategy=st)
+            assert list(out.items()) == list(live.items()), (st, n, sel)
+        assert [[k[0], k[1], list(v)] for k, v in live.items()] == case["expected"], (st, n, sel)
 
 
 def test_channel_selection_bit_exact_vs_golden():
@@ -178,9 +197,13 @@ def test_harvester_bit_exact_vs_reference_hook_and_selection():
                 ref.channel_hook_accumulate(feat_att, (name.split('.')[-1], i), x)
     assert set(h.activation) == set(feat_mlp) and set(h.attention_activation) == set(feat_att)
     for key, ent in list(h.activation.items()) + list(h.attention_activation.items()):
-        name = ('mlp.' if key[0] in ('gate_proj', 'up_proj', 'down_proj') else 'self_attn.') + key[0]
         assert ent.steps == 2
-        assert torch.equal(ent.acc.cpu(), ref.channel_acc_fp64(seen[(name, key[1])]))
+        want = feat_mlp[key] if key[0] in ('gate_proj', 'up_proj', 'down_proj') else feat_att[key]
+        assert torch.equal(ent.acc.cpu(), want)
+    # q/k/v (gate/up) read one input: one shared accumulator each
+    assert h.attention_activation[('q_proj', 0)] is h.attention_activation[('v_proj', 0)]
+    assert h.activation[('gate_proj', 1)] is h.activation[('up_proj', 1)]
+    assert h.activation[('down_proj', 1)] is not h.activation[('up_proj', 1)]
     got = smt_helper.select_channel_based_on_activation(h.attention_activation, 16)
     assert dict(got) == dict(ref.select_channel(feat_att, 16))
     got = smt_helper.select_channel_based_on_activation(h.activation, 16, calculate_strategy="L2")

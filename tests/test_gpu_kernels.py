@@ -1,6 +1,7 @@
 """GPU parity of every HIP kernel against the CPU oracle (through the C ABI, ctypes)."""
 import math
 
+import numpy as np
 import pytest
 import torch
 
@@ -145,15 +146,22 @@ def test_grad_accumulate_bit_exact():
 # ---------------------------------------------------------------- block scores (smt_helper.py:67-78, 233-251)
 @pytest.mark.parametrize("strategy", ["mean_abs", "abs_mean", "L1", "L2"])
 def test_block_scores_match_fp64_oracle(strategy):
+    from sparse_matrix_tuning_amd.smt import ranking
     from sparse_matrix_tuning_amd.smt.smt_helper import finalize_scores
     g = torch.randn(768, 1024) * torch.rand(768, 1024)
-    raw = _hip.block_scores([g.to(DEV)], [(3, 4)], _hip.__dict__["SCORE_" + {"mean_abs": "MEAN_ABS", "abs_mean": "ABS_MEAN", "L1": "L1", "L2": "L2"}[strategy]])[0]
-    got = finalize_scores(raw.cpu().numpy(), strategy).reshape(3, 4)
-    want = ref.block_stat_fp64(g, 3, 4, strategy).numpy()
-    assert (got == want).all()
-    # and within a few fp32 ulps of the reference's fp32 CPU reduction
-    lit = ref.block_stat(g, 3, 4, strategy).numpy()
-    assert abs(got - lit).max() <= 1e-5 * abs(lit).max()
+    g[:256, :256] = 0.0                                             # an exact (all-zero) block
+    code = _hip.__dict__["SCORE_" + {"mean_abs": "MEAN_ABS", "abs_mean": "ABS_MEAN", "L1": "L1", "L2": "L2"}[strategy]]
+    raw = _hip.block_scores([g.to(DEV)], [(3, 4)], code)[0].cpu()
+    want = ref.block_raw_fp64(g, 3, 4, strategy)
+    # fp64 sums of the same fp32 terms in another order: equal to ~1e-15 relative
+    assert torch.allclose(raw, want, rtol=1e-13, atol=0)
+    got = finalize_scores(raw.numpy(), strategy).reshape(3, 4)
+    assert (got == ref.block_stat_fp64(g, 3, 4, strategy).numpy()).all()
+    # the reference's fp32 ATen values lie inside the intervals the ranking uses
+    _nom, lo, hi = ranking.block_intervals(raw.numpy(), strategy)
+    lit = ref.block_stat(g, 3, 4, strategy).numpy().reshape(-1)
+    assert np.all(lo <= lit) and np.all(lit <= hi)
+    assert lo[0] == hi[0] == 0.0
 
 
 # ---------------------------------------------------------------- sq-norm + AdamW (DeepSpeed FusedAdam, external)

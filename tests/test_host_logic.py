@@ -244,9 +244,8 @@ def test_rank_channels_matches_reference_heap_on_golden_cases():
     from tests.golden.make_golden import channel_inputs
     spec = json.load(open(os.path.join(GOLDEN, "channel_selection_expected.json")))
     act = channel_inputs()
-    accs = {k: ref.channel_acc_fp64([v]) for k, v in act.items()}
     for case in spec["cases"]:
-        pool = {k: a for k, a in accs.items()
+        pool = {k: a for k, a in act.items()
                 if (k[0] in ("q_proj", "k_proj", "v_proj")) == (case["pool"] == "attention")}
         stats = {k: ref.channel_stat_fp64(a, case["strategy"]).numpy() for k, a in pool.items()}
         out = smt_helper.rank_channels(stats, case["n"], case["selection_strategy"])
