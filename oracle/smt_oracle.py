@@ -395,6 +395,64 @@ def ref_convert(model, selected_mlp, selected_att):
     return model
 
 
+def _attn_name(name):
+    return ('q_proj' if 'q_proj' in name else 'k_proj' if 'k_proj' in name else 'v_proj' if 'v_proj' in name
+            else 'o_proj' if 'o_proj' in name else None)
+
+
+def _mlp_name(name):
+    return 'gate_proj' if 'gate_proj' in name else 'up_proj' if 'up_proj' in name else 'down_proj'
+
+
+def _layer_of(name):
+    match = _LAYER.search(name)
+    return int(match.group(1)) if match else None
+
+
+def freeze_flags(param_names: Sequence[str], select_parameters, select_attention_parameters,
+                 mixture=False, layernorm=False) -> Dict[str, bool]:
+    """smt.py:641-745: the requires_grad each named parameter ends up with."""
+    out = {}
+    for name in param_names:
+        if mixture:
+            if "mlp" in name:
+                out[name] = (_mlp_name(name), _layer_of(name)) in select_parameters.keys()
+            elif "self_attn" in name:
+                out[name] = (_attn_name(name), _layer_of(name)) in select_parameters.keys()
+            elif "embed_tokens" in name:
+                out[name] = ('embed_tokens', None) in select_parameters.keys()
+            elif ("input_layernorm" in name) or ("post_attention_layernorm" in name):
+                out[name] = bool(layernorm)
+            else:
+                out[name] = False
+        else:
+            if "mlp" in name:
+                out[name] = (_mlp_name(name), _layer_of(name)) in select_parameters.keys()
+            elif "self_attn" in name:
+                out[name] = (_attn_name(name), _layer_of(name)) in select_attention_parameters.keys()
+            else:
+                out[name] = False
+    return out
+
+
+def convert_plan(linears: Sequence[Tuple[str, bool]], selected_submatrix, selected_submatrix_attention,
+                 part_module_name=('.layers',), mixture=False) -> Dict[str, list]:
+    """smt.py:83-179: which ``nn.Linear`` (by name, given whether its weight requires grad) becomes an
+    SMT module with which ``index_list`` (``KeyError`` where the reference raises one)."""
+    plan = {}
+    for name, trainable in linears:
+        if not any(part in name for part in part_module_name):
+            continue
+        if "mlp" in name and trainable:
+            plan[name] = list(selected_submatrix[(_mlp_name(name), _layer_of(name))])
+        if "self_attn" in name and trainable:
+            src = selected_submatrix if mixture else selected_submatrix_attention
+            plan[name] = list(src[(_attn_name(name), _layer_of(name))])
+        if mixture and "embed_tokens" in name and trainable:
+            plan[name] = list(selected_submatrix[('embed_tokens', None)])
+    return plan
+
+
 class RefLinearChannel(torch.autograd.Function):
     """smt.py:217-296."""
 

@@ -7,55 +7,86 @@ consumers accumulate into ONE buffer through the GEMM's C operand (``addmm_``, b
 hipBLASLt epilogue reads C once instead of an extra read-read-write pass) and only the last of them
 to run hands it to autograd; the others return ``None`` (a zero contribution).
 
-The consumers are counted at forward time on the input tensor (keyed by its version), so every
-registered consumer must run its backward for the gradient to be handed over -- true for the
-decoder, whose q/k/v and gate/up outputs all feed the loss. A tensor with one consumer takes the
-plain path.
+"Last" is decided when each consumer's backward runs, not counted at forward time: every consumer
+records its autograd node, and a consumer hands the buffer over as soon as no other consumer that
+has not run yet will be executed by the running backward (``torch._C._will_engine_execute_node``).
+So a consumer whose output does not reach the loss, a partial ``torch.autograd.grad``, or separate
+backward calls over different consumers never strand a contribution: each backward pass hands over
+exactly the sum of the consumers it ran. A tensor with one consumer takes the plain path.
 """
 from __future__ import annotations
 
-from typing import Optional
+import weakref
+from typing import List, Optional
 
 import torch
 
 
 class SharedInputGrad:
-    __slots__ = ("version", "consumers", "pending", "buf")
+    __slots__ = ("version", "nodes", "done", "buf")
 
     def __init__(self, version: int):
         self.version = version
-        self.consumers = 0
-        self.pending = 0
+        # weak references to the consumers' autograd nodes (their ctx): the input tensor keeps this
+        # object alive, and the nodes keep the input alive through their saved tensors
+        self.nodes: List[weakref.ref] = []
+        self.done: List[bool] = []
         self.buf: Optional[torch.Tensor] = None
 
+    @property
+    def consumers(self) -> int:
+        return len(self.nodes)
 
-def register(x: torch.Tensor) -> Optional[SharedInputGrad]:
-    """Count one more linear consumer of ``x`` (call from the consumer's forward)."""
-    if not x.requires_grad:
+
+class _Slot:
+    """What one consumer keeps: the shared accumulator and its own position in it."""
+    __slots__ = ("acc", "index")
+
+    def __init__(self, acc: SharedInputGrad, index: int):
+        self.acc = acc
+        self.index = index
+
+
+def register(x: torch.Tensor, node=None) -> Optional[_Slot]:
+    """Count one more linear consumer of ``x`` (call from the consumer's forward with its ``ctx``)."""
+    if not x.requires_grad or node is None:
         return None
     acc = x.__dict__.get("_smt_gacc")
     if acc is None or acc.version != x._version:
         acc = SharedInputGrad(x._version)
         x._smt_gacc = acc
-    acc.consumers += 1
-    return acc
+    acc.nodes.append(weakref.ref(node))
+    acc.done.append(False)
+    return _Slot(acc, len(acc.nodes) - 1)
 
 
-def input_grad(acc: Optional[SharedInputGrad], grad_output: torch.Tensor, mat: torch.Tensor) -> Optional[torch.Tensor]:
+def _others_pending(acc: SharedInputGrad, me: int) -> bool:
+    for i, ref in enumerate(acc.nodes):
+        if i == me or acc.done[i]:
+            continue
+        node = ref()
+        if node is not None and torch._C._will_engine_execute_node(node):
+            return True
+    return False
+
+
+def input_grad(slot: Optional[_Slot], grad_output: torch.Tensor, mat: torch.Tensor) -> Optional[torch.Tensor]:
     """``grad_output [..., out] @ mat [out, in]`` for one consumer; with a shared accumulator, the
-    summed gradient of all consumers from the last one and ``None`` from the others."""
+    summed gradient of the consumers this backward runs from the last of them and ``None`` from the
+    others."""
     lead = grad_output.shape[:-1]
     g2 = grad_output.reshape(-1, grad_output.shape[-1])
+    acc = None if slot is None else slot.acc
     if acc is None or acc.consumers <= 1:
         out = torch.matmul(g2, mat)
         return out.view(*lead, out.shape[-1])
     if acc.buf is None:
         acc.buf = torch.matmul(g2, mat)
-        acc.pending = acc.consumers - 1
     else:
         acc.buf.addmm_(g2, mat)
-        acc.pending -= 1
-    if acc.pending > 0:
+    acc.done[slot.index] = True
+    if _others_pending(acc, slot.index):
         return None
     buf, acc.buf = acc.buf, None
+    acc.done = [False] * len(acc.done)           # a later backward over the same graph starts afresh
     return buf.view(*lead, buf.shape[-1])

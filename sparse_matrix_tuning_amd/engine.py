@@ -104,7 +104,7 @@ class FrozenLinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, weight_t, bias):
         ctx.save_for_backward(weight_t)
-        ctx.acc = dgrad.register(x)
+        ctx.acc = dgrad.register(x, ctx)
         return torch.nn.functional.linear(x, weight, bias)
 
     @staticmethod
@@ -203,19 +203,25 @@ def detach_transposed_weights(model: torch.nn.Module) -> None:
 class _GradSink:
     """Where ``linearZ.backward`` writes one module's fp32 tile gradients."""
 
-    __slots__ = ("buffer", "engine", "buckets", "index")
+    __slots__ = ("buffer", "engine", "group", "buckets", "index")
 
-    def __init__(self, buffer: torch.Tensor, engine: "SMTEngine", buckets: "TileGradBuckets" = None, index: int = 0):
+    def __init__(self, buffer: torch.Tensor, engine: "SMTEngine", group: "_TileGroup" = None,
+                 buckets: "TileGradBuckets" = None, index: int = 0):
         self.buffer = buffer
         self.engine = engine
+        self.group = group
         self.buckets = buckets
         self.index = index
 
     def take_accumulate(self) -> bool:
-        return self.engine._accumulate_tiles
+        """Add to the buffer when this module already wrote into it in the current accumulation
+        window (a later micro-step, or a second backward through the module), else overwrite."""
+        return self.group is not None and self.group.reported[self.index]
 
     def mark_ready(self) -> None:
         """Called by ``linearZ.backward`` once this module's tile-gradient kernels are enqueued."""
+        if self.group is not None:
+            self.group.reported[self.index] = True
         if self.buckets is not None:
             self.buckets.ready(self.index)
 
@@ -225,18 +231,21 @@ class TileGradBuckets:
 
     ``module_ranges``: ascending, contiguous ``(start, end)`` element ranges of the modules in the
     buffer (forward order). Consecutive modules are grouped into buckets of at least
-    ``bucket_elems`` elements. After :meth:`arm`, every :meth:`ready` call counts one module of its
-    bucket; the last one issues ``all_reduce(buffer[bucket], async_op=True)``. The collective is
-    enqueued on the process group's stream behind the current stream's work (the tile-gradient
-    kernels), so it runs while backward continues. :meth:`finish` issues the buckets whose modules
-    did not report (not used in this forward) and makes the current stream wait for all of them."""
+    ``bucket_elems`` elements (``<= 0``: one bucket). After :meth:`arm`, every :meth:`ready` call
+    counts one module of its bucket. Buckets are issued as ``all_reduce(buffer[bucket],
+    async_op=True)`` strictly from the last bucket to the first -- the order backward completes them
+    in -- each as soon as it and every later bucket are complete, so all ranks issue the collectives
+    in the same order whatever the timing. A collective is enqueued on the process group's stream
+    behind the current stream's work (the tile-gradient kernels) and runs while backward continues.
+    :meth:`finish` issues what is left (buckets with a module that did not run backward in this
+    step: the engine zeroed such modules first) and makes the current stream wait for all of them."""
 
     def __init__(self, buffer: torch.Tensor, module_ranges: List[tuple], bucket_elems: int):
         self.buffer = buffer
         self.buckets: List[list] = []          # [start, end, n_modules]
         self.bucket_of: List[int] = []
         for s, e in module_ranges:
-            if not self.buckets or self.buckets[-1][1] - self.buckets[-1][0] >= bucket_elems:
+            if not self.buckets or (bucket_elems > 0 and self.buckets[-1][1] - self.buckets[-1][0] >= bucket_elems):
                 self.buckets.append([s, e, 0])
             b = self.buckets[-1]
             if s != b[1] and b[2]:
@@ -246,20 +255,31 @@ class TileGradBuckets:
             self.bucket_of.append(len(self.buckets) - 1)
         self.pending: List[int] = []
         self.works: list = []
+        self.seen: set = set()
+        self.next = -1                         # next bucket to issue (descending)
         self.armed = False
 
     def arm(self) -> None:
         self.pending = [b[2] for b in self.buckets]
         self.works = [None] * len(self.buckets)
+        self.seen = set()
+        self.next = len(self.buckets) - 1
         self.armed = True
 
     def ready(self, module_index: int) -> None:
         if not self.armed:
             return
         b = self.bucket_of[module_index]
+        if module_index in self.seen:
+            if self.works[b] is not None:
+                raise RuntimeError(f"module {module_index} ran backward again after its gradient bucket was "
+                                   "all-reduced (a module used twice in one step is not supported with DP buckets)")
+            return
+        self.seen.add(module_index)
         self.pending[b] -= 1
-        if self.pending[b] == 0:
-            self._launch(b)
+        while self.next >= 0 and self.pending[self.next] == 0:
+            self._launch(self.next)
+            self.next -= 1
 
     def _launch(self, b: int) -> None:
         start, end, _ = self.buckets[b]
@@ -268,19 +288,97 @@ class TileGradBuckets:
     def finish(self) -> None:
         if not self.armed:
             return
-        for b, w in enumerate(self.works):
-            if w is None:
-                self._launch(b)
+        while self.next >= 0:
+            self._launch(self.next)
+            self.next -= 1
         for w in self.works:
             w.wait()
         self.armed = False
+
+
+class DenseGradBuckets:
+    """Bucketed, backward-overlapped all-reduce of the dense gradients of the full fine-tuning
+    warm-up (fine_tune.py:160-190; DeepSpeed's ``reduce_bucket_size`` buckets, deepspeed_helpers.py:73).
+
+    Parameters are grouped in reverse registration order (the order backward produces their
+    gradients) into buckets of at least ``bucket_elems`` elements. A post-accumulate-grad hook counts
+    each parameter; buckets are issued in order, each as soon as it and every earlier bucket are
+    complete: the bucket's gradients are packed into one flat buffer (same dtype) and all-reduced
+    (sum) asynchronously. :meth:`finish` issues the rest (a parameter without a gradient contributes
+    zeros on every rank), waits, and writes the averaged values back into ``p.grad``."""
+
+    def __init__(self, params: List[torch.Tensor], bucket_elems: int, world: int):
+        self.world = world
+        self.buckets: List[List[torch.Tensor]] = []
+        cur, n = [], 0
+        for p in reversed(params):
+            cur.append(p)
+            n += p.numel()
+            if bucket_elems > 0 and n >= bucket_elems:
+                self.buckets.append(cur)
+                cur, n = [], 0
+        if cur:
+            self.buckets.append(cur)
+        self.bucket_of = {id(p): i for i, b in enumerate(self.buckets) for p in b}
+        self.handles = [p.register_post_accumulate_grad_hook(self._hook) for p in params]
+        self.armed = False
+        self.works: list = []
+        self.flats: list = []
+
+    def arm(self) -> None:
+        self.pending = [len(b) for b in self.buckets]
+        self.works = [None] * len(self.buckets)
+        self.flats = [None] * len(self.buckets)
+        self.seen = set()
+        self.next = 0
+        self.armed = True
+
+    def _hook(self, p: torch.Tensor) -> None:
+        if not self.armed or id(p) in self.seen:
+            return
+        self.seen.add(id(p))
+        self.pending[self.bucket_of[id(p)]] -= 1
+        while self.next < len(self.buckets) and self.pending[self.next] == 0:
+            self._launch(self.next)
+            self.next += 1
+
+    def _launch(self, b: int) -> None:
+        params = self.buckets[b]
+        for p in params:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+        flat = torch.cat([p.grad.reshape(-1) for p in params])
+        self.flats[b] = flat
+        self.works[b] = dist.all_reduce(flat, async_op=True)
+
+    def finish(self) -> None:
+        if not self.armed:
+            return
+        while self.next < len(self.buckets):
+            self._launch(self.next)
+            self.next += 1
+        for b, w in enumerate(self.works):
+            w.wait()
+            flat = self.flats[b].div_(float(self.world))
+            off = 0
+            for p in self.buckets[b]:
+                n = p.numel()
+                p.grad.copy_(flat[off:off + n].view_as(p.grad))
+                off += n
+        self.works, self.flats = [], []
+        self.armed = False
+
+    def remove(self) -> None:
+        for h in self.handles:
+            h.remove()
+        self.handles = []
 
 
 class _TileGroup:
     """All SMT tiles of one optimizer parameter group, packed tile-major."""
 
     def __init__(self, group: dict, modules: List[LinearLayer_MatrixSparsity], device, engine,
-                 bucket_elems: int = 0):
+                 bucket_elems: Optional[int] = None):
         self.group = group
         self.modules = modules
         n_tiles = sum(len(m.tiles) for m in modules)
@@ -292,7 +390,10 @@ class _TileGroup:
         for m in modules:
             ranges.append((off * TILE_ELEMS, (off + len(m.tiles)) * TILE_ELEMS))
             off += len(m.tiles)
-        self.buckets = TileGradBuckets(self.grad, ranges, bucket_elems) if bucket_elems > 0 else None
+        self.ranges = ranges
+        self.reported = [False] * len(modules)          # wrote its tile gradients in this accumulation window
+        # bucket_elems None: one rank, no exchange; <= 0: one bucket for the whole buffer
+        self.buckets = TileGradBuckets(self.grad, ranges, bucket_elems) if bucket_elems is not None else None
         descs, tdescs, off = [], [], 0
         for idx, m in enumerate(modules):
             k = len(m.tiles)
@@ -300,7 +401,7 @@ class _TileGroup:
             view.copy_(m.selected_weight.data)
             m.selected_weight.data = view                       # re-point the Parameter's storage
             m.selected_weight._smt_grad_sink = _GradSink(
-                self.grad[off * TILE_ELEMS:(off + k) * TILE_ELEMS].view(k * 256, 256), engine, self.buckets, idx)
+                self.grad[off * TILE_ELEMS:(off + k) * TILE_ELEMS].view(k * 256, 256), engine, self, self.buckets, idx)
             m.writeback_on_forward = False                      # the AdamW epilogue scatters into W
             m.sync_weight()                                     # W (and W^T) consistent with the tiles now
             wt = getattr(m.weight, "_smt_weight_t", None)
@@ -325,6 +426,17 @@ class _TileGroup:
         self.fp8_groups = [(g, torch.tensor(sorted(cbs), dtype=torch.int32).to(device)) for g, cbs in union.values()]
         self.step = 0
 
+    def begin_window(self) -> None:
+        self.reported = [False] * len(self.modules)
+
+    def zero_unreported(self) -> None:
+        """Modules whose backward did not run in this accumulation window contribute zeros (their
+        slice still holds an earlier step's gradient)."""
+        for i, done in enumerate(self.reported):
+            if not done:
+                s, e = self.ranges[i]
+                self.grad[s:e].zero_()
+
 
 class SMTEngine:
     """``deepspeed.initialize`` result surface: ``backward``, ``step``, ``module``, ``train``/``eval``;
@@ -347,7 +459,6 @@ class SMTEngine:
         self.max_grad_norm = float(cfg.get("gradient_clipping", 0.0) or 0.0)
         self.micro_steps = 0
         self.global_steps = 0
-        self._accumulate_tiles = False
         self.device = next(model.parameters()).device
 
         zero = cfg.get("zero_optimization") or {}
@@ -375,10 +486,13 @@ class SMTEngine:
                     if any(m.weight.dtype != torch.bfloat16 for m in mods):
                         raise NotImplementedError("SMT engine: bf16 models only")
                     self.tile_groups.append(_TileGroup(group, mods, self.device, self,
-                                                       self.reduce_bucket_size if self.world > 1 else 0))
+                                                       self.reduce_bucket_size if self.world > 1 else None))
                 if dense:
                     self.dense_groups.append((group, dense))
         self._norm_sq = torch.zeros(1, dtype=torch.float64, device=self.device)
+        dense_params = [p for _g, ps in self.dense_groups for p in ps]
+        self.dense_buckets = (DenseGradBuckets(dense_params, self.reduce_bucket_size, self.world)
+                              if self.world > 1 and dense_params else None)
 
     # -- DeepSpeed surface ----------------------------------------------------------------------
     def __call__(self, *args, **kwargs):
@@ -402,20 +516,29 @@ class SMTEngine:
 
     def backward(self, loss: torch.Tensor):
         """Scale by 1/gas, run autograd (tile grads land in the packed fp32 buffer), and at the
-        accumulation boundary all-reduce the gradients across ranks."""
-        self._accumulate_tiles = (self.micro_steps % self.gradient_accumulation_steps) != 0
+        accumulation boundary all-reduce the gradients across ranks (bucketed, overlapped with the
+        backward pass)."""
+        if self.micro_steps % self.gradient_accumulation_steps == 0:
+            for tg in self.tile_groups:
+                tg.begin_window()
         if self.gradient_accumulation_steps > 1:
             loss = loss / self.gradient_accumulation_steps
-        boundary = self.is_gradient_accumulation_boundary() and self.world > 1
-        if boundary:
+        boundary = self.is_gradient_accumulation_boundary()
+        exchange = boundary and self.world > 1
+        if exchange:
             for tg in self.tile_groups:
                 tg.buckets.arm()                # tile buckets all-reduce while backward runs
+            if self.dense_buckets is not None:
+                self.dense_buckets.arm()
         loss.backward()
         if boundary:
             for tg in self.tile_groups:
+                tg.zero_unreported()
+        if exchange:
+            for tg in self.tile_groups:
                 tg.buckets.finish()
-            dense = [p.grad for _g, ps in self.dense_groups for p in ps if p.grad is not None]
-            allreduce_gradients([], dense, self.world)
+            if self.dense_buckets is not None:
+                self.dense_buckets.finish()
         return loss
 
     def _grad_scale(self) -> float:
@@ -501,6 +624,9 @@ class SMTEngine:
 
     def release(self):
         """Drop optimizer state and packed buffers (e.g. the warm-up engine before SMT starts)."""
+        if self.dense_buckets is not None:
+            self.dense_buckets.remove()
+            self.dense_buckets = None
         for tg in self.tile_groups:
             for m in tg.modules:
                 if hasattr(m.selected_weight, "_smt_grad_sink"):

@@ -27,6 +27,7 @@ from __future__ import annotations
 from typing import Optional
 
 import os
+import weakref
 
 import torch
 
@@ -207,14 +208,14 @@ class GroupGrad:
     ``prequant``: the members' output gradients already quantised as one row by their producer
     (:func:`swiglu_bwd_quant` for gate/up), used instead of quantising the collected parts."""
 
-    __slots__ = ("version", "group", "registered", "parts", "pending", "prequant")
+    __slots__ = ("version", "group", "nodes", "done", "parts", "prequant")
 
     def __init__(self, version: int, group: Fp8Group):
         self.version = version
         self.group = group
-        self.registered = 0
+        self.nodes = []          # weak references to the members' autograd nodes (dgrad.py)
+        self.done = []
         self.parts = {}
-        self.pending = 0
         self.prequant = None
 
 
@@ -224,12 +225,12 @@ FUSED_SWIGLU_QUANT = os.environ.get("SMT_FP8_FUSED_SWIGLU", "1") != "0"
 FUSED_SWIGLU_FWD_QUANT = os.environ.get("SMT_FP8_FUSED_SWIGLU_FWD", "1") != "0"
 
 
-def tag_group_output(y: torch.Tensor, acc, fw: "Fp8Weight", needs_bf16_grad: bool) -> torch.Tensor:
+def tag_group_output(y: torch.Tensor, reg, fw: "Fp8Weight", needs_bf16_grad: bool) -> torch.Tensor:
     """Mark a group member's output so that its consumer can hand the member's gradient over
     pre-quantised (``needs_bf16_grad``: the member also needs the bf16 gradient itself, e.g. an SMT
-    module's tile weight gradient)."""
-    if acc is not None:
-        y._smt_gout = (acc, fw.group_index, needs_bf16_grad)
+    module's tile weight gradient). ``reg``: what :func:`register_group` returned."""
+    if reg is not None:
+        y._smt_gout = (reg[0], fw.group_index, needs_bf16_grad)
     return y
 
 
@@ -323,29 +324,35 @@ def swiglu_bwd_quant(g: torch.Tensor, u: torch.Tensor, dh: torch.Tensor, need_dg
     return q.view(F8), sq, dg, du
 
 
-def register_group(x: torch.Tensor, fw: Fp8Weight):
-    """Count one more group member reading ``x`` (call from the member's forward); None when the
-    weight is not grouped or ``x`` needs no gradient."""
-    if fw.group is None or not x.requires_grad:
+def register_group(x: torch.Tensor, fw: Fp8Weight, node=None):
+    """Count one more group member reading ``x`` (call from the member's forward with its ``ctx``);
+    None when the weight is not grouped or ``x`` needs no gradient. Returns ``(acc, slot)``."""
+    if fw.group is None or not x.requires_grad or node is None:
         return None
     acc = x.__dict__.get("_smt_gacc8")
     if acc is None or acc.version != x._version or acc.group is not fw.group:
         acc = GroupGrad(x._version, fw.group)
         x._smt_gacc8 = acc
-    acc.registered += 1
-    return acc
+    acc.nodes.append(weakref.ref(node))
+    acc.done.append(False)
+    return acc, len(acc.nodes) - 1
 
 
-def group_input_grad(acc: GroupGrad, fw: Fp8Weight, grad_output: torch.Tensor):
-    """The summed input gradient of all group members from the last one to run (one joint fp8 GEMM
-    when every member of the group took part), None from the others."""
-    if not acc.parts:
-        acc.pending = acc.registered
+def group_input_grad(reg, fw: Fp8Weight, grad_output: torch.Tensor):
+    """The summed input gradient of the group members this backward runs, from the last of them to
+    run (one joint fp8 GEMM when every member of the group took part), None from the others. "Last" is
+    decided by the autograd engine's plan, as in :mod:`..dgrad`: a member whose output does not reach
+    the loss never strands the others' contributions."""
+    acc, slot = reg
     acc.parts[fw.group_index] = grad_output
-    acc.pending -= 1
-    if acc.pending > 0:
-        return None
+    acc.done[slot] = True
+    for i, ref in enumerate(acc.nodes):
+        if i != slot and not acc.done[i]:
+            node = ref()
+            if node is not None and torch._C._will_engine_execute_node(node):
+                return None
     parts, acc.parts = acc.parts, {}
+    acc.done = [False] * len(acc.done)
     g = acc.group
     lead = grad_output.shape[:-1]
     pre, acc.prequant = acc.prequant, None
@@ -377,7 +384,7 @@ class Fp8LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, fw, bias):
         ctx.fw = fw
-        ctx.gacc = register_group(x, fw)
+        ctx.gacc = register_group(x, fw, ctx)
         y = fp8_linear_forward(x, fw)
         return tag_group_output(y if bias is None else y + bias, ctx.gacc, fw, False)
 

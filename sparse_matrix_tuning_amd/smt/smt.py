@@ -281,10 +281,10 @@ class linearZ(torch.autograd.Function):
         # or run as one joint GEMM (fp8 group)
         fw = getattr(weight, "_smt_fp8", None)
         if fw is None:
-            ctx.acc = dgrad.register(input)
+            ctx.acc = dgrad.register(input, ctx)
         else:
             from ..fp8 import register_group, tag_group_output
-            ctx.acc = register_group(input, fw)
+            ctx.acc = register_group(input, fw, ctx)
             # the tile weight gradient reads the bf16 output gradient: ask the consumer for it
             return tag_group_output(_dense_forward(input, weight), ctx.acc, fw, True)
         return _dense_forward(input, weight)

@@ -1,0 +1,103 @@
+"""Worker of tests/test_gpu_dp_equivalence.py (run as a child process, never collected by pytest).
+
+    python tests/dp_equivalence_worker.py --mode acc --out a.pt
+    python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port P \
+        tests/dp_equivalence_worker.py --mode dp --out d.pt
+
+One full fine-tuning warm-up step with the gradient harvest, selection + conversion, then one SMT
+step (fused clip + AdamW), of a 2-layer mini-LLaMA (fused HIP ops, smt_flash attention) on cuda:0:
+
+* ``dp``: 2 ranks (gloo; both on cuda:0), micro-batch 2 each: the engine's bucketed all-reduce of
+  the dense warm-up gradients and of the packed tile gradients, the rank-0 selection broadcast;
+* ``acc``: 1 rank, the same two micro-batches as 2 gradient-accumulation micro-steps;
+* ``big``: 1 rank, the concatenated micro-batch of 4.
+
+Writes the post-warm-up weights, the selection, the tile optimizer state and the SMT modules'
+weights after the SMT step (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mode", choices=("dp", "acc", "big"), required=True)
+    ap.add_argument("--out", required=True)
+    args = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    if world > 1:
+        dist.init_process_group("gloo")
+
+    import bench
+    from sparse_matrix_tuning_amd import trainer
+    from sparse_matrix_tuning_amd.engine import SMTFusedAdam, initialize
+    from sparse_matrix_tuning_amd.fused_llama import patch_llama
+    from sparse_matrix_tuning_amd.smt.smt import LinearLayer_MatrixSparsity
+
+    cfg = dict(bench.MODELS["mini"])
+    cfg["num_hidden_layers"] = 2
+    bench.MODELS["_dp"] = cfg
+    model = bench.build_model("_dp", dev)
+    patch_llama(model)
+    model.train()
+    vocab = cfg["vocab_size"]
+
+    def halves(offset):
+        full = bench.batches(1, 4, 128, vocab, 0, dev, offset=offset)[0]
+        parts = [{k: v[2 * i:2 * i + 2] for k, v in full.items()} for i in range(2)]
+        if args.mode == "big":
+            return [full]
+        if args.mode == "dp":
+            return [parts[rank]]
+        return parts
+
+    micro = 4 if args.mode == "big" else 2
+    ds = {"gradient_clipping": 1.0, "train_micro_batch_size_per_gpu": micro, "train_batch_size": 4,
+          "reduce_bucket_size": 300000}                 # several buckets on this small model
+    dims = trainer.get_targeted_module_dims(model)
+    n_att, n_mlp = trainer.block_budgets(trainer.count_total_blocks(model), 0.05, 0.05)
+    opt = SMTFusedAdam(model.parameters(), lr=1e-3, betas=(0.9, 0.95))
+    engine, opt, _, _ = initialize(model=model, optimizer=opt, config=ds)
+    harvester = trainer.GradHarvester(model, n_mlp, n_att)
+    for b in halves(1000):
+        engine.backward(engine(**b, use_cache=False).loss)
+        if engine.is_gradient_accumulation_boundary():
+            harvester.harvest()                          # the DP-averaged (accumulated) gradients
+        engine.step()
+    warm = {n: p.detach().cpu().clone() for n, p in model.named_parameters()}
+    engine, opt, sched, sel_mlp, sel_att = trainer.select_and_convert(
+        engine, harvester, dims, n_att, n_mlp, calculate_strategy="abs_mean", smt_lr=1e-3, num_training_steps=10,
+        ds_config=ds)
+    for b in halves(2000):
+        loss = engine(**b, use_cache=False).loss
+        engine.backward(loss)
+        engine.step()
+    torch.cuda.synchronize()
+    tg = engine.tile_groups[0]
+    out = {"warm": warm, "sel_mlp": [(k, list(v)) for k, v in sel_mlp.items()],
+           "sel_att": [(k, list(v)) for k, v in sel_att.items()],
+           "master": tg.master.cpu(), "exp_avg": tg.exp_avg.cpu(), "exp_avg_sq": tg.exp_avg_sq.cpu(),
+           "W": {n: m.weight.detach().cpu().clone() for n, m in model.named_modules()
+                 if isinstance(m, LinearLayer_MatrixSparsity)},
+           "buckets": len(tg.buckets.buckets) if tg.buckets is not None else 0}
+    if rank == 0:
+        torch.save(out, args.out)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

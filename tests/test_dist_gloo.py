@@ -100,3 +100,86 @@ def test_gloo_world2_bucketed_tile_allreduce():
     for p in procs:
         p.join(timeout=60)
     assert res == {0: True, 1: True}
+
+
+def _dense_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from sparse_matrix_tuning_amd.engine import DenseGradBuckets
+    torch.manual_seed(0)                                # same weights on both ranks
+    net = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 4))
+    unused = torch.nn.Parameter(torch.ones(3))          # never gets a gradient
+    params = [unused] + list(net.parameters())         # reversed: last layer first, `unused` last
+    buckets = DenseGradBuckets(params, bucket_elems=50, world=world)
+    ok = [[p.numel() for p in b] for b in buckets.buckets] == [[4, 64], [16, 128], [3]]
+    x = torch.randn(5, 8, generator=torch.Generator().manual_seed(10 + rank))
+    for step in range(2):
+        for p in params:
+            p.grad = None
+        buckets.arm()
+        net(x).pow(2).sum().backward()
+        ok &= buckets.next >= 1                         # the last layer's bucket went out during backward
+        local = [p.grad.clone() for p in net.parameters()]
+        gathered = [[torch.zeros_like(g) for _ in range(world)] for g in local]
+        buckets.finish()
+        for g, bucket in zip(local, gathered):
+            dist.all_gather(bucket, g)
+        ok &= all(torch.allclose(p.grad, sum(b) / world) for p, b in zip(net.parameters(), gathered))
+        ok &= torch.equal(unused.grad, torch.zeros(3))
+    buckets.remove()
+    q.put((rank, bool(ok)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_bucketed_dense_allreduce():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dense_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: True, 1: True}
+
+
+def _order_worker(rank, world, port, q):
+    """Buckets are issued in the same order on every rank whatever order their modules report in."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from sparse_matrix_tuning_amd.engine import TileGradBuckets
+    ranges = [(i * 16, (i + 1) * 16) for i in range(4)]
+    buf = torch.full((64,), float(rank + 1))
+    b = TileGradBuckets(buf, ranges, bucket_elems=16)  # one module per bucket
+    b.arm()
+    order = [0, 3, 1, 2] if rank == 0 else [3, 2, 1, 0]
+    issued = []
+    for i in order:
+        b.ready(i)
+        issued.append([w is not None for w in b.works])
+    b.finish()
+    ok = torch.equal(buf, torch.full((64,), 3.0))
+    if rank == 0:           # 0 first: nothing may go out before bucket 3 (the last) does
+        ok &= issued[0] == [False] * 4 and issued[1] == [False, False, False, True]
+    b2 = TileGradBuckets(buf, ranges, bucket_elems=0)  # <= 0: one bucket
+    ok &= len(b2.buckets) == 1
+    q.put((rank, bool(ok)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_bucket_issue_order_is_rank_independent():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_order_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: True, 1: True}

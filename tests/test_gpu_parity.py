@@ -286,7 +286,9 @@ def test_engine_sink_grads_are_fp32_and_exact():
 # ------------------------------------------------------------------ end to end: mini LLaMA vs oracle
 def test_end_to_end_mini_llama_loss_matches_reference_restatement():
     """Same weights, same batch: loss of the SMT model on MI355X vs the CPU restatement of the
-    reference modules (smt.py:302-413); tile grads through the whole network."""
+    reference modules (smt.py:302-413). Tile grads: per module against fp64 truth from the module's
+    own bf16 input and output gradient, bar max(1e-3, 1.1 x the reference algorithm's error on the
+    same operands)."""
     torch.manual_seed(10)
     model = _mini_llama(2)
     sd = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
@@ -294,9 +296,20 @@ def test_end_to_end_mini_llama_loss_matches_reference_restatement():
     sel_att = defaultdict(list, {('v_proj', 1): [(0, 1)], ('q_proj', 0): [(1, 1)]})
     smt.freeze_unselected_matrix_layer(model, sel_mlp, sel_att)
     smt.convert_linear_layer_to_matrix_sparsity(model, sel_mlp, sel_att)
+    gpu_mods = {n: m for n, m in model.named_modules() if isinstance(m, smt.LinearLayer_MatrixSparsity)}
+    seen_x, seen_g = {}, {}
+
+    def capture(name):
+        def hook(_m, inp, out):
+            seen_x[name] = inp[0].detach().clone()
+            out.register_hook(lambda g: seen_g.__setitem__(name, g.detach().clone()))
+        return hook
+    handles = [m.register_forward_hook(capture(n)) for n, m in gpu_mods.items()]
     ids = torch.randint(0, 4096, (2, 128), generator=torch.Generator().manual_seed(0))
     out = model(input_ids=ids.to(DEV), labels=ids.to(DEV), use_cache=False)
     out.loss.backward()
+    for h in handles:
+        h.remove()
 
     import bench
     from transformers import LlamaConfig, LlamaForCausalLM
@@ -312,12 +325,16 @@ def test_end_to_end_mini_llama_loss_matches_reference_restatement():
     out_ref.loss.backward()
     rel = abs(out.loss.item() - out_ref.loss.item()) / abs(out_ref.loss.item())
     assert rel <= 1e-3, (out.loss.item(), out_ref.loss.item())
-    gpu_mods = {n: m for n, m in model.named_modules() if isinstance(m, smt.LinearLayer_MatrixSparsity)}
     cpu_mods = {n: m for n, m in cpu.named_modules() if isinstance(m, ref.RefLinearLayer_MatrixSparsity)}
     assert sorted(gpu_mods) == sorted(cpu_mods)
-    for n in gpu_mods:
-        e = _rel(gpu_mods[n].selected_weight.grad, cpu_mods[n].selected_weight.grad)
-        assert e < 3e-2, (n, e)      # whole-network bf16 pipelines on two devices
+    for n, m in gpu_mods.items():
+        x, g = seen_x[n].cpu(), seen_g[n].cpu()
+        truth = ref.tile_grads_fp64(g, x, m.index_list)
+        _gi, ref_gw = ref.linearz_backward(g, x, m.weight.detach().cpu(), m.index_list)
+        err = _rel(m.selected_weight.grad, truth)
+        assert err <= max(1e-3, 1.1 * _rel(ref_gw, truth)), (n, err)
+        # and across devices (different stock kernels upstream feed each side's modules)
+        assert _rel(m.selected_weight.grad, cpu_mods[n].selected_weight.grad) < 3e-2, n
 
 
 def test_shared_input_data_gradients_accumulate_once():
@@ -340,3 +357,28 @@ def test_shared_input_data_gradients_accumulate_once():
         outs = [net.q(xi), net.k(xi), net.v(xi)]
         torch.autograd.backward(outs, gs)
         assert _rel(xi.grad, truth) < 5e-3, transposed
+
+
+def test_shared_input_consumer_off_the_loss_keeps_the_others_gradient():
+    """one of q/k/v's outputs does not reach the loss; the input gradient is
+    still the sum of the two consumers that ran (SMT modules and a frozen nn.Linear, with and without
+    the transposed copies the engine attaches)."""
+    from sparse_matrix_tuning_amd.engine import attach_transposed_weights
+    torch.manual_seed(13)
+    net = nn.Module()
+    Ws = [nn.Parameter((torch.randn(o, 512) * 0.05).bfloat16().to(DEV), requires_grad=False) for o in (512, 256)]
+    net.q = smt.LinearLayer_MatrixSparsity(Ws[0], index_list=[(1, 1)])
+    net.k = smt.LinearLayer_MatrixSparsity(Ws[1], index_list=[(0, 0)])
+    net.v = nn.Linear(512, 256, bias=False).to(DEV).bfloat16().requires_grad_(False)
+    x = torch.randn(2, 96, 512).bfloat16().to(DEV)
+    gq = torch.randn(2, 96, 512).bfloat16().to(DEV)
+    gv = torch.randn(2, 96, 256).bfloat16().to(DEV)
+    truth = gq.double() @ net.q.weight.detach().double() + gv.double() @ net.v.weight.detach().double()
+    for transposed in (False, True):
+        if transposed:
+            attach_transposed_weights(net)
+        xi = x.clone().requires_grad_(True)
+        q, _k, v = net.q(xi), net.k(xi), net.v(xi)            # k's output is dropped
+        torch.autograd.backward([q, v], [gq, gv])
+        assert _rel(xi.grad, truth) < 5e-3, transposed
+        assert net.k.selected_weight.grad is None

@@ -327,3 +327,17 @@ def test_tile_index_column_blocks_first_use_order():
     from sparse_matrix_tuning_amd.smt.smt import TileIndex
     t = TileIndex([(1, 6), (0, 2), (1, 2), (3, 6), (2, 0)])
     assert t.column_blocks() == [6, 2, 0]
+
+
+def test_top_level_smt_package_serves_fine_tune_imports():
+    """fine_tune.py:39-40 imports, unchanged, resolve to the MI355X implementation."""
+    from smt.smt import (convert_linear_layer_to_matrix_sparsity, get_optimizer_sparse_grouped_parameters,  # noqa: F401
+                         get_optimizer_qk_augment_grouped_parameters, freeze_unselected_matrix_layer,
+                         freeze_unselected_channel_layer, convert_linear_layer_to_channel_sparsity)
+    from smt.smt_helper import (select_submatrix_based_on_grads, get_blocks, get_named_linears,  # noqa: F401
+                                select_channel_based_on_activation)
+    import smt.smt as top
+    assert top.LinearLayer_MatrixSparsity is smt.LinearLayer_MatrixSparsity
+    assert select_submatrix_based_on_grads is smt_helper.select_submatrix_based_on_grads
+    import torch.distributed as dist
+    assert not dist.is_initialized()                 # no process group at import (smt.py:20 does one)
