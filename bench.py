@@ -18,12 +18,17 @@ One process per GPU (RCCL over xGMI for N > 1, weak scaling: B=16 x S=2048 per G
    (ratios 0.00356, = 57.1 M trainable params = 0.71 %), MLP scored ``abs_mean``, attention
    ``mean_abs``.
 4. SMT phase: W untimed steps, then K timed steps (forward + engine.backward + engine.step),
-   bracketed by barrier + synchronize; the max over ranks is reported.
+   bracketed by barrier + synchronize; the max over ranks is reported. ``value`` is the K steps'
+   tokens over their wall time; HIP events at the step boundaries also give the median step
+   (BASELINE.md's definition: median over steps 10-60 after the conversion = the defaults).
+   The reference's memory policy (per-layer recompute) is then timed over as many steps
+   (``grad_ckpt_mode``).
 
 Rank 0 prints ONE JSON line. ``roofline`` is for the dominant hand-written kernel (the grouped
 tile-wgrad, smt_tile_wgrad = wgrad_dma + wgrad_reduce), timed with HIP events on its launch
-stream over the timed region. ``cpu_baseline`` times the oracle's restatement of the reference path
-(oracle/smt_oracle.py) on this host's cores.
+stream over the timed region, against the MFMA roof (its HBM rate on counter bytes beside it).
+``cpu_baseline`` times the oracle's restatement of the reference path (oracle/smt_oracle.py) on this
+host's cores for BASELINE.md's four units, each beside the same unit on the GPU.
 """
 from __future__ import annotations
 
@@ -58,8 +63,9 @@ MODELS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    # defaults: BASELINE.md's definition, steps 10-60 after the conversion (10 untimed, 50 timed)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--model", default="llama3-8b", choices=sorted(MODELS))
     ap.add_argument("--batch", type=int, default=16, help="per-GPU micro batch (deepspeed/README.md:39)")
     ap.add_argument("--seq", type=int, default=2048)
@@ -73,9 +79,14 @@ def parse():
                          "fine_tune.py:192 memory policy) for the timed steps; default: activations stay "
                          "resident in HBM (the SMT phase then peaks below the warm-up phase)")
     ap.add_argument("--no-grad-ckpt", action="store_true", help=argparse.SUPPRESS)   # the default now
-    ap.add_argument("--ref-mode-steps", type=int, default=4,
+    ap.add_argument("--ref-mode-steps", type=int, default=None,
                     help="after the timed steps, also time this many steps with gradient checkpointing "
-                         "(reported under 'grad_ckpt_mode'; 0 disables)")
+                         "(reported under 'grad_ckpt_mode'; default: as many as --steps; 0 disables)")
+    ap.add_argument("--tile-spread", default="layers", choices=("layers", "none"),
+                    help="layers: scale each layer's harvested gradients to a common mean |g| before the "
+                         "selection, so the 872 tiles spread over all 32 layers as in a real fine-tune (random "
+                         "init + uniform tokens otherwise concentrate them in layers 0-4); none: select on the "
+                         "raw harvest")
     ap.add_argument("--sdpa-attention", action="store_true",
                     help="keep transformers' sdpa (aotriton) attention instead of the gfx950 flash attention")
     ap.add_argument("--eager-ops", action="store_true",
@@ -90,6 +101,8 @@ def parse():
     default_ratio = (0.0043 if args.fp8 else 0.00356) if args.model == "llama3-8b" else 0.03
     args.att_ratio = default_ratio if args.att_ratio is None else args.att_ratio
     args.mlp_ratio = default_ratio if args.mlp_ratio is None else args.mlp_ratio
+    if args.ref_mode_steps is None:
+        args.ref_mode_steps = args.steps
     return args
 
 
@@ -182,6 +195,88 @@ def install_attn_timer(timer: AttnTimer):
     fn_cls.backward = staticmethod(timer.wrap(bwd, lambda ctx, do: 5 * unit(ctx.saved_tensors[0])))
 
 
+class LaunchTimer:
+    """HIP events around the launches of one wrapped function (current stream)."""
+
+    def __init__(self):
+        self.enabled = False
+        self.records = []      # (start, end, units)
+
+    def wrap(self, fn, units_fn):
+        def timed(*a, **k):
+            if not self.enabled:
+                return fn(*a, **k)
+            s = torch.cuda.current_stream()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            r = fn(*a, **k)
+            e1.record(s)
+            self.records.append((e0, e1, units_fn(*a, **k)))
+            return r
+        return timed
+
+    def summary(self):
+        if not self.records:
+            return None
+        torch.cuda.synchronize()
+        t = sum(a.elapsed_time(b) for a, b, _ in self.records) * 1e-3
+        return dict(launches=len(self.records), seconds=t, units=sum(r[2] for r in self.records))
+
+
+def install_adam_timer(timer: LaunchTimer):
+    """The fused clip + AdamW + scatter over the packed tiles (engine.step), params per launch."""
+    from sparse_matrix_tuning_amd import _hip
+    orig = _hip.adamw_step
+
+    def units(grad, master, *a, tiles=None, n_tiles=0, **k):
+        return master.numel() if tiles is not None else 0
+    _hip.adamw_step = timer.wrap(orig, units)
+
+
+class SelectionTimer:
+    """Wall time (device-synchronised) and gradient elements of the product's selection calls
+    (smt_helper.select_submatrix_based_on_grads as trainer.select_and_convert calls it)."""
+
+    def __init__(self):
+        self.seconds = 0.0
+        self.elements = 0
+        self.reports = []
+
+    def install(self):
+        from sparse_matrix_tuning_amd import trainer
+        from sparse_matrix_tuning_amd.smt import ranking
+        orig = trainer.select_submatrix_based_on_grads
+
+        def timed(grads, *a, **k):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            r = orig(grads, *a, **k)
+            torch.cuda.synchronize()
+            self.seconds += time.perf_counter() - t0
+            self.elements += sum(g.numel() for g in grads.values())
+            rep = dict(ranking.LAST_REPORT)
+            self.reports.append({"flagged_blocks": rep.get("flagged"), "rescored_keys": len(rep.get("rescored_keys", [])),
+                                 "worst_case_bound": rep.get("worst_case_bound")})
+            return r
+        trainer.select_submatrix_based_on_grads = timed
+
+
+@torch.no_grad()
+def spread_over_layers(harvester):
+    """--tile-spread layers: scale every layer's harvested gradients (per pool) to a common mean |g|,
+    so that the reference's selection picks blocks from every layer (a stand-in for the spread a real
+    fine-tune's gradients have; uniform random tokens on a random-init model concentrate the gradient
+    in the first layers). The selection itself is unchanged."""
+    for pool in (harvester.warmup_grads, harvester.attention_warmup_grads):
+        by_layer = {}
+        for key, g in pool.items():
+            by_layer.setdefault(key[1], []).append(g)
+        for layer, gs in by_layer.items():
+            m = torch.stack([g.abs().mean() for g in gs]).mean()
+            for g in gs:
+                g.div_(m)
+
+
 def build_model(name, device):
     from transformers import LlamaConfig, LlamaForCausalLM
     cfg = LlamaConfig(**MODELS[name])
@@ -210,56 +305,284 @@ def batches(n, B, S, vocab, rank, device, offset=0):
 def pmc_traffic(args):
     """HBM bytes per wgrad launch from the committed rocprofv3 --pmc passes of this same bench
     configuration (scripts/pmc_traffic.py; FETCH_SIZE x2 + WRITE_SIZE), or None."""
-    path = os.path.join(ROOT, "profiles", "r01_wgrad_pmc.json")
-    if args.model != "llama3-8b" or not os.path.exists(path):
+    path = None
+    for cand in ("r02_wgrad_pmc.json", "r01_wgrad_pmc.json"):
+        if os.path.exists(os.path.join(ROOT, "profiles", cand)):
+            path = os.path.join(ROOT, "profiles", cand)
+            break
+    if args.model != "llama3-8b" or args.fp8 or path is None:
         return None, None
     with open(path) as f:
         d = json.load(f)
-    return round(d.get("hbm_bytes_per_call", d.get("hbm_bytes_per_launch"))), f"profiles/r01_wgrad_pmc.json ({d['correction']})"
+    return round(d.get("hbm_bytes_per_call", d.get("hbm_bytes_per_launch"))), f"profiles/{os.path.basename(path)} ({d['correction']})"
 
 
-def cpu_baseline(seconds: float, selection_tiles: dict, model_name: str):
-    """Oracle restatement of the reference's SMT linears (smt.py:350-413, per-tile loop, bf16) for
-    one decoder layer at B=1, S=512, timed on this host; scaled to tokens/s of the 32-layer stack."""
-    if seconds <= 0:
-        return None
+def _host_cores() -> int:
+    """The GPU box grants each GPU a CPU share (OMP_NUM_THREADS, 16 per GPU there)."""
+    n = len(os.sched_getaffinity(0))
+    return min(n, int(os.environ.get("OMP_NUM_THREADS", "0")) or n)
+
+
+def _layer_shapes(cfg):
+    h, inter = cfg["hidden_size"], cfg["intermediate_size"]
+    kv = h // cfg["num_attention_heads"] * cfg["num_key_value_heads"]
+    return {"q_proj": (h, h), "k_proj": (kv, h), "v_proj": (kv, h), "o_proj": (h, h),
+            "gate_proj": (inter, h), "up_proj": (inter, h), "down_proj": (h, inter)}
+
+
+def _layer_operands(cfg, S, gen, dtype=torch.bfloat16):
+    ops = {}
+    for name, (o, i) in _layer_shapes(cfg).items():
+        ops[name] = ((torch.randn(o, i, generator=gen) * 0.02).to(dtype), torch.randn(1, S, i, generator=gen).to(dtype),
+                     torch.randn(1, S, o, generator=gen).to(dtype))
+    return ops
+
+
+def cpu_unit_layer(seconds, tiles, cfg, S=2048):
+    """Unit 1, CPU: the reference's SMT linears of one decoder layer (smt.py:350-413: dense forward,
+    per-tile batched-matmul + sum loop, dense data gradient) in bf16 on the host, B=1."""
     from oracle import smt_oracle as ref
-    # the GPU box grants each GPU a CPU share (OMP_NUM_THREADS, 16 per GPU there); use that many threads
-    cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0)))
-    torch.set_num_threads(cores)
-    cfg = MODELS[model_name]
-    h, inter, kv = cfg["hidden_size"], cfg["intermediate_size"], cfg["hidden_size"] // cfg["num_attention_heads"] * cfg["num_key_value_heads"]
-    shapes = {"q_proj": (h, h), "k_proj": (kv, h), "v_proj": (kv, h), "o_proj": (h, h),
-              "gate_proj": (inter, h), "up_proj": (inter, h), "down_proj": (h, inter)}
-    S = 512                      # bounded sample: B=1, S=512 tokens per layer pass
-    gen = torch.Generator().manual_seed(0)
-    mods = []
-    for name, (o, i) in shapes.items():
-        tiles = selection_tiles.get(name, [])
-        W = (torch.randn(o, i, generator=gen) * 0.02).bfloat16()
-        x = torch.randn(1, S, i, generator=gen).bfloat16()
-        g = torch.randn(1, S, o, generator=gen).bfloat16()
-        mods.append((W, x, g, tiles))
+    ops = _layer_operands(cfg, S, torch.Generator().manual_seed(0))
     t0 = time.perf_counter()
-    layers = 0
+    passes = 0
     while True:
-        for W, x, g, tiles in mods:
+        for name, (W, x, g) in ops.items():
             ref.linearz_forward(x, W)
-            if tiles:
-                ref.linearz_backward(g, x, W, tiles)
+            if tiles.get(name):
+                ref.linearz_backward(g, x, W, tiles[name])
             else:
                 torch.matmul(g, W)
-        layers += 1
+        passes += 1
         el = time.perf_counter() - t0
         if el >= seconds:
             break
-    per_layer = el / layers
-    tok_s = S / (per_layer * cfg["num_hidden_layers"])
-    ntiles = sum(len(t) for t in selection_tiles.values())
-    return {"value": tok_s, "unit": "tokens/s", "cores": cores, "kind": "port",
-            "sample": (f"oracle linearZ fwd+bwd (reference per-tile loop, bf16 CPU) of the 7 linears of one "
-                       f"decoder layer, B=1 S={S}, {ntiles} tiles; {layers} layer passes in {el:.1f}s, "
-                       f"scaled x{cfg['num_hidden_layers']} layers; excludes attention/norms/head (optimistic)")}
+    return S * passes / el, f"{passes} passes in {el:.1f}s"
+
+
+def gpu_unit_layer(tiles, cfg, device, S=2048, iters=10):
+    """Unit 1, GPU: the same layer through the product's SMT modules (linearZ)."""
+    from sparse_matrix_tuning_amd.smt.smt import LinearLayer_MatrixSparsity
+    ops = _layer_operands(cfg, S, torch.Generator().manual_seed(0))
+    mods = []
+    for name, (W, x, g) in ops.items():
+        Wd = torch.nn.Parameter(W.to(device), requires_grad=False)
+        m = LinearLayer_MatrixSparsity(Wd, index_list=tiles.get(name, [])) if tiles.get(name) else None
+        mods.append((m, Wd, x.to(device).requires_grad_(True), g.to(device)))
+
+    def run():
+        for m, Wd, x, g in mods:
+            y = m(x) if m is not None else torch.nn.functional.linear(x, Wd)
+            y.backward(g)
+    run()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    return S * iters / (e0.elapsed_time(e1) * 1e-3)
+
+
+def cpu_unit_selection(model_name, layers=4):
+    """Unit 2, CPU: the reference's block scan + heap selection (smt_helper.py:40-146, fp32 ATen on the
+    host) over `layers` layers of the LLaMA-3-8B-shaped pools (bounded sample; elements/s scale
+    linearly in the layer count). Attention: mean_abs, MLP: abs_mean, n = 436 each."""
+    from oracle import smt_oracle as ref
+    cfg = MODELS[model_name]
+    shapes = _layer_shapes(cfg)
+    gen = torch.Generator().manual_seed(5)
+    dims = {k: list(v) for k, v in shapes.items()}
+    pools = {"att": {}, "mlp": {}}
+    for layer in range(layers):
+        for m in ("q_proj", "k_proj", "v_proj"):
+            pools["att"][(m, layer)] = torch.randn(*shapes[m], generator=gen) * 1e-4
+        for m in ("gate_proj", "up_proj", "down_proj"):
+            pools["mlp"][(m, layer)] = torch.randn(*shapes[m], generator=gen) * 1e-4
+    elems = sum(g.numel() for p in pools.values() for g in p.values())
+    t0 = time.perf_counter()
+    ref.select_submatrix(pools["att"], dims, 436)
+    ref.select_submatrix(pools["mlp"], dims, 436, calculate_strategy="abs_mean")
+    el = time.perf_counter() - t0
+    return elems / el, f"{layers} of {cfg['num_hidden_layers']} layers ({elems / 1e9:.2f} G elements) in {el:.1f}s"
+
+
+def cpu_unit_adam(n_params, seconds=5.0):
+    """Unit 3, CPU: DeepSpeed FusedAdam's update restated (oracle.fused_adam_step, fp32 torch on the
+    host) plus the global-norm clip, over n_params parameters."""
+    from oracle import smt_oracle as ref
+    gen = torch.Generator().manual_seed(3)
+    p = torch.randn(n_params, generator=gen) * 0.02
+    g = torch.randn(n_params, generator=gen) * 1e-4
+    m, v = torch.zeros(n_params), torch.zeros(n_params)
+    t0 = time.perf_counter()
+    steps = 0
+    while True:
+        steps += 1
+        coef = ref.clip_coef([g], 1.0)
+        ref.fused_adam_step(p, g * coef, m, v, steps, 9.865e-6, (0.9, 0.95))
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return n_params * steps / el, f"{steps} steps over {n_params / 1e6:.1f} M params in {el:.1f}s"
+
+
+OPT_125M = dict(vocab_size=50272, hidden_size=768, ffn_dim=3072, num_hidden_layers=12, num_attention_heads=12,
+                word_embed_proj_dim=768, max_position_embeddings=2048)
+
+
+def _opt_model(device):
+    from transformers import OPTConfig, OPTForCausalLM
+    cfg = OPTConfig(**OPT_125M)
+    cfg._attn_implementation = "sdpa"
+    torch.manual_seed(1234)
+    prev = torch.get_default_dtype()
+    torch.set_default_dtype(torch.bfloat16)
+    try:
+        with torch.device(device):
+            return OPTForCausalLM(cfg)
+    finally:
+        torch.set_default_dtype(prev)
+
+
+def _opt_batch(step, B=4, S=128):
+    g = torch.Generator().manual_seed(777 + step)
+    ids = torch.randint(2, OPT_125M["vocab_size"], (B, S), generator=g)
+    return {"input_ids": ids, "attention_mask": torch.ones_like(ids), "labels": ids}
+
+
+def gpu_unit_opt(device, steps=10):
+    """Unit 4, GPU: config 1 (OPT-125m SMT(1%): 19 attention tiles, MLP ratio < 0) through the
+    product: one full-FT warm-up step with the harvest, selection + conversion, then timed SMT steps
+    (B=4, S=128 synthetic). Returns (steps/s, selection)."""
+    from sparse_matrix_tuning_amd import trainer
+    from sparse_matrix_tuning_amd.engine import SMTFusedAdam, initialize
+    model = _opt_model(device)
+    dims = trainer.get_targeted_module_dims(model)
+    n_att, n_mlp = trainer.block_budgets(trainer.count_total_blocks(model), 0.01, -1)
+    opt = SMTFusedAdam(model.parameters(), lr=1e-5, betas=(0.9, 0.95))
+    engine, _, _, _ = initialize(model=model, optimizer=opt, config={"gradient_clipping": 1.0})
+    harvester = trainer.GradHarvester(model, n_mlp, n_att)
+    b = {k: v.to(device) for k, v in _opt_batch(0).items()}
+    engine.backward(engine(**b, use_cache=False).loss)
+    harvester.harvest()
+    engine.step()
+    engine, _o, _s, sel_mlp, sel_att = trainer.select_and_convert(engine, harvester, dims, n_att, n_mlp,
+                                                                 smt_lr=1e-4, num_training_steps=100)
+    batches_ = [{k: v.to(device) for k, v in _opt_batch(1 + i).items()} for i in range(steps + 2)]
+
+    def step(b):
+        engine.backward(engine(**b, use_cache=False).loss)
+        engine.step()
+    for b in batches_[:2]:
+        step(b)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for b in batches_[2:]:
+        step(b)
+    torch.cuda.synchronize()
+    rate = steps / (time.perf_counter() - t0)
+    del engine, model
+    torch.cuda.empty_cache()
+    return rate, dict(sel_att)
+
+
+def cpu_unit_opt(sel_att, seconds=10.0):
+    """Unit 4, CPU: the reference's SMT step of config 1 on the host (oracle modules: tile write-back
+    every forward, per-tile wgrad loop; clip + FusedAdam restated), bf16, B=4, S=128."""
+    from oracle import smt_oracle as ref
+    model = _opt_model("cpu")
+    names = [n for n, _ in model.named_parameters()]
+    flags = ref.freeze_flags(names, {}, sel_att)
+    for n, p in model.named_parameters():
+        p.requires_grad = flags[n]
+    ref.ref_convert(model, {}, sel_att)
+    tiles = [m.selected_weight for m in model.modules() if isinstance(m, ref.RefLinearLayer_MatrixSparsity)]
+    master = [t.detach().float() for t in tiles]
+    mom = [(torch.zeros_like(t), torch.zeros_like(t)) for t in master]
+    steps = 0
+    t0 = time.perf_counter()
+    while True:
+        out = model(**_opt_batch(100 + steps), use_cache=False)
+        out.loss.backward()
+        grads = [t.grad.float() for t in tiles]
+        coef = ref.clip_coef(grads, 1.0)
+        steps += 1
+        for t, p, g, (m, v) in zip(tiles, master, grads, mom):
+            ref.fused_adam_step(p, g * coef, m, v, steps, 1e-4)
+            t.data.copy_(p)
+            t.grad = None
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return steps / el, f"{steps} steps in {el:.1f}s"
+
+
+def cpu_baseline(seconds: float, tiles_one_layer: dict, model_name: str, gpu: dict, device):
+    """BASELINE.md CPU-baseline units 1-4 (the oracle's restatement of the reference path timed on this
+    host's cores), each next to the same unit on the GPU. Unit 1 is the headline ``value``."""
+    if seconds <= 0:
+        return None
+    cores = _host_cores()
+    torch.set_num_threads(cores)
+    cfg = MODELS[model_name]
+    units = []
+    gpu_layer = gpu_unit_layer(tiles_one_layer, cfg, device)
+    cpu_layer, s1 = cpu_unit_layer(seconds, tiles_one_layer, cfg)
+    units.append({"unit": 1, "what": "one decoder layer's 7 SMT linears, fwd + bwd, B=1 S=2048 "
+                  f"({sum(len(v) for v in tiles_one_layer.values())} tiles)", "metric": "tokens/s",
+                  "cpu": round(cpu_layer, 2), "gpu": round(gpu_layer, 1), "cpu_sample": s1})
+    if gpu.get("selection"):
+        cpu_sel, s2 = cpu_unit_selection(model_name)
+        units.append({"unit": 2, "what": "block scan + top-n selection (attention mean_abs, MLP abs_mean, n=436 each)",
+                      "metric": "elements/s", "cpu": round(cpu_sel), "gpu": round(gpu["selection"]["elements_per_s"]),
+                      "cpu_sample": s2, "gpu_sample": gpu["selection"]["sample"]})
+    if gpu.get("adam"):
+        cpu_adam, s3 = cpu_unit_adam(gpu["adam"]["params"])
+        units.append({"unit": 3, "what": "sparse AdamW (clip + update) over the trainable tiles", "metric": "params/s",
+                      "cpu": round(cpu_adam), "gpu": round(gpu["adam"]["params_per_s"]), "cpu_sample": s3,
+                      "gpu_sample": gpu["adam"]["sample"]})
+    try:
+        gpu_opt, sel = gpu_unit_opt(device)
+        cpu_opt, s4 = cpu_unit_opt(sel)
+        units.append({"unit": 4, "what": "config 1: OPT-125m SMT(1%) training step (19 attention tiles), B=4 S=128",
+                      "metric": "steps/s", "cpu": round(cpu_opt, 3), "gpu": round(gpu_opt, 2), "cpu_sample": s4})
+    except Exception as exc:                     # keep the headline line even if the side unit fails
+        units.append({"unit": 4, "error": repr(exc)[:300]})
+    for u in units:
+        if "cpu" in u and u["cpu"]:
+            u["gpu_over_cpu"] = round(u["gpu"] / u["cpu"], 1)
+    return {"value": round(cpu_layer, 2), "unit": units[0]["metric"] + " (unit 1: " + units[0]["what"] + ")",
+            "cores": cores, "kind": "port",
+            "sample": "oracle/smt_oracle.py restatement of the reference path on the host CPU; " + s1,
+            "units": units}
+
+
+def _median(xs):
+    xs = sorted(xs)
+    n = len(xs)
+    return xs[n // 2] if n % 2 else 0.5 * (xs[n // 2 - 1] + xs[n // 2])
+
+
+def timed_steps(step, batch_list, world, device):
+    """Run the steps between barrier + synchronize on both sides; HIP events at every step boundary
+    give per-step durations (for the median) without synchronising inside the region."""
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(batch_list) + 1)]
+    t0 = time.perf_counter()
+    evs[0].record()
+    loss = None
+    for i, b in enumerate(batch_list):
+        loss = step(b)
+        evs[i + 1].record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    per_step = [evs[i].elapsed_time(evs[i + 1]) * 1e-3 for i in range(len(batch_list))]
+    return elapsed, per_step, loss
 
 
 def main():
@@ -280,7 +603,7 @@ def main():
 
     from sparse_matrix_tuning_amd import _hip
     _hip.load(build_if_missing=True)
-    from sparse_matrix_tuning_amd.engine import SMTFusedAdam, initialize, linear_lr_lambda
+    from sparse_matrix_tuning_amd.engine import SMTFusedAdam, initialize
     from sparse_matrix_tuning_amd import trainer
 
     timer = WgradTimer()
@@ -288,14 +611,18 @@ def main():
     atimer = AttnTimer()
     if not (args.eager_ops or args.sdpa_attention):
         install_attn_timer(atimer)
+    adam_timer = LaunchTimer()
+    install_adam_timer(adam_timer)
+    sel_timer = SelectionTimer()
+    sel_timer.install()
 
     t_setup = time.time()
     model = build_model(args.model, device)
     if not args.eager_ops:
         from sparse_matrix_tuning_amd.fused_llama import patch_llama
         patch_llama(model, attention=not args.sdpa_attention)
-    # warm-up (full fine-tuning: fp32 master/moments for all 8 B params) always checkpoints;
-    # --no-grad-ckpt turns it off for the SMT phase only (keeps activations in the 288 GB HBM)
+    # warm-up (full fine-tuning: fp32 master/moments for all 8 B params) always checkpoints
+    # (fine_tune.py:192); the SMT phase keeps activations resident unless --grad-ckpt
     model.gradient_checkpointing_enable()
     model.train()
     log(f"model built in {time.time() - t_setup:.1f}s, params {sum(p.numel() for p in model.parameters()) / 1e9:.3f} B")
@@ -328,8 +655,11 @@ def main():
         engine.step()
     torch.cuda.synchronize()
     warm_peak = torch.cuda.max_memory_allocated(device) / 1e9
-    log(f"warm-up {args.full_ft_steps} full-FT steps in {time.time() - t_w:.1f}s, peak {warm_peak:.1f} GB, loss {loss.item():.4f}")
+    warm_s = time.time() - t_w
+    log(f"warm-up {args.full_ft_steps} full-FT steps in {warm_s:.1f}s, peak {warm_peak:.1f} GB, loss {loss.item():.4f}")
     del warm_batches, loss
+    if args.tile_spread == "layers":
+        spread_over_layers(harvester)
 
     # ---- selection + conversion (fine_tune.py:257-384) ----
     t_s = time.time()
@@ -343,10 +673,12 @@ def main():
     n_tiles = sum(len(v) for v in sel_mlp.values()) + sum(len(v) for v in sel_att.values())
     trainable = sum(p.numel() for p in engine.module.parameters() if p.requires_grad)
     total_params = sum(p.numel() for p in engine.module.parameters())
-    log(f"selection+conversion {time.time() - t_s:.1f}s: {n_tiles} tiles, trainable {trainable} "
-        f"({100.0 * trainable / total_params:.3f}% of {total_params})")
+    log(f"selection+conversion {time.time() - t_s:.1f}s (selection {sel_timer.seconds:.2f}s over "
+        f"{sel_timer.elements / 1e9:.2f} G elements; band {sel_timer.reports}): {n_tiles} tiles, trainable "
+        f"{trainable} ({100.0 * trainable / total_params:.3f}% of {total_params})")
     tile_layers = sorted({l for (_m, l) in list(sel_mlp) + list(sel_att) if l is not None})
-    log(f"tiles in {len(sel_mlp) + len(sel_att)} modules of layers {tile_layers}")
+    n_modules = len(sel_mlp) + len(sel_att)
+    log(f"tiles in {n_modules} modules of {len(tile_layers)} layers {tile_layers}")
 
     # ---- SMT phase ----
     if not args.grad_ckpt:
@@ -365,30 +697,21 @@ def main():
 
     for i in range(args.warmup):
         step(smt_batches[i])
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    timer.enabled = True
-    atimer.enabled = True
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        loss = step(smt_batches[args.warmup + i])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    timer.enabled = False
-    atimer.enabled = False
-    t_max = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    timer.enabled = atimer.enabled = adam_timer.enabled = True
+    elapsed, per_step, loss = timed_steps(step, smt_batches[args.warmup:], world, device)
+    timer.enabled = atimer.enabled = adam_timer.enabled = False
+    t_max = torch.tensor([elapsed, _median(per_step)], dtype=torch.float64, device=device)
     peak = torch.tensor([torch.cuda.max_memory_allocated(device) / 1e9], dtype=torch.float64, device=device)
     if world > 1:
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
         dist.all_reduce(peak, op=dist.ReduceOp.MAX)
-    elapsed = t_max.item()
+    elapsed, med = t_max[0].item(), t_max[1].item()
     tokens = world * B * S * args.steps
     value = tokens / elapsed
     w = timer.summary()
     a_sum = atimer.summary()
+    adam = adam_timer.summary()
+    del smt_batches
 
     # ---- the reference's memory policy (per-layer recompute), same engine and tiles ----
     ckpt_mode = None
@@ -398,46 +721,71 @@ def main():
         step(ref_batches[0])
         torch.cuda.synchronize()
         torch.cuda.reset_peak_memory_stats(device)
-        if world > 1:
-            dist.barrier()
-        t1 = time.perf_counter()
-        for b in ref_batches[1:]:
-            step(b)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        r = torch.tensor([time.perf_counter() - t1, torch.cuda.max_memory_allocated(device) / 1e9],
+        el2, per2, _ = timed_steps(step, ref_batches[1:], world, device)
+        r = torch.tensor([el2, _median(per2), torch.cuda.max_memory_allocated(device) / 1e9],
                          dtype=torch.float64, device=device)
         if world > 1:
             dist.all_reduce(r, op=dist.ReduceOp.MAX)
         ckpt_mode = {"grad_ckpt": True, "steps": args.ref_mode_steps,
                      "value": round(world * B * S * args.ref_mode_steps / r[0].item(), 1),
                      "ms_per_step": round(r[0].item() / args.ref_mode_steps * 1e3, 2),
-                     "peak_hbm_gb": round(r[1].item(), 2)}
+                     "median_ms_per_step": round(r[1].item() * 1e3, 2),
+                     "median_tokens_per_s": round(world * B * S / r[1].item(), 1),
+                     "peak_hbm_gb": round(r[2].item(), 2)}
+        engine.module.gradient_checkpointing_disable()
         del ref_batches
 
     if rank == 0:
         per_gpu = value / world
         roofline = None
         if w and w["seconds"] > 0:
-            achieved = w["bytes"] / w["seconds"] / 1e9
+            avg = w["seconds"] / w["launches"]
+            tflops = w["flops"] / w["seconds"] / 1e12
+            alg_bytes = w["bytes"] / w["launches"]
+            alg_gbs = alg_bytes / avg / 1e9
             traffic, tsrc = pmc_traffic(args)
-            roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                        "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
+            # The roof: HBM while the counter bytes are at least ~the algorithmic bytes (no operand slice
+            # is shared between the module's tiles, the bench's spread selection: intensity 128 F/B, below
+            # the 312 F/B ridge); MFMA when L2/MALL reuse brings the real bytes well below them.
+            hbm_bound = traffic is None or traffic >= 0.8 * alg_bytes
+            hbm = {"achieved": round(alg_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                   "frac": round(alg_gbs / PEAK_HBM_GBS, 4),
+                   "on_counter_bytes": None if traffic is None else round(traffic / avg / 1e9, 1),
+                   "frac_on_counter_bytes": None if traffic is None else round(traffic / avg / 1e9 / PEAK_HBM_GBS, 4)}
+            mfma = {"achieved": round(tflops, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(tflops / PEAK_BF16_TFLOPS, 4)}
+            roof = hbm if hbm_bound else mfma
+            roofline = {"bound": "hbm" if hbm_bound else "mfma", "achieved": roof["achieved"], "peak": roof["peak"],
+                        "unit": roof["unit"], "frac": roof["frac"], "traffic": traffic, "traffic_source": tsrc,
                         "kernel": "smt_tile_wgrad (wgrad_dma_kernel + wgrad_reduce_kernel)",
-                        "launches": w["launches"], "avg_launch_us": round(w["seconds"] / w["launches"] * 1e6, 2),
-                        "algorithmic_bytes_per_launch": round(w["bytes"] / w["launches"]),
-                        "mfma_tflops": round(w["flops"] / w["seconds"] / 1e12, 1)}
+                        "launches": w["launches"], "avg_launch_us": round(avg * 1e6, 2),
+                        "algorithmic_bytes_per_launch": round(alg_bytes),
+                        "flops_per_launch": round(w["flops"] / w["launches"]),
+                        "hbm": hbm, "mfma": mfma,
+                        "bytes_note": ("algorithmic bytes per launch = tiles x (2 operand slices T x 256 x 2 B + the "
+                                       "fp32 tile); traffic = FETCH_SIZE x2 + WRITE_SIZE (rocprofv3 --pmc) per call, "
+                                       "including the split-K slabs and their reduce")}
         tiles_by_module = {}
         for (m, _l), v in list(sel_mlp.items()) + list(sel_att.items()):
-            tiles_by_module.setdefault(m, [])
-            tiles_by_module[m].extend(v)
-        per_layer = {m: v[: max(1, round(len(v) / MODELS[args.model]["num_hidden_layers"]))] for m, v in tiles_by_module.items()}
+            tiles_by_module.setdefault(m, []).extend(v)
+        nl = MODELS[args.model]["num_hidden_layers"]
+        per_layer = {m: v[: max(1, round(len(v) / nl))] for m, v in tiles_by_module.items()}
+        gpu_units = {}
+        if sel_timer.seconds > 0:
+            gpu_units["selection"] = {"elements_per_s": sel_timer.elements / sel_timer.seconds,
+                                      "sample": f"{sel_timer.elements / 1e9:.2f} G harvested elements in "
+                                                f"{sel_timer.seconds:.2f}s (GPU scan + host ranking + re-score)"}
+        if adam and adam["units"]:
+            gpu_units["adam"] = {"params": adam["units"] // adam["launches"],
+                                 "params_per_s": adam["units"] / adam["seconds"],
+                                 "sample": f"{adam['launches']} launches of smt_adamw_step over the tiles"}
         # the CPU baseline is a property of the N = 1 line; a multi-GPU run does not repeat it
-        cpu = cpu_baseline(args.cpu_baseline_seconds, per_layer, args.model) if world == 1 else None
+        cpu = (cpu_baseline(args.cpu_baseline_seconds, per_layer, args.model, gpu_units, device)
+               if world == 1 else None)
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "tokens/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2),
+            "median_ms_per_step": round(med * 1e3, 2), "median_tokens_per_s": round(world * B * S / med, 1),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "fp8-e4m3 (rowwise-scaled decoder GEMMs) + bf16" if args.fp8 else "bf16",
             "data": "synthetic (uniform token ids, labels=inputs; random-init weights)",
@@ -446,18 +794,26 @@ def main():
                                    (f"{'DeepSeek-R1-Distill-LLaMA-8B (LLaMA-3-8B architecture)' if args.model == 'llama3-8b' else args.model}"
                                     " SMT(0.86%) fp8 training step (fwd+bwd+sparse AdamW)"),
                        "global_batch": B * world, "seq_len": S, "parallelism": f"dp{world}",
-                       "tiles": n_tiles, "trainable_params": trainable,
+                       "tiles": n_tiles, "tile_modules": n_modules, "tile_layers": len(tile_layers),
+                       "trainable_params": trainable,
+                       "tile_spread": ("layer-normalised harvest (tiles over all layers, as in a real fine-tune)"
+                                       if args.tile_spread == "layers" else "raw harvest"),
+                       "activations": "recomputed per layer (fine_tune.py:192)" if args.grad_ckpt else
+                                      "resident in HBM (MI355X default; the reference's recompute policy: grad_ckpt_mode)",
                        "grad_ckpt": bool(args.grad_ckpt), "full_ft_steps": args.full_ft_steps,
                        "fused_llama_ops": not args.eager_ops,
                        "attention": "sdpa" if (args.eager_ops or args.sdpa_attention) else "smt_flash",
                        "loss": "transformers" if args.eager_ops else "smt_ce"},
             "peak_hbm_gb": round(peak.item(), 2), "warmup_peak_hbm_gb": round(warm_peak, 2),
+            "warmup_full_ft_s_per_step": round(warm_s / max(1, args.full_ft_steps), 2),
+            "selection": {"seconds": round(sel_timer.seconds, 3), "elements": sel_timer.elements,
+                          "band": sel_timer.reports},
             "grad_ckpt_mode": ckpt_mode,
             "step_mfma_frac": (round(per_gpu * F_ALG_GFLOP_PER_TOKEN * 1e9 / (PEAK_BF16_TFLOPS * 1e12), 4)
                                if args.model == "llama3-8b" else None),
             "roofline": roofline,
             "roofline_attention": None if not a_sum else {
-                "bound": "mfma", "kernel": "smt_flash causal GQA attention (attn_fwd / attn_delta + attn_dq + attn_dkdv)",
+                "bound": "mfma", "kernel": "smt_flash causal GQA attention (attn_fwd / attn_dq + attn_dkdv)",
                 "achieved": round(a_sum["flops"] / a_sum["seconds"] / 1e12, 1), "peak": PEAK_BF16_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(a_sum["flops"] / a_sum["seconds"] / 1e12 / PEAK_BF16_TFLOPS, 4),
                 "launches": a_sum["launches"], "avg_launch_us": round(a_sum["seconds"] / a_sum["launches"] * 1e6, 1),

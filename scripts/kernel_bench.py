@@ -27,12 +27,20 @@ def timeit(fn, iters=20, warmup=3):
     return e0.elapsed_time(e1) / iters * 1e-3
 
 
+def _split(T, n):
+    ws = _hip.wgrad_workspace_bytes(T, n)
+    return ws // (n * 65536 * 4) if ws else 1
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--T", type=int, default=32768)
     ap.add_argument("--out", type=int, default=14336)
     ap.add_argument("--inp", type=int, default=4096)
     ap.add_argument("--tiles", type=int, nargs="*", default=[1, 8, 27, 64, 128, 256])
+    ap.add_argument("--patterns", nargs="*", default=["random", "clustered"])
+    ap.add_argument("--orders", nargs="*", type=int, default=[0, 1])
+    ap.add_argument("--tag", default=os.environ.get("SMT_WGRAD_SLOTS", "5"))
     args = ap.parse_args()
     dev = torch.device("cuda")
     torch.manual_seed(0)
@@ -41,9 +49,9 @@ def main():
     x = torch.randn(T, args.inp, device=dev).bfloat16()
     rb, cb = args.out // 256, args.inp // 256
     lib = _hip.load()
-    for pattern in ("random", "clustered"):
+    for pattern in args.patterns:
         for n in args.tiles:
-          for use_order in (False, True):
+          for use_order in [bool(o) for o in args.orders]:
             gen = torch.Generator().manual_seed(n)
             if pattern == "random":
                 perm = torch.randperm(rb * cb, generator=gen)[:n].tolist()
@@ -68,7 +76,7 @@ def main():
             flops = 2.0 * T * 65536 * n
             bytes_alg = n * (T * 256 * 2 * 2 + 65536 * 4)
             uniq = (len({r for r, _ in tiles}) + len({c for _, c in tiles})) * T * 512 + n * 65536 * 4
-            print(json.dumps(dict(pattern=pattern, order=use_order, tiles=n, us=round(t * 1e6, 1), alg_tbs=round(bytes_alg / t / 1e12, 3),
+            print(json.dumps(dict(tag=args.tag, pattern=pattern, order=use_order, tiles=n, S=_split(T, n), us=round(t * 1e6, 1), alg_tbs=round(bytes_alg / t / 1e12, 3),
                                   unique_slice_tbs=round(uniq / t / 1e12, 3), tflops=round(flops / t / 1e12, 1),
                                   ws_mb=round(wsb / 2**20, 1))), flush=True)
 

@@ -6,9 +6,19 @@ lost. Here an SMT checkpoint is what is needed to resume bit-for-bi
 base model:
 
 * ``smt_meta.json``: format tag, per-module ``(name, index_list, weight shape)`` in selection
-  order, the optimizer param-group hyper-parameters, step counters, the LR-scheduler state;
+  order, the optimizer param-group hyper-parameters, step counters, the LR-scheduler state, and a
+  fingerprint of every frozen parameter (SMT modules' W with their tile blocks masked out);
 * ``smt_state.safetensors``: the bf16 tiles of every module and, per engine tile group, the fp32
-  master / exp_avg / exp_avg_sq (0.8 GB at the LLaMA-3-8B operating point instead of 16 GB of W).
+  master / exp_avg / exp_avg_sq (0.8 GB at the LLaMA-3-8B operating point);
+* ``smt_frozen.safetensors`` (``include_frozen=True``, the default, as DeepSpeed's
+  ``save_checkpoint`` also saves the module): every other weight of the model as it is now. The
+  full fine-tuning warm-up (fine_tune.py:160-190) changed all of them before the selection, so a
+  freshly loaded base model is NOT what the tiles were trained on. :func:`restore_model` loads them
+  when present and, either way, checks every frozen parameter against its fingerprint and raises on
+  a mismatch instead of resuming on the wrong weights.
+
+Only rank 0 writes (the tiles and the optimizer state are replicated), each file to a temporary
+name first and then renamed; every rank waits at a barrier before returning.
 
 :func:`save_merged_model` writes the plain HF-style state dict with the tiles merged into W and
 no ``selected_weight`` keys (``convert_matrix_sparsity_to_linear_layer`` semantics, smt.py:416-457).
@@ -27,21 +37,69 @@ from safetensors.torch import load_file, save_file
 from .smt.smt import (LinearLayer_MatrixSparsity, _attn_module_name, _layer_number, _mlp_module_name,
                       convert_linear_layer_to_matrix_sparsity, freeze_unselected_matrix_layer)
 
-FORMAT = "smt-mi355x-v1"
+FORMAT = "smt-mi355x-v2"
 META = "smt_meta.json"
 STATE = "smt_state.safetensors"
+FROZEN = "smt_frozen.safetensors"
 
 
 def _smt_modules(model):
     return [(n, m) for n, m in model.named_modules() if isinstance(m, LinearLayer_MatrixSparsity)]
 
 
-def save_checkpoint(engine, save_dir: str, client_state: Optional[dict] = None) -> str:
+def _dist():
+    import torch.distributed as dist
+    return dist if dist.is_available() and dist.is_initialized() else None
+
+
+@torch.no_grad()
+def fingerprint(t: torch.Tensor, tiles=None) -> str:
+    """Order-sensitive integer digest of a tensor's bits (exact, so independent of the reduction
+    order): ``sum_i bits[i] * (i mod 1000003 + 1)`` mod 2^64, with the 256x256 ``tiles`` of a 2-D
+    weight masked to zero first."""
+    t = t.detach()
+    if tiles:
+        t = t.clone()
+        for r, c in tiles:
+            t[r * 256:(r + 1) * 256, c * 256:(c + 1) * 256] = 0
+    t = t.contiguous()
+    itype = {1: torch.uint8, 2: torch.int16, 4: torch.int32, 8: torch.int64}[t.element_size()]
+    bits = t.view(itype).reshape(-1).to(torch.int64)
+    w = torch.arange(bits.numel(), device=bits.device, dtype=torch.int64) % 1000003 + 1
+    digest = int((bits * w).sum().item()) & ((1 << 64) - 1)
+    return f"{t.dtype}:{tuple(t.shape)}:{digest:016x}"
+
+
+def _frozen_fingerprints(model) -> Dict[str, str]:
+    """Every parameter except the trainable tiles; SMT modules' W with the tile blocks masked (they
+    hold the tiles, restored from the checkpoint)."""
+    tiles_of = {id(m.weight): m.index_list for _n, m in _smt_modules(model)}
+    out = {}
+    for name, p in model.named_parameters():
+        if name.endswith("selected_weight"):
+            continue
+        out[name] = fingerprint(p, tiles_of.get(id(p)))
+    return out
+
+
+def _atomic(path: str, write) -> None:
+    tmp = path + ".tmp"
+    write(tmp)
+    os.replace(tmp, path)
+
+
+def save_checkpoint(engine, save_dir: str, client_state: Optional[dict] = None, include_frozen: bool = True) -> str:
     """Write selection + tiles + optimizer state of an :class:`SMTEngine` (DeepSpeed
-    ``engine.save_checkpoint`` counterpart). Returns the directory."""
-    os.makedirs(save_dir, exist_ok=True)
+    ``engine.save_checkpoint`` counterpart), and with ``include_frozen`` every frozen weight.
+    Returns the directory."""
+    dist = _dist()
+    rank = dist.get_rank() if dist is not None else 0
     model = engine.module
     torch.cuda.synchronize()
+    if rank != 0:
+        dist.barrier()
+        return save_dir
+    os.makedirs(save_dir, exist_ok=True)
     tensors: Dict[str, torch.Tensor] = {}
     modules = []
     for name, m in _smt_modules(model):
@@ -59,10 +117,20 @@ def save_checkpoint(engine, save_dir: str, client_state: Optional[dict] = None) 
     meta = {"format": FORMAT, "modules": modules, "groups": groups, "global_steps": engine.global_steps,
             "micro_steps": engine.micro_steps,
             "lr_scheduler": engine.lr_scheduler.state_dict() if engine.lr_scheduler is not None else None,
-            "client_state": client_state or {}}
-    save_file(tensors, os.path.join(save_dir, STATE))
-    with open(os.path.join(save_dir, META), "w") as f:
-        json.dump(meta, f, indent=1, default=_json_default)
+            "client_state": client_state or {}, "frozen_fingerprints": _frozen_fingerprints(model),
+            "includes_frozen": bool(include_frozen)}
+    _atomic(os.path.join(save_dir, STATE), lambda p: save_file(tensors, p))
+    if include_frozen:
+        frozen = {n: p.detach().contiguous().cpu() for n, p in model.named_parameters()
+                  if not n.endswith("selected_weight")}
+        _atomic(os.path.join(save_dir, FROZEN), lambda p: save_file(frozen, p))
+
+    def write_meta(p):
+        with open(p, "w") as f:
+            json.dump(meta, f, indent=1, default=_json_default)
+    _atomic(os.path.join(save_dir, META), write_meta)          # last: its presence marks a complete save
+    if dist is not None:
+        dist.barrier()
     return save_dir
 
 
@@ -77,7 +145,7 @@ def read_selection(load_dir: str) -> Tuple[dict, dict]:
     checkpoint, keyed like fine_tune.py: ``(module_name, layer)``."""
     with open(os.path.join(load_dir, META)) as f:
         meta = json.load(f)
-    if meta.get("format") != FORMAT:
+    if meta.get("format") not in (FORMAT, "smt-mi355x-v1"):
         raise ValueError(f"not an SMT checkpoint: {meta.get('format')}")
     sel_mlp, sel_att = defaultdict(list), defaultdict(list)
     for mod in meta["modules"]:
@@ -91,10 +159,24 @@ def read_selection(load_dir: str) -> Tuple[dict, dict]:
 
 
 def restore_model(model, load_dir: str):
-    """Re-apply a checkpoint's selection to a freshly loaded BASE model (same weights as at
-    selection time): freeze -> convert (smt.py:641-745, 83-134) -> load the saved tiles and scatter
-    them into W. Returns the model."""
+    """Re-apply a checkpoint to a model of the same architecture: load the saved frozen weights when
+    the checkpoint has them (the post-warm-up weights), freeze -> convert (smt.py:641-745, 83-134),
+    load the saved tiles and scatter them into W, then check every frozen parameter against the
+    checkpoint's fingerprint. A model whose weights are not the ones the checkpoint was saved from
+    (e.g. the pre-warm-up base) raises ``ValueError``. Returns the model."""
+    with open(os.path.join(load_dir, META)) as f:
+        meta = json.load(f)
     sel_mlp, sel_att = read_selection(load_dir)
+    frozen_path = os.path.join(load_dir, FROZEN)
+    if meta.get("includes_frozen") and os.path.exists(frozen_path):
+        frozen = load_file(frozen_path)
+        params = dict(model.named_parameters())
+        missing = [n for n in frozen if n not in params]
+        if missing:
+            raise KeyError(f"checkpoint weights not in the model: {missing[:5]}")
+        with torch.no_grad():
+            for n, t in frozen.items():
+                params[n].data.copy_(t.to(params[n].device))
     freeze_unselected_matrix_layer(model, sel_mlp, sel_att)
     convert_linear_layer_to_matrix_sparsity(model, sel_mlp, sel_att)
     state = load_file(os.path.join(load_dir, STATE))
@@ -105,6 +187,13 @@ def restore_model(model, load_dir: str):
         with torch.no_grad():
             m.selected_weight.data.copy_(t.to(m.selected_weight.device))
         m.sync_weight()
+    want = meta.get("frozen_fingerprints") or {}
+    got = _frozen_fingerprints(model)
+    bad = [n for n, fp in want.items() if got.get(n) != fp]
+    if bad:
+        raise ValueError(f"{len(bad)} frozen weights differ from the checkpoint's (first: {bad[:3]}): restore "
+                         "onto the model the checkpoint was saved from (after the full fine-tuning warm-up), or "
+                         "save with include_frozen=True")
     return model
 
 

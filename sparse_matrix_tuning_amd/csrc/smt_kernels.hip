@@ -291,8 +291,22 @@ void wgrad_partial_kernel(const uint16_t* __restrict__ g, int64_t ldg,
 // ------------------------------------------------------------------------------------------------
 constexpr int kDmaBK = 32;                                 // rows per stage
 constexpr int kDmaImg = kDmaBK * kRowBytes;                // 16 KiB per operand per stage
-constexpr int kDmaSlots = 4;                               // ring slots (2 in flight + 1 computing + 1 WAR margin)
 constexpr int kDmaSlotBytes = 2 * kDmaImg;                 // A + B
+// ring slots: (SLOTS - 2) stages in flight + 1 computing + 1 WAR margin. 4 slots (128 KiB, 2 stages
+// in flight) is the default: 5 slots (160 KiB, the whole LDS of a gfx950 CU, 3 in flight) measured
+// 1-10 % SLOWER at 4-436 tiles, T = 32768 (profiles/r02_wgrad_ring_depth.jsonl): the kernel is not
+// bound by the bytes in flight per CU.
+constexpr int kDmaSlotsDefault = 4;
+
+// s_waitcnt vmcnt(n) for a run-time n in {0, 4, 8, 12} (the immediate must be a constant)
+__device__ __forceinline__ void wait_vm_stages(int stages_in_flight) {
+    switch (stages_in_flight) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    }
+}
 
 typedef __attribute__((address_space(3))) uint8_t lds_u8_t;
 
@@ -321,14 +335,16 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base,
     return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
 }
 
-template <int OUT>
-__global__ __launch_bounds__(kWgThreads, 2)
+template <int OUT, int SLOTS>
+__global__ __launch_bounds__(kWgThreads, 1)
 void wgrad_dma_kernel(const uint16_t* __restrict__ g, int64_t ldg,
                       const uint16_t* __restrict__ x, int64_t ldx,
                       int64_t T, int64_t chunk, int S, int n_tiles,
                       const int32_t* __restrict__ tile_rc, const int32_t* __restrict__ order,
                       void* __restrict__ out_ptr, int accumulate) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kDmaSlots * kDmaSlotBytes];   // 128 KiB, one array
+    static_assert(SLOTS >= 3 && SLOTS <= 5, "ring depth");
+    constexpr int AHEAD = SLOTS - 2;                       // stages in flight beside the one computed
+    __shared__ __attribute__((aligned(16))) uint8_t lds[SLOTS * kDmaSlotBytes];   // one array (T-trap 4a)
 
     const int total = n_tiles * S;
     const int b = blockIdx.x;
@@ -369,7 +385,7 @@ void wgrad_dma_kernel(const uint16_t* __restrict__ g, int64_t ldg,
 
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(lds));
     auto issue = [&](int st) {
-        const uint32_t slot = lds0 + (uint32_t)((st % kDmaSlots) * kDmaSlotBytes);
+        const uint32_t slot = lds0 + (uint32_t)((st % SLOTS) * kDmaSlotBytes);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const uint32_t row0 = (uint32_t)(4 * wave + 2 * j) * kRowBytes;
@@ -392,20 +408,21 @@ void wgrad_dma_kernel(const uint16_t* __restrict__ g, int64_t ldg,
     const uint32_t feat_byte = 2u * (16u * (gi & 1) + 4u * p);
     const uint32_t krow = 8u * (gi >> 1) + q;
 
-    if (nst > 0) issue(0);
-    if (nst > 1) issue(1);
+#pragma unroll
+    for (int i = 0; i < AHEAD; ++i)
+        if (i < nst) issue(i);
     for (int st = 0; st < nst; ++st) {
-        if (st + 2 < nst) {
-            issue(st + 2);
-            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");     // stage st landed (st+1, st+2 in flight)
-        } else if (st + 1 < nst) {
-            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        // 4 DMA instructions per wave per stage: stage st has landed once at most 4 * (stages issued
+        // after it) are outstanding
+        if (st + AHEAD < nst) {
+            issue(st + AHEAD);
+            wait_vm_stages(AHEAD);
         } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            wait_vm_stages(nst - 1 - st);
         }
         __builtin_amdgcn_s_barrier();                              // every wave's DMA for stage st landed
         __builtin_amdgcn_sched_barrier(0);
-        const uint8_t* A = lds + (st % kDmaSlots) * kDmaSlotBytes;
+        const uint8_t* A = lds + (st % SLOTS) * kDmaSlotBytes;
         const uint8_t* B = A + kDmaImg;
 #pragma unroll
         for (int ks = 0; ks < kDmaBK / 16; ++ks) {
@@ -1017,16 +1034,23 @@ int smt_tile_wgrad(const void* grad_out, int64_t ld_grad_out, const void* x, int
     // with SMT_WGRAD_IMPL=reg) the register-staged kernel, which addresses with 64 bits.
     const int64_t max_ld = ld_grad_out > ld_x ? ld_grad_out : ld_x;
     static const bool force_reg = [] { const char* e = getenv("SMT_WGRAD_IMPL"); return e && strcmp(e, "reg") == 0; }();
+    // SMT_WGRAD_SLOTS=5: the 3-in-flight ring (A/B runs); default 4 (2 stages in flight)
+    static const int slots = [] { const char* e = getenv("SMT_WGRAD_SLOTS"); return (e && atoi(e) == 5) ? 5 : kDmaSlotsDefault; }();
     const bool dma = !force_reg && sp.chunk * max_ld * 2 < (int64_t)0x7fffffff;
+#define SMT_WGRAD_DMA(OUT, S_, DST, ACC)                                                                        \
+    do {                                                                                                        \
+        if (slots == 5) hipLaunchKernelGGL((wgrad_dma_kernel<OUT, 5>), grid, block, 0, stream, gp, ld_grad_out, xp, \
+                                           ld_x, T, sp.chunk, S_, n_tiles, tile_rc_dev, order_dev, DST, ACC);  \
+        else hipLaunchKernelGGL((wgrad_dma_kernel<OUT, 4>), grid, block, 0, stream, gp, ld_grad_out, xp, ld_x,     \
+                                T, sp.chunk, S_, n_tiles, tile_rc_dev, order_dev, DST, ACC);                    \
+    } while (0)
     if (sp.S == 1) {
         if (out_dtype == SMT_DTYPE_FP32) {
-            if (dma) hipLaunchKernelGGL(wgrad_dma_kernel<kOutF32>, grid, block, 0, stream, gp, ld_grad_out, xp, ld_x,
-                                        T, sp.chunk, 1, n_tiles, tile_rc_dev, order_dev, grad_tiles, accumulate);
+            if (dma) SMT_WGRAD_DMA(kOutF32, 1, grad_tiles, accumulate);
             else hipLaunchKernelGGL(wgrad_partial_kernel<kOutF32>, grid, block, 0, stream, gp, ld_grad_out, xp, ld_x,
                                     T, sp.chunk, 1, n_tiles, tile_rc_dev, order_dev, grad_tiles, accumulate);
         } else {
-            if (dma) hipLaunchKernelGGL(wgrad_dma_kernel<kOutBF16>, grid, block, 0, stream, gp, ld_grad_out, xp, ld_x,
-                                        T, sp.chunk, 1, n_tiles, tile_rc_dev, order_dev, grad_tiles, accumulate);
+            if (dma) SMT_WGRAD_DMA(kOutBF16, 1, grad_tiles, accumulate);
             else hipLaunchKernelGGL(wgrad_partial_kernel<kOutBF16>, grid, block, 0, stream, gp, ld_grad_out, xp, ld_x,
                                     T, sp.chunk, 1, n_tiles, tile_rc_dev, order_dev, grad_tiles, accumulate);
         }
@@ -1038,8 +1062,7 @@ int smt_tile_wgrad(const void* grad_out, int64_t ld_grad_out, const void* x, int
     if (!aligned16(workspace)) return fail(SMT_E_ALIGN, "smt_tile_wgrad: workspace not 16-byte aligned");
     float* slab = static_cast<float*>(workspace);
     if (dma)
-        hipLaunchKernelGGL(wgrad_dma_kernel<kOutSlab>, grid, block, 0, stream, gp, ld_grad_out, xp, ld_x,
-                           T, sp.chunk, sp.S, n_tiles, tile_rc_dev, order_dev, slab, 0);
+        SMT_WGRAD_DMA(kOutSlab, sp.S, slab, 0);
     else
         hipLaunchKernelGGL(wgrad_partial_kernel<kOutSlab>, grid, block, 0, stream, gp, ld_grad_out, xp, ld_x,
                            T, sp.chunk, sp.S, n_tiles, tile_rc_dev, order_dev, slab, 0);
@@ -1051,6 +1074,7 @@ int smt_tile_wgrad(const void* grad_out, int64_t ld_grad_out, const void* x, int
         hipLaunchKernelGGL(wgrad_reduce_kernel<false>, dim3(n_tiles * 64), dim3(256), 0, stream, slab, sp.S, grad_tiles, accumulate);
     return check_launch("wgrad_reduce_kernel");
 }
+#undef SMT_WGRAD_DMA
 
 static int tile_copy(bool scatter, void* weight, int64_t ld_weight, int32_t elem_bytes, const int32_t* tile_rc_dev,
                      int32_t n_tiles, void* tiles, hipStream_t stream) {

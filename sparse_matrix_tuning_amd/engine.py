@@ -606,13 +606,14 @@ class SMTEngine:
             return None
         return sink.buffer * self._grad_scale()
 
-    def save_checkpoint(self, save_dir: str, tag=None, client_state: Optional[dict] = None) -> str:
-        """DeepSpeed ``save_checkpoint`` surface: selection + tiles + tile optimizer state
-        (:mod:`sparse_matrix_tuning_amd.checkpoint`)."""
+    def save_checkpoint(self, save_dir: str, tag=None, client_state: Optional[dict] = None,
+                        include_frozen: bool = True) -> str:
+        """DeepSpeed ``save_checkpoint`` surface: selection + tiles + tile optimizer state, and the
+        frozen weights (:mod:`sparse_matrix_tuning_amd.checkpoint`)."""
         import os
         from . import checkpoint
         d = os.path.join(save_dir, str(tag)) if tag is not None else save_dir
-        return checkpoint.save_checkpoint(self, d, client_state)
+        return checkpoint.save_checkpoint(self, d, client_state, include_frozen=include_frozen)
 
     def load_checkpoint(self, load_dir: str, tag=None) -> dict:
         """Load the tile optimizer state / counters saved by :meth:`save_checkpoint` into this

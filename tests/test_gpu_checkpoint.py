@@ -114,3 +114,42 @@ def test_selection_roundtrip_and_merged_export(tmp_path):
     up = eng.module.model.layers[0].mlp.up_proj
     w = sd["model.layers.0.mlp.up_proj.weight"]
     assert torch.equal(ref.gather_tiles(w, up.index_list), up.selected_weight.detach().cpu())
+
+
+def test_resume_after_full_ft_warmup(tmp_path):
+    """the warm-up updates every weight before the selection. A checkpoint restored onto a
+    fresh base model must not silently revert them: with the frozen weights saved it resumes
+    bit-identically, without them the fingerprint check refuses the base model."""
+    base_sd = {k: v.clone() for k, v in _base().state_dict().items()}
+
+    def warm(net):
+        opt = SMTFusedAdam(net.parameters(), lr=1e-2, betas=(0.9, 0.95))
+        eng, _, _, _ = initialize(model=net, optimizer=opt, config={"gradient_clipping": 1.0})
+        _step(eng, 99)                                  # one full fine-tuning step: every W moves
+        eng.release()
+        return net
+    a = _engine(warm(_base()))
+    for i in range(4):
+        _step(a, i)
+    b = _engine(warm(_base()))
+    for i in range(2):
+        _step(b, i)
+    b.save_checkpoint(str(tmp_path), tag="full")
+    b.save_checkpoint(str(tmp_path), tag="lean", include_frozen=False)
+    del b
+    fresh = _base()
+    fresh.load_state_dict(base_sd)
+    with pytest.raises(ValueError, match="frozen weights differ"):
+        checkpoint.restore_model(fresh, str(tmp_path / "lean"))
+    net = _base()
+    net.load_state_dict(base_sd)
+    checkpoint.restore_model(net, str(tmp_path / "full"))
+    c = _engine_restored(net)
+    c.load_checkpoint(str(tmp_path), tag="full")
+    for i in range(2, 4):
+        _step(c, i)
+    torch.cuda.synchronize()
+    for ta, tc in zip(a.tile_groups, c.tile_groups):
+        assert torch.equal(ta.master, tc.master) and torch.equal(ta.exp_avg_sq, tc.exp_avg_sq)
+    for (na, pa), (nc, pc) in zip(a.module.named_parameters(), c.module.named_parameters()):
+        assert na == nc and torch.equal(pa, pc), na
