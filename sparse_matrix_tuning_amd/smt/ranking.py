@@ -56,19 +56,22 @@ def gamma(k: int) -> float:
 
 class KeyScores:
     """Scores of one key (module, layer): nominal fp32 values and an interval around each that
-    contains the reference's value, with a callable that computes the exact reference values."""
+    contains the reference's value, with a callable that computes exact reference values.
+
+    ``rescore(flat_indices) -> (covered_flat_indices, fp32 values)`` returns the reference's values
+    of at least the requested elements (a whole key, or the block rows holding them)."""
 
     __slots__ = ("key", "shape", "nominal", "lo", "hi", "exact", "_rescore", "_bounds")
 
     def __init__(self, key: Hashable, shape: tuple, nominal: np.ndarray, lo: np.ndarray, hi: np.ndarray,
-                 rescore: Callable[[], np.ndarray], bounds: Optional[Callable[[bool], tuple]] = None):
+                 rescore: Callable, bounds: Optional[Callable[[bool], tuple]] = None):
         self.key = key
         self.shape = tuple(shape)
         self.nominal = np.asarray(nominal, dtype=np.float32).reshape(-1)
         self.lo = np.asarray(lo, dtype=np.float64).reshape(-1)
         self.hi = np.asarray(hi, dtype=np.float64).reshape(-1)
         # an interval of width zero is an exact value (an all-zero block)
-        self.exact = bool(np.all(self.lo == self.hi))
+        self.exact = self.lo == self.hi
         self._rescore = rescore
         self._bounds = bounds
 
@@ -76,24 +79,45 @@ class KeyScores:
     def size(self) -> int:
         return self.nominal.size
 
-    def make_exact(self) -> bool:
-        """Replace the estimates by the reference's values; False if one fell outside its interval."""
-        vals = np.asarray(self._rescore(), dtype=np.float32).reshape(-1)
-        if vals.size != self.nominal.size:
-            raise RuntimeError(f"re-score of {self.key} returned {vals.size} values, expected {self.nominal.size}")
+    @property
+    def all_exact(self) -> bool:
+        return bool(self.exact.all())
+
+    def make_exact(self, flat: Optional[np.ndarray] = None) -> bool:
+        """Replace the estimates of (at least) ``flat`` (default: every element) by the reference's
+        values; False if one fell outside its interval."""
+        if flat is None:
+            flat = np.arange(self.size)
+        covered, vals = self._rescore(np.asarray(flat, dtype=np.int64))
+        covered = np.asarray(covered, dtype=np.int64).reshape(-1)
+        vals = np.asarray(vals, dtype=np.float32).reshape(-1)
+        if vals.size != covered.size:
+            raise RuntimeError(f"re-score of {self.key} returned {vals.size} values for {covered.size} elements")
         v64 = vals.astype(np.float64)
         finite = np.isfinite(v64)
-        ok = bool(np.all((v64[finite] >= self.lo[finite]) & (v64[finite] <= self.hi[finite])))
-        self.nominal = vals
-        self.lo = v64.copy()
-        self.hi = v64.copy()
-        self.exact = True
+        lo, hi = self.lo[covered], self.hi[covered]
+        ok = bool(np.all((v64[finite] >= lo[finite]) & (v64[finite] <= hi[finite])))
+        self.nominal[covered] = vals
+        self.lo[covered] = v64
+        self.hi[covered] = v64
+        self.exact[covered] = True
         return ok
 
     def widen(self) -> None:
-        """Switch an inexact key to the order-independent bound."""
-        if not self.exact and self._bounds is not None:
-            self.lo, self.hi = self._bounds(True)
+        """Switch the inexact elements to the order-independent bound."""
+        if not self.all_exact and self._bounds is not None:
+            lo, hi = self._bounds(True)
+            keep = ~self.exact
+            self.lo[keep] = np.asarray(lo, dtype=np.float64).reshape(-1)[keep]
+            self.hi[keep] = np.asarray(hi, dtype=np.float64).reshape(-1)[keep]
+
+
+def whole_key(values_fn: Callable[[], np.ndarray]) -> Callable:
+    """A ``rescore`` that computes every element of the key at once."""
+    def rescore(_flat):
+        vals = np.asarray(values_fn(), dtype=np.float32).reshape(-1)
+        return np.arange(vals.size), vals
+    return rescore
 
 
 # ------------------------------------------------------------------------------------------------
@@ -200,7 +224,7 @@ class _Flat:
         self.val = np.concatenate([e.nominal.astype(np.float64) for e in entries])
         self.lo = np.concatenate([e.lo for e in entries])
         self.hi = np.concatenate([e.hi for e in entries])
-        self.exact = np.concatenate([np.full(e.size, e.exact, dtype=bool) for e in entries])
+        self.exact = np.concatenate([e.exact for e in entries])
 
 
 def _key_ranks(entries: Sequence[KeyScores]) -> np.ndarray:
@@ -217,20 +241,25 @@ def _key_ranks(entries: Sequence[KeyScores]) -> np.ndarray:
     return rank
 
 
-def _rescore(entries: Sequence[KeyScores], owners, report: dict) -> bool:
+def _rescore(entries: Sequence[KeyScores], owners: np.ndarray, flats: np.ndarray, report: dict) -> bool:
     ok = True
-    for o in sorted(set(int(x) for x in owners)):
-        e = entries[o]
-        if e.exact:
+    for o in np.unique(owners):
+        e = entries[int(o)]
+        want = flats[owners == o]
+        want = want[~e.exact[want]]
+        if not want.size:
             continue
-        ok &= e.make_exact()
+        before = int(e.exact.sum())
+        ok &= e.make_exact(want)
         report["rescored_keys"].append(e.key)
+        report["rescored_elements"] += int(e.exact.sum()) - before
     return ok
 
 
 def _new_report(kind: str, n: int, entries: Sequence[KeyScores]) -> dict:
     return {"kind": kind, "n": n, "keys": len(entries), "candidates": int(sum(e.size for e in entries)),
-            "flagged": 0, "rescored_keys": [], "iterations": 0, "worst_case_bound": False, "seconds": 0.0}
+            "flagged": 0, "rescored_keys": [], "rescored_elements": 0, "iterations": 0, "worst_case_bound": False,
+            "seconds": 0.0}
 
 
 def _restart_worst_case(entries: Sequence[KeyScores], report: dict) -> None:
@@ -246,7 +275,7 @@ def top_n(entries: Sequence[KeyScores], n: int) -> List[tuple]:
     report = _new_report("no_restriction", n, entries)
     rank = _key_ranks(entries)
     result = None
-    for _ in range(len(entries) + 2):
+    for _ in range(sum(e.size for e in entries) + 2):
         report["iterations"] += 1
         F = _Flat(entries)
         if not np.all(np.isfinite(F.val)):
@@ -272,7 +301,7 @@ def top_n(entries: Sequence[KeyScores], n: int) -> List[tuple]:
             result = [(int(F.owner[i]), int(F.flat[i])) for i in top]
             break
         report["flagged"] += int(undecided.sum())
-        if not _rescore(entries, F.owner[undecided], report):
+        if not _rescore(entries, F.owner[undecided], F.flat[undecided], report):
             _restart_worst_case(entries, report)
     if result is None:                     # cannot happen: every round makes at least one key exact
         raise RuntimeError("SMT ranking did not converge")
@@ -289,19 +318,20 @@ def top_n_per_key(entries: Sequence[KeyScores], n: int) -> List[List[int]]:
     report = _new_report("norm_dist", n, entries)
     out = []
     for e in entries:
-        for _ in range(3):
+        for _ in range(e.size + 3):
             report["iterations"] += 1
             val = e.nominal.astype(np.float64)
             idx = np.arange(e.size)
             if not np.all(np.isfinite(val)):
-                if not e.exact:
-                    _rescore(entries, [entries.index(e)], report)
+                if not e.all_exact:
+                    e.make_exact()
+                    report["rescored_keys"].append(e.key)
                     continue
                 order = np.asarray(sorted(idx.tolist(), key=lambda i: -val[i] if val[i] == val[i] else -math.inf))
             else:
                 order = np.lexsort((idx, -val))
             top, rest = order[:n], order[n:]        # Python slicing, as indices[:n] of smt_helper.py:93
-            if e.exact or not top.size:
+            if e.all_exact or not top.size:
                 out.append([int(i) for i in top])
                 break
             undecided = np.zeros(e.size, dtype=bool)
@@ -311,13 +341,17 @@ def top_n_per_key(entries: Sequence[KeyScores], n: int) -> List[List[int]]:
                     undecided[near] = True
                     undecided[top[e.lo[top] <= e.hi[near].max()]] = True
             undecided[top[_overlaps_in_order(top, e.lo, e.hi)]] = True
+            undecided &= ~e.exact
             if not undecided.any():
                 out.append([int(i) for i in top])
                 break
             report["flagged"] += int(undecided.sum())
-            if not e.make_exact():
-                report["worst_case_bound"] = True          # exact now either way
+            before = int(e.exact.sum())
+            if not e.make_exact(np.nonzero(undecided)[0]):
+                report["worst_case_bound"] = True
+                e.widen()
             report["rescored_keys"].append(e.key)
+            report["rescored_elements"] += int(e.exact.sum()) - before
         else:
             raise RuntimeError("SMT per-key ranking did not converge")
     report["seconds"] = time.perf_counter() - t0
@@ -330,7 +364,7 @@ def _literal_heap(entries: Sequence[KeyScores], n: int, report: dict) -> List[tu
     """Non-finite scores (a diverged warm-up): NaN breaks the total order the fast path relies on,
     so every key is re-scored and the reference's heap loop (smt_helper.py:111-119) runs as written."""
     for i, e in enumerate(entries):
-        if not e.exact:
+        if not e.all_exact:
             e.make_exact()
             report["rescored_keys"].append(e.key)
     report["literal_heap"] = True

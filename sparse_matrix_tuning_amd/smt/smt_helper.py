@@ -114,6 +114,37 @@ def reference_block_stat(grad: torch.Tensor, d1: int, d2: int, strategy: str) ->
     return s.numpy().reshape(-1)
 
 
+# Whether ATen's value of a block equals its value computed over just the block's row of blocks
+# (the per-output reduction order does not depend on the other rows): checked once per strategy and
+# process against the whole key; if it ever differed, whole keys would be re-scored.
+_ROW_SLICE_OK: Dict[str, bool] = {}
+
+
+def block_rescorer(grad: torch.Tensor, d1: int, d2: int, strategy: str):
+    """``rescore(flat)`` for :class:`ranking.KeyScores`: the reference's values of the 256-row block
+    rows holding the requested blocks (reference_block_stat on ``grad[r*256:(r+1)*256]``: the same
+    expression over a slice, 1/d1 of the key's bytes to copy and reduce)."""
+    def rescore(flat):
+        rows = np.unique(np.asarray(flat, dtype=np.int64) // d2)
+        ok = _ROW_SLICE_OK.get(strategy)
+        if ok is None:
+            full = reference_block_stat(grad, d1, d2, strategy)
+            r0 = int(rows[0])
+            part = reference_block_stat(grad[r0 * Block_dimension:(r0 + 1) * Block_dimension], 1, d2, strategy)
+            ok = _ROW_SLICE_OK[strategy] = bool(np.array_equal(part, full[r0 * d2:(r0 + 1) * d2]))
+            if not ok:
+                return np.arange(d1 * d2), full
+        if not ok:
+            return np.arange(d1 * d2), reference_block_stat(grad, d1, d2, strategy)
+        covered, vals = [], []
+        for r in rows:
+            r = int(r)
+            covered.append(np.arange(r * d2, (r + 1) * d2))
+            vals.append(reference_block_stat(grad[r * Block_dimension:(r + 1) * Block_dimension], 1, d2, strategy))
+        return np.concatenate(covered), np.concatenate(vals)
+    return rescore
+
+
 def _to_device(t: torch.Tensor) -> torch.Tensor:
     if t.device.type == "cuda":
         return t if t.dtype == torch.float32 else t.float()
@@ -153,9 +184,9 @@ def score_block_entries(grads: Dict[Hashable, torch.Tensor], targeted_module_dim
         raw = host[off:off + d1 * d2]
         off += d1 * d2
         nominal, lo, hi = ranking.block_intervals(raw, calculate_strategy)
+        g2 = src.reshape(d1 * Block_dimension, d2 * Block_dimension)
         entries.append(ranking.KeyScores(
-            key, (d1, d2), nominal, lo, hi,
-            rescore=lambda src=src, d1=d1, d2=d2: reference_block_stat(src, d1, d2, calculate_strategy),
+            key, (d1, d2), nominal, lo, hi, rescore=block_rescorer(g2, d1, d2, calculate_strategy),
             bounds=lambda worst, raw=raw: ranking.block_intervals(raw, calculate_strategy, worst)[1:]))
     return entries
 
@@ -173,8 +204,7 @@ def _exact_entries(values: Dict[Hashable, np.ndarray]) -> List[ranking.KeyScores
         a = np.asarray(v, dtype=np.float32)
         shape = a.shape if a.ndim else (1,)
         a64 = a.reshape(-1).astype(np.float64)
-        e = ranking.KeyScores(key, shape, a, a64, a64, rescore=lambda a=a: a)
-        e.exact = True
+        e = ranking.KeyScores(key, shape, a, a64, a64, rescore=ranking.whole_key(lambda a=a: a))
         out.append(e)
     return out
 
@@ -327,7 +357,7 @@ def score_channel_entries(activation: Dict[Hashable, object], calculate_strategy
         nominal, lo, hi = ranking.channel_intervals(raw, B, S, calculate_strategy)
         entries.append(ranking.KeyScores(
             key, (C,), nominal, lo, hi,
-            rescore=lambda src=src: reference_channel_stat(src, calculate_strategy),
+            rescore=ranking.whole_key(lambda src=src: reference_channel_stat(src, calculate_strategy)),
             bounds=lambda worst, raw=raw, B=B, S=S: ranking.channel_intervals(raw, B, S, calculate_strategy,
                                                                                worst)[1:]))
     return entries

@@ -29,8 +29,7 @@ def _block_entries(grads, dims, strategy):
         raw = ref.block_raw_fp64(g, d1, d2, strategy).numpy()
         nominal, lo, hi = ranking.block_intervals(raw, strategy)
         out.append(ranking.KeyScores(
-            key, (d1, d2), nominal, lo, hi,
-            rescore=lambda g=g, d1=d1, d2=d2: smt_helper.reference_block_stat(g, d1, d2, strategy),
+            key, (d1, d2), nominal, lo, hi, rescore=smt_helper.block_rescorer(g, d1, d2, strategy),
             bounds=lambda worst, raw=raw: ranking.block_intervals(raw, strategy, worst)[1:]))
     return out
 
@@ -42,7 +41,7 @@ def _channel_entries(act, strategy):
         raw = ref.channel_raw_fp64(a, strategy).numpy()
         nominal, lo, hi = ranking.channel_intervals(raw, B, S, strategy)
         out.append(ranking.KeyScores(key, (C,), nominal, lo, hi,
-                                     rescore=lambda a=a: smt_helper.reference_channel_stat(a, strategy)))
+                                     rescore=ranking.whole_key(lambda a=a: smt_helper.reference_channel_stat(a, strategy))))
     return out
 
 
@@ -185,3 +184,19 @@ def test_non_finite_scores_follow_the_literal_heap():
         want = ref.select_submatrix(g, dims, n, calculate_strategy="abs_mean")
         got = smt_helper._rank_block_entries(_block_entries(g, dims, "abs_mean"), n, "no_restriction")
         assert _items(got) == _items(want), n
+
+
+@pytest.mark.parametrize("strategy", STRATEGIES)
+def test_block_row_rescore_equals_whole_key(strategy):
+    """The host re-score reads only the block rows holding the undecided blocks: ATen's value of a
+    block computed over its row of blocks equals its value in the whole key (checked here on the
+    LLaMA-3-8B q/gate/down shapes, and once per strategy at run time by block_rescorer)."""
+    gen = torch.Generator().manual_seed(8)
+    for r, c in ((4096, 4096), (14336, 4096), (4096, 14336)):
+        x = torch.randn(r, c, generator=gen)
+        d1, d2 = r // 256, c // 256
+        full = smt_helper.reference_block_stat(x, d1, d2, strategy)
+        covered, vals = smt_helper.block_rescorer(x, d1, d2, strategy)(np.array([0, d2 * (d1 // 2) + 3, d1 * d2 - 1]))
+        assert np.array_equal(vals, full[covered])
+        assert covered.size == 3 * d2
+    assert smt_helper._ROW_SLICE_OK[strategy]
