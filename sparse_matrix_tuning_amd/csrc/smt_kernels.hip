@@ -443,6 +443,170 @@ void wgrad_dma_kernel(const uint16_t* __restrict__ g, int64_t ldg,
     wgrad_store<OUT>(acc, out_ptr, tile, s, S, wm, wn, lane, accumulate);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Quarter-tile variant for modules with few tiles (the HBM-bound regime: no two tiles share an
+// operand slice). A 256-thread workgroup owns one 128x128 quarter of a tile for one chunk of T rows
+// (4 waves as 2x2, 64x64 outputs each = 2x2 accumulators of v_mfma_f32_32x32x16_bf16), so a tile
+// splits 4 ways over its OUTPUT before it splits over T: 4x fewer split-K slabs for the same number
+// of workgroups, and two workgroups fit per CU (64 KiB LDS each: a 4-slot ring of 32-row stages of
+// two 32 x 128 bf16 half-slices). The four quarters of a (tile, chunk) are consecutive logical ids,
+// so they run on one XCD at the same time and each half-slice is read from HBM once and from L2 by
+// the quarter beside it. Same LDS-DMA / transposed-read machinery and swizzle as wgrad_dma_kernel;
+// slabs use the same [tile][S][256][256] layout, so wgrad_reduce_kernel is shared.
+// ------------------------------------------------------------------------------------------------
+constexpr int kQThreads = 256;
+constexpr int kQRowBytes = 128 * 2;                         // 256 B: one half-slice row
+constexpr int kQImg = kDmaBK * kQRowBytes;                  // 8 KiB per operand per stage
+constexpr int kQSlotBytes = 2 * kQImg;
+constexpr int kQSlots = 4;
+
+__device__ __forceinline__ uint32_t qimg_off(uint32_t k, uint32_t byte_in_row) {
+    return k * kQRowBytes + (byte_in_row ^ ((k & 3u) << 6));
+}
+
+__device__ __forceinline__ bf16x8_t qtr_frag(const uint8_t* img, uint32_t k, uint32_t byte_in_row) {
+    s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(img + qimg_off(k, byte_in_row)));
+    s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(img + qimg_off(k + 4, byte_in_row)));
+    const s16x8_t both = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8_t, both);
+}
+
+template <int OUT>
+__device__ __forceinline__ void wgrad_store_q(f32x16_t (&acc)[2][2], void* __restrict__ out_ptr, int tile, int s, int S,
+                                              int m0, int n0, int lane, int accumulate) {
+    const int col = lane & 31;
+    const int h = lane >> 5;
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int m = m0 + mb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                const int n = n0 + nb * 32 + col;
+                float v = acc[mb][nb][i];
+                if (OUT == kOutSlab) {
+                    static_cast<float*>(out_ptr)[(int64_t)(tile * S + s) * kTileElems + m * kTile + n] = v;
+                } else if (OUT == kOutF32) {
+                    float* out = static_cast<float*>(out_ptr) + (int64_t)tile * kTileElems;
+                    if (accumulate) v += out[m * kTile + n];
+                    out[m * kTile + n] = v;
+                } else {
+                    uint16_t* out = static_cast<uint16_t*>(out_ptr) + (int64_t)tile * kTileElems;
+                    if (accumulate) v += bf16_bits_to_f32(out[m * kTile + n]);
+                    out[m * kTile + n] = f32_to_bf16_bits(v);
+                }
+            }
+}
+
+template <int OUT>
+__global__ __launch_bounds__(kQThreads, 2)
+void wgrad_quarter_kernel(const uint16_t* __restrict__ g, int64_t ldg,
+                          const uint16_t* __restrict__ x, int64_t ldx,
+                          int64_t T, int64_t chunk, int S, int n_tiles,
+                          const int32_t* __restrict__ tile_rc, const int32_t* __restrict__ order,
+                          void* __restrict__ out_ptr, int accumulate) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kQSlots * kQSlotBytes];     // 64 KiB, one array
+
+    // logical id L = (s * n_tiles + i) * 4 + quarter, dealt XCD-contiguously (bijective remap)
+    const int total = n_tiles * S * 4;
+    const int b = blockIdx.x;
+    const int q8 = total >> 3, r8 = total & 7, xcd = b & 7;
+    const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+    const int qd = L & 3;
+    const int ts = L >> 2;
+    const int s = ts / n_tiles;
+    const int li = ts - s * n_tiles;
+    const int tile = order != nullptr ? order[li] : li;
+    const int qm = qd >> 1, qn = qd & 1;
+    const int r = tile_rc[2 * tile];
+    const int c = tile_rc[2 * tile + 1];
+    const int64_t t_begin = (int64_t)s * chunk;
+    const int64_t t_end = (t_begin + chunk < T) ? (t_begin + chunk) : T;
+    const int rows = (t_end > t_begin) ? (int)(t_end - t_begin) : 0;
+    const int nst = (rows + kDmaBK - 1) / kDmaBK;
+
+    const __amdgpu_buffer_rsrc_t rg = uniform_rsrc(g + t_begin * ldg + (int64_t)r * kTile + qm * 128, (int64_t)rows * ldg * 2);
+    const __amdgpu_buffer_rsrc_t rx = uniform_rsrc(x + t_begin * ldx + (int64_t)c * kTile + qn * 128, (int64_t)rows * ldx * 2);
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1;
+    const int wn = wave & 1;
+
+    // DMA geometry: wave w fills image rows 8w .. 8w+7 of each operand (two 1 KiB instructions of
+    // 4 rows x 256 B); lane l of instruction j lands at row k = 8w + 4j + (l>>4), physical byte
+    // 16*(l&15), which holds logical byte (16*(l&15)) ^ ((k&3) << 6) of that row.
+    int voff_g[2], voff_x[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int k = 8 * wave + 4 * j + (lane >> 4);
+        const int lb = (16 * (lane & 15)) ^ ((k & 3) << 6);
+        voff_g[j] = (int)(k * ldg * 2) + lb;
+        voff_x[j] = (int)(k * ldx * 2) + lb;
+    }
+    const int step_g = (int)(kDmaBK * ldg * 2), step_x = (int)(kDmaBK * ldx * 2);
+
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(lds));
+    auto issue = [&](int st) {
+        const uint32_t slot = lds0 + (uint32_t)((st % kQSlots) * kQSlotBytes);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const uint32_t row0 = (uint32_t)(8 * wave + 4 * j) * kQRowBytes;
+            dma16(rg, __builtin_amdgcn_readfirstlane(slot + row0), voff_g[j] + st * step_g);
+            dma16(rx, __builtin_amdgcn_readfirstlane(slot + kQImg + row0), voff_x[j] + st * step_x);
+        }
+    };
+
+    f32x16_t acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    const int gi = lane >> 4;
+    const int q = (lane >> 2) & 3;
+    const int p = lane & 3;
+    const uint32_t feat_byte = 2u * (16u * (gi & 1) + 4u * p);
+    const uint32_t krow = 8u * (gi >> 1) + q;
+
+    if (nst > 0) issue(0);
+    if (nst > 1) issue(1);
+    for (int st = 0; st < nst; ++st) {
+        if (st + 2 < nst) {
+            issue(st + 2);
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");     // stage st landed (st+1, st+2 in flight)
+        } else if (st + 1 < nst) {
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        const uint8_t* A = lds + (st % kQSlots) * kQSlotBytes;
+        const uint8_t* B = A + kQImg;
+#pragma unroll
+        for (int ks = 0; ks < kDmaBK / 16; ++ks) {
+            bf16x8_t af[2], bfr[2];
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb)
+                af[mb] = qtr_frag(A, ks * 16 + krow, 2u * (wm * 64 + mb * 32) + feat_byte);
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb)
+                bfr[nb] = qtr_frag(B, ks * 16 + krow, 2u * (wn * 64 + nb * 32) + feat_byte);
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb)
+                    acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mb], bfr[nb], acc[mb][nb], 0, 0, 0);
+        }
+    }
+    wgrad_store_q<OUT>(acc, out_ptr, tile, s, S, qm * 128 + wm * 64, qn * 128 + wn * 64, lane, accumulate);
+}
+
 // Sum the S partial slabs of each tile in order s = 0..S-1 (deterministic) and write the tile.
 // 64 workgroups x 256 threads x 4 elements per tile.
 template <bool OUT_F32>
@@ -964,24 +1128,38 @@ void channel_score_kernel(const float* __restrict__ acc, int32_t B, int32_t S, i
 // n = 27 -> S = 9 (243 workgroups, one round); n = 436 -> S = 4 (7 rounds of T/4 instead of 2 rounds
 // of T). S == 1: the tile is written straight from the accumulators.
 constexpr int kCUs = 256;
-struct WgradSplit { int S; int64_t chunk; };
+struct WgradSplit { int S; int64_t chunk; bool quarter; };
+
+// Quarter-tile kernel for modules with at most this many tiles (SMT_WGRAD_QUARTER_MAX; 0 disables).
+// Measured at T = 32768 (profiles/r02_wgrad_quarter.jsonl): 1.1-1.2x faster than the full-tile
+// kernel at 1-8 tiles, even at 16, slower from 27.
+int quarter_max_tiles() {
+    static const int v = [] { const char* e = getenv("SMT_WGRAD_QUARTER_MAX"); return e ? atoi(e) : 8; }();
+    return v;
+}
 
 WgradSplit wgrad_split(int64_t T, int32_t n_tiles) {
-    WgradSplit sp{1, kBK};
+    WgradSplit sp{1, kBK, false};
     if (T <= 0 || n_tiles <= 0) return sp;
-    // Time model (measured rates): a workgroup streams its 1 KiB/row of g+x slices at ~25 GB/s per
-    // CU and, when S > 1, writes a 256 KiB fp32 slab; the reduce re-reads the n*S slabs (~5 TB/s).
     const int64_t s_max = std::max<int64_t>(1, std::min<int64_t>(64, (T + 511) / 512));
-    double best = 1e30;
     int64_t S = 1;
-    for (int64_t cand = 1; cand <= s_max; ++cand) {
-        const int64_t rounds = (n_tiles * cand + kCUs - 1) / kCUs;
-        const double rows = std::ceil((double)T / (double)cand);
-        const double slab = cand > 1 ? 262144.0 : 0.0;
-        const double t_wg = (rows * 1024.0 + slab) / 25e9;
-        const double t_red = cand > 1 ? (double)n_tiles * cand * 262144.0 * 2.0 / 5e12 : 0.0;
-        const double cost = (double)rounds * t_wg + t_red;
-        if (cost < best * (1.0 - 1e-6)) { best = cost; S = cand; }
+    if (n_tiles <= quarter_max_tiles()) {
+        // quarter tiles, two workgroups per CU: fill the 512 workgroup slots once (chunks >= 512 rows)
+        sp.quarter = true;
+        S = std::min<int64_t>(s_max, std::max<int64_t>(1, (2 * kCUs + 4 * n_tiles - 1) / (4 * n_tiles)));
+    } else {
+        // Time model (measured rates): a workgroup streams its 1 KiB/row of g+x slices at ~25 GB/s per
+        // CU and, when S > 1, writes a 256 KiB fp32 slab; the reduce re-reads the n*S slabs (~5 TB/s).
+        double best = 1e30;
+        for (int64_t cand = 1; cand <= s_max; ++cand) {
+            const int64_t rounds = (n_tiles * cand + kCUs - 1) / kCUs;
+            const double rows = std::ceil((double)T / (double)cand);
+            const double slab = cand > 1 ? 262144.0 : 0.0;
+            const double t_wg = (rows * 1024.0 + slab) / 25e9;
+            const double t_red = cand > 1 ? (double)n_tiles * cand * 262144.0 * 2.0 / 5e12 : 0.0;
+            const double cost = (double)rounds * t_wg + t_red;
+            if (cost < best * (1.0 - 1e-6)) { best = cost; S = cand; }
+        }
     }
     int64_t chunk = (T + S - 1) / S;
     chunk = (chunk + kBK - 1) / kBK * kBK;
@@ -1030,6 +1208,7 @@ int smt_tile_wgrad(const void* grad_out, int64_t ld_grad_out, const void* x, int
     const uint16_t* gp = static_cast<const uint16_t*>(grad_out);
     const uint16_t* xp = static_cast<const uint16_t*>(x);
     const dim3 grid(n_tiles * sp.S), block(kWgThreads);
+    const dim3 qgrid(n_tiles * sp.S * 4), qblock(kQThreads);
     // LDS-DMA kernel by default; its 32-bit buffer offsets need chunk * ld * 2 < 2^31, otherwise (and
     // with SMT_WGRAD_IMPL=reg) the register-staged kernel, which addresses with 64 bits.
     const int64_t max_ld = ld_grad_out > ld_x ? ld_grad_out : ld_x;
@@ -1037,9 +1216,12 @@ int smt_tile_wgrad(const void* grad_out, int64_t ld_grad_out, const void* x, int
     // SMT_WGRAD_SLOTS=5: the 3-in-flight ring (A/B runs); default 4 (2 stages in flight)
     static const int slots = [] { const char* e = getenv("SMT_WGRAD_SLOTS"); return (e && atoi(e) == 5) ? 5 : kDmaSlotsDefault; }();
     const bool dma = !force_reg && sp.chunk * max_ld * 2 < (int64_t)0x7fffffff;
+    const bool quarter = dma && sp.quarter;
 #define SMT_WGRAD_DMA(OUT, S_, DST, ACC)                                                                        \
     do {                                                                                                        \
-        if (slots == 5) hipLaunchKernelGGL((wgrad_dma_kernel<OUT, 5>), grid, block, 0, stream, gp, ld_grad_out, xp, \
+        if (quarter) hipLaunchKernelGGL((wgrad_quarter_kernel<OUT>), qgrid, qblock, 0, stream, gp, ld_grad_out, xp, \
+                                        ld_x, T, sp.chunk, S_, n_tiles, tile_rc_dev, order_dev, DST, ACC);     \
+        else if (slots == 5) hipLaunchKernelGGL((wgrad_dma_kernel<OUT, 5>), grid, block, 0, stream, gp, ld_grad_out, xp, \
                                            ld_x, T, sp.chunk, S_, n_tiles, tile_rc_dev, order_dev, DST, ACC);  \
         else hipLaunchKernelGGL((wgrad_dma_kernel<OUT, 4>), grid, block, 0, stream, gp, ld_grad_out, xp, ld_x,     \
                                 T, sp.chunk, S_, n_tiles, tile_rc_dev, order_dev, DST, ACC);                    \

@@ -1,6 +1,7 @@
 """Tile weight gradient at the bench geometry: T = B*S = 16*2048 = 32768 rows,
-the LLaMA-3-8B module shapes, 27-436 tiles per call (the slab path S > 1 and the direct path S == 1 of
-``smt_tile_wgrad``), bf16 and fp32 outputs, accumulation, and linearZ's packed-column input.
+the LLaMA-3-8B module shapes, 4-436 tiles per call (the quarter-tile kernel at <= 8 tiles, the
+full-tile kernel's slab path S > 1 and direct path S == 1), bf16 and fp32 outputs, accumulation,
+and linearZ's packed-column input.
 
 Truth is fp64 on the GPU from the same bf16 operands. The reference's own result (smt.py:397-404:
 one bf16 matmul per sample, each ``[256, 256]`` partial rounded to bf16, then ``sum(dim=0)``) is
@@ -50,7 +51,8 @@ def _reference(go, x, r, c):
     return torch.sum(torch.matmul(g3.permute(0, 2, 1), x3), dim=0)
 
 
-@pytest.mark.parametrize("module,n", [("q_proj", 27), ("q_proj", 256), ("k_proj", 27), ("k_proj", 64),
+@pytest.mark.parametrize("module,n", [("k_proj", 4), ("gate_proj", 8),          # quarter-tile kernel
+                                      ("q_proj", 27), ("q_proj", 256), ("k_proj", 27), ("k_proj", 64),
                                       ("gate_proj", 67), ("gate_proj", 436), ("down_proj", 67), ("down_proj", 436)])
 @pytest.mark.parametrize("out_dtype", [torch.bfloat16, torch.float32])
 def test_tile_wgrad_bench_geometry(module, n, out_dtype):
