@@ -757,7 +757,7 @@ def main():
             roof = hbm if hbm_bound else mfma
             roofline = {"bound": "hbm" if hbm_bound else "mfma", "achieved": roof["achieved"], "peak": roof["peak"],
                         "unit": roof["unit"], "frac": roof["frac"], "traffic": traffic, "traffic_source": tsrc,
-                        "kernel": "smt_tile_wgrad (wgrad_dma_kernel + wgrad_reduce_kernel)",
+                        "kernel": "smt_tile_wgrad (wgrad_dma_kernel | wgrad_quarter_kernel, + wgrad_reduce_kernel when split)",
                         "launches": w["launches"], "avg_launch_us": round(avg * 1e6, 2),
                         "algorithmic_bytes_per_launch": round(alg_bytes),
                         "flops_per_launch": round(w["flops"] / w["launches"]),

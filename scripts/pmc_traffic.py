@@ -27,13 +27,13 @@ def per_dispatch(path, counter):
 def main(fetch_csv, write_csv, out_json):
     f, fn = per_dispatch(fetch_csv, "FETCH_SIZE")
     w, wn = per_dispatch(write_csv, "WRITE_SIZE")
-    # one smt_tile_wgrad call = one main kernel (wgrad_dma / wgrad_partial) + a wgrad_reduce when split
-    main_k = lambda n: "wgrad_dma" in n or "wgrad_partial" in n
+    # one smt_tile_wgrad call = one main kernel (wgrad_dma / wgrad_quarter) + a wgrad_reduce when split
+    main_k = lambda n: "wgrad_dma" in n or "wgrad_quarter" in n or "wgrad_partial" in n
     every = lambda names: [d for d, n in names.items() if "wgrad_" in n]
     calls = lambda names: max(1, sum(1 for n in names.values() if main_k(n)))
     fetch_kib = sum(f[d] for d in every(fn)) / calls(fn)
     write_kib = sum(w[d] for d in every(wn)) / calls(wn)
-    res = {"kernel": "smt_tile_wgrad (wgrad_dma_kernel + wgrad_reduce_kernel)",
+    res = {"kernel": "smt_tile_wgrad (wgrad_dma_kernel | wgrad_quarter_kernel, + wgrad_reduce_kernel when split)",
            "launches_fetch_pass": calls(fn), "launches_write_pass": calls(wn),
            "fetch_kib_per_call_raw": fetch_kib, "write_kib_per_call": write_kib,
            "hbm_bytes_per_call": (2.0 * fetch_kib + write_kib) * 1024.0,
