@@ -24,6 +24,10 @@
  *   smt_adamw_step        DeepSpeed FusedAdam(adam_w_mode=True) step over the tiles
  *                         (deepspeed/fine_tune.py:352,361-363,773; DeepSpeed 0.16.5, external),
  *                         fused with clip, bf16 cast and the tile -> W scatter
+ *   smt_mx_quant_cols,    MX-fp8 (e4m3 + e8m0 per 32 tokens) column blocks and the tile weight
+ *   smt_tile_wgrad_mx     gradient over them (config 5's fp8 tiles; no reference counterpart)
+ *   smt_adamw_multi       the same step over many dense parameters in one launch (the warm-up
+ *                         full fine-tune's FusedAdam multi_tensor_apply, fine_tune.py:352-363)
  *   Channel path (activation-selected rows; SURVEY §8(f) row 1, ABI v3):
  *   smt_row_gather        deepspeed/smt/smt.py:200-204   selected_weight[i, :] = W[index_list[i], :]
  *   smt_row_scatter       deepspeed/smt/smt.py:211-213   per-forward write-back rows -> W
@@ -108,6 +112,15 @@ typedef struct smt_adamw_args {
     int32_t grad_dtype;             /* SMT_DTYPE_BF16 or SMT_DTYPE_FP32            */
 } smt_adamw_args;
 
+typedef struct smt_adamw_tensor {
+    const void* grad;               /* n gradient elements (args->grad_dtype)     */
+    float* master;                  /* n fp32 master values                       */
+    float* exp_avg;
+    float* exp_avg_sq;
+    void* param;                    /* n bf16 parameter values (written)          */
+    int64_t n;
+} smt_adamw_tensor;                 /* all five buffers 16-byte aligned          */
+
 const char* smt_last_error(void);
 int smt_abi_version(void);
 
@@ -177,6 +190,42 @@ int smt_adamw_step(const void* grad, float* master, float* exp_avg, float* exp_a
                    void* param_bf16, const smt_tile_desc* tiles_dev, int32_t n_tiles,
                    int64_t n_elems, const double* grad_sq_norm_dev,
                    const smt_adamw_args* args, hipStream_t stream);
+
+/*
+ * Multi-tensor form of the flat step (ABI v5): one launch over n_tensors independent parameters
+ * sharing the same args (DeepSpeed FusedAdam's multi_tensor_apply over a param group,
+ * fine_tune.py:352-363). tensors_dev: device table; block_start_dev: device int64[n_tensors + 1],
+ * block_start[t] = sum over u < t of ceil(n_u / 2048), n_blocks = block_start[n_tensors].
+ */
+int smt_adamw_multi(const smt_adamw_tensor* tensors_dev, const int64_t* block_start_dev, int32_t n_tensors,
+                    int64_t n_blocks, const double* grad_sq_norm_dev, const smt_adamw_args* args,
+                    hipStream_t stream);
+
+/* ---- MX-fp8 tile weight gradient (ABI v5; BASELINE config 5) -------------
+ * No reference counterpart (the reference has no fp8, deepspeed/fine_tune.py:955-959): the bf16
+ * smt_tile_wgrad (smt.py:397-404) is the bar. "MX column blocks" of a bf16 [T, C] matrix, for a list
+ * of n_blocks 256-column blocks, with ldq = T rounded up to a multiple of 64:
+ *   q       e4m3 (OCP) [n_blocks][256][ldq]   K-major: row f holds column f of the block over T (zero past T)
+ *   scales  e8m0 [n_blocks][ldq/32][256]      exponent e + 127 of each 32-row group of each column
+ * with e the smallest integer such that the group's max |x| <= 448 * 2^e (-127 for an all-zero
+ * group) and q = e4m3_rne(x * 2^-e), so value = e4m3(q) * 2^e exactly reproduces the quantised x.
+ */
+int smt_mx_quant_cols(const void* x, int64_t ld_x, int64_t T, const int32_t* blocks_dev, int32_t n_blocks,
+                      int64_t ldq, void* q, void* scales, hipStream_t stream);
+
+/* fp32 split-K workspace bytes smt_tile_wgrad_mx needs (0 when the tiles are written directly). */
+size_t smt_wgrad_mx_workspace_bytes(int64_t ldq, int32_t n_tiles);
+
+/*
+ * grad_tiles[i] (+)= A_i^T B_i for tile i, where A_i / B_i are the MX column blocks
+ * tile_rc_dev[i] = (index into qg/sg, index into qx/sx) of the output gradient g and the input x
+ * (v_mfma_scale_f32_32x32x64_f8f6f4, fp32 accumulation, one rounding to out_dtype). order_dev: the
+ * schedule as for smt_tile_wgrad, or NULL.
+ */
+int smt_tile_wgrad_mx(const void* qg, const void* sg, const void* qx, const void* sx, int64_t ldq,
+                      const int32_t* tile_rc_dev, const int32_t* order_dev, int32_t n_tiles, void* grad_tiles,
+                      int32_t out_dtype, int32_t accumulate, void* workspace, size_t workspace_bytes,
+                      hipStream_t stream);
 
 /* ---- channel path (ABI v3) ------------------------------------------------------------------- */
 

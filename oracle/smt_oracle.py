@@ -507,3 +507,52 @@ def ref_convert_channel(model, selected_channel, selected_channel_attention):
             setattr(parent, parts[-1], RefLinearLayer_ChannelSparsity(module.weight,
                                                                       selected_channel_attention[(mod, layer)]))
     return model
+
+
+# ------------------------------------------------------------------------------------------------
+# MX-fp8 tile weight gradient (config 5). The reference has no fp8 (fine_tune.py:955-959): this
+# restates the build's own documented format (include/smt_hip.h, smt_mx_quant_cols) -- OCP MX with
+# 32-element groups along T, e4m3 elements, e8m0 exponents chosen so that nothing saturates -- as the
+# checker of the HIP quantiser (bit for bit) and of the MX MFMA kernel (fp64 products of the
+# dequantised operands). Its tile gradients are compared with the bf16 path under a stated tolerance.
+# ------------------------------------------------------------------------------------------------
+def mx_exponent(amax: torch.Tensor) -> torch.Tensor:
+    """Smallest e with amax <= 448 * 2^e (amax fp32 >= 0), clamped to >= -127; -127 for amax == 0."""
+    bits = amax.float().contiguous().view(torch.int32).to(torch.int64)
+    ef = (bits >> 23) & 255
+    e = ef - 127 - 8 + ((bits & 0x7FFFFF) > 0x600000).to(torch.int64)
+    e = torch.where(ef == 0, torch.full_like(e, -127), e)
+    return e.clamp_min(-127)
+
+
+def mx_quant_cols(x: torch.Tensor, blocks: Sequence[int]):
+    """bf16 [T, C] -> (q uint8 [n, 256, ldq] e4m3 bits, s uint8 [n, ldq/32, 256] e8m0), ldq = ceil64(T)."""
+    T = x.shape[0]
+    ldq = (T + 63) // 64 * 64
+    n = len(blocks)
+    q = torch.zeros(n, 256, ldq, dtype=torch.uint8)
+    s = torch.empty(n, ldq // 32, 256, dtype=torch.uint8)
+    for i, b in enumerate(blocks):
+        v = torch.zeros(ldq, 256, dtype=torch.float32)
+        v[:T] = x[:, b * 256:(b + 1) * 256].float()
+        g = v.view(ldq // 32, 32, 256)
+        e = mx_exponent(g.abs().amax(dim=1))                               # [ldq/32, 256]
+        inv = torch.pow(2.0, (-e).double()).float()                        # exact powers of two
+        qv = (g * inv[:, None, :]).view(ldq, 256)
+        q[i] = qv.to(torch.float8_e4m3fn).view(torch.uint8).t()
+        s[i] = (e + 127).to(torch.uint8)
+    return q, s
+
+
+def mx_dequant(q: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
+    """(q [n, 256, ldq], s [n, ldq/32, 256]) -> fp64 [n, ldq, 256] values."""
+    vals = q.view(torch.float8_e4m3fn).double().transpose(1, 2)            # [n, ldq, 256]
+    scale = torch.pow(2.0, s.double() - 127.0)                             # [n, ldq/32, 256]
+    return vals * scale.repeat_interleave(32, dim=1)
+
+
+def mx_tile_grads_fp64(qg, sg, qx, sx, table: Sequence[Tuple[int, int]]) -> torch.Tensor:
+    """fp64 A_i^T B_i over the dequantised MX blocks, [n*256, 256]."""
+    a = mx_dequant(qg, sg)
+    b = mx_dequant(qx, sx)
+    return torch.cat([a[i].t() @ b[j] for i, j in table]) if table else torch.zeros(0, 256, dtype=torch.float64)

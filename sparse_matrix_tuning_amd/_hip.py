@@ -10,7 +10,7 @@ from __future__ import annotations
 import ctypes
 import os
 import threading
-from typing import Optional, Sequence
+from typing import NamedTuple, Optional, Sequence
 
 import torch  # imported first: its libamdhip64.so.7 is the HIP runtime the library binds to
 
@@ -30,7 +30,8 @@ _DT = {torch.bfloat16: DTYPE_BF16, torch.float32: DTYPE_FP32, torch.float16: DTY
 ABI_FUNCTIONS = (
     "smt_last_error", "smt_abi_version", "smt_wgrad_workspace_bytes", "smt_tile_wgrad", "smt_colblock_gather", "smt_tile_scatter_t",
     "smt_tile_gather", "smt_tile_scatter", "smt_grad_accumulate", "smt_block_score",
-    "smt_sq_norm", "smt_adamw_step",
+    "smt_sq_norm", "smt_adamw_step", "smt_adamw_multi",
+    "smt_mx_quant_cols", "smt_wgrad_mx_workspace_bytes", "smt_tile_wgrad_mx",
     "smt_row_gather", "smt_row_scatter", "smt_column_gather", "smt_act_accumulate", "smt_channel_score",
     "smt_model_ops_last_error", "smt_rmsnorm_fwd", "smt_rmsnorm_bwd_waves", "smt_rmsnorm_bwd",
     "smt_add_rmsnorm_fwd", "smt_rmsnorm_bwd_add",
@@ -65,6 +66,11 @@ class AdamWArgs(ctypes.Structure):
                 ("bias_correction1", ctypes.c_float), ("bias_correction2", ctypes.c_float),
                 ("max_grad_norm", ctypes.c_float), ("grad_scale", ctypes.c_float),
                 ("mode", ctypes.c_int32), ("grad_dtype", ctypes.c_int32)]
+
+
+class AdamWTensor(ctypes.Structure):
+    _fields_ = [("grad", ctypes.c_void_p), ("master", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p),
+                ("exp_avg_sq", ctypes.c_void_p), ("param", ctypes.c_void_p), ("n", ctypes.c_int64)]
 
 
 class RopeTensor(ctypes.Structure):
@@ -105,6 +111,10 @@ _SIGS = {
     "smt_block_score": (ctypes.c_int, [_P, _I32, _I64, _P]),
     "smt_sq_norm": (ctypes.c_int, [_P, _I64, _P, _I32, _P, _P]),
     "smt_adamw_step": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I32, _I64, _P, ctypes.POINTER(AdamWArgs), _P]),
+    "smt_adamw_multi": (ctypes.c_int, [_P, _P, _I32, _I64, _P, ctypes.POINTER(AdamWArgs), _P]),
+    "smt_mx_quant_cols": (ctypes.c_int, [_P, _I64, _I64, _P, _I32, _I64, _P, _P, _P]),
+    "smt_wgrad_mx_workspace_bytes": (_SZ, [_I64, _I32]),
+    "smt_tile_wgrad_mx": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _P, _I32, _P, _I32, _I32, _P, _SZ, _P]),
     "smt_row_gather": (ctypes.c_int, [_P, _I64, _I32, _I64, _P, _I32, _P, _I64, _P]),
     "smt_row_scatter": (ctypes.c_int, [_P, _I64, _I32, _I64, _P, _I32, _P, _I64, _P]),
     "smt_column_gather": (ctypes.c_int, [_P, _I64, _I64, _P, _I32, _P, _I64, _P]),
@@ -269,6 +279,63 @@ def tile_wgrad(grad_out2d: torch.Tensor, x2d: torch.Tensor, tile_rc: torch.Tenso
     return out
 
 
+class MxBlocks(NamedTuple):
+    """MX-fp8 column blocks of a [T, C] bf16 matrix (include/smt_hip.h, smt_mx_quant_cols):
+    ``q`` uint8 e4m3 [n, 256, ldq] (K-major), ``scales`` uint8 e8m0 [n, ldq/32, 256], ``T`` rows."""
+    q: torch.Tensor
+    scales: torch.Tensor
+    T: int
+
+    @property
+    def ldq(self) -> int:
+        return self.q.shape[2]
+
+
+def mx_ld(T: int) -> int:
+    return (T + 63) // 64 * 64
+
+
+def mx_quant_cols(x2d: torch.Tensor, blocks: torch.Tensor) -> MxBlocks:
+    """MX-fp8 (e4m3 + one e8m0 exponent per 32 rows) copies of the 256-column blocks ``blocks``
+    (device int32) of the bf16 matrix x2d, laid out for smt_tile_wgrad_mx."""
+    dev = _require_device(x2d, blocks)
+    if x2d.dim() != 2 or x2d.stride(1) != 1 or x2d.dtype != torch.bfloat16:
+        raise ValueError("mx_quant_cols: x must be a 2-D row-major bf16 tensor")
+    if blocks.dtype != torch.int32 or blocks.dim() != 1:
+        raise ValueError("mx_quant_cols: blocks must be device int32 [n]")
+    T, n = x2d.shape[0], blocks.numel()
+    ldq = mx_ld(T)
+    q = torch.empty(n, BLOCK, ldq, dtype=torch.uint8, device=dev)
+    sc = torch.empty(n, ldq // 32, BLOCK, dtype=torch.uint8, device=dev)
+    rc = load().smt_mx_quant_cols(_ptr(x2d), x2d.stride(0), T, _ptr(blocks), n, ldq, _ptr(q), _ptr(sc), _stream(dev))
+    _check(rc, "smt_mx_quant_cols")
+    return MxBlocks(q, sc, T)
+
+
+def tile_wgrad_mx(g: MxBlocks, x: MxBlocks, tile_rc: torch.Tensor, out: torch.Tensor, accumulate: bool = False,
+                  order: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out[i] (+)= A_i^T B_i over MX column blocks: tile_rc[i] = (block of ``g``, block of ``x``).
+    The table is built from a validated host list (no device read-back here, this is per step)."""
+    dev = _require_device(g.q, x.q, tile_rc, out, order)
+    if out.dtype not in (torch.bfloat16, torch.float32) or not out.is_contiguous():
+        raise ValueError("tile_wgrad_mx: out must be a contiguous bf16/fp32 tensor")
+    n = tile_rc.shape[0]
+    if out.numel() != n * TILE_ELEMS:
+        raise ValueError(f"tile_wgrad_mx: out has {out.numel()} elements, expected {n * TILE_ELEMS}")
+    if g.T != x.T or g.ldq != x.ldq:
+        raise ValueError("tile_wgrad_mx: operands cover different rows")
+    if order is not None and (order.dtype != torch.int32 or order.numel() != n):
+        raise ValueError("tile_wgrad_mx: order must be int32 [n_tiles]")
+    ldq = g.ldq
+    ws_bytes = load().smt_wgrad_mx_workspace_bytes(ldq, n)
+    ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=dev)
+    rc = load().smt_tile_wgrad_mx(_ptr(g.q), _ptr(g.scales), _ptr(x.q), _ptr(x.scales), ldq, _ptr(tile_rc),
+                                  _ptr(order), n, _ptr(out), _DT[out.dtype], int(bool(accumulate)), _ptr(ws),
+                                  ws_bytes, _stream(dev))
+    _check(rc, "smt_tile_wgrad_mx")
+    return out
+
+
 def colblock_gather(x2d: torch.Tensor, col_blocks: torch.Tensor) -> torch.Tensor:
     """[T, n_cb*256] packed copy of the 256-column blocks ``col_blocks`` (device int32) of x2d."""
     dev = _require_device(x2d, col_blocks)
@@ -384,6 +451,39 @@ def adamw_step(grad: torch.Tensor, master: torch.Tensor, exp_avg: torch.Tensor, 
     rc = load().smt_adamw_step(_ptr(grad), _ptr(master), _ptr(exp_avg), _ptr(exp_avg_sq), _ptr(param_bf16),
                                _ptr(tiles), int(n_tiles), n, _ptr(grad_sq_norm), ctypes.byref(args), _stream(dev))
     _check(rc, "smt_adamw_step")
+
+
+ADAM_MULTI_BLOCK = 2048
+
+
+def adamw_multi(tensors, args: AdamWArgs, grad_sq_norm: Optional[torch.Tensor] = None) -> None:
+    """One ``smt_adamw_multi`` launch over ``tensors`` = [(grad, master, exp_avg, exp_avg_sq, param_bf16)]
+    (all on one device, one gradient dtype, every buffer contiguous and 16-byte aligned)."""
+    if not tensors:
+        return
+    dev = _require_device(*[t for row in tensors for t in row], grad_sq_norm)
+    gdt = tensors[0][0].dtype
+    rows, starts = [], [0]
+    for grad, master, m, v, p in tensors:
+        for t in (master, m, v):
+            if t.dtype != torch.float32 or not t.is_contiguous():
+                raise ValueError("adamw_multi: master/exp_avg/exp_avg_sq must be contiguous fp32")
+        if p.dtype != torch.bfloat16 or not p.is_contiguous() or not grad.is_contiguous() or grad.dtype != gdt:
+            raise ValueError("adamw_multi: param must be contiguous bf16, grads contiguous and of one dtype")
+        n = master.numel()
+        if not (grad.numel() == n == m.numel() == v.numel() == p.numel()):
+            raise ValueError("adamw_multi: buffer sizes differ")
+        if any(t.data_ptr() % 16 for t in (grad, master, m, v, p)):
+            raise ValueError("adamw_multi: buffers must be 16-byte aligned")
+        rows.append(AdamWTensor(_ptr(grad), _ptr(master), _ptr(m), _ptr(v), _ptr(p), n))
+        starts.append(starts[-1] + (n + ADAM_MULTI_BLOCK - 1) // ADAM_MULTI_BLOCK)
+    # stream-ordered: the caching allocator reuses the tables only after this launch on the stream
+    table_dev = _device_table(rows, AdamWTensor, dev)
+    starts_dev = torch.tensor(starts, dtype=torch.int64).to(dev)
+    args.grad_dtype = _DT[gdt]
+    rc = load().smt_adamw_multi(_ptr(table_dev), _ptr(starts_dev), len(tensors), starts[-1], _ptr(grad_sq_norm),
+                                ctypes.byref(args), _stream(dev))
+    _check(rc, "smt_adamw_multi")
 
 
 def tile_scatter_t(descs: torch.Tensor, n_tiles: int, tiles: torch.Tensor) -> None:

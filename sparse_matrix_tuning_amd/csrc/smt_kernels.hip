@@ -23,6 +23,7 @@
 #include <cmath>
 
 #include "smt_hip.h"
+#include "fp8_math.h"
 
 namespace {
 
@@ -645,6 +646,230 @@ void wgrad_reduce_kernel(const float* __restrict__ slab, int S, void* __restrict
 }
 
 // ------------------------------------------------------------------------------------------------
+// MX-fp8 tile weight gradient (BASELINE config 5, SURVEY §8(f) row 2: the reference has no fp8,
+// fine_tune.py:955-959, so the bar is the bf16 tile path, not the reference).
+//
+// Operand format ("MX column blocks"), written by mx_quant_cols_kernel from a bf16 [T, C] matrix for
+// a list of 256-column blocks, K-major so that no transpose is needed on the way to the MFMA:
+//   q[blk][f][t]      e4m3 (OCP), f in [0,256), t in [0, ldq), rows T..ldq-1 zero; ldq % 64 == 0
+//   s[blk][t/32][f]   e8m0 shared exponent of the 32 values q[blk][f][32j .. 32j+31]
+// value(t, f) = e4m3(q) * 2^(s - 127). The exponent is the smallest e with amax <= 448 * 2^e, so
+// nothing saturates (amax = the 32 values' max |x|; e = -127 for an all-zero group; computed from
+// the bits of amax, exact), and q = e4m3_rne(x * 2^-e) (a power-of-two multiply: exact).
+// ------------------------------------------------------------------------------------------------
+constexpr int kMxRows = 64;                                // T rows per quantiser workgroup
+
+__device__ __forceinline__ int mx_exponent(float amax) {
+    const uint32_t b = __float_as_uint(amax);
+    const int ef = (int)((b >> 23) & 255u);
+    if (ef == 0) return -127;                              // zero or fp32-subnormal amax
+    const int e = ef - 127 - 8 + ((b & 0x7fffffu) > 0x600000u ? 1 : 0);   // 448 = 1.75 * 2^8
+    return e < -127 ? -127 : e;
+}
+
+__global__ __launch_bounds__(256)
+void mx_quant_cols_kernel(const uint16_t* __restrict__ x, int64_t ldx, int64_t T, const int32_t* __restrict__ blocks,
+                          int64_t ldq, uint8_t* __restrict__ q, uint8_t* __restrict__ sc) {
+    __shared__ __attribute__((aligned(16))) uint16_t slab[kMxRows][kTile];
+    const int blk = blockIdx.x;
+    const int64_t t0 = (int64_t)blockIdx.y * kMxRows;
+    const int tid = threadIdx.x;
+    const uint16_t* src = x + (int64_t)blocks[blk] * kTile;
+#pragma unroll
+    for (int i = 0; i < kMxRows * 32 / 256; ++i) {           // 64 rows x 32 chunks of 16 B
+        const int cid = tid + 256 * i;
+        const int rr = cid >> 5, ch = cid & 31;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (t0 + rr < T) v = *reinterpret_cast<const uint4*>(src + (t0 + rr) * ldx + ch * 8);
+        *reinterpret_cast<uint4*>(&slab[rr][ch * 8]) = v;
+    }
+    __syncthreads();
+    // thread = feature f: two 32-row groups -> 64 contiguous bytes of q[blk][f] and two exponents
+    uint32_t w[16];
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        float amax = 0.f;
+#pragma unroll
+        for (int k = 0; k < 32; ++k) amax = fmaxf(amax, fabsf(bf16_bits_to_f32(slab[32 * g + k][tid])));
+        const int e = mx_exponent(amax);
+        const float inv = __uint_as_float((uint32_t)(127 - e) << 23);     // 2^-e, e in [-127, 121]
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int r = 32 * g + 4 * k;
+            w[8 * g + k] = pack4(bf16_bits_to_f32(slab[r][tid]) * inv, bf16_bits_to_f32(slab[r + 1][tid]) * inv,
+                                 bf16_bits_to_f32(slab[r + 2][tid]) * inv, bf16_bits_to_f32(slab[r + 3][tid]) * inv);
+        }
+        sc[((int64_t)blk * (ldq >> 5) + (t0 >> 5) + g) * kTile + tid] = (uint8_t)(e + 127);
+    }
+    uint4* dst = reinterpret_cast<uint4*>(q + ((int64_t)blk * kTile + tid) * ldq + t0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dst[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+}
+
+// The MX wgrad: C[m][n] = sum_t A(t, m) * B(t, n) over the MX column blocks of g (A, the tile's row
+// block) and x (B, its column block), one 512-thread workgroup per (tile, T-chunk), 8 waves as
+// 2(M) x 4(N) with 128x64 outputs each = 8 accumulators of v_mfma_scale_f32_32x32x64_f8f6f4 (e4m3 x
+// e4m3, per-lane e8m0 scales): 2x the bf16 MFMA rate and half the operand bytes of the bf16 kernel.
+// Lane l of a 32x32x64 operand holds row (l & 31) and two 16-token runs of it (see mx_frag): two
+// ds_read_b128 from an LDS image of [256 rows][64 B] per 64-token stage, with chunk c of row f
+// stored at chunk c ^ ((f >> 2) & 3) (16 lanes of a b128 read then cover all 64 banks once); the
+// lane's scale is the exponent of (its row, k-block 2*stage + (l >> 5)).
+// Stages stream through a 4-slot LDS-DMA ring (2 stages in flight, counted vmcnt, raw s_barrier)
+// exactly as wgrad_dma_kernel; slabs / epilogue / reduce are shared with it.
+constexpr int kMxBK = 64;                                   // tokens per stage = one MFMA K step
+constexpr int kMxImg = kTile * kMxBK;                       // 16 KiB per operand per stage
+constexpr int kMxSlotBytes = 2 * kMxImg + 2 * 2 * kTile;    // + 2 k-blocks x 256 exponents per operand
+constexpr int kMxSlots = 4;
+
+typedef int i32x8_t __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) uint4 lds_u4_t;
+
+__device__ __forceinline__ void dma4(__amdgpu_buffer_rsrc_t rsrc, uint32_t lds_base, int voff) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+                 "buffer_load_dword %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(lds_base) : "memory");
+}
+
+// s_waitcnt vmcnt for a run-time count in {0, 4, 5, 8, 10}
+__device__ __forceinline__ void wait_vm_n(int n) {
+    switch (n) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+        case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    }
+}
+
+// Lane (row, h) of a 32x32x64 f8 operand: bytes 0-15 are k = 16h .. 16h+15, bytes 16-31 are
+// k = 32 + 16h .. 32 + 16h + 15 (measured with one-hot operands: scripts/mx_probe.py), and its
+// scale is the exponent of k-block h (k = 32h .. 32h+31). 16-B chunk c of a 64-token row holds
+// tokens 16c .. 16c+15, so the lane reads chunks h and 2 + h.
+__device__ __forceinline__ i32x8_t mx_frag(const uint8_t* img, int row, int h) {
+    const int sw = (row >> 2) & 3;
+    const uint4 lo = *reinterpret_cast<const uint4*>(img + row * kMxBK + ((h ^ sw) << 4));
+    const uint4 hi = *reinterpret_cast<const uint4*>(img + row * kMxBK + (((2 + h) ^ sw) << 4));
+    i32x8_t f;
+    f[0] = (int)lo.x; f[1] = (int)lo.y; f[2] = (int)lo.z; f[3] = (int)lo.w;
+    f[4] = (int)hi.x; f[5] = (int)hi.y; f[6] = (int)hi.z; f[7] = (int)hi.w;
+    return f;
+}
+
+template <int OUT>
+__global__ __launch_bounds__(kWgThreads, 1)
+void wgrad_mx_kernel(const uint8_t* __restrict__ qa, const uint8_t* __restrict__ sa,
+                     const uint8_t* __restrict__ qb, const uint8_t* __restrict__ sb, int64_t ldq,
+                     int64_t chunk, int S, int n_tiles, const int32_t* __restrict__ tile_rc,
+                     const int32_t* __restrict__ order, void* __restrict__ out_ptr, int accumulate) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kMxSlots * kMxSlotBytes];   // 132 KiB, one array
+
+    const int total = n_tiles * S;
+    const int b = blockIdx.x;
+    const int q8 = total >> 3, r8 = total & 7, xcd = b & 7;
+    const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+    const int s = L / n_tiles;
+    const int li = L - s * n_tiles;
+    const int tile = order != nullptr ? order[li] : li;
+    const int r = tile_rc[2 * tile];
+    const int c = tile_rc[2 * tile + 1];
+    const int64_t t_begin = (int64_t)s * chunk;
+    const int64_t t_end = (t_begin + chunk < ldq) ? (t_begin + chunk) : ldq;
+    const int nst = (t_end > t_begin) ? (int)((t_end - t_begin) / kMxBK) : 0;   // ldq, chunk % 64 == 0
+
+    const int64_t blk_bytes = (int64_t)kTile * ldq;
+    const int64_t sc_bytes = (ldq >> 5) * kTile;
+    const __amdgpu_buffer_rsrc_t rqa = uniform_rsrc(qa + r * blk_bytes + t_begin, blk_bytes - t_begin);
+    const __amdgpu_buffer_rsrc_t rqb = uniform_rsrc(qb + c * blk_bytes + t_begin, blk_bytes - t_begin);
+    const __amdgpu_buffer_rsrc_t rsa = uniform_rsrc(sa + r * sc_bytes + (t_begin >> 5) * kTile, sc_bytes - (t_begin >> 5) * kTile);
+    const __amdgpu_buffer_rsrc_t rsb = uniform_rsrc(sb + c * sc_bytes + (t_begin >> 5) * kTile, sc_bytes - (t_begin >> 5) * kTile);
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2;
+    const int wn = wave & 3;
+
+    // DMA geometry: instruction j of wave w fills image rows 16*(2w+j) .. +15 (1 KiB); lane l lands at
+    // row 16*(2w+j) + (l>>2), physical chunk l&3, which holds logical chunk (l&3) ^ ((row>>2)&3).
+    int voff[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int row = 16 * (2 * wave + j) + (lane >> 2);
+        voff[j] = (int)(row * ldq) + ((((lane & 3) ^ ((row >> 2) & 3))) << 4);
+    }
+    // exponents: waves 0-3 each move one 256-B k-block row (A kb0, A kb1, B kb0, B kb1) per stage
+    const int sc_kb = wave & 1;
+    const int sc_voff = sc_kb * kTile + 4 * lane;
+    const int per_stage = wave < 4 ? 5 : 4;                 // DMA instructions per stage of this wave
+
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(lds));
+    auto issue = [&](int st) {
+        const uint32_t slot = lds0 + (uint32_t)((st % kMxSlots) * kMxSlotBytes);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const uint32_t row0 = (uint32_t)(2 * wave + j) * 1024u;
+            dma16(rqa, __builtin_amdgcn_readfirstlane(slot + row0), voff[j] + st * kMxBK);
+            dma16(rqb, __builtin_amdgcn_readfirstlane(slot + kMxImg + row0), voff[j] + st * kMxBK);
+        }
+        if (wave < 2)
+            dma4(rsa, __builtin_amdgcn_readfirstlane(slot + 2 * kMxImg + sc_kb * kTile), sc_voff + st * 2 * kTile);
+        else if (wave < 4)
+            dma4(rsb, __builtin_amdgcn_readfirstlane(slot + 2 * kMxImg + 2 * kTile + sc_kb * kTile), sc_voff + st * 2 * kTile);
+    };
+
+    f32x16_t acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    const int r32 = lane & 31;
+    const int h = lane >> 5;
+    if (nst > 0) issue(0);
+    if (nst > 1) issue(1);
+    for (int st = 0; st < nst; ++st) {
+        if (st + 2 < nst) {
+            issue(st + 2);
+            wait_vm_n(2 * per_stage);                       // stage st landed (st+1, st+2 in flight)
+        } else if (st + 1 < nst) {
+            wait_vm_n(per_stage);
+        } else {
+            wait_vm_n(0);
+        }
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        const uint8_t* A = lds + (st % kMxSlots) * kMxSlotBytes;
+        const uint8_t* B = A + kMxImg;
+        const uint8_t* SA = A + 2 * kMxImg + h * kTile;     // this lane's k-block of the stage
+        const uint8_t* SB = SA + 2 * kTile;
+        i32x8_t af[4], bfr[2];
+        int as[4], bs[2];
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) {
+            const int row = wm * 128 + mb * 32 + r32;
+            af[mb] = mx_frag(A, row, h);
+            as[mb] = SA[row];
+        }
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+            const int col = wn * 64 + nb * 32 + r32;
+            bfr[nb] = mx_frag(B, col, h);
+            bs[nb] = SB[col];
+        }
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb)
+                acc[mb][nb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af[mb], bfr[nb], acc[mb][nb],
+                                                                               0, 0, 0, as[mb], 0, bs[nb]);
+    }
+    wgrad_store<OUT>(acc, out_ptr, tile, s, S, wm, wn, lane, accumulate);
+}
+
+// ------------------------------------------------------------------------------------------------
 // Tile gather / scatter (smt.py:317-325 and 332-341): 16 B per thread, 32 workgroups per tile.
 // ------------------------------------------------------------------------------------------------
 template <bool SCATTER, int ELEM_BYTES>
@@ -975,6 +1200,38 @@ void adamw_flat_kernel(const void* __restrict__ grad, float* __restrict__ master
     }
 }
 
+// Multi-tensor flat AdamW: one launch over every dense parameter of the warm-up full fine-tune
+// (DeepSpeed FusedAdam's multi_tensor_apply, external). Workgroup w covers 2048 elements of the
+// tensor t with block_start[t] <= w < block_start[t+1] (binary search over the n+1 prefix).
+template <int GDT>
+__global__ __launch_bounds__(256)
+void adamw_multi_kernel(const smt_adamw_tensor* __restrict__ tensors, const int64_t* __restrict__ block_start,
+                        int32_t n_tensors, const double* __restrict__ norm_sq, smt_adamw_args a) {
+    const int64_t w = blockIdx.x;
+    int lo = 0, hi = n_tensors - 1;
+    while (lo < hi) {                                   // last t with block_start[t] <= w
+        const int mid = (lo + hi + 1) >> 1;
+        if (block_start[mid] <= w) lo = mid; else hi = mid - 1;
+    }
+    const smt_adamw_tensor d = tensors[lo];
+    const int64_t f = ((w - block_start[lo]) * 256 + threadIdx.x) * 8;
+    if (f >= d.n) return;
+    const AdamStep st{a.lr, a.beta1, a.beta2, a.eps, a.weight_decay, a.bias_correction1, a.bias_correction2, a.mode};
+    const float gscale = clip_scale(norm_sq, a.max_grad_norm, a.grad_scale);
+    uint16_t* param = static_cast<uint16_t*>(d.param);
+    if (f + 8 <= d.n) {
+        uint4 packed;
+        adam8<GDT>(d.grad, d.master, d.exp_avg, d.exp_avg_sq, param, f, gscale, st, &packed);
+    } else {
+        for (int64_t i = f; i < d.n; ++i) {
+            float pp = d.master[i], mm = d.exp_avg[i], vv = d.exp_avg_sq[i];
+            st.apply(load_elem<GDT>(d.grad, i) * gscale, pp, mm, vv);
+            d.master[i] = pp; d.exp_avg[i] = mm; d.exp_avg_sq[i] = vv;
+            param[i] = f32_to_bf16_bits(pp);
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // Channel path (smt.py:185-296, smt_helper.py:149-230, fine_tune.py:636-667).
 // ------------------------------------------------------------------------------------------------
@@ -1138,12 +1395,13 @@ int quarter_max_tiles() {
     return v;
 }
 
-WgradSplit wgrad_split(int64_t T, int32_t n_tiles) {
+// row_bytes: operand bytes per T row of one tile (1 KiB bf16, 512 B MX-fp8)
+WgradSplit wgrad_split(int64_t T, int32_t n_tiles, bool allow_quarter = true, double row_bytes = 1024.0) {
     WgradSplit sp{1, kBK, false};
     if (T <= 0 || n_tiles <= 0) return sp;
     const int64_t s_max = std::max<int64_t>(1, std::min<int64_t>(64, (T + 511) / 512));
     int64_t S = 1;
-    if (n_tiles <= quarter_max_tiles()) {
+    if (allow_quarter && n_tiles <= quarter_max_tiles()) {
         // quarter tiles, two workgroups per CU: fill the 512 workgroup slots once (chunks >= 512 rows)
         sp.quarter = true;
         S = std::min<int64_t>(s_max, std::max<int64_t>(1, (2 * kCUs + 4 * n_tiles - 1) / (4 * n_tiles)));
@@ -1155,7 +1413,7 @@ WgradSplit wgrad_split(int64_t T, int32_t n_tiles) {
             const int64_t rounds = (n_tiles * cand + kCUs - 1) / kCUs;
             const double rows = std::ceil((double)T / (double)cand);
             const double slab = cand > 1 ? 262144.0 : 0.0;
-            const double t_wg = (rows * 1024.0 + slab) / 25e9;
+            const double t_wg = (rows * row_bytes + slab) / 25e9;
             const double t_red = cand > 1 ? (double)n_tiles * cand * 262144.0 * 2.0 / 5e12 : 0.0;
             const double cost = (double)rounds * t_wg + t_red;
             if (cost < best * (1.0 - 1e-6)) { best = cost; S = cand; }
@@ -1177,7 +1435,7 @@ extern "C" {
 
 const char* smt_last_error(void) { return g_err; }
 
-int smt_abi_version(void) { return 4; }
+int smt_abi_version(void) { return 5; }
 
 size_t smt_wgrad_workspace_bytes(int64_t T, int32_t n_tiles) {
     if (T <= 0 || n_tiles <= 0) return 0;
@@ -1257,6 +1515,79 @@ int smt_tile_wgrad(const void* grad_out, int64_t ld_grad_out, const void* x, int
     return check_launch("wgrad_reduce_kernel");
 }
 #undef SMT_WGRAD_DMA
+
+size_t smt_wgrad_mx_workspace_bytes(int64_t ldq, int32_t n_tiles) {
+    if (ldq <= 0 || n_tiles <= 0) return 0;
+    const WgradSplit sp = wgrad_split(ldq, n_tiles, false, 512.0);
+    if (sp.S == 1) return 0;
+    return (size_t)n_tiles * (size_t)sp.S * (size_t)kTileElems * sizeof(float);
+}
+
+int smt_mx_quant_cols(const void* x, int64_t ld_x, int64_t T, const int32_t* blocks_dev, int32_t n_blocks,
+                      int64_t ldq, void* q, void* scales, hipStream_t stream) {
+    if (T < 0 || n_blocks < 0 || ldq < 0) return fail(SMT_E_INVALID, "smt_mx_quant_cols: negative size");
+    if (ldq % 64 || ldq < T) return fail(SMT_E_INVALID, "smt_mx_quant_cols: ldq %lld must be a multiple of 64 and >= T %lld",
+                                         (long long)ldq, (long long)T);
+    if (n_blocks == 0 || ldq == 0) return SMT_OK;
+    if (!x || !blocks_dev || !q || !scales) return fail(SMT_E_INVALID, "smt_mx_quant_cols: null pointer");
+    if (!aligned16(x) || (ld_x & 7) || !aligned16(q))
+        return fail(SMT_E_ALIGN, "smt_mx_quant_cols: 16-byte aligned rows required (ld %% 8 == 0)");
+    if (ldq / 64 > 65535) return fail(SMT_E_INVALID, "smt_mx_quant_cols: T too large");
+    hipLaunchKernelGGL(mx_quant_cols_kernel, dim3(n_blocks, (unsigned)(ldq / 64)), dim3(256), 0, stream,
+                       static_cast<const uint16_t*>(x), ld_x, T, blocks_dev, ldq, static_cast<uint8_t*>(q),
+                       static_cast<uint8_t*>(scales));
+    return check_launch("mx_quant_cols_kernel");
+}
+
+int smt_tile_wgrad_mx(const void* qg, const void* sg, const void* qx, const void* sx, int64_t ldq,
+                      const int32_t* tile_rc_dev, const int32_t* order_dev, int32_t n_tiles, void* grad_tiles,
+                      int32_t out_dtype, int32_t accumulate, void* workspace, size_t workspace_bytes,
+                      hipStream_t stream) {
+    if (n_tiles < 0 || ldq < 0) return fail(SMT_E_INVALID, "smt_tile_wgrad_mx: negative size");
+    if (n_tiles == 0) return SMT_OK;
+    if (ldq % 64) return fail(SMT_E_INVALID, "smt_tile_wgrad_mx: ldq %lld not a multiple of 64", (long long)ldq);
+    if (out_dtype != SMT_DTYPE_BF16 && out_dtype != SMT_DTYPE_FP32)
+        return fail(SMT_E_INVALID, "smt_tile_wgrad_mx: out_dtype %d not supported", out_dtype);
+    if (!tile_rc_dev || !grad_tiles) return fail(SMT_E_INVALID, "smt_tile_wgrad_mx: null tile table or output");
+    if (!aligned16(grad_tiles)) return fail(SMT_E_ALIGN, "smt_tile_wgrad_mx: output not 16-byte aligned");
+    if (ldq == 0) {
+        if (accumulate) return SMT_OK;
+        const size_t bytes = (size_t)n_tiles * kTileElems * (out_dtype == SMT_DTYPE_FP32 ? 4 : 2);
+        hipError_t e = hipMemsetAsync(grad_tiles, 0, bytes, stream);
+        return e == hipSuccess ? SMT_OK : fail(SMT_E_LAUNCH, "smt_tile_wgrad_mx: memset: %s", hipGetErrorString(e));
+    }
+    if (!qg || !sg || !qx || !sx) return fail(SMT_E_INVALID, "smt_tile_wgrad_mx: null operand");
+    if (!aligned16(qg) || !aligned16(qx) || !aligned16(sg) || !aligned16(sx))
+        return fail(SMT_E_ALIGN, "smt_tile_wgrad_mx: operands not 16-byte aligned");
+    if ((int64_t)kTile * ldq >= (int64_t)0x7fffffff) return fail(SMT_E_INVALID, "smt_tile_wgrad_mx: T too large for 32-bit offsets");
+    const WgradSplit sp = wgrad_split(ldq, n_tiles, false, 512.0);
+    const uint8_t *a = static_cast<const uint8_t*>(qg), *as = static_cast<const uint8_t*>(sg);
+    const uint8_t *b = static_cast<const uint8_t*>(qx), *bs = static_cast<const uint8_t*>(sx);
+    const dim3 grid(n_tiles * sp.S), block(kWgThreads);
+    if (sp.S == 1) {
+        if (out_dtype == SMT_DTYPE_FP32)
+            hipLaunchKernelGGL(wgrad_mx_kernel<kOutF32>, grid, block, 0, stream, a, as, b, bs, ldq, sp.chunk, 1, n_tiles,
+                               tile_rc_dev, order_dev, grad_tiles, accumulate);
+        else
+            hipLaunchKernelGGL(wgrad_mx_kernel<kOutBF16>, grid, block, 0, stream, a, as, b, bs, ldq, sp.chunk, 1, n_tiles,
+                               tile_rc_dev, order_dev, grad_tiles, accumulate);
+        return check_launch("wgrad_mx_kernel");
+    }
+    const size_t need = (size_t)n_tiles * sp.S * kTileElems * sizeof(float);
+    if (!workspace || workspace_bytes < need)
+        return fail(SMT_E_WORKSPACE, "smt_tile_wgrad_mx: workspace %zu < %zu bytes", workspace_bytes, need);
+    if (!aligned16(workspace)) return fail(SMT_E_ALIGN, "smt_tile_wgrad_mx: workspace not 16-byte aligned");
+    float* slab = static_cast<float*>(workspace);
+    hipLaunchKernelGGL(wgrad_mx_kernel<kOutSlab>, grid, block, 0, stream, a, as, b, bs, ldq, sp.chunk, sp.S, n_tiles,
+                       tile_rc_dev, order_dev, slab, 0);
+    int rc = check_launch("wgrad_mx_kernel");
+    if (rc) return rc;
+    if (out_dtype == SMT_DTYPE_FP32)
+        hipLaunchKernelGGL(wgrad_reduce_kernel<true>, dim3(n_tiles * 64), dim3(256), 0, stream, slab, sp.S, grad_tiles, accumulate);
+    else
+        hipLaunchKernelGGL(wgrad_reduce_kernel<false>, dim3(n_tiles * 64), dim3(256), 0, stream, slab, sp.S, grad_tiles, accumulate);
+    return check_launch("wgrad_reduce_kernel");
+}
 
 static int tile_copy(bool scatter, void* weight, int64_t ld_weight, int32_t elem_bytes, const int32_t* tile_rc_dev,
                      int32_t n_tiles, void* tiles, hipStream_t stream) {
@@ -1352,6 +1683,29 @@ int smt_adamw_step(const void* grad, float* master, float* exp_avg, float* exp_a
     else
         hipLaunchKernelGGL(adamw_flat_kernel<SMT_DTYPE_BF16>, dim3((unsigned)blocks), dim3(256), 0, stream, grad, master, exp_avg, exp_avg_sq, p, n_elems, grad_sq_norm_dev, a);
     return check_launch("adamw_flat_kernel");
+}
+
+int smt_adamw_multi(const smt_adamw_tensor* tensors_dev, const int64_t* block_start_dev, int32_t n_tensors,
+                    int64_t n_blocks, const double* grad_sq_norm_dev, const smt_adamw_args* args, hipStream_t stream) {
+    if (!args) return fail(SMT_E_INVALID, "smt_adamw_multi: null args");
+    if (args->grad_dtype != SMT_DTYPE_BF16 && args->grad_dtype != SMT_DTYPE_FP32)
+        return fail(SMT_E_INVALID, "smt_adamw_multi: grad_dtype %d not supported", args->grad_dtype);
+    if (args->mode != SMT_ADAM_DEEPSPEED && args->mode != SMT_ADAM_TORCH)
+        return fail(SMT_E_INVALID, "smt_adamw_multi: mode %d", args->mode);
+    if (!(args->bias_correction1 > 0.f) || !(args->bias_correction2 > 0.f))
+        return fail(SMT_E_INVALID, "smt_adamw_multi: bias corrections must be > 0");
+    if (n_tensors < 0 || n_blocks < 0) return fail(SMT_E_INVALID, "smt_adamw_multi: negative size");
+    if (n_tensors == 0 || n_blocks == 0) return SMT_OK;
+    if (!tensors_dev || !block_start_dev) return fail(SMT_E_INVALID, "smt_adamw_multi: null table");
+    if (n_blocks > 0x7fffffffLL) return fail(SMT_E_INVALID, "smt_adamw_multi: too many elements");
+    const smt_adamw_args a = *args;
+    if (a.grad_dtype == SMT_DTYPE_FP32)
+        hipLaunchKernelGGL(adamw_multi_kernel<SMT_DTYPE_FP32>, dim3((unsigned)n_blocks), dim3(256), 0, stream,
+                           tensors_dev, block_start_dev, n_tensors, grad_sq_norm_dev, a);
+    else
+        hipLaunchKernelGGL(adamw_multi_kernel<SMT_DTYPE_BF16>, dim3((unsigned)n_blocks), dim3(256), 0, stream,
+                           tensors_dev, block_start_dev, n_tensors, grad_sq_norm_dev, a);
+    return check_launch("adamw_multi_kernel");
 }
 
 static int row_copy(bool scatter, void* weight, int64_t ld_weight, int32_t elem_bytes, int64_t n_cols,

@@ -53,7 +53,7 @@ class SMTFusedAdam(torch.optim.Optimizer):
         m = b1*m + (1-b1)*g ;  v = b2*v + (1-b2)*g*g
         p = p - lr * ( (m/bc1) / (sqrt(v/bc2) + eps) + wd*p )
     ``adam_w_mode=False`` is not supported (the reference always uses AdamW). Used standalone,
-    ``step()`` runs the fused HIP kernel per parameter (flat mode) on ``p.grad``; under
+    ``step()`` runs one multi-tensor HIP launch per parameter group on the ``p.grad``s; under
     :class:`SMTEngine` the engine owns packed buffers and drives the kernel itself.
     """
 
@@ -80,6 +80,7 @@ class SMTFusedAdam(torch.optim.Optimizer):
     def step(self, closure=None):
         loss = closure() if closure is not None else None
         for group in self.param_groups:
+            batches = {}
             for p in group["params"]:
                 if p.grad is None:
                     continue
@@ -92,8 +93,10 @@ class SMTFusedAdam(torch.optim.Optimizer):
                     st["exp_avg"] = torch.zeros_like(st["master"])
                     st["exp_avg_sq"] = torch.zeros_like(st["master"])
                 st["step"] += 1
-                _hip.adamw_step(p.grad.contiguous(), st["master"], st["exp_avg"], st["exp_avg_sq"], p.data,
-                                self._args(group, st["step"]))
+                batches.setdefault((st["step"], p.grad.dtype), []).append(
+                    (p.grad.contiguous(), st["master"], st["exp_avg"], st["exp_avg_sq"], p.data))
+            for (step, _dt), rows in batches.items():
+                _hip.adamw_multi(rows, self._args(group, step))
         return loss
 
 
@@ -574,6 +577,8 @@ class SMTEngine:
             for g, cb in tg.fp8_groups:
                 g.refresh(cb)
         for group, params in self.dense_groups:
+            # one multi-tensor launch per (group, step count, grad dtype): the warm-up's full fine-tune
+            batches = {}
             for p in params:
                 if p.grad is None:
                     continue
@@ -584,9 +589,11 @@ class SMTEngine:
                     st["exp_avg_sq"] = torch.zeros_like(st["master"])
                     self._dense_state[id(p)] = st
                 st["step"] += 1
-                args = self.optimizer._args(group, st["step"], self.max_grad_norm, 1.0)
-                _hip.adamw_step(p.grad.contiguous(), st["master"], st["exp_avg"], st["exp_avg_sq"], p.data, args,
-                                grad_sq_norm=norm)
+                batches.setdefault((st["step"], p.grad.dtype), []).append(
+                    (p.grad.contiguous(), st["master"], st["exp_avg"], st["exp_avg_sq"], p.data))
+            for (step, _dt), rows in batches.items():
+                _hip.adamw_multi(rows, self.optimizer._args(group, step, self.max_grad_norm, 1.0), grad_sq_norm=norm)
+            for p in params:
                 p.grad = None
         self.global_steps += 1
         if self.lr_scheduler is not None:

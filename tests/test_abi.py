@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
     out = subprocess.run(["nm", "-D", "--defined-only", _hip.lib_path()], capture_output=True, text=True).stdout
     for name in declared_functions():
         assert re.search(rf"\bT {name}$", out, re.M), name
-    assert lib.smt_abi_version() == 4
+    assert lib.smt_abi_version() == 5
 
 
 def test_library_carries_gfx950_code_object():
@@ -44,6 +44,7 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(_hip.ScoreEntry) == 48
     assert ctypes.sizeof(_hip.AdamWArgs) == 44
     assert ctypes.sizeof(_hip.RopeTensor) == 72
+    assert ctypes.sizeof(_hip.AdamWTensor) == 48
 
 
 def test_validation_errors_without_gpu():
@@ -56,6 +57,12 @@ def test_validation_errors_without_gpu():
                           bias_correction2=0.1, max_grad_norm=0.0, grad_scale=1.0, mode=0, grad_dtype=0)
     assert lib.smt_adamw_step(None, None, None, None, None, None, 0, 8, None, ctypes.byref(args), None) == -1
     assert b"bias" in lib.smt_last_error()
+    assert lib.smt_adamw_multi(None, None, 3, 5, None, ctypes.byref(args), None) == -1
+    assert b"bias" in lib.smt_last_error()
+    args.bias_correction1 = 0.1
+    assert lib.smt_adamw_multi(None, None, 0, 0, None, ctypes.byref(args), None) == 0      # nothing to do
+    assert lib.smt_adamw_multi(None, None, 3, 5, None, ctypes.byref(args), None) == -1
+    assert b"null table" in lib.smt_last_error()
     assert lib.smt_tile_gather(None, 256, 3, None, 1, None, None) == -1
     assert lib.smt_sq_norm(None, 10, None, 0, None, None) == -1
     assert lib.smt_wgrad_workspace_bytes(32768, 27) == 27 * 9 * 65536 * 4

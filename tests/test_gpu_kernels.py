@@ -204,6 +204,33 @@ def test_adamw_matches_oracle(tiled):
         assert torch.equal(tiles_now.reshape(-1), param.cpu())
 
 
+@pytest.mark.parametrize("gdt", [torch.bfloat16, torch.float32])
+def test_adamw_multi_equals_per_tensor_steps(gdt):
+    """One smt_adamw_multi launch over ragged tensors (tails of 1-2047 elements, a 1-element
+    tensor, one spanning many workgroups) equals smt_adamw_step per tensor bit for bit."""
+    gen = torch.Generator().manual_seed(4)
+    sizes = [1, 7, 2048, 2049, 65536 * 3 + 5, 4096, 13]
+    states = []
+    for n in sizes:
+        p0 = torch.randn(n, generator=gen)
+        g = (torch.randn(n, generator=gen) * 0.01).to(gdt).to(DEV)
+        a = [p0.to(DEV), torch.zeros(n, device=DEV), torch.zeros(n, device=DEV), p0.bfloat16().to(DEV)]
+        b = [t.clone() for t in a]
+        states.append((g, a, b))
+    norm = torch.tensor([4.0], dtype=torch.float64, device=DEV)
+    for step in range(1, 4):
+        args = lambda: _hip.AdamWArgs(lr=1e-3, beta1=0.9, beta2=0.95, eps=1e-8, weight_decay=0.01,
+                                      bias_correction1=1 - 0.9 ** step, bias_correction2=1 - 0.95 ** step,
+                                      max_grad_norm=1.0, grad_scale=0.5, mode=_hip.ADAM_DEEPSPEED, grad_dtype=0)
+        _hip.adamw_multi([(g, *a) for g, a, _b in states], args(), grad_sq_norm=norm)
+        for g, _a, b in states:
+            _hip.adamw_step(g, *b, args(), grad_sq_norm=norm)
+    torch.cuda.synchronize()
+    for g, a, b in states:
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
+
+
 # ---------------------------------------------------------------- packed input column blocks (smt.py:351-358)
 @pytest.mark.parametrize("T,in_f,cbs", [(300, 1024, [3, 0]), (4096, 14336, [55, 7, 8, 30]), (1, 512, [1])])
 def test_colblock_gather_bit_exact(T, in_f, cbs):

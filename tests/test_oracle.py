@@ -216,3 +216,36 @@ def test_channel_selection_error_paths():
         ref.select_channel(act, n=3, calculate_strategy="bogus")
     with pytest.raises(UnboundLocalError):
         ref.select_channel(act, n=0)
+
+
+# ---------------------------------------------------------------- MX-fp8 format (config 5, no reference counterpart)
+def test_mx_exponent_rule():
+    amax = torch.tensor([0.0, 448.0, 448.0 * (1 + 2 ** -23), 1.0, 2.0 ** -130, 3.0e38, 449.0, 0.875])
+    e = ref.mx_exponent(amax).tolist()
+    assert e == [-127, 0, 1, -8, -127, 120, 1, -9]
+    # smallest e with amax <= 448 * 2^e (checked in fp64)
+    for a, k in zip(amax.double().tolist(), e):
+        if a > 2.0 ** -126:
+            assert a <= 448.0 * 2.0 ** k and a > 448.0 * 2.0 ** (k - 1)
+
+
+def test_mx_quant_round_trip_and_no_saturation():
+    gen = torch.Generator().manual_seed(0)
+    x = (torch.randn(200, 512, generator=gen) * torch.exp(2 * torch.randn(200, 512, generator=gen))).bfloat16()
+    q, s = ref.mx_quant_cols(x, [1, 0])
+    assert q.shape == (2, 256, 256) and s.shape == (2, 8, 256)
+    vals = q.view(torch.float8_e4m3fn).float()
+    assert vals.abs().max() <= 448.0 and not torch.isnan(vals).any()
+    d = ref.mx_dequant(q, s)
+    assert torch.all(d[:, 200:] == 0)                                  # rows past T are zero
+    # e4m3 relative rounding of normal values <= 2^-4; every group's max is a normal value
+    for i, b in enumerate([1, 0]):
+        o = x[:, b * 256:(b + 1) * 256].double()
+        dd = d[i, :200]
+        big = o.abs() > 0
+        rel = ((dd - o).abs() / o.abs().clamp_min(1e-300))[big]
+        assert rel.median() < 2 ** -4
+    # exactly representable data is reproduced exactly
+    ints = torch.randint(-15, 16, (64, 256), generator=gen).bfloat16()
+    q2, s2 = ref.mx_quant_cols(ints, [0])
+    assert torch.equal(ref.mx_dequant(q2, s2)[0], ints.double())
