@@ -47,6 +47,7 @@ sys.path.insert(0, ROOT)
 METRIC = "train tokens/sec + peak GB HBM, LLaMA-3-8B SMT(0.71%) at 1/2/4/8 MI355X"
 PEAK_BF16_TFLOPS = 2500.0          # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0              # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PEAK_MXFP8_TFLOPS = 5000.0         # block-scaled e4m3 MFMA, 2x bf16 per clock (MI355X_MICROARCH.md)
 F_ALG_GFLOP_PER_TOKEN = 31.744     # fwd 15.009 + dgrad 15.009 + wgrad 0.114 + attn 1.611
 
 MODELS = {
@@ -118,7 +119,7 @@ class WgradTimer:
         self.enabled = False
         self.records = []      # (start, end, algorithmic bytes, flops)
 
-    def hook(self, T, n_tiles, out_bytes, stream_fn):
+    def hook(self, T, n_tiles, out_bytes, stream_fn, operand_bytes=2):
         if not self.enabled:
             return stream_fn()
         s = torch.cuda.current_stream()
@@ -127,7 +128,8 @@ class WgradTimer:
         e0.record(s)
         r = stream_fn()
         e1.record(s)
-        self.records.append((e0, e1, n_tiles * (T * 256 * 2 * 2 + 65536 * out_bytes), 2.0 * T * 65536 * n_tiles))
+        self.records.append((e0, e1, n_tiles * (T * 256 * operand_bytes * 2 + 65536 * out_bytes),
+                             2.0 * T * 65536 * n_tiles))
         return r
 
     def summary(self):
@@ -148,6 +150,17 @@ def install_wgrad_timer(timer: WgradTimer):
         return timer.hook(g2.shape[0], rc.shape[0], out.element_size(),
                           lambda: orig(g2, x2, rc, out, accumulate=accumulate, order=order))
     _hip.tile_wgrad = timed
+
+
+def install_mx_wgrad_timer(timer: WgradTimer):
+    """The fp8 path's smt_tile_wgrad_mx (1-byte operands; T = the MX blocks' padded rows)."""
+    from sparse_matrix_tuning_amd import _hip
+    orig = _hip.tile_wgrad_mx
+
+    def timed(g, x, rc, out, accumulate=False, order=None):
+        return timer.hook(g.ldq, rc.shape[0], out.element_size(),
+                          lambda: orig(g, x, rc, out, accumulate=accumulate, order=order), operand_bytes=1)
+    _hip.tile_wgrad_mx = timed
 
 
 class AttnTimer:
@@ -608,6 +621,8 @@ def main():
 
     timer = WgradTimer()
     install_wgrad_timer(timer)
+    mx_timer = WgradTimer()
+    install_mx_wgrad_timer(mx_timer)
     atimer = AttnTimer()
     if not (args.eager_ops or args.sdpa_attention):
         install_attn_timer(atimer)
@@ -697,9 +712,9 @@ def main():
 
     for i in range(args.warmup):
         step(smt_batches[i])
-    timer.enabled = atimer.enabled = adam_timer.enabled = True
+    timer.enabled = mx_timer.enabled = atimer.enabled = adam_timer.enabled = True
     elapsed, per_step, loss = timed_steps(step, smt_batches[args.warmup:], world, device)
-    timer.enabled = atimer.enabled = adam_timer.enabled = False
+    timer.enabled = mx_timer.enabled = atimer.enabled = adam_timer.enabled = False
     t_max = torch.tensor([elapsed, _median(per_step)], dtype=torch.float64, device=device)
     peak = torch.tensor([torch.cuda.max_memory_allocated(device) / 1e9], dtype=torch.float64, device=device)
     if world > 1:
@@ -709,6 +724,7 @@ def main():
     tokens = world * B * S * args.steps
     value = tokens / elapsed
     w = timer.summary()
+    w_mx = mx_timer.summary()
     a_sum = atimer.summary()
     adam = adam_timer.summary()
     del smt_batches
@@ -738,12 +754,16 @@ def main():
     if rank == 0:
         per_gpu = value / world
         roofline = None
+        mx = bool(w_mx and w_mx["seconds"] > 0)
+        if mx:                              # the fp8 path: the MX-fp8 tile wgrad is the SMT kernel
+            w = w_mx
         if w and w["seconds"] > 0:
             avg = w["seconds"] / w["launches"]
             tflops = w["flops"] / w["seconds"] / 1e12
             alg_bytes = w["bytes"] / w["launches"]
             alg_gbs = alg_bytes / avg / 1e9
-            traffic, tsrc = pmc_traffic(args)
+            traffic, tsrc = (None, None) if mx else pmc_traffic(args)
+            peak_mfma = PEAK_MXFP8_TFLOPS if mx else PEAK_BF16_TFLOPS
             # The roof: HBM while the counter bytes are at least ~the algorithmic bytes (no operand slice
             # is shared between the module's tiles, the bench's spread selection: intensity 128 F/B, below
             # the 312 F/B ridge); MFMA when L2/MALL reuse brings the real bytes well below them.
@@ -752,19 +772,24 @@ def main():
                    "frac": round(alg_gbs / PEAK_HBM_GBS, 4),
                    "on_counter_bytes": None if traffic is None else round(traffic / avg / 1e9, 1),
                    "frac_on_counter_bytes": None if traffic is None else round(traffic / avg / 1e9 / PEAK_HBM_GBS, 4)}
-            mfma = {"achieved": round(tflops, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(tflops / PEAK_BF16_TFLOPS, 4)}
+            mfma = {"achieved": round(tflops, 1), "peak": peak_mfma, "unit": "TFLOP/s",
+                    "frac": round(tflops / peak_mfma, 4)}
             roof = hbm if hbm_bound else mfma
             roofline = {"bound": "hbm" if hbm_bound else "mfma", "achieved": roof["achieved"], "peak": roof["peak"],
                         "unit": roof["unit"], "frac": roof["frac"], "traffic": traffic, "traffic_source": tsrc,
-                        "kernel": "smt_tile_wgrad (wgrad_dma_kernel | wgrad_quarter_kernel, + wgrad_reduce_kernel when split)",
+                        "kernel": ("smt_tile_wgrad_mx (wgrad_mx_kernel, + wgrad_reduce_kernel when split; MX-fp8 operands)"
+                                   if mx else "smt_tile_wgrad (wgrad_dma_kernel | wgrad_quarter_kernel, + "
+                                              "wgrad_reduce_kernel when split)"),
                         "launches": w["launches"], "avg_launch_us": round(avg * 1e6, 2),
                         "algorithmic_bytes_per_launch": round(alg_bytes),
                         "flops_per_launch": round(w["flops"] / w["launches"]),
                         "hbm": hbm, "mfma": mfma,
-                        "bytes_note": ("algorithmic bytes per launch = tiles x (2 operand slices T x 256 x 2 B + the "
-                                       "fp32 tile); traffic = FETCH_SIZE x2 + WRITE_SIZE (rocprofv3 --pmc) per call, "
-                                       "including the split-K slabs and their reduce")}
+                        "bytes_note": (("algorithmic bytes per launch = tiles x (2 operand slices T x 256 x 1 B + the "
+                                        "fp32 tile); the MX quantisation of the operands is a separate launch")
+                                       if mx else
+                                       ("algorithmic bytes per launch = tiles x (2 operand slices T x 256 x 2 B + the "
+                                        "fp32 tile); traffic = FETCH_SIZE x2 + WRITE_SIZE (rocprofv3 --pmc) per call, "
+                                        "including the split-K slabs and their reduce"))}
         tiles_by_module = {}
         for (m, _l), v in list(sel_mlp.items()) + list(sel_att.items()):
             tiles_by_module.setdefault(m, []).extend(v)

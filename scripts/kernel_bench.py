@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--patterns", nargs="*", default=["random", "clustered"])
     ap.add_argument("--orders", nargs="*", type=int, default=[0, 1])
     ap.add_argument("--tag", default=os.environ.get("SMT_WGRAD_SLOTS", "5"))
+    ap.add_argument("--mx", action="store_true", help="time smt_mx_quant_cols + smt_tile_wgrad_mx instead")
     args = ap.parse_args()
     dev = torch.device("cuda")
     torch.manual_seed(0)
@@ -67,6 +68,24 @@ def main():
             wsb = _hip.wgrad_workspace_bytes(T, n)
             ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)
             st = torch.cuda.current_stream().cuda_stream
+
+            if args.mx:
+                rbs = sorted({r for r, _ in tiles})
+                cbs = sorted({c for _, c in tiles})
+                rb_dev = torch.tensor(rbs, dtype=torch.int32, device=dev)
+                cb_dev = torch.tensor(cbs, dtype=torch.int32, device=dev)
+                qg = _hip.mx_quant_cols(g, rb_dev)
+                qx = _hip.mx_quant_cols(x, cb_dev)
+                prc = _hip.tile_table([(rbs.index(r), cbs.index(c)) for r, c in tiles], dev)
+                t_q = timeit(lambda: (_hip.mx_quant_cols(g, rb_dev), _hip.mx_quant_cols(x, cb_dev)))
+                t = timeit(lambda: _hip.tile_wgrad_mx(qg, qx, prc, out, order=order if use_order else None))
+                flops = 2.0 * T * 65536 * n
+                bytes_alg = n * (T * 256 * 2 + 65536 * 4)
+                q_bytes = (len(rbs) + len(cbs)) * T * 256 * (2 + 1 + 1 / 32)
+                print(json.dumps(dict(tag="mx", pattern=pattern, order=use_order, tiles=n, us=round(t * 1e6, 1),
+                                      alg_tbs=round(bytes_alg / t / 1e12, 3), tflops=round(flops / t / 1e12, 1),
+                                      quant_us=round(t_q * 1e6, 1), quant_tbs=round(q_bytes / t_q / 1e12, 3))), flush=True)
+                continue
 
             def run():
                 assert lib.smt_tile_wgrad(g.data_ptr(), g.stride(0), x.data_ptr(), x.stride(0), T, rc.data_ptr(),

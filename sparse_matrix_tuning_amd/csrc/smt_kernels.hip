@@ -657,8 +657,6 @@ void wgrad_reduce_kernel(const float* __restrict__ slab, int S, void* __restrict
 // nothing saturates (amax = the 32 values' max |x|; e = -127 for an all-zero group; computed from
 // the bits of amax, exact), and q = e4m3_rne(x * 2^-e) (a power-of-two multiply: exact).
 // ------------------------------------------------------------------------------------------------
-constexpr int kMxRows = 64;                                // T rows per quantiser workgroup
-
 __device__ __forceinline__ int mx_exponent(float amax) {
     const uint32_t b = __float_as_uint(amax);
     const int ef = (int)((b >> 23) & 255u);
@@ -667,43 +665,61 @@ __device__ __forceinline__ int mx_exponent(float amax) {
     return e < -127 ? -127 : e;
 }
 
+// One workgroup per (column block, ROWS rows of T). The [ROWS][256] bf16 slab is staged through
+// LDS with coalesced 16-B row loads; LDS chunk ch of row r is stored at ch ^ (((r >> 4) & 3) << 2)
+// so that the column reads below are conflict-free. Then LPF = ROWS/16 lanes share one column f:
+// lane c quantises rows 16c .. 16c+15 of it (the 32-row group's amax is one shuffle with the
+// neighbour lane) and the LPF lanes write the column's ROWS bytes of q[blk][f] as one contiguous
+// run (ROWS = 128: whole 128-B lines).
+__device__ __forceinline__ int mx_slab_off(int r, int f) {
+    return r * kTile + ((((f >> 3) ^ (((r >> 4) & 3) << 2))) << 3) + (f & 7);
+}
+
+template <int ROWS>
 __global__ __launch_bounds__(256)
 void mx_quant_cols_kernel(const uint16_t* __restrict__ x, int64_t ldx, int64_t T, const int32_t* __restrict__ blocks,
                           int64_t ldq, uint8_t* __restrict__ q, uint8_t* __restrict__ sc) {
-    __shared__ __attribute__((aligned(16))) uint16_t slab[kMxRows][kTile];
+    constexpr int LPF = ROWS / 16;                          // lanes per column
+    constexpr int FPP = 256 / LPF;                          // columns per pass
+    __shared__ __attribute__((aligned(16))) uint16_t slab[ROWS * kTile];
     const int blk = blockIdx.x;
-    const int64_t t0 = (int64_t)blockIdx.y * kMxRows;
+    const int64_t t0 = (int64_t)blockIdx.y * ROWS;
     const int tid = threadIdx.x;
     const uint16_t* src = x + (int64_t)blocks[blk] * kTile;
 #pragma unroll
-    for (int i = 0; i < kMxRows * 32 / 256; ++i) {           // 64 rows x 32 chunks of 16 B
+    for (int i = 0; i < ROWS * 32 / 256; ++i) {               // ROWS rows x 32 chunks of 16 B
         const int cid = tid + 256 * i;
         const int rr = cid >> 5, ch = cid & 31;
         uint4 v = make_uint4(0, 0, 0, 0);
         if (t0 + rr < T) v = *reinterpret_cast<const uint4*>(src + (t0 + rr) * ldx + ch * 8);
-        *reinterpret_cast<uint4*>(&slab[rr][ch * 8]) = v;
+        *reinterpret_cast<uint4*>(&slab[mx_slab_off(rr, ch * 8)]) = v;
     }
     __syncthreads();
-    // thread = feature f: two 32-row groups -> 64 contiguous bytes of q[blk][f] and two exponents
-    uint32_t w[16];
+    const int c = tid % LPF;                                 // 16-row run of the column
+    const bool live = t0 + 16 * c < ldq;                     // the last workgroup may be half empty
 #pragma unroll
-    for (int g = 0; g < 2; ++g) {
+    for (int pass = 0; pass < LPF; ++pass) {
+        const int f = pass * FPP + tid / LPF;
+        float v[16];
         float amax = 0.f;
 #pragma unroll
-        for (int k = 0; k < 32; ++k) amax = fmaxf(amax, fabsf(bf16_bits_to_f32(slab[32 * g + k][tid])));
+        for (int k = 0; k < 16; ++k) {
+            v[k] = bf16_bits_to_f32(slab[mx_slab_off(16 * c + k, f)]);
+            amax = fmaxf(amax, fabsf(v[k]));
+        }
+        amax = fmaxf(amax, __shfl_xor(amax, 1, 64));         // the other half of the 32-row group
         const int e = mx_exponent(amax);
         const float inv = __uint_as_float((uint32_t)(127 - e) << 23);     // 2^-e, e in [-127, 121]
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int r = 32 * g + 4 * k;
-            w[8 * g + k] = pack4(bf16_bits_to_f32(slab[r][tid]) * inv, bf16_bits_to_f32(slab[r + 1][tid]) * inv,
-                                 bf16_bits_to_f32(slab[r + 2][tid]) * inv, bf16_bits_to_f32(slab[r + 3][tid]) * inv);
+        uint4 w;
+        w.x = pack4(v[0] * inv, v[1] * inv, v[2] * inv, v[3] * inv);
+        w.y = pack4(v[4] * inv, v[5] * inv, v[6] * inv, v[7] * inv);
+        w.z = pack4(v[8] * inv, v[9] * inv, v[10] * inv, v[11] * inv);
+        w.w = pack4(v[12] * inv, v[13] * inv, v[14] * inv, v[15] * inv);
+        if (live) {
+            *reinterpret_cast<uint4*>(q + ((int64_t)blk * kTile + f) * ldq + t0 + 16 * c) = w;
+            if ((c & 1) == 0) sc[((int64_t)blk * (ldq >> 5) + (t0 >> 5) + (c >> 1)) * kTile + f] = (uint8_t)(e + 127);
         }
-        sc[((int64_t)blk * (ldq >> 5) + (t0 >> 5) + g) * kTile + tid] = (uint8_t)(e + 127);
     }
-    uint4* dst = reinterpret_cast<uint4*>(q + ((int64_t)blk * kTile + tid) * ldq + t0);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) dst[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
 }
 
 // The MX wgrad: C[m][n] = sum_t A(t, m) * B(t, n) over the MX column blocks of g (A, the tile's row
@@ -1532,10 +1548,23 @@ int smt_mx_quant_cols(const void* x, int64_t ld_x, int64_t T, const int32_t* blo
     if (!x || !blocks_dev || !q || !scales) return fail(SMT_E_INVALID, "smt_mx_quant_cols: null pointer");
     if (!aligned16(x) || (ld_x & 7) || !aligned16(q))
         return fail(SMT_E_ALIGN, "smt_mx_quant_cols: 16-byte aligned rows required (ld %% 8 == 0)");
-    if (ldq / 64 > 65535) return fail(SMT_E_INVALID, "smt_mx_quant_cols: T too large");
-    hipLaunchKernelGGL(mx_quant_cols_kernel, dim3(n_blocks, (unsigned)(ldq / 64)), dim3(256), 0, stream,
-                       static_cast<const uint16_t*>(x), ld_x, T, blocks_dev, ldq, static_cast<uint8_t*>(q),
-                       static_cast<uint8_t*>(scales));
+    // SMT_MX_QUANT_ROWS = 32 | 64 (default) | 128 rows per workgroup (A/B runs)
+    static const int rows = [] { const char* e = getenv("SMT_MX_QUANT_ROWS"); const int v = e ? atoi(e) : 64;
+                                 return (v == 32 || v == 128) ? v : 64; }();
+    const int64_t wgs = (ldq + rows - 1) / rows;
+    if (wgs > 65535) return fail(SMT_E_INVALID, "smt_mx_quant_cols: T too large");
+    if (rows == 32)
+        hipLaunchKernelGGL(mx_quant_cols_kernel<32>, dim3(n_blocks, (unsigned)wgs), dim3(256), 0, stream,
+                           static_cast<const uint16_t*>(x), ld_x, T, blocks_dev, ldq, static_cast<uint8_t*>(q),
+                           static_cast<uint8_t*>(scales));
+    else if (rows == 64)
+        hipLaunchKernelGGL(mx_quant_cols_kernel<64>, dim3(n_blocks, (unsigned)wgs), dim3(256), 0, stream,
+                           static_cast<const uint16_t*>(x), ld_x, T, blocks_dev, ldq, static_cast<uint8_t*>(q),
+                           static_cast<uint8_t*>(scales));
+    else
+        hipLaunchKernelGGL(mx_quant_cols_kernel<128>, dim3(n_blocks, (unsigned)wgs), dim3(256), 0, stream,
+                           static_cast<const uint16_t*>(x), ld_x, T, blocks_dev, ldq, static_cast<uint8_t*>(q),
+                           static_cast<uint8_t*>(scales));
     return check_launch("mx_quant_cols_kernel");
 }
 

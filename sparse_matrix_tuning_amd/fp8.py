@@ -24,10 +24,9 @@ No CPU path: every entry point raises without a ROCm device.
 """
 from __future__ import annotations
 
-from typing import Optional
-
 import os
 import weakref
+from typing import Optional
 
 import torch
 
@@ -144,6 +143,9 @@ class Fp8Weight:
 
     def __init__(self, weight: torch.Tensor, group: "Fp8Group" = None, group_index: int = 0):
         w = weight.detach()
+        # the tile weight gradient of an SMT module over this weight: MX-fp8 operands (e4m3, one
+        # e8m0 exponent per 32 tokens; smt_tile_wgrad_mx) by default, bf16 with SMT_FP8_TILE_WGRAD=bf16
+        self.mx_wgrad = os.environ.get("SMT_FP8_TILE_WGRAD", "mx") != "bf16"
         self.w8, self.sw = quant_rows(w)                  # [out, in], per output row
         self.sw_row = self.sw.view(1, -1)
         self.group = group

@@ -132,6 +132,24 @@ class TileIndex:
             self._dev[key] = t
         return t
 
+    def mx_tables(self, device: torch.device):
+        """Device tables of the MX-fp8 wgrad (fp8 path): int32 [n_rb] row blocks, int32 [n_cb] column
+        blocks (both in order of first use) and the int32 [n, 2] table of (row-block position,
+        column-block position)."""
+        key = ("mx", device.type, device.index)
+        t = self._dev.get(key)
+        if t is None:
+            rbs = {}
+            for r, _c in self.index_list:
+                rbs.setdefault(r, len(rbs))
+            cbs = self.column_blocks()
+            pos = {c: i for i, c in enumerate(cbs)}
+            t = (torch.tensor(list(rbs), dtype=torch.int32).to(device),
+                 torch.tensor(cbs, dtype=torch.int32).to(device),
+                 _hip.tile_table([(rbs[r], pos[c]) for r, c in self.index_list], device))
+            self._dev[key] = t
+        return t
+
     def transposed_descs(self, weight_t: torch.Tensor) -> torch.Tensor:
         """Device smt_tile_desc[] for the transposed write-back of ``selected_weight`` into W^T."""
         key = ("wt", weight_t.data_ptr(), weight_t.device.index)
@@ -269,9 +287,18 @@ class linearZ(torch.autograd.Function):
         ctx.tiles = tiles
         ctx.sink = getattr(selected_weight, "_smt_grad_sink", None)
         ctx.packed = False
+        ctx.mx = None
         saved = input
         in_blocks = weight.shape[1] // Block_dimension
-        if (ctx.needs_input_grad[1] and len(tiles) and input.device.type == "cuda"
+        fw = getattr(weight, "_smt_fp8", None)
+        if (fw is not None and fw.mx_wgrad and ctx.needs_input_grad[1] and len(tiles)
+                and input.device.type == "cuda"):
+            # fp8 path: the tile weight gradient runs on MX-fp8 operands; keep only the input's
+            # column blocks, quantised (half the bytes of the bf16 blocks)
+            _rb, cb_dev, _table = tiles.mx_tables(input.device)
+            ctx.mx = _hip.mx_quant_cols(_rows_ready(input.reshape(-1, weight.shape[1])), cb_dev)
+            saved = None
+        elif (ctx.needs_input_grad[1] and len(tiles) and input.device.type == "cuda"
                 and 2 * len(tiles.column_blocks()) <= in_blocks):
             cb_dev, _ = tiles.packed_tables(input.device)
             saved = _hip.colblock_gather(_rows_ready(input.reshape(-1, weight.shape[1])), cb_dev)
@@ -279,7 +306,6 @@ class linearZ(torch.autograd.Function):
         ctx.save_for_backward(saved, weight)
         # q/k/v (gate/up) share their input: their data gradients accumulate in one buffer (bf16)
         # or run as one joint GEMM (fp8 group)
-        fw = getattr(weight, "_smt_fp8", None)
         if fw is None:
             ctx.acc = dgrad.register(input, ctx)
         else:
@@ -295,7 +321,21 @@ class linearZ(torch.autograd.Function):
         tiles = ctx.tiles
         n = len(tiles)
         grad_input = grad_weight = None
-        if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1] and ctx.mx is not None:
+            g2 = _rows_ready(grad_output.reshape(-1, weight.shape[0]))
+            rb_dev, _cb, table = tiles.mx_tables(g2.device)
+            qg = _hip.mx_quant_cols(g2, rb_dev)
+            sink = ctx.sink
+            if sink is not None:
+                _hip.tile_wgrad_mx(qg, ctx.mx, table, sink.buffer, accumulate=sink.take_accumulate(),
+                                   order=tiles.schedule(g2.device))
+                sink.mark_ready()
+            else:
+                grad_weight = torch.empty(n * Block_dimension, Block_dimension,
+                                          dtype=grad_output.dtype, device=grad_output.device)
+                _hip.tile_wgrad_mx(qg, ctx.mx, table, grad_weight, order=tiles.schedule(g2.device))
+            ctx.mx = None
+        elif ctx.needs_input_grad[1]:
             out_f = weight.shape[0]
             g2 = _rows_ready(grad_output.reshape(-1, out_f))
             dev = g2.device

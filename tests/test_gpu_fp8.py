@@ -99,7 +99,18 @@ def test_smt_module_fp8_forward_backward():
     y8.backward(g)
     assert _rel(y8, x.float() @ W.float().t()) < 8e-2
     assert _rel(x8.grad, gi_bf16) < 8e-2
-    assert torch.equal(mod.selected_weight.grad, gw_bf16)          # tile gradients stay bf16-exact
+    # tile gradients: the MX-fp8 kernel on the MX column blocks of g and x (bit-identical to calling
+    # it directly), within the MX quantisation bound of the bf16 path (tests/test_gpu_mx.py)
+    rb, cb, table = mod.tiles.mx_tables(DEV)
+    want = torch.empty_like(gw_bf16)
+    _hip.tile_wgrad_mx(_hip.mx_quant_cols(g.view(-1, 512), rb), _hip.mx_quant_cols(x.view(-1, 768), cb), table, want)
+    assert torch.equal(mod.selected_weight.grad, want)
+    assert _rel(mod.selected_weight.grad, gw_bf16) < 6e-2
+    # SMT_FP8_TILE_WGRAD=bf16: the bf16 tile kernel, bf16-exact
+    mod.selected_weight.grad = None
+    W._smt_fp8.mx_wgrad = False
+    mod(x.clone().requires_grad_(True)).backward(g)
+    assert torch.equal(mod.selected_weight.grad, gw_bf16)
     del W._smt_fp8
 
 
