@@ -95,6 +95,13 @@ def parse():
     ap.add_argument("--fp8", action="store_true",
                     help="BASELINE config 5 (DeepSeek-R1-Distill-LLaMA-8B = the LLaMA-3-8B architecture, "
                          "SMT(0.86%%)): the decoder layers' frozen linears run as rowwise-scaled e4m3 GEMMs")
+    ap.add_argument("--no-overlap-wgrad", action="store_true",
+                    help="run the tile weight gradients on the current stream (default: their own stream, "
+                         "overlapped with the data-gradient GEMMs)")
+    ap.add_argument("--roofline-steps", type=int, default=5,
+                    help="extra SMT steps after the timed region with the wgrad stream joined, on which the "
+                         "tile-wgrad roofline is measured (the kernel alone; in the timed region it shares the "
+                         "chip with the data-gradient GEMM)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0, help="0 disables the CPU leg")
     ap.add_argument("--out", default=None, help="also write the JSON line here")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm) or gloo (functional tests)")
@@ -651,7 +658,7 @@ def main():
 
     # ---- warm-up: full fine-tuning + gradient harvest (fine_tune.py:710-775) ----
     ds_config = {"gradient_clipping": 1.0, "train_micro_batch_size_per_gpu": B, "train_batch_size": B * world}
-    smt_config = dict(ds_config, fp8_linears=bool(args.fp8))
+    smt_config = dict(ds_config, fp8_linears=bool(args.fp8), overlap_wgrad=not args.no_overlap_wgrad)
     from sparse_matrix_tuning_amd.smt.smt import _NO_DECAY
     groups = [{"params": [p for n, p in model.named_parameters() if not any(nd in n.lower() for nd in _NO_DECAY)],
                "weight_decay": 0.0},
@@ -729,6 +736,28 @@ def main():
     adam = adam_timer.summary()
     del smt_batches
 
+    # ---- the tile wgrad alone (its roofline): the same steps with the wgrad stream joined ----
+    overlapped = {"bf16": w, "mx": w_mx}
+    if engine.wgrad_stream is not None and args.roofline_steps > 0:
+        side = engine.wgrad_stream
+        engine.wgrad_stream = None
+        for tg in engine.tile_groups:
+            if tg.buckets is not None:
+                tg.buckets.side_stream = None
+        iso = batches(args.roofline_steps, B, S, vocab, rank, device, offset=70000)
+        timer.records, mx_timer.records = [], []
+        timer.enabled = mx_timer.enabled = True
+        for b in iso:
+            step(b)
+        torch.cuda.synchronize()
+        timer.enabled = mx_timer.enabled = False
+        w, w_mx = timer.summary(), mx_timer.summary()
+        engine.wgrad_stream = side
+        for tg in engine.tile_groups:
+            if tg.buckets is not None:
+                tg.buckets.side_stream = side
+        del iso
+
     # ---- the reference's memory policy (per-layer recompute), same engine and tiles ----
     ckpt_mode = None
     if args.ref_mode_steps > 0 and not args.grad_ckpt:
@@ -757,6 +786,7 @@ def main():
         mx = bool(w_mx and w_mx["seconds"] > 0)
         if mx:                              # the fp8 path: the MX-fp8 tile wgrad is the SMT kernel
             w = w_mx
+        w_ov = overlapped["mx" if mx else "bf16"]
         if w and w["seconds"] > 0:
             avg = w["seconds"] / w["launches"]
             tflops = w["flops"] / w["seconds"] / 1e12
@@ -781,6 +811,15 @@ def main():
                                    if mx else "smt_tile_wgrad (wgrad_dma_kernel | wgrad_quarter_kernel, + "
                                               "wgrad_reduce_kernel when split)"),
                         "launches": w["launches"], "avg_launch_us": round(avg * 1e6, 2),
+                        "measured_on": (f"{args.roofline_steps} SMT steps after the timed region with the wgrad "
+                                        "stream joined (the kernel alone)" if engine.wgrad_stream is not None
+                                        and args.roofline_steps > 0 else "the timed region"),
+                        "timed_region_avg_launch_us": (round(w_ov["seconds"] / w_ov["launches"] * 1e6, 2)
+                                                       if w_ov and w_ov["launches"] else None),
+                        "timed_region_note": ("in the timed region the tile wgrad runs on its own stream beside "
+                                              "the MFMA-bound data-gradient GEMM: its launches stretch over the "
+                                              "GEMM's duration while the step gets shorter"
+                                              if engine.wgrad_stream is not None else None),
                         "algorithmic_bytes_per_launch": round(alg_bytes),
                         "flops_per_launch": round(w["flops"] / w["launches"]),
                         "hbm": hbm, "mfma": mfma,

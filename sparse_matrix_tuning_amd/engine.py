@@ -221,6 +221,21 @@ class _GradSink:
         window (a later micro-step, or a second backward through the module), else overwrite."""
         return self.group is not None and self.group.reported[self.index]
 
+    def run(self, launch, *keep: torch.Tensor) -> None:
+        """Enqueue this module's tile-gradient kernels (``launch()``): on the engine's wgrad stream
+        when it has one, after the work already on the current stream (the output gradient), so the
+        HBM-bound tile GEMM overlaps the MFMA-bound data-gradient GEMM. ``keep``: tensors the kernels
+        read, held for the caching allocator until the wgrad stream has passed them."""
+        side = self.engine.wgrad_stream if self.engine is not None else None
+        if side is None:
+            launch()
+            return
+        side.wait_stream(torch.cuda.current_stream(side.device))
+        with torch.cuda.stream(side):
+            launch()
+        for t in keep:
+            t.record_stream(side)
+
     def mark_ready(self) -> None:
         """Called by ``linearZ.backward`` once this module's tile-gradient kernels are enqueued."""
         if self.group is not None:
@@ -261,6 +276,7 @@ class TileGradBuckets:
         self.seen: set = set()
         self.next = -1                         # next bucket to issue (descending)
         self.armed = False
+        self.side_stream = None                # the engine's wgrad stream: joined before a collective
 
     def arm(self) -> None:
         self.pending = [b[2] for b in self.buckets]
@@ -286,6 +302,8 @@ class TileGradBuckets:
 
     def _launch(self, b: int) -> None:
         start, end, _ = self.buckets[b]
+        if self.side_stream is not None:
+            torch.cuda.current_stream(self.side_stream.device).wait_stream(self.side_stream)
         self.works[b] = dist.all_reduce(self.buffer[start:end], async_op=True)
 
     def finish(self) -> None:
@@ -493,6 +511,13 @@ class SMTEngine:
                 if dense:
                     self.dense_groups.append((group, dense))
         self._norm_sq = torch.zeros(1, dtype=torch.float64, device=self.device)
+        # tile-gradient kernels on a stream of their own (overlap_wgrad, default on): joined before
+        # every collective over the tile buffer and at the end of backward
+        self.wgrad_stream = (torch.cuda.Stream(self.device) if self.tile_groups and self.device.type == "cuda"
+                             and cfg.get("overlap_wgrad", True) else None)
+        for tg in self.tile_groups:
+            if tg.buckets is not None:
+                tg.buckets.side_stream = self.wgrad_stream
         dense_params = [p for _g, ps in self.dense_groups for p in ps]
         self.dense_buckets = (DenseGradBuckets(dense_params, self.reduce_bucket_size, self.world)
                               if self.world > 1 and dense_params else None)
@@ -534,6 +559,8 @@ class SMTEngine:
             if self.dense_buckets is not None:
                 self.dense_buckets.arm()
         loss.backward()
+        if self.wgrad_stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.wgrad_stream)
         if boundary:
             for tg in self.tile_groups:
                 tg.zero_unreported()

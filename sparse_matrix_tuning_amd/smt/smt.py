@@ -324,16 +324,18 @@ class linearZ(torch.autograd.Function):
         if ctx.needs_input_grad[1] and ctx.mx is not None:
             g2 = _rows_ready(grad_output.reshape(-1, weight.shape[0]))
             rb_dev, _cb, table = tiles.mx_tables(g2.device)
-            qg = _hip.mx_quant_cols(g2, rb_dev)
             sink = ctx.sink
             if sink is not None:
-                _hip.tile_wgrad_mx(qg, ctx.mx, table, sink.buffer, accumulate=sink.take_accumulate(),
-                                   order=tiles.schedule(g2.device))
+                acc, mx, order = sink.take_accumulate(), ctx.mx, tiles.schedule(g2.device)
+                sink.run(lambda: _hip.tile_wgrad_mx(_hip.mx_quant_cols(g2, rb_dev), mx, table, sink.buffer,
+                                                    accumulate=acc, order=order),
+                         g2, mx.q, mx.scales)
                 sink.mark_ready()
             else:
                 grad_weight = torch.empty(n * Block_dimension, Block_dimension,
                                           dtype=grad_output.dtype, device=grad_output.device)
-                _hip.tile_wgrad_mx(qg, ctx.mx, table, grad_weight, order=tiles.schedule(g2.device))
+                _hip.tile_wgrad_mx(_hip.mx_quant_cols(g2, rb_dev), ctx.mx, table, grad_weight,
+                                   order=tiles.schedule(g2.device))
             ctx.mx = None
         elif ctx.needs_input_grad[1]:
             out_f = weight.shape[0]
@@ -345,8 +347,8 @@ class linearZ(torch.autograd.Function):
                 x2, table = _rows_ready(saved.reshape(-1, weight.shape[1])), tiles.device_table(dev)
             sink = ctx.sink
             if sink is not None:
-                _hip.tile_wgrad(g2, x2, table, sink.buffer, accumulate=sink.take_accumulate(),
-                                order=tiles.schedule(dev))
+                acc, order = sink.take_accumulate(), tiles.schedule(dev)
+                sink.run(lambda: _hip.tile_wgrad(g2, x2, table, sink.buffer, accumulate=acc, order=order), g2, x2)
                 sink.mark_ready()
             else:
                 grad_weight = torch.empty(n * Block_dimension, Block_dimension,
