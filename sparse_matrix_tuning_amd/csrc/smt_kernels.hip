@@ -642,14 +642,16 @@ __device__ __forceinline__ void wgrad_store_q(f32x16_t (&acc)[2][2], void* __res
             }
 }
 
-template <int OUT>
+template <int OUT, int QS = kQSlots>
 __global__ __launch_bounds__(kQThreads, 2)
 void wgrad_quarter_kernel(const uint16_t* __restrict__ g, int64_t ldg,
                           const uint16_t* __restrict__ x, int64_t ldx,
                           int64_t T, int64_t chunk, int S, int n_tiles,
                           const int32_t* __restrict__ tile_rc, const int32_t* __restrict__ order,
                           void* __restrict__ out_ptr, int accumulate) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kQSlots * kQSlotBytes];     // 64 KiB, one array
+    static_assert(QS >= 3 && QS <= 5, "ring depth");
+    constexpr int AHEAD = QS - 2;                          // stages in flight beside the one computed
+    __shared__ __attribute__((aligned(16))) uint8_t lds[QS * kQSlotBytes];          // 64 KiB (4 slots), one array
 
     // logical id L = (s * n_tiles + i) * 4 + quarter, dealt XCD-contiguously (bijective remap)
     const int total = n_tiles * S * 4;
@@ -693,7 +695,7 @@ void wgrad_quarter_kernel(const uint16_t* __restrict__ g, int64_t ldg,
 
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(lds));
     auto issue = [&](int st) {
-        const uint32_t slot = lds0 + (uint32_t)((st % kQSlots) * kQSlotBytes);
+        const uint32_t slot = lds0 + (uint32_t)((st % QS) * kQSlotBytes);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const uint32_t row0 = (uint32_t)(8 * wave + 4 * j) * kQRowBytes;
@@ -716,20 +718,20 @@ void wgrad_quarter_kernel(const uint16_t* __restrict__ g, int64_t ldg,
     const uint32_t feat_byte = 2u * (16u * (gi & 1) + 4u * p);
     const uint32_t krow = 8u * (gi >> 1) + q;
 
-    if (nst > 0) issue(0);
-    if (nst > 1) issue(1);
+#pragma unroll
+    for (int i = 0; i < AHEAD; ++i)
+        if (i < nst) issue(i);
     for (int st = 0; st < nst; ++st) {
-        if (st + 2 < nst) {
-            issue(st + 2);
-            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");     // stage st landed (st+1, st+2 in flight)
-        } else if (st + 1 < nst) {
-            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        // 4 DMA instructions per wave per stage (as wgrad_dma_kernel)
+        if (st + AHEAD < nst) {
+            issue(st + AHEAD);
+            wait_vm_stages(AHEAD);
         } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            wait_vm_stages(nst - 1 - st);
         }
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
-        const uint8_t* A = lds + (st % kQSlots) * kQSlotBytes;
+        const uint8_t* A = lds + (st % QS) * kQSlotBytes;
         const uint8_t* B = A + kQImg;
 #pragma unroll
         for (int ks = 0; ks < kDmaBK / 16; ++ks) {
@@ -1560,9 +1562,10 @@ WgradSplit wgrad_split(int64_t T, int32_t n_tiles, bool allow_quarter = true, do
     const int64_t s_max = std::max<int64_t>(1, std::min<int64_t>(64, (T + 511) / 512));
     int64_t S = 1;
     if (allow_quarter && n_tiles <= quarter_max_tiles()) {
-        // quarter tiles, two workgroups per CU: fill the 512 workgroup slots once (chunks >= 512 rows)
+        // quarter tiles, two workgroups per CU: fill the 512 workgroup slots once, never more (a
+        // 513th workgroup is a second round: n = 6 with ceil(512/24) = 22 ran 57 us, floor = 21 fits)
         sp.quarter = true;
-        S = std::min<int64_t>(s_max, std::max<int64_t>(1, (2 * kCUs + 4 * n_tiles - 1) / (4 * n_tiles)));
+        S = std::min<int64_t>(s_max, std::max<int64_t>(1, (2 * kCUs) / (4 * n_tiles)));
     } else {
         // Time model (measured rates): a workgroup streams its 1 KiB/row of g+x slices at ~25 GB/s per
         // CU and, when S > 1, writes a 256 KiB fp32 slab; the reduce re-reads the n*S slabs (~5 TB/s).
@@ -1634,11 +1637,15 @@ int smt_tile_wgrad(const void* grad_out, int64_t ld_grad_out, const void* x, int
     // SMT_WGRAD_WAVES=4: the wide-wave full-tile kernel (4 waves of 128x128) instead of 8 of 128x64
     static const bool w4 = [] { const char* e = getenv("SMT_WGRAD_WAVES"); return e && atoi(e) == 4; }();
     const dim3 block4(kW4Threads);
+    // SMT_WGRAD_QSLOTS=5: the quarter kernel with 3 stages in flight (80 KiB LDS per workgroup)
+    static const int qslots = [] { const char* e = getenv("SMT_WGRAD_QSLOTS"); return (e && atoi(e) == 5) ? 5 : kQSlots; }();
     const bool dma = !force_reg && sp.chunk * max_ld * 2 < (int64_t)0x7fffffff;
     const bool quarter = dma && sp.quarter;
 #define SMT_WGRAD_DMA(OUT, S_, DST, ACC)                                                                        \
     do {                                                                                                        \
-        if (quarter) hipLaunchKernelGGL((wgrad_quarter_kernel<OUT>), qgrid, qblock, 0, stream, gp, ld_grad_out, xp, \
+        if (quarter && qslots == 5) hipLaunchKernelGGL((wgrad_quarter_kernel<OUT, 5>), qgrid, qblock, 0, stream, gp,  \
+                                        ld_grad_out, xp, ld_x, T, sp.chunk, S_, n_tiles, tile_rc_dev, order_dev, DST, ACC); \
+        else if (quarter) hipLaunchKernelGGL((wgrad_quarter_kernel<OUT>), qgrid, qblock, 0, stream, gp, ld_grad_out, xp, \
                                         ld_x, T, sp.chunk, S_, n_tiles, tile_rc_dev, order_dev, DST, ACC);     \
         else if (w4) hipLaunchKernelGGL((wgrad_w4_kernel<OUT>), grid, block4, 0, stream, gp, ld_grad_out, xp, ld_x, \
                                         T, sp.chunk, S_, n_tiles, tile_rc_dev, order_dev, DST, ACC);            \

@@ -12,6 +12,8 @@ step (fused clip + AdamW), of a 2-layer mini-LLaMA (fused HIP ops, smt_flash att
 * ``acc``: 1 rank, the same two micro-batches as 2 gradient-accumulation micro-steps;
 * ``big``: 1 rank, the concatenated micro-batch of 4.
 
+``--fp8``: the SMT phase on the fp8 path (e4m3 decoder GEMMs, MX-fp8 tile weight gradients).
+
 Writes the post-warm-up weights, the selection, the tile optimizer state and the SMT modules'
 weights after the SMT step (rank 0).
 """
@@ -32,6 +34,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mode", choices=("dp", "acc", "big"), required=True)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--fp8", action="store_true", help="SMT phase on the fp8 path (MX-fp8 tile gradients)")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -79,7 +82,7 @@ def main():
     warm = {n: p.detach().cpu().clone() for n, p in model.named_parameters()}
     engine, opt, sched, sel_mlp, sel_att = trainer.select_and_convert(
         engine, harvester, dims, n_att, n_mlp, calculate_strategy="abs_mean", smt_lr=1e-3, num_training_steps=10,
-        ds_config=ds)
+        ds_config=dict(ds, fp8_linears=args.fp8))
     for b in halves(2000):
         loss = engine(**b, use_cache=False).loss
         engine.backward(loss)

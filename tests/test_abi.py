@@ -67,6 +67,7 @@ def test_validation_errors_without_gpu():
     assert lib.smt_sq_norm(None, 10, None, 0, None, None) == -1
     assert lib.smt_wgrad_workspace_bytes(32768, 27) == 27 * 9 * 65536 * 4
     assert lib.smt_wgrad_workspace_bytes(32768, 8) == 8 * 16 * 65536 * 4       # quarter tiles: 8 x 16 x 4 workgroups
+    assert lib.smt_wgrad_workspace_bytes(32768, 6) == 6 * 21 * 65536 * 4       # 504 <= 512 workgroup slots, one round
     assert lib.smt_wgrad_workspace_bytes(32768, 256) == 0          # S == 1: no slabs
     assert lib.smt_wgrad_workspace_bytes(32768, 128) == 128 * 2 * 65536 * 4
     assert lib.smt_wgrad_workspace_bytes(0, 27) == 0

@@ -64,3 +64,25 @@ def test_dp2_equals_gradient_accumulation_bit_for_bit(tmp_path):
         rel = ((dp["exp_avg"] - big["exp_avg"]).norm() / big["exp_avg"].norm()).item()
         assert rel < 5e-2, rel
         assert (dp["master"] - big["master"]).abs().max().item() <= 4.2e-3    # 2 AdamW steps of lr
+
+
+def test_dp2_equals_gradient_accumulation_fp8_mx(tmp_path):
+    """The fp8 path (config 5): per-token e4m3 rows and MX groups of 32 tokens never straddle two
+    micro-batches, so 2 ranks equal 2 accumulation micro-steps bit for bit here too."""
+    outs = {}
+    for mode in ("acc", "dp"):
+        out = str(tmp_path / f"{mode}.pt")
+        if mode == "dp":
+            cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                   "--master-addr", "127.0.0.1", "--master-port", str(_port()), WORKER, "--mode", "dp", "--fp8",
+                   "--out", out]
+        else:
+            cmd = [sys.executable, WORKER, "--mode", mode, "--fp8", "--out", out]
+        _run(cmd, tmp_path)
+        outs[mode] = torch.load(out, weights_only=True)
+    dp, acc = outs["dp"], outs["acc"]
+    assert dp["sel_mlp"] == acc["sel_mlp"] and dp["sel_att"] == acc["sel_att"]
+    for k in ("master", "exp_avg", "exp_avg_sq"):
+        assert torch.equal(dp[k], acc[k]), k
+    for n in acc["W"]:
+        assert torch.equal(dp["W"][n], acc["W"][n]), n
