@@ -445,148 +445,6 @@ void wgrad_dma_kernel(const uint16_t* __restrict__ g, int64_t ldg,
 }
 
 // ------------------------------------------------------------------------------------------------
-// Wide-wave variant: 4 waves (2 x 2) of 128 x 128 outputs each (16 accumulators of
-// v_mfma_f32_32x32x16_bf16, 256 fp32 per lane, held in AGPRs). Per 16-row k-step a wave reads 8
-// fragments for 16 MFMAs instead of 6 for 8, so the LDS bytes read per FLOP halve against
-// wgrad_dma_kernel (64 KiB vs 96 KiB per 32-row stage at the same MFMA work); one wave per SIMD.
-// Same LDS image, swizzle, 4-slot DMA ring and slab layout as wgrad_dma_kernel.
-// ------------------------------------------------------------------------------------------------
-constexpr int kW4Threads = 256;
-
-template <int OUT>
-__device__ __forceinline__ void wgrad_store_w4(f32x16_t (&acc)[4][4], void* __restrict__ out_ptr, int tile, int s,
-                                               int S, int wm, int wn, int lane, int accumulate) {
-    const int col = lane & 31;
-    const int h = lane >> 5;
-#pragma unroll
-    for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-        for (int nb = 0; nb < 4; ++nb)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int m = wm * 128 + mb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-                const int n = wn * 128 + nb * 32 + col;
-                float v = acc[mb][nb][i];
-                if (OUT == kOutSlab) {
-                    static_cast<float*>(out_ptr)[(int64_t)(tile * S + s) * kTileElems + m * kTile + n] = v;
-                } else if (OUT == kOutF32) {
-                    float* out = static_cast<float*>(out_ptr) + (int64_t)tile * kTileElems;
-                    if (accumulate) v += out[m * kTile + n];
-                    out[m * kTile + n] = v;
-                } else {
-                    uint16_t* out = static_cast<uint16_t*>(out_ptr) + (int64_t)tile * kTileElems;
-                    if (accumulate) v += bf16_bits_to_f32(out[m * kTile + n]);
-                    out[m * kTile + n] = f32_to_bf16_bits(v);
-                }
-            }
-}
-
-template <int OUT>
-__global__ __launch_bounds__(kW4Threads, 1)
-void wgrad_w4_kernel(const uint16_t* __restrict__ g, int64_t ldg,
-                     const uint16_t* __restrict__ x, int64_t ldx,
-                     int64_t T, int64_t chunk, int S, int n_tiles,
-                     const int32_t* __restrict__ tile_rc, const int32_t* __restrict__ order,
-                     void* __restrict__ out_ptr, int accumulate) {
-    constexpr int SLOTS = 4;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[SLOTS * kDmaSlotBytes];   // 128 KiB, one array
-
-    const int total = n_tiles * S;
-    const int b = blockIdx.x;
-    const int q8 = total >> 3, r8 = total & 7, xcd = b & 7;
-    const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
-    const int s = L / n_tiles;
-    const int li = L - s * n_tiles;
-    const int tile = order != nullptr ? order[li] : li;
-    const int r = tile_rc[2 * tile];
-    const int c = tile_rc[2 * tile + 1];
-    const int64_t t_begin = (int64_t)s * chunk;
-    const int64_t t_end = (t_begin + chunk < T) ? (t_begin + chunk) : T;
-    const int rows = (t_end > t_begin) ? (int)(t_end - t_begin) : 0;
-    const int nst = (rows + kDmaBK - 1) / kDmaBK;
-
-    const __amdgpu_buffer_rsrc_t rg = uniform_rsrc(g + t_begin * ldg + (int64_t)r * kTile, (int64_t)rows * ldg * 2);
-    const __amdgpu_buffer_rsrc_t rx = uniform_rsrc(x + t_begin * ldx + (int64_t)c * kTile, (int64_t)rows * ldx * 2);
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave >> 1;
-    const int wn = wave & 1;
-
-    // DMA geometry: wave w fills image rows 8w .. 8w+7 of each operand (four 1 KiB instructions);
-    // lane l of instruction j lands at row k = 8w + 2j + (l>>5), physical byte 16*(l&31), which
-    // holds logical byte (16*(l&31)) ^ ((k&3) << 6) of that row.
-    int voff_g[4], voff_x[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int k = 8 * wave + 2 * j + (lane >> 5);
-        const int lb = (16 * (lane & 31)) ^ ((k & 3) << 6);
-        voff_g[j] = (int)(k * ldg * 2) + lb;
-        voff_x[j] = (int)(k * ldx * 2) + lb;
-    }
-    const int step_g = (int)(kDmaBK * ldg * 2), step_x = (int)(kDmaBK * ldx * 2);
-
-    const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(lds));
-    auto issue = [&](int st) {
-        const uint32_t slot = lds0 + (uint32_t)((st % SLOTS) * kDmaSlotBytes);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t row0 = (uint32_t)(8 * wave + 2 * j) * kRowBytes;
-            dma16(rg, __builtin_amdgcn_readfirstlane(slot + row0), voff_g[j] + st * step_g);
-            dma16(rx, __builtin_amdgcn_readfirstlane(slot + kDmaImg + row0), voff_x[j] + st * step_x);
-        }
-    };
-
-    f32x16_t acc[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-
-    const int gi = lane >> 4;
-    const int q = (lane >> 2) & 3;
-    const int p = lane & 3;
-    const uint32_t feat_byte = 2u * (16u * (gi & 1) + 4u * p);
-    const uint32_t krow = 8u * (gi >> 1) + q;
-
-    if (nst > 0) issue(0);
-    if (nst > 1) issue(1);
-    for (int st = 0; st < nst; ++st) {
-        if (st + 2 < nst) {
-            issue(st + 2);
-            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");    // stage st landed (st+1, st+2 in flight)
-        } else if (st + 1 < nst) {
-            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        const uint8_t* A = lds + (st % SLOTS) * kDmaSlotBytes;
-        const uint8_t* B = A + kDmaImg;
-#pragma unroll
-        for (int ks = 0; ks < kDmaBK / 16; ++ks) {
-            bf16x8_t af[4], bfr[4];
-#pragma unroll
-            for (int mb = 0; mb < 4; ++mb)
-                af[mb] = tr_frag(A, ks * 16 + krow, 2u * (wm * 128 + mb * 32) + feat_byte);
-#pragma unroll
-            for (int nb = 0; nb < 4; ++nb)
-                bfr[nb] = tr_frag(B, ks * 16 + krow, 2u * (wn * 128 + nb * 32) + feat_byte);
-#pragma unroll
-            for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-                for (int nb = 0; nb < 4; ++nb)
-                    acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mb], bfr[nb], acc[mb][nb], 0, 0, 0);
-        }
-    }
-    wgrad_store_w4<OUT>(acc, out_ptr, tile, s, S, wm, wn, lane, accumulate);
-}
-
-// ------------------------------------------------------------------------------------------------
 // Quarter-tile variant for modules with few tiles (the HBM-bound regime: no two tiles share an
 // operand slice). A 256-thread workgroup owns one 128x128 quarter of a tile for one chunk of T rows
 // (4 waves as 2x2, 64x64 outputs each = 2x2 accumulators of v_mfma_f32_32x32x16_bf16), so a tile
@@ -1634,9 +1492,6 @@ int smt_tile_wgrad(const void* grad_out, int64_t ld_grad_out, const void* x, int
     static const bool force_reg = [] { const char* e = getenv("SMT_WGRAD_IMPL"); return e && strcmp(e, "reg") == 0; }();
     // SMT_WGRAD_SLOTS=5: the 3-in-flight ring (A/B runs); default 4 (2 stages in flight)
     static const int slots = [] { const char* e = getenv("SMT_WGRAD_SLOTS"); return (e && atoi(e) == 5) ? 5 : kDmaSlotsDefault; }();
-    // SMT_WGRAD_WAVES=4: the wide-wave full-tile kernel (4 waves of 128x128) instead of 8 of 128x64
-    static const bool w4 = [] { const char* e = getenv("SMT_WGRAD_WAVES"); return e && atoi(e) == 4; }();
-    const dim3 block4(kW4Threads);
     // SMT_WGRAD_QSLOTS=5: the quarter kernel with 3 stages in flight (80 KiB LDS per workgroup)
     static const int qslots = [] { const char* e = getenv("SMT_WGRAD_QSLOTS"); return (e && atoi(e) == 5) ? 5 : kQSlots; }();
     const bool dma = !force_reg && sp.chunk * max_ld * 2 < (int64_t)0x7fffffff;
@@ -1647,8 +1502,6 @@ int smt_tile_wgrad(const void* grad_out, int64_t ld_grad_out, const void* x, int
                                         ld_grad_out, xp, ld_x, T, sp.chunk, S_, n_tiles, tile_rc_dev, order_dev, DST, ACC); \
         else if (quarter) hipLaunchKernelGGL((wgrad_quarter_kernel<OUT>), qgrid, qblock, 0, stream, gp, ld_grad_out, xp, \
                                         ld_x, T, sp.chunk, S_, n_tiles, tile_rc_dev, order_dev, DST, ACC);     \
-        else if (w4) hipLaunchKernelGGL((wgrad_w4_kernel<OUT>), grid, block4, 0, stream, gp, ld_grad_out, xp, ld_x, \
-                                        T, sp.chunk, S_, n_tiles, tile_rc_dev, order_dev, DST, ACC);            \
         else if (slots == 5) hipLaunchKernelGGL((wgrad_dma_kernel<OUT, 5>), grid, block, 0, stream, gp, ld_grad_out, xp, \
                                            ld_x, T, sp.chunk, S_, n_tiles, tile_rc_dev, order_dev, DST, ACC);  \
         else hipLaunchKernelGGL((wgrad_dma_kernel<OUT, 4>), grid, block, 0, stream, gp, ld_grad_out, xp, ld_x,     \
