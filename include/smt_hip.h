@@ -205,7 +205,8 @@ int smt_adamw_multi(const smt_adamw_tensor* tensors_dev, const int64_t* block_st
  * No reference counterpart (the reference has no fp8, deepspeed/fine_tune.py:955-959): the bf16
  * smt_tile_wgrad (smt.py:397-404) is the bar. "MX column blocks" of a bf16 [T, C] matrix, for a list
  * of n_blocks 256-column blocks, with ldq = T rounded up to a multiple of 64:
- *   q       e4m3 (OCP) [n_blocks][256][ldq]   K-major: row f holds column f of the block over T (zero past T)
+ *   q       e4m3 (OCP) [n_blocks][ldq/64][256][64]   K-major in 64-token panels: q[b][t/64][f][t%64]
+ *           is column f of block b at row t (zero past T); one panel (16 KiB) is one wgrad stage
  *   scales  e8m0 [n_blocks][ldq/32][256]      exponent e + 127 of each 32-row group of each column
  * with e the smallest integer such that the group's max |x| <= 448 * 2^e (-127 for an all-zero
  * group) and q = e4m3_rne(x * 2^-e), so value = e4m3(q) * 2^e exactly reproduces the quantised x.

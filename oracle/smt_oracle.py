@@ -526,11 +526,12 @@ def mx_exponent(amax: torch.Tensor) -> torch.Tensor:
 
 
 def mx_quant_cols(x: torch.Tensor, blocks: Sequence[int]):
-    """bf16 [T, C] -> (q uint8 [n, 256, ldq] e4m3 bits, s uint8 [n, ldq/32, 256] e8m0), ldq = ceil64(T)."""
+    """bf16 [T, C] -> (q uint8 [n, ldq/64, 256, 64] e4m3 bits: q[b][t/64][f][t%64] is column f at
+    row t; s uint8 [n, ldq/32, 256] e8m0), ldq = ceil64(T)."""
     T = x.shape[0]
     ldq = (T + 63) // 64 * 64
     n = len(blocks)
-    q = torch.zeros(n, 256, ldq, dtype=torch.uint8)
+    q = torch.zeros(n, ldq // 64, 256, 64, dtype=torch.uint8)
     s = torch.empty(n, ldq // 32, 256, dtype=torch.uint8)
     for i, b in enumerate(blocks):
         v = torch.zeros(ldq, 256, dtype=torch.float32)
@@ -539,14 +540,15 @@ def mx_quant_cols(x: torch.Tensor, blocks: Sequence[int]):
         e = mx_exponent(g.abs().amax(dim=1))                               # [ldq/32, 256]
         inv = torch.pow(2.0, (-e).double()).float()                        # exact powers of two
         qv = (g * inv[:, None, :]).view(ldq, 256)
-        q[i] = qv.to(torch.float8_e4m3fn).view(torch.uint8).t()
+        q[i] = qv.to(torch.float8_e4m3fn).view(torch.uint8).view(ldq // 64, 64, 256).transpose(1, 2)
         s[i] = (e + 127).to(torch.uint8)
     return q, s
 
 
 def mx_dequant(q: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
-    """(q [n, 256, ldq], s [n, ldq/32, 256]) -> fp64 [n, ldq, 256] values."""
-    vals = q.view(torch.float8_e4m3fn).double().transpose(1, 2)            # [n, ldq, 256]
+    """(q [n, ldq/64, 256, 64], s [n, ldq/32, 256]) -> fp64 [n, ldq, 256] values."""
+    n, panels = q.shape[0], q.shape[1]
+    vals = q.view(torch.float8_e4m3fn).double().transpose(2, 3).reshape(n, panels * 64, 256)
     scale = torch.pow(2.0, s.double() - 127.0)                             # [n, ldq/32, 256]
     return vals * scale.repeat_interleave(32, dim=1)
 

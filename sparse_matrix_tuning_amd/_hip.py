@@ -281,14 +281,15 @@ def tile_wgrad(grad_out2d: torch.Tensor, x2d: torch.Tensor, tile_rc: torch.Tenso
 
 class MxBlocks(NamedTuple):
     """MX-fp8 column blocks of a [T, C] bf16 matrix (include/smt_hip.h, smt_mx_quant_cols):
-    ``q`` uint8 e4m3 [n, 256, ldq] (K-major), ``scales`` uint8 e8m0 [n, ldq/32, 256], ``T`` rows."""
+    ``q`` uint8 e4m3 [n, ldq/64, 256, 64] (K-major 64-token panels), ``scales`` uint8 e8m0
+    [n, ldq/32, 256], ``T`` rows."""
     q: torch.Tensor
     scales: torch.Tensor
     T: int
 
     @property
     def ldq(self) -> int:
-        return self.q.shape[2]
+        return self.q.shape[1] * 64
 
 
 def mx_ld(T: int) -> int:
@@ -305,7 +306,7 @@ def mx_quant_cols(x2d: torch.Tensor, blocks: torch.Tensor) -> MxBlocks:
         raise ValueError("mx_quant_cols: blocks must be device int32 [n]")
     T, n = x2d.shape[0], blocks.numel()
     ldq = mx_ld(T)
-    q = torch.empty(n, BLOCK, ldq, dtype=torch.uint8, device=dev)
+    q = torch.empty(n, ldq // 64, BLOCK, 64, dtype=torch.uint8, device=dev)
     sc = torch.empty(n, ldq // 32, BLOCK, dtype=torch.uint8, device=dev)
     rc = load().smt_mx_quant_cols(_ptr(x2d), x2d.stride(0), T, _ptr(blocks), n, ldq, _ptr(q), _ptr(sc), _stream(dev))
     _check(rc, "smt_mx_quant_cols")

@@ -653,7 +653,8 @@ void wgrad_reduce_kernel(const float* __restrict__ slab, int S, void* __restrict
 //
 // Operand format ("MX column blocks"), written by mx_quant_cols_kernel from a bf16 [T, C] matrix for
 // a list of 256-column blocks, K-major so that no transpose is needed on the way to the MFMA:
-//   q[blk][f][t]      e4m3 (OCP), f in [0,256), t in [0, ldq), rows T..ldq-1 zero; ldq % 64 == 0
+//   q[blk][t/64][f][t%64]  e4m3 (OCP), f in [0,256), t in [0, ldq), rows T..ldq-1 zero; ldq % 64 == 0
+//                     (K-major in 64-token panels: one stage of the wgrad is 16 KiB contiguous)
 //   s[blk][t/32][f]   e8m0 shared exponent of the 32 values q[blk][f][32j .. 32j+31]
 // value(t, f) = e4m3(q) * 2^(s - 127). The exponent is the smallest e with amax <= 448 * 2^e, so
 // nothing saturates (amax = the 32 values' max |x|; e = -127 for an all-zero group; computed from
@@ -718,7 +719,8 @@ void mx_quant_cols_kernel(const uint16_t* __restrict__ x, int64_t ldx, int64_t T
         w.z = pack4(v[8] * inv, v[9] * inv, v[10] * inv, v[11] * inv);
         w.w = pack4(v[12] * inv, v[13] * inv, v[14] * inv, v[15] * inv);
         if (live) {
-            *reinterpret_cast<uint4*>(q + ((int64_t)blk * kTile + f) * ldq + t0 + 16 * c) = w;
+            const int64_t t = t0 + 16 * c;
+            *reinterpret_cast<uint4*>(q + (((int64_t)blk * (ldq >> 6) + (t >> 6)) * kTile + f) * 64 + (t & 63)) = w;
             if ((c & 1) == 0) sc[((int64_t)blk * (ldq >> 5) + (t0 >> 5) + (c >> 1)) * kTile + f] = (uint8_t)(e + 127);
         }
     }
@@ -795,10 +797,10 @@ void wgrad_mx_kernel(const uint8_t* __restrict__ qa, const uint8_t* __restrict__
     const int64_t t_end = (t_begin + chunk < ldq) ? (t_begin + chunk) : ldq;
     const int nst = (t_end > t_begin) ? (int)((t_end - t_begin) / kMxBK) : 0;   // ldq, chunk % 64 == 0
 
-    const int64_t blk_bytes = (int64_t)kTile * ldq;
+    const int64_t blk_bytes = (int64_t)kTile * ldq;       // = (ldq / 64) panels of 16 KiB
     const int64_t sc_bytes = (ldq >> 5) * kTile;
-    const __amdgpu_buffer_rsrc_t rqa = uniform_rsrc(qa + r * blk_bytes + t_begin, blk_bytes - t_begin);
-    const __amdgpu_buffer_rsrc_t rqb = uniform_rsrc(qb + c * blk_bytes + t_begin, blk_bytes - t_begin);
+    const __amdgpu_buffer_rsrc_t rqa = uniform_rsrc(qa + r * blk_bytes + t_begin * kTile, blk_bytes - t_begin * kTile);
+    const __amdgpu_buffer_rsrc_t rqb = uniform_rsrc(qb + c * blk_bytes + t_begin * kTile, blk_bytes - t_begin * kTile);
     const __amdgpu_buffer_rsrc_t rsa = uniform_rsrc(sa + r * sc_bytes + (t_begin >> 5) * kTile, sc_bytes - (t_begin >> 5) * kTile);
     const __amdgpu_buffer_rsrc_t rsb = uniform_rsrc(sb + c * sc_bytes + (t_begin >> 5) * kTile, sc_bytes - (t_begin >> 5) * kTile);
 
@@ -808,13 +810,14 @@ void wgrad_mx_kernel(const uint8_t* __restrict__ qa, const uint8_t* __restrict__
     const int wm = wave >> 2;
     const int wn = wave & 3;
 
-    // DMA geometry: instruction j of wave w fills image rows 16*(2w+j) .. +15 (1 KiB); lane l lands at
-    // row 16*(2w+j) + (l>>2), physical chunk l&3, which holds logical chunk (l&3) ^ ((row>>2)&3).
+    // DMA geometry: instruction j of wave w fills image rows 16*(2w+j) .. +15 (1 KiB, contiguous in the
+    // 64-token panel of the block); lane l lands at row 16*(2w+j) + (l>>2), physical chunk l&3, which
+    // holds logical chunk (l&3) ^ ((row>>2)&3).
     int voff[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
         const int row = 16 * (2 * wave + j) + (lane >> 2);
-        voff[j] = (int)(row * ldq) + ((((lane & 3) ^ ((row >> 2) & 3))) << 4);
+        voff[j] = row * kMxBK + ((((lane & 3) ^ ((row >> 2) & 3))) << 4);
     }
     // exponents: waves 0-3 each move one 256-B k-block row (A kb0, A kb1, B kb0, B kb1) per stage
     const int sc_kb = wave & 1;
@@ -827,8 +830,8 @@ void wgrad_mx_kernel(const uint8_t* __restrict__ qa, const uint8_t* __restrict__
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const uint32_t row0 = (uint32_t)(2 * wave + j) * 1024u;
-            dma16(rqa, __builtin_amdgcn_readfirstlane(slot + row0), voff[j] + st * kMxBK);
-            dma16(rqb, __builtin_amdgcn_readfirstlane(slot + kMxImg + row0), voff[j] + st * kMxBK);
+            dma16(rqa, __builtin_amdgcn_readfirstlane(slot + row0), voff[j] + st * kMxImg);
+            dma16(rqb, __builtin_amdgcn_readfirstlane(slot + kMxImg + row0), voff[j] + st * kMxImg);
         }
         if (wave < 2)
             dma4(rsa, __builtin_amdgcn_readfirstlane(slot + 2 * kMxImg + sc_kb * kTile), sc_voff + st * 2 * kTile);
@@ -885,6 +888,133 @@ void wgrad_mx_kernel(const uint8_t* __restrict__ qa, const uint8_t* __restrict__
                                                                                0, 0, 0, as[mb], 0, bs[nb]);
     }
     wgrad_store<OUT>(acc, out_ptr, tile, s, S, wm, wn, lane, accumulate);
+}
+
+// Quarter-tile MX variant for modules with few tiles (the fill-bound regime, as wgrad_quarter_kernel):
+// 256 threads (4 waves as 2x2, 64x64 outputs each = 2x2 accumulators), one 128x128 quarter of a tile
+// per workgroup, 4-slot ring of 64-token stages of two [128 rows][64 B] images + 2 x 256 B of
+// exponents (66 KiB: two workgroups per CU). Logical ids, schedule, slabs and epilogue as
+// wgrad_quarter_kernel; fragment / scale maps as wgrad_mx_kernel.
+constexpr int kMxQImg = 128 * kMxBK;                        // 8 KiB per operand per stage
+constexpr int kMxQSlotBytes = 2 * kMxQImg + 2 * 256;
+
+template <int OUT>
+__global__ __launch_bounds__(kQThreads, 2)
+void wgrad_mx_quarter_kernel(const uint8_t* __restrict__ qa, const uint8_t* __restrict__ sa,
+                             const uint8_t* __restrict__ qb, const uint8_t* __restrict__ sb, int64_t ldq,
+                             int64_t chunk, int S, int n_tiles, const int32_t* __restrict__ tile_rc,
+                             const int32_t* __restrict__ order, void* __restrict__ out_ptr, int accumulate) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kMxSlots * kMxQSlotBytes];  // 66 KiB, one array
+
+    const int total = n_tiles * S * 4;
+    const int b = blockIdx.x;
+    const int q8 = total >> 3, r8 = total & 7, xcd = b & 7;
+    const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+    const int qd = L & 3;
+    const int ts = L >> 2;
+    const int s = ts / n_tiles;
+    const int li = ts - s * n_tiles;
+    const int tile = order != nullptr ? order[li] : li;
+    const int qm = qd >> 1, qn = qd & 1;
+    const int r = tile_rc[2 * tile];
+    const int c = tile_rc[2 * tile + 1];
+    const int64_t t_begin = (int64_t)s * chunk;
+    const int64_t t_end = (t_begin + chunk < ldq) ? (t_begin + chunk) : ldq;
+    const int nst = (t_end > t_begin) ? (int)((t_end - t_begin) / kMxBK) : 0;
+
+    const int64_t blk_bytes = (int64_t)kTile * ldq;
+    const int64_t sc_bytes = (ldq >> 5) * kTile;
+    // this quarter's 128 rows of the A / B blocks
+    const __amdgpu_buffer_rsrc_t rqa = uniform_rsrc(qa + r * blk_bytes + t_begin * kTile + qm * 128 * kMxBK,
+                                                    blk_bytes - t_begin * kTile - qm * 128 * kMxBK);
+    const __amdgpu_buffer_rsrc_t rqb = uniform_rsrc(qb + c * blk_bytes + t_begin * kTile + qn * 128 * kMxBK,
+                                                    blk_bytes - t_begin * kTile - qn * 128 * kMxBK);
+    const __amdgpu_buffer_rsrc_t rsa = uniform_rsrc(sa + r * sc_bytes + (t_begin >> 5) * kTile, sc_bytes - (t_begin >> 5) * kTile);
+    const __amdgpu_buffer_rsrc_t rsb = uniform_rsrc(sb + c * sc_bytes + (t_begin >> 5) * kTile, sc_bytes - (t_begin >> 5) * kTile);
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1;
+    const int wn = wave & 1;
+
+    // image DMA: instruction j of wave w fills rows 16*(2w+j) .. +15 of each 128-row image (1 KiB
+    // contiguous in the panel layout)
+    int voff[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int row = 16 * (2 * wave + j) + (lane >> 2);
+        voff[j] = row * kMxBK + ((((lane & 3) ^ ((row >> 2) & 3))) << 4);
+    }
+    // exponents: wave 0 moves A's, wave 1 B's: lanes 0-31 the quarter's 128 B of k-block 2st,
+    // lanes 32-63 those of k-block 2st+1
+    const int sc_voff = (lane >> 5) * kTile + (wave == 0 ? qm : qn) * 128 + 4 * (lane & 31);
+    const int per_stage = wave < 2 ? 5 : 4;
+
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(lds));
+    auto issue = [&](int st) {
+        const uint32_t slot = lds0 + (uint32_t)((st % kMxSlots) * kMxQSlotBytes);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const uint32_t row0 = (uint32_t)(2 * wave + j) * 1024u;
+            dma16(rqa, __builtin_amdgcn_readfirstlane(slot + row0), voff[j] + st * kMxImg);
+            dma16(rqb, __builtin_amdgcn_readfirstlane(slot + kMxQImg + row0), voff[j] + st * kMxImg);
+        }
+        if (wave == 0)
+            dma4(rsa, __builtin_amdgcn_readfirstlane(slot + 2 * kMxQImg), sc_voff + st * 2 * kTile);
+        else if (wave == 1)
+            dma4(rsb, __builtin_amdgcn_readfirstlane(slot + 2 * kMxQImg + 256), sc_voff + st * 2 * kTile);
+    };
+
+    f32x16_t acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    const int r32 = lane & 31;
+    const int h = lane >> 5;
+    if (nst > 0) issue(0);
+    if (nst > 1) issue(1);
+    for (int st = 0; st < nst; ++st) {
+        if (st + 2 < nst) {
+            issue(st + 2);
+            wait_vm_n(2 * per_stage);
+        } else if (st + 1 < nst) {
+            wait_vm_n(per_stage);
+        } else {
+            wait_vm_n(0);
+        }
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        const uint8_t* A = lds + (st % kMxSlots) * kMxQSlotBytes;
+        const uint8_t* B = A + kMxQImg;
+        const uint8_t* SA = A + 2 * kMxQImg + h * 128;     // this lane's k-block of the stage
+        const uint8_t* SB = SA + 256;
+        i32x8_t af[2], bfr[2];
+        int as[2], bs[2];
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb) {
+            const int row = wm * 64 + mb * 32 + r32;
+            af[mb] = mx_frag(A, row, h);
+            as[mb] = SA[row];
+        }
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+            const int col = wn * 64 + nb * 32 + r32;
+            bfr[nb] = mx_frag(B, col, h);
+            bs[nb] = SB[col];
+        }
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb)
+                acc[mb][nb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af[mb], bfr[nb], acc[mb][nb],
+                                                                               0, 0, 0, as[mb], 0, bs[nb]);
+    }
+    wgrad_store_q<OUT>(acc, out_ptr, tile, s, S, qm * 128 + wm * 64, qn * 128 + wn * 64, lane, accumulate);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1541,7 +1671,7 @@ int smt_tile_wgrad(const void* grad_out, int64_t ld_grad_out, const void* x, int
 
 size_t smt_wgrad_mx_workspace_bytes(int64_t ldq, int32_t n_tiles) {
     if (ldq <= 0 || n_tiles <= 0) return 0;
-    const WgradSplit sp = wgrad_split(ldq, n_tiles, false, 512.0);
+    const WgradSplit sp = wgrad_split(ldq, n_tiles, true, 512.0);
     if (sp.S == 1) return 0;
     return (size_t)n_tiles * (size_t)sp.S * (size_t)kTileElems * sizeof(float);
 }
@@ -1596,17 +1726,21 @@ int smt_tile_wgrad_mx(const void* qg, const void* sg, const void* qx, const void
     if (!aligned16(qg) || !aligned16(qx) || !aligned16(sg) || !aligned16(sx))
         return fail(SMT_E_ALIGN, "smt_tile_wgrad_mx: operands not 16-byte aligned");
     if ((int64_t)kTile * ldq >= (int64_t)0x7fffffff) return fail(SMT_E_INVALID, "smt_tile_wgrad_mx: T too large for 32-bit offsets");
-    const WgradSplit sp = wgrad_split(ldq, n_tiles, false, 512.0);
+    const WgradSplit sp = wgrad_split(ldq, n_tiles, true, 512.0);
     const uint8_t *a = static_cast<const uint8_t*>(qg), *as = static_cast<const uint8_t*>(sg);
     const uint8_t *b = static_cast<const uint8_t*>(qx), *bs = static_cast<const uint8_t*>(sx);
     const dim3 grid(n_tiles * sp.S), block(kWgThreads);
+    const dim3 qgrid(n_tiles * sp.S * 4), qblock(kQThreads);
+#define SMT_WGRAD_MX(OUT, S_, DST, ACC)                                                                         \
+    do {                                                                                                        \
+        if (sp.quarter) hipLaunchKernelGGL((wgrad_mx_quarter_kernel<OUT>), qgrid, qblock, 0, stream, a, as, b, bs,  \
+                                           ldq, sp.chunk, S_, n_tiles, tile_rc_dev, order_dev, DST, ACC);       \
+        else hipLaunchKernelGGL((wgrad_mx_kernel<OUT>), grid, block, 0, stream, a, as, b, bs, ldq, sp.chunk, S_,    \
+                                n_tiles, tile_rc_dev, order_dev, DST, ACC);                                     \
+    } while (0)
     if (sp.S == 1) {
-        if (out_dtype == SMT_DTYPE_FP32)
-            hipLaunchKernelGGL(wgrad_mx_kernel<kOutF32>, grid, block, 0, stream, a, as, b, bs, ldq, sp.chunk, 1, n_tiles,
-                               tile_rc_dev, order_dev, grad_tiles, accumulate);
-        else
-            hipLaunchKernelGGL(wgrad_mx_kernel<kOutBF16>, grid, block, 0, stream, a, as, b, bs, ldq, sp.chunk, 1, n_tiles,
-                               tile_rc_dev, order_dev, grad_tiles, accumulate);
+        if (out_dtype == SMT_DTYPE_FP32) SMT_WGRAD_MX(kOutF32, 1, grad_tiles, accumulate);
+        else SMT_WGRAD_MX(kOutBF16, 1, grad_tiles, accumulate);
         return check_launch("wgrad_mx_kernel");
     }
     const size_t need = (size_t)n_tiles * sp.S * kTileElems * sizeof(float);
@@ -1614,8 +1748,8 @@ int smt_tile_wgrad_mx(const void* qg, const void* sg, const void* qx, const void
         return fail(SMT_E_WORKSPACE, "smt_tile_wgrad_mx: workspace %zu < %zu bytes", workspace_bytes, need);
     if (!aligned16(workspace)) return fail(SMT_E_ALIGN, "smt_tile_wgrad_mx: workspace not 16-byte aligned");
     float* slab = static_cast<float*>(workspace);
-    hipLaunchKernelGGL(wgrad_mx_kernel<kOutSlab>, grid, block, 0, stream, a, as, b, bs, ldq, sp.chunk, sp.S, n_tiles,
-                       tile_rc_dev, order_dev, slab, 0);
+    SMT_WGRAD_MX(kOutSlab, sp.S, slab, 0);
+#undef SMT_WGRAD_MX
     int rc = check_launch("wgrad_mx_kernel");
     if (rc) return rc;
     if (out_dtype == SMT_DTYPE_FP32)

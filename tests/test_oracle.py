@@ -233,7 +233,7 @@ def test_mx_quant_round_trip_and_no_saturation():
     gen = torch.Generator().manual_seed(0)
     x = (torch.randn(200, 512, generator=gen) * torch.exp(2 * torch.randn(200, 512, generator=gen))).bfloat16()
     q, s = ref.mx_quant_cols(x, [1, 0])
-    assert q.shape == (2, 256, 256) and s.shape == (2, 8, 256)
+    assert q.shape == (2, 4, 256, 64) and s.shape == (2, 8, 256)
     vals = q.view(torch.float8_e4m3fn).float()
     assert vals.abs().max() <= 448.0 and not torch.isnan(vals).any()
     d = ref.mx_dequant(q, s)
