@@ -15,7 +15,7 @@
  *   smt_tile_scatter_t    deepspeed/smt/smt.py:332-341 / 406   write-back into the transposed copy W^T
  *                         that the data-gradient GEMM grad_input = g @ W reads (as g @ (W^T)^T)
  *   smt_colblock_gather   deepspeed/smt/smt.py:351-358   ctx.list1: the input column slices linearZ keeps
- *                         for its backward (packed copy of the distinct 256-column blocks)
+ *                         for its backward (block-major copy of the distinct 256-column blocks)
  *   smt_grad_accumulate   deepspeed/fine_tune.py:724-741, 751-764   warm-up fp32 grad harvest
  *   smt_block_score       deepspeed/smt/smt_helper.py:67-78, 233-251   per-256x256-block scores
  *                         (fp64 sum + magnitude sum: the host bounds ATen's fp32 value with them)
@@ -128,8 +128,10 @@ int smt_abi_version(void);
 size_t smt_wgrad_workspace_bytes(int64_t T, int32_t n_tiles);
 
 /*
- * grad_tiles[i] (+)= sum_{t<T} grad_out[t, r_i*256 : r_i*256+256]^T  x[t, c_i*256 : c_i*256+256]
- * grad_out [T, ld_grad_out], x [T, ld_x]: bf16 row-major; tile_rc_dev: device int32 [n_tiles][2];
+ * grad_tiles[i] (+)= sum_{t<T} grad_out[t, r_i*256 : r_i*256+256]^T  X_{c_i}[t, 0:256]
+ * grad_out [T, ld_grad_out] bf16 row-major; X_c = x + c * x_block_stride, rows of ld_x elements:
+ * x_block_stride = 256 for a row-major x [T, ld_x], or T*256 (ld_x = 256) for the block-major copy
+ * smt_colblock_gather writes (each block a contiguous [T, 256]); tile_rc_dev: device int32 [n_tiles][2];
  * order_dev: optional device int32 [n_tiles] permutation giving the SCHEDULE order of the tiles
  * (tiles sharing a column / row block adjacent, for L2 reuse); NULL = index order. Results do not
  * depend on it. grad_tiles: [n_tiles*256, 256] row-major of out_dtype (bf16 or fp32). fp32 MFMA
@@ -137,14 +139,15 @@ size_t smt_wgrad_workspace_bytes(int64_t T, int32_t n_tiles);
  * partial to bf16 first). Deterministic (fixed split and summation order).
  */
 int smt_tile_wgrad(const void* grad_out, int64_t ld_grad_out,
-                   const void* x, int64_t ld_x, int64_t T,
+                   const void* x, int64_t ld_x, int64_t x_block_stride, int64_t T,
                    const int32_t* tile_rc_dev, const int32_t* order_dev, int32_t n_tiles,
                    void* grad_tiles, int32_t out_dtype, int32_t accumulate,
                    void* workspace, size_t workspace_bytes, hipStream_t stream);
 
 /*
- * out[t, j*256 : j*256+256] = x[t, c_j*256 : c_j*256+256] for the n_cb column blocks c_j of
- * col_blocks_dev (device int32); x [T, ld_x] and out [T, n_cb*256] row-major, 16-bit elements.
+ * out[j, t, 0:256] = x[t, c_j*256 : c_j*256+256] for the n_cb column blocks c_j of col_blocks_dev
+ * (device int32); x [T, ld_x] row-major, out [n_cb, T, 256] block-major (ABI v5; was [T, n_cb*256]),
+ * 16-bit elements: each block's rows contiguous for smt_tile_wgrad (x_block_stride = T*256).
  */
 int smt_colblock_gather(const void* x, int64_t ld_x, int64_t T, const int32_t* col_blocks_dev, int32_t n_cb,
                         void* out, hipStream_t stream);

@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--orders", nargs="*", type=int, default=[0, 1])
     ap.add_argument("--tag", default=os.environ.get("SMT_WGRAD_SLOTS", "5"))
     ap.add_argument("--mx", action="store_true", help="time smt_mx_quant_cols + smt_tile_wgrad_mx instead")
+    ap.add_argument("--xblock", action="store_true",
+                    help="x from the block-major copy linearZ saves (smt_colblock_gather), as in training")
     args = ap.parse_args()
     dev = torch.device("cuda")
     torch.manual_seed(0)
@@ -87,15 +89,22 @@ def main():
                                       quant_us=round(t_q * 1e6, 1), quant_tbs=round(q_bytes / t_q / 1e12, 3))), flush=True)
                 continue
 
+            xs, ldx, xbs, rc_x = x, x.stride(0), 256, rc
+            if args.xblock:
+                cbs = sorted({c for _, c in tiles})
+                xs = _hip.colblock_gather(x, torch.tensor(cbs, dtype=torch.int32, device=dev))
+                ldx, xbs = 256, T * 256
+                rc_x = _hip.tile_table([(r, cbs.index(c)) for r, c in tiles], dev)
+
             def run():
-                assert lib.smt_tile_wgrad(g.data_ptr(), g.stride(0), x.data_ptr(), x.stride(0), T, rc.data_ptr(),
+                assert lib.smt_tile_wgrad(g.data_ptr(), g.stride(0), xs.data_ptr(), ldx, xbs, T, rc_x.data_ptr(),
                                           order.data_ptr() if use_order else None, n,
                                           out.data_ptr(), 1, 0, ws.data_ptr(), wsb, st) == 0
             t = timeit(run)
             flops = 2.0 * T * 65536 * n
             bytes_alg = n * (T * 256 * 2 * 2 + 65536 * 4)
             uniq = (len({r for r, _ in tiles}) + len({c for _, c in tiles})) * T * 512 + n * 65536 * 4
-            print(json.dumps(dict(tag=args.tag, pattern=pattern, order=use_order, tiles=n, S=_split(T, n), us=round(t * 1e6, 1), alg_tbs=round(bytes_alg / t / 1e12, 3),
+            print(json.dumps(dict(tag=args.tag + ("+xblock" if args.xblock else ""), pattern=pattern, order=use_order, tiles=n, S=_split(T, n), us=round(t * 1e6, 1), alg_tbs=round(bytes_alg / t / 1e12, 3),
                                   unique_slice_tbs=round(uniq / t / 1e12, 3), tflops=round(flops / t / 1e12, 1),
                                   ws_mb=round(wsb / 2**20, 1))), flush=True)
 

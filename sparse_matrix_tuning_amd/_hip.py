@@ -102,7 +102,7 @@ _SIGS = {
     "smt_last_error": (ctypes.c_char_p, []),
     "smt_abi_version": (ctypes.c_int, []),
     "smt_wgrad_workspace_bytes": (_SZ, [_I64, _I32]),
-    "smt_tile_wgrad": (ctypes.c_int, [_P, _I64, _P, _I64, _I64, _P, _P, _I32, _P, _I32, _I32, _P, _SZ, _P]),
+    "smt_tile_wgrad": (ctypes.c_int, [_P, _I64, _P, _I64, _I64, _I64, _P, _P, _I32, _P, _I32, _I32, _P, _SZ, _P]),
     "smt_colblock_gather": (ctypes.c_int, [_P, _I64, _I64, _P, _I32, _P, _P]),
     "smt_tile_scatter_t": (ctypes.c_int, [_P, _I32, _P, _P]),
     "smt_tile_gather": (ctypes.c_int, [_P, _I64, _I32, _P, _I32, _P, _P]),
@@ -253,29 +253,52 @@ def wgrad_workspace_bytes(T: int, n_tiles: int) -> int:
     return int(load().smt_wgrad_workspace_bytes(int(T), int(n_tiles)))
 
 
-def tile_wgrad(grad_out2d: torch.Tensor, x2d: torch.Tensor, tile_rc: torch.Tensor, out: torch.Tensor,
+def tile_wgrad(grad_out2d: torch.Tensor, x: torch.Tensor, tile_rc: torch.Tensor, out: torch.Tensor,
                accumulate: bool = False, order: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """out[i] (+)= grad_out2d[:, r_i-block]^T @ x2d[:, c_i-block] for every tile (smt.py:397-404).
-    ``order``: optional device int32 schedule permutation (speed only)."""
-    dev = _require_device(grad_out2d, x2d, tile_rc, out, order)
-    if grad_out2d.dtype != torch.bfloat16 or x2d.dtype != torch.bfloat16:
-        raise NotImplementedError(f"tile_wgrad: bf16 operands only (got {grad_out2d.dtype}, {x2d.dtype})")
+    """out[i] (+)= grad_out2d[:, r_i-block]^T @ X_{c_i} for every tile (smt.py:397-404): ``x`` is the
+    input, row-major [T, in] (X_c = its c-th 256-column block), or the block-major [n_cb, T, 256]
+    copy of ``colblock_gather`` (X_c = x[c]). ``order``: optional device int32 schedule permutation
+    (speed only)."""
+    dev = _require_device(grad_out2d, x, tile_rc, out, order)
+    if grad_out2d.dtype != torch.bfloat16 or x.dtype != torch.bfloat16:
+        raise NotImplementedError(f"tile_wgrad: bf16 operands only (got {grad_out2d.dtype}, {x.dtype})")
     if out.dtype not in (torch.bfloat16, torch.float32) or not out.is_contiguous():
         raise ValueError("tile_wgrad: out must be a contiguous bf16/fp32 tensor")
     n = tile_rc.shape[0]
     if out.numel() != n * TILE_ELEMS:
         raise ValueError(f"tile_wgrad: out has {out.numel()} elements, expected {n * TILE_ELEMS}")
     T = grad_out2d.shape[0]
-    if x2d.shape[0] != T or grad_out2d.stride(1) != 1 or x2d.stride(1) != 1:
-        raise ValueError("tile_wgrad: operands must be [T, features] with unit feature stride")
+    if x.dim() == 3:                      # block-major [n_cb, T, 256]
+        if not x.is_contiguous() or x.shape[1:] != (T, BLOCK):
+            raise ValueError("tile_wgrad: a block-major x must be a contiguous [n_cb, T, 256] tensor")
+        ld_x, xbs = BLOCK, T * BLOCK
+    else:
+        if x.dim() != 2 or x.shape[0] != T or x.stride(1) != 1:
+            raise ValueError("tile_wgrad: x must be [T, features] with unit feature stride")
+        ld_x, xbs = x.stride(0), BLOCK
+    if grad_out2d.stride(1) != 1:
+        raise ValueError("tile_wgrad: grad_out must be [T, features] with unit feature stride")
     ws_bytes = wgrad_workspace_bytes(T, n)
     ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=dev)
     if order is not None and (order.dtype != torch.int32 or order.numel() != n):
         raise ValueError("tile_wgrad: order must be int32 [n_tiles]")
-    rc = load().smt_tile_wgrad(_ptr(grad_out2d), grad_out2d.stride(0), _ptr(x2d), x2d.stride(0), T,
+    rc = load().smt_tile_wgrad(_ptr(grad_out2d), grad_out2d.stride(0), _ptr(x), ld_x, xbs, T,
                                _ptr(tile_rc), _ptr(order), n, _ptr(out), _DT[out.dtype], int(bool(accumulate)),
                                _ptr(ws), ws_bytes, _stream(dev))
     _check(rc, "smt_tile_wgrad")
+    return out
+
+
+def colblock_gather(x2d: torch.Tensor, col_blocks: torch.Tensor) -> torch.Tensor:
+    """[n_cb, T, 256] block-major copy of the 256-column blocks ``col_blocks`` (device int32) of x2d."""
+    dev = _require_device(x2d, col_blocks)
+    if x2d.dim() != 2 or x2d.stride(1) != 1 or x2d.element_size() != 2:
+        raise ValueError("colblock_gather: x must be a 2-D row-major 16-bit tensor")
+    n_cb = col_blocks.numel()
+    out = torch.empty(n_cb, x2d.shape[0], BLOCK, dtype=x2d.dtype, device=dev)
+    rc = load().smt_colblock_gather(_ptr(x2d), x2d.stride(0), x2d.shape[0], _ptr(col_blocks), n_cb, _ptr(out),
+                                    _stream(dev))
+    _check(rc, "smt_colblock_gather")
     return out
 
 
@@ -334,19 +357,6 @@ def tile_wgrad_mx(g: MxBlocks, x: MxBlocks, tile_rc: torch.Tensor, out: torch.Te
                                   _ptr(order), n, _ptr(out), _DT[out.dtype], int(bool(accumulate)), _ptr(ws),
                                   ws_bytes, _stream(dev))
     _check(rc, "smt_tile_wgrad_mx")
-    return out
-
-
-def colblock_gather(x2d: torch.Tensor, col_blocks: torch.Tensor) -> torch.Tensor:
-    """[T, n_cb*256] packed copy of the 256-column blocks ``col_blocks`` (device int32) of x2d."""
-    dev = _require_device(x2d, col_blocks)
-    if x2d.dim() != 2 or x2d.stride(1) != 1 or x2d.element_size() != 2:
-        raise ValueError("colblock_gather: x must be a 2-D row-major 16-bit tensor")
-    n_cb = col_blocks.numel()
-    out = torch.empty(x2d.shape[0], n_cb * BLOCK, dtype=x2d.dtype, device=dev)
-    rc = load().smt_colblock_gather(_ptr(x2d), x2d.stride(0), x2d.shape[0], _ptr(col_blocks), n_cb, _ptr(out),
-                                    _stream(dev))
-    _check(rc, "smt_colblock_gather")
     return out
 
 

@@ -156,7 +156,7 @@ __device__ __forceinline__ void wgrad_store(f32x16_t (&acc)[4][2], void* __restr
 template <int OUT>
 __global__ __launch_bounds__(kWgThreads, 2)
 void wgrad_partial_kernel(const uint16_t* __restrict__ g, int64_t ldg,
-                          const uint16_t* __restrict__ x, int64_t ldx,
+                          const uint16_t* __restrict__ x, int64_t ldx, int64_t xbs,
                           int64_t T, int64_t chunk, int S, int n_tiles,
                           const int32_t* __restrict__ tile_rc, const int32_t* __restrict__ order,
                           void* __restrict__ out_ptr, int accumulate) {
@@ -182,7 +182,7 @@ void wgrad_partial_kernel(const uint16_t* __restrict__ g, int64_t ldg,
     const int nst = (t_end > t_begin) ? (int)((t_end - t_begin + kBK - 1) / kBK) : 0;
 
     const uint16_t* gb = g + (int64_t)r * kTile;
-    const uint16_t* xb = x + (int64_t)c * kTile;
+    const uint16_t* xb = x + (int64_t)c * xbs;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -339,7 +339,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base,
 template <int OUT, int SLOTS>
 __global__ __launch_bounds__(kWgThreads, 1)
 void wgrad_dma_kernel(const uint16_t* __restrict__ g, int64_t ldg,
-                      const uint16_t* __restrict__ x, int64_t ldx,
+                      const uint16_t* __restrict__ x, int64_t ldx, int64_t xbs,
                       int64_t T, int64_t chunk, int S, int n_tiles,
                       const int32_t* __restrict__ tile_rc, const int32_t* __restrict__ order,
                       void* __restrict__ out_ptr, int accumulate) {
@@ -363,7 +363,7 @@ void wgrad_dma_kernel(const uint16_t* __restrict__ g, int64_t ldg,
 
     // descriptors over this chunk's rows of the two column slices (host guarantees rows*ld*2 < 2^31)
     const __amdgpu_buffer_rsrc_t rg = uniform_rsrc(g + t_begin * ldg + (int64_t)r * kTile, (int64_t)rows * ldg * 2);
-    const __amdgpu_buffer_rsrc_t rx = uniform_rsrc(x + t_begin * ldx + (int64_t)c * kTile, (int64_t)rows * ldx * 2);
+    const __amdgpu_buffer_rsrc_t rx = uniform_rsrc(x + t_begin * ldx + (int64_t)c * xbs, (int64_t)rows * ldx * 2);
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -503,7 +503,7 @@ __device__ __forceinline__ void wgrad_store_q(f32x16_t (&acc)[2][2], void* __res
 template <int OUT, int QS = kQSlots>
 __global__ __launch_bounds__(kQThreads, 2)
 void wgrad_quarter_kernel(const uint16_t* __restrict__ g, int64_t ldg,
-                          const uint16_t* __restrict__ x, int64_t ldx,
+                          const uint16_t* __restrict__ x, int64_t ldx, int64_t xbs,
                           int64_t T, int64_t chunk, int S, int n_tiles,
                           const int32_t* __restrict__ tile_rc, const int32_t* __restrict__ order,
                           void* __restrict__ out_ptr, int accumulate) {
@@ -530,7 +530,7 @@ void wgrad_quarter_kernel(const uint16_t* __restrict__ g, int64_t ldg,
     const int nst = (rows + kDmaBK - 1) / kDmaBK;
 
     const __amdgpu_buffer_rsrc_t rg = uniform_rsrc(g + t_begin * ldg + (int64_t)r * kTile + qm * 128, (int64_t)rows * ldg * 2);
-    const __amdgpu_buffer_rsrc_t rx = uniform_rsrc(x + t_begin * ldx + (int64_t)c * kTile + qn * 128, (int64_t)rows * ldx * 2);
+    const __amdgpu_buffer_rsrc_t rx = uniform_rsrc(x + t_begin * ldx + (int64_t)c * xbs + qn * 128, (int64_t)rows * ldx * 2);
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1460,10 +1460,11 @@ void tile_scatter_t_kernel(const smt_tile_desc* __restrict__ descs, const uint16
     }
 }
 
-// The 256-column blocks of x that a module's tiles read, packed side by side:
-// out[t, j*256 + k] = x[t, col_blocks[j]*256 + k]. linearZ saves this [T, n_cb*256] slab for its
-// backward instead of the whole input (the tile wgrad reads nothing else). 16 B per thread; one
-// wave covers two (row, block) pairs of 512 contiguous bytes on both sides.
+// The 256-column blocks of x that a module's tiles read, block-major:
+// out[j, t, k] = x[t, col_blocks[j]*256 + k]. linearZ saves this [n_cb, T, 256] copy for its
+// backward instead of the whole input (the tile wgrad reads nothing else), each block's rows
+// contiguous so that the wgrad's x stages are contiguous 16 KiB reads. 16 B per thread; one wave
+// covers two (row, block) pairs of 512 contiguous bytes on both sides.
 __global__ __launch_bounds__(256)
 void colblock_gather_kernel(const uint16_t* __restrict__ x, int64_t ld_x, int64_t T,
                             const int32_t* __restrict__ col_blocks, int32_t n_cb, uint16_t* __restrict__ out) {
@@ -1474,7 +1475,7 @@ void colblock_gather_kernel(const uint16_t* __restrict__ x, int64_t ld_x, int64_
     const int r = (int)(v - t * per_row);
     const int j = r >> 5, ch = r & 31;
     const uint4 val = *reinterpret_cast<const uint4*>(x + t * ld_x + (int64_t)col_blocks[j] * kTile + ch * 8);
-    *reinterpret_cast<uint4*>(out + t * per_row * 8 + (int64_t)j * kTile + ch * 8) = val;
+    *reinterpret_cast<uint4*>(out + ((int64_t)j * T + t) * kTile + ch * 8) = val;     // block-major [n_cb][T][256]
 }
 
 // Activation harvest, the forward hook of fine_tune.py:636-667: the reference keeps, per key, the
@@ -1593,7 +1594,7 @@ size_t smt_wgrad_workspace_bytes(int64_t T, int32_t n_tiles) {
     return (size_t)n_tiles * (size_t)sp.S * (size_t)kTileElems * sizeof(float);
 }
 
-int smt_tile_wgrad(const void* grad_out, int64_t ld_grad_out, const void* x, int64_t ld_x, int64_t T,
+int smt_tile_wgrad(const void* grad_out, int64_t ld_grad_out, const void* x, int64_t ld_x, int64_t x_block_stride, int64_t T,
                    const int32_t* tile_rc_dev, const int32_t* order_dev, int32_t n_tiles, void* grad_tiles,
                    int32_t out_dtype, int32_t accumulate, void* workspace, size_t workspace_bytes, hipStream_t stream) {
     if (n_tiles < 0 || T < 0) return fail(SMT_E_INVALID, "smt_tile_wgrad: negative size (T=%lld, n_tiles=%d)", (long long)T, n_tiles);
@@ -1611,6 +1612,9 @@ int smt_tile_wgrad(const void* grad_out, int64_t ld_grad_out, const void* x, int
     if (!grad_out || !x) return fail(SMT_E_INVALID, "smt_tile_wgrad: null operand");
     if (!aligned16(grad_out) || !aligned16(x) || (ld_grad_out & 7) || (ld_x & 7))
         return fail(SMT_E_ALIGN, "smt_tile_wgrad: operands need 16-byte aligned rows (ld %% 8 == 0)");
+    const int64_t xbs = x_block_stride;
+    if (xbs < kTile || (xbs & 7)) return fail(SMT_E_INVALID, "smt_tile_wgrad: x_block_stride %lld (>= 256, %% 8 == 0)",
+                                              (long long)xbs);
     const WgradSplit sp = wgrad_split(T, n_tiles);
     const uint16_t* gp = static_cast<const uint16_t*>(grad_out);
     const uint16_t* xp = static_cast<const uint16_t*>(x);
@@ -1629,22 +1633,22 @@ int smt_tile_wgrad(const void* grad_out, int64_t ld_grad_out, const void* x, int
 #define SMT_WGRAD_DMA(OUT, S_, DST, ACC)                                                                        \
     do {                                                                                                        \
         if (quarter && qslots == 5) hipLaunchKernelGGL((wgrad_quarter_kernel<OUT, 5>), qgrid, qblock, 0, stream, gp,  \
-                                        ld_grad_out, xp, ld_x, T, sp.chunk, S_, n_tiles, tile_rc_dev, order_dev, DST, ACC); \
+                                        ld_grad_out, xp, ld_x, xbs, T, sp.chunk, S_, n_tiles, tile_rc_dev, order_dev, DST, ACC); \
         else if (quarter) hipLaunchKernelGGL((wgrad_quarter_kernel<OUT>), qgrid, qblock, 0, stream, gp, ld_grad_out, xp, \
-                                        ld_x, T, sp.chunk, S_, n_tiles, tile_rc_dev, order_dev, DST, ACC);     \
+                                        ld_x, xbs, T, sp.chunk, S_, n_tiles, tile_rc_dev, order_dev, DST, ACC); \
         else if (slots == 5) hipLaunchKernelGGL((wgrad_dma_kernel<OUT, 5>), grid, block, 0, stream, gp, ld_grad_out, xp, \
-                                           ld_x, T, sp.chunk, S_, n_tiles, tile_rc_dev, order_dev, DST, ACC);  \
-        else hipLaunchKernelGGL((wgrad_dma_kernel<OUT, 4>), grid, block, 0, stream, gp, ld_grad_out, xp, ld_x,     \
+                                           ld_x, xbs, T, sp.chunk, S_, n_tiles, tile_rc_dev, order_dev, DST, ACC); \
+        else hipLaunchKernelGGL((wgrad_dma_kernel<OUT, 4>), grid, block, 0, stream, gp, ld_grad_out, xp, ld_x, xbs,     \
                                 T, sp.chunk, S_, n_tiles, tile_rc_dev, order_dev, DST, ACC);                    \
     } while (0)
     if (sp.S == 1) {
         if (out_dtype == SMT_DTYPE_FP32) {
             if (dma) SMT_WGRAD_DMA(kOutF32, 1, grad_tiles, accumulate);
-            else hipLaunchKernelGGL(wgrad_partial_kernel<kOutF32>, grid, block, 0, stream, gp, ld_grad_out, xp, ld_x,
+            else hipLaunchKernelGGL(wgrad_partial_kernel<kOutF32>, grid, block, 0, stream, gp, ld_grad_out, xp, ld_x, xbs,
                                     T, sp.chunk, 1, n_tiles, tile_rc_dev, order_dev, grad_tiles, accumulate);
         } else {
             if (dma) SMT_WGRAD_DMA(kOutBF16, 1, grad_tiles, accumulate);
-            else hipLaunchKernelGGL(wgrad_partial_kernel<kOutBF16>, grid, block, 0, stream, gp, ld_grad_out, xp, ld_x,
+            else hipLaunchKernelGGL(wgrad_partial_kernel<kOutBF16>, grid, block, 0, stream, gp, ld_grad_out, xp, ld_x, xbs,
                                     T, sp.chunk, 1, n_tiles, tile_rc_dev, order_dev, grad_tiles, accumulate);
         }
         return check_launch("wgrad_partial_kernel");
@@ -1657,7 +1661,7 @@ int smt_tile_wgrad(const void* grad_out, int64_t ld_grad_out, const void* x, int
     if (dma)
         SMT_WGRAD_DMA(kOutSlab, sp.S, slab, 0);
     else
-        hipLaunchKernelGGL(wgrad_partial_kernel<kOutSlab>, grid, block, 0, stream, gp, ld_grad_out, xp, ld_x,
+        hipLaunchKernelGGL(wgrad_partial_kernel<kOutSlab>, grid, block, 0, stream, gp, ld_grad_out, xp, ld_x, xbs,
                            T, sp.chunk, sp.S, n_tiles, tile_rc_dev, order_dev, slab, 0);
     int rc = check_launch("wgrad_partial_kernel");
     if (rc) return rc;

@@ -49,9 +49,9 @@ def test_struct_layouts_match_header():
 
 def test_validation_errors_without_gpu():
     lib = _hip.load()
-    assert lib.smt_tile_wgrad(None, 0, None, 0, 16, None, None, -1, None, 0, 0, None, 0, None) == -1
+    assert lib.smt_tile_wgrad(None, 0, None, 0, 256, 16, None, None, -1, None, 0, 0, None, 0, None) == -1
     assert b"negative" in lib.smt_last_error()
-    assert lib.smt_tile_wgrad(None, 0, None, 0, 16, None, None, 0, None, 0, 0, None, 0, None) == 0   # no tiles: no-op
+    assert lib.smt_tile_wgrad(None, 0, None, 0, 256, 16, None, None, 0, None, 0, 0, None, 0, None) == 0   # no tiles: no-op
     assert lib.smt_adamw_step(None, None, None, None, None, None, 0, 0, None, None, None) == -1
     args = _hip.AdamWArgs(lr=1e-3, beta1=0.9, beta2=0.95, eps=1e-8, weight_decay=0.0, bias_correction1=0.0,
                           bias_correction2=0.1, max_grad_norm=0.0, grad_scale=1.0, mode=0, grad_dtype=0)

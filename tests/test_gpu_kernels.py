@@ -236,8 +236,8 @@ def test_adamw_multi_equals_per_tensor_steps(gdt):
 def test_colblock_gather_bit_exact(T, in_f, cbs):
     x = torch.randn(T, in_f).bfloat16().to(DEV)
     out = _hip.colblock_gather(x, torch.tensor(cbs, dtype=torch.int32, device=DEV))
-    want = torch.cat([x[:, c * 256:(c + 1) * 256] for c in cbs], dim=1)
-    assert out.shape == (T, 256 * len(cbs)) and torch.equal(out, want)
+    want = torch.stack([x[:, c * 256:(c + 1) * 256] for c in cbs])      # block-major [n_cb, T, 256]
+    assert out.shape == (len(cbs), T, 256) and torch.equal(out, want)
 
 
 def test_linearz_packed_input_grads_bit_identical():
