@@ -243,9 +243,11 @@ int smt_row_scatter(void* weight, int64_t ld_weight, int32_t elem_bytes, int64_t
 
 /*
  * out[t, j] = x[t, cols_dev[j]] for j < n_cols and 0 for n_cols <= j < ld_out (bf16/fp16 bits,
- * 2-byte elements); x [T, ld_x], out [T, ld_out] row-major, ld_out % 8 == 0.
+ * 2-byte elements); x [T, ld_x] with every cols_dev[j] < n_in <= ld_x (n_in <= 32768: rows are
+ * staged in LDS), out [T, ld_out] row-major; ld_x, ld_out % 8 == 0; cols_dev 16-byte aligned.
+ * (ABI v5: n_in added.)
  */
-int smt_column_gather(const void* x, int64_t ld_x, int64_t T, const int32_t* cols_dev, int32_t n_cols,
+int smt_column_gather(const void* x, int64_t ld_x, int64_t n_in, int64_t T, const int32_t* cols_dev, int32_t n_cols,
                       void* out, int64_t ld_out, hipStream_t stream);
 
 /*
@@ -259,11 +261,14 @@ int smt_act_accumulate(const void* x, int32_t x_dtype, int64_t ld_x, int64_t bat
 
 /*
  * out[c] = sum_{s<S} A_s (strategy MEAN_ABS, ABS_MEAN, L1) or sum_{s<S} A_s^2 (L2) in fp64, with
- * A_s = sum_{b<B} |acc[b, s, c]| and acc a contiguous fp32 [B, S, n_cols] accumulator. The caller
- * divides by S (means) or takes the square root (L2) and rounds to fp32 once.
+ * A_s = sum_{b<B} |acc[b, s, c]| and acc a contiguous fp32 [B, S, n_cols] accumulator; summed as
+ * 32-row partials (s ascending inside each) added in ascending order. partials: caller workspace of
+ * smt_channel_score_workspace_bytes(S, n_cols) bytes (ABI v5). The caller divides by S (means) or
+ * takes the square root (L2) and rounds to fp32 once.
  */
-int smt_channel_score(const float* acc, int32_t B, int32_t S, int32_t n_cols, int32_t strategy, double* out,
-                      hipStream_t stream);
+size_t smt_channel_score_workspace_bytes(int32_t S, int32_t n_cols);
+int smt_channel_score(const float* acc, int32_t B, int32_t S, int32_t n_cols, int32_t strategy, double* partials,
+                      size_t partial_bytes, double* out, hipStream_t stream);
 
 #ifdef __cplusplus
 }

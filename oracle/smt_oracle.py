@@ -208,14 +208,17 @@ def channel_hook_accumulate(feat: dict, key, x: torch.Tensor) -> None:
 def channel_raw_fp64(act: torch.Tensor, strategy: str) -> torch.Tensor:
     """What ``smt_channel_score`` computes, restated with its operation order: per channel
     ``sum_s A_s`` (``sum_s A_s^2`` for L2) in fp64, ``A_s = sum_b |act[b, s, c]|`` with b ascending
-    from 0, s ascending."""
+    from 0; s ascending inside 32-row partials, the partials added in ascending order."""
     a = act.detach().cpu().to(torch.float32).abs().double()
     tot = torch.zeros(a.shape[2], dtype=torch.float64)
-    for s in range(a.shape[1]):
-        col = torch.zeros(a.shape[2], dtype=torch.float64)
-        for b in range(a.shape[0]):
-            col = col + a[b, s]
-        tot = tot + (col * col if strategy == 'L2' else col)
+    for s0 in range(0, a.shape[1], 32):
+        part = torch.zeros(a.shape[2], dtype=torch.float64)
+        for s in range(s0, min(a.shape[1], s0 + 32)):
+            col = torch.zeros(a.shape[2], dtype=torch.float64)
+            for b in range(a.shape[0]):
+                col = col + a[b, s]
+            part = part + (col * col if strategy == 'L2' else col)
+        tot = tot + part
     return tot
 
 

@@ -32,7 +32,8 @@ ABI_FUNCTIONS = (
     "smt_tile_gather", "smt_tile_scatter", "smt_grad_accumulate", "smt_block_score",
     "smt_sq_norm", "smt_adamw_step", "smt_adamw_multi",
     "smt_mx_quant_cols", "smt_wgrad_mx_workspace_bytes", "smt_tile_wgrad_mx",
-    "smt_row_gather", "smt_row_scatter", "smt_column_gather", "smt_act_accumulate", "smt_channel_score",
+    "smt_row_gather", "smt_row_scatter", "smt_column_gather", "smt_act_accumulate",
+    "smt_channel_score_workspace_bytes", "smt_channel_score",
     "smt_model_ops_last_error", "smt_rmsnorm_fwd", "smt_rmsnorm_bwd_waves", "smt_rmsnorm_bwd",
     "smt_add_rmsnorm_fwd", "smt_rmsnorm_bwd_add",
     "smt_rope_fwd", "smt_rope_bwd", "smt_swiglu_fwd", "smt_swiglu_bwd", "smt_ce_fwd", "smt_ce_bwd",
@@ -117,9 +118,10 @@ _SIGS = {
     "smt_tile_wgrad_mx": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _P, _I32, _P, _I32, _I32, _P, _SZ, _P]),
     "smt_row_gather": (ctypes.c_int, [_P, _I64, _I32, _I64, _P, _I32, _P, _I64, _P]),
     "smt_row_scatter": (ctypes.c_int, [_P, _I64, _I32, _I64, _P, _I32, _P, _I64, _P]),
-    "smt_column_gather": (ctypes.c_int, [_P, _I64, _I64, _P, _I32, _P, _I64, _P]),
+    "smt_column_gather": (ctypes.c_int, [_P, _I64, _I64, _I64, _P, _I32, _P, _I64, _P]),
     "smt_act_accumulate": (ctypes.c_int, [_P, _I32, _I64, _I64, _I32, _I32, _I32, _P, _I32, _P]),
-    "smt_channel_score": (ctypes.c_int, [_P, _I32, _I32, _I32, _I32, _P, _P]),
+    "smt_channel_score_workspace_bytes": (_SZ, [_I32, _I32]),
+    "smt_channel_score": (ctypes.c_int, [_P, _I32, _I32, _I32, _I32, _P, _SZ, _P, _P]),
     "smt_attn_last_error": (ctypes.c_char_p, []),
     "smt_attn_fwd": (ctypes.c_int, [ctypes.POINTER(AttnTensor)] * 4 + [_P, ctypes.POINTER(AttnShape), _P]),
     "smt_attn_bwd": (ctypes.c_int, [ctypes.POINTER(AttnTensor)] * 5 + [_P, _P] + [ctypes.POINTER(AttnTensor)] * 3
@@ -555,8 +557,8 @@ def column_gather(x2d: torch.Tensor, cols_dev: torch.Tensor, n_cols: int, ld_out
     if x2d.dim() != 2 or x2d.stride(1) != 1 or x2d.element_size() != 2:
         raise ValueError("column_gather: x must be a 2-D row-major 16-bit tensor")
     out = torch.empty(x2d.shape[0], ld_out, dtype=x2d.dtype, device=dev)
-    rc = load().smt_column_gather(_ptr(x2d), x2d.stride(0), x2d.shape[0], _ptr(cols_dev), int(n_cols), _ptr(out),
-                                  ld_out, _stream(dev))
+    rc = load().smt_column_gather(_ptr(x2d), x2d.stride(0), x2d.shape[1], x2d.shape[0], _ptr(cols_dev), int(n_cols),
+                                  _ptr(out), ld_out, _stream(dev))
     _check(rc, "smt_column_gather")
     return out
 
@@ -582,7 +584,9 @@ def channel_scores(acc: torch.Tensor, strategy: int) -> torch.Tensor:
     if acc.dtype != torch.float32 or not acc.is_contiguous() or acc.dim() != 3:
         raise ValueError("channel_scores: contiguous fp32 [B, S, C] accumulator expected")
     out = torch.empty(acc.shape[2], dtype=torch.float64, device=dev)
-    rc = load().smt_channel_score(_ptr(acc), acc.shape[0], acc.shape[1], acc.shape[2], int(strategy), _ptr(out),
-                                  _stream(dev))
+    ws_bytes = load().smt_channel_score_workspace_bytes(acc.shape[1], acc.shape[2])
+    ws = torch.empty(max(ws_bytes // 8, 2), dtype=torch.float64, device=dev)
+    rc = load().smt_channel_score(_ptr(acc), acc.shape[0], acc.shape[1], acc.shape[2], int(strategy), _ptr(ws),
+                                  ws_bytes, _ptr(out), _stream(dev))
     _check(rc, "smt_channel_score")
     return out

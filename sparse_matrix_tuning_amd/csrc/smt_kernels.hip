@@ -1403,26 +1403,58 @@ void row_copy_kernel(uint8_t* __restrict__ weight, int64_t ld_w_bytes, const int
 
 // partial_input of linearChannel.forward (smt.py:225-233): out[t, j] = x[t, cols[j]] for j < n_cols,
 // 0 for n_cols <= j < ld_out (zero columns pad the operand to a whole number of 256-blocks for the
-// tile wgrad). Each thread writes 8 consecutive outputs (one 16 B store, coalesced across the wave);
-// the 8 reads are 2 B gathers inside row t, served from L2 (a row is <= 28 KiB).
+// tile wgrad). Each workgroup stages up to 4 rows of x (their first n_in elements) into LDS with
+// coalesced 16-B loads, then each thread gathers 8 consecutive outputs from LDS and writes them as
+// one 16-B store (the previous version gathered 2-B elements from global memory: 0.15 of HBM).
 __global__ __launch_bounds__(256)
-void column_gather_kernel(const uint16_t* __restrict__ x, int64_t ld_x, int64_t T, const int32_t* __restrict__ cols,
-                          int32_t n_cols, uint16_t* __restrict__ out, int64_t ld_out) {
-    const int64_t vec_per_row = ld_out >> 3;
-    const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int64_t t = v / vec_per_row;
-    if (t >= T) return;
-    const int j0 = (int)(v - t * vec_per_row) * 8;
-    const uint16_t* xr = x + t * ld_x;
-    uint32_t w[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int ja = j0 + 2 * q, jb = ja + 1;
-        const uint32_t lo = ja < n_cols ? xr[cols[ja]] : 0u;
-        const uint32_t hi = jb < n_cols ? xr[cols[jb]] : 0u;
-        w[q] = lo | (hi << 16);
+void column_gather_kernel(const uint16_t* __restrict__ x, int64_t ld_x, int64_t n_in, int64_t T,
+                          const int32_t* __restrict__ cols, int32_t n_cols, uint16_t* __restrict__ out,
+                          int64_t ld_out, int rows) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t rowbuf[];      // [rows][n_in8]
+    const int64_t n_in8 = (n_in + 7) & ~(int64_t)7;
+    const int64_t t0 = (int64_t)blockIdx.x * rows;
+    const int tid = threadIdx.x;
+    const int64_t chunks = n_in8 >> 3;
+    for (int r = 0; r < rows; ++r) {
+        const int64_t t = t0 + r;
+        if (t >= T) break;
+        const uint16_t* xr = x + t * ld_x;
+        for (int64_t k = tid; k < chunks; k += 256) {
+            if (8 * k + 8 <= n_in) {
+                *reinterpret_cast<uint4*>(rowbuf + r * n_in8 + 8 * k) = *reinterpret_cast<const uint4*>(xr + 8 * k);
+            } else {
+                for (int64_t e = 8 * k; e < n_in8; ++e) rowbuf[r * n_in8 + e] = e < n_in ? xr[e] : 0;
+            }
+        }
     }
-    *reinterpret_cast<uint4*>(out + t * ld_out + j0) = make_uint4(w[0], w[1], w[2], w[3]);
+    __syncthreads();
+    const int64_t vec_per_row = ld_out >> 3;
+    for (int r = 0; r < rows; ++r) {
+        const int64_t t = t0 + r;
+        if (t >= T) break;
+        const uint16_t* br = rowbuf + r * n_in8;
+        for (int64_t v = tid; v < vec_per_row; v += 256) {
+            const int j0 = (int)(v * 8);
+            int idx[8];
+            if (j0 + 8 <= n_cols) {                               // 8 indices as two 16-B loads
+                const int4 a = *reinterpret_cast<const int4*>(cols + j0);
+                const int4 b = *reinterpret_cast<const int4*>(cols + j0 + 4);
+                idx[0] = a.x; idx[1] = a.y; idx[2] = a.z; idx[3] = a.w;
+                idx[4] = b.x; idx[5] = b.y; idx[6] = b.z; idx[7] = b.w;
+            } else {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) idx[q] = j0 + q < n_cols ? cols[j0 + q] : -1;
+            }
+            uint32_t w[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t lo = idx[2 * q] >= 0 ? br[idx[2 * q]] : 0u;
+                const uint32_t hi = idx[2 * q + 1] >= 0 ? br[idx[2 * q + 1]] : 0u;
+                w[q] = lo | (hi << 16);
+            }
+            *reinterpret_cast<uint4*>(out + t * ld_out + j0) = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+    }
 }
 
 // Transposed tile scatter: Wt[c*256 + j, r*256 + k] = tile[k, j] for every descriptor (weight = the
@@ -1508,22 +1540,36 @@ void act_accumulate_kernel(const void* __restrict__ x, int64_t ld_x, int64_t sb,
 // over the batch (`torch.sum(act.abs(), dim=0)`, fp32) and reduces the [S, in] result over the
 // sequence. Here, in fp64 (nearly exact): out[c] = sum_s A_s (mean_abs / abs_mean / L1) or
 // sum_s A_s^2 (L2) with A_s = sum_b |acc[b, s, c]|. The host divides by S / takes the square root,
-// rounds to fp32 once, and bounds the reference's fp32 value around it (smt_helper.py). One thread per
-// column; a wave reads 256 contiguous bytes of a row per (b, s).
-#pragma clang fp contract(off)
+// rounds to fp32 once, and bounds the reference's fp32 value around it (smt_helper.py). Two passes
+// for parallelism (a [16, 2048, 5120] accumulator is 671 MB): thread (c, p) sums rows
+// s in [32p, 32p+32) into partials[p][c]; then out[c] = sum_p partials[p][c], p ascending. A wave
+// reads 256 contiguous bytes of a row per (b, s).
+constexpr int kChanRows = 32;
+
 __global__ __launch_bounds__(256)
-void channel_score_kernel(const float* __restrict__ acc, int32_t B, int32_t S, int32_t n_cols, int32_t square,
-                          double* __restrict__ out) {
+void channel_partial_kernel(const float* __restrict__ acc, int32_t B, int32_t S, int32_t n_cols, int32_t square,
+                            double* __restrict__ partials) {
     const int c = blockIdx.x * 256 + threadIdx.x;
     if (c >= n_cols) return;
+    const int p = blockIdx.y;
+    const int s0 = p * kChanRows, s1 = min(S, s0 + kChanRows);
     const int64_t bstride = (int64_t)S * n_cols;
     double tot = 0.0;
-    for (int s = 0; s < S; ++s) {
-        const float* p = acc + (int64_t)s * n_cols + c;
+    for (int s = s0; s < s1; ++s) {
+        const float* q = acc + (int64_t)s * n_cols + c;
         double a = 0.0;
-        for (int b = 0; b < B; ++b) a += (double)fabsf(p[b * bstride]);
+        for (int b = 0; b < B; ++b) a += (double)fabsf(q[b * bstride]);
         tot += square ? a * a : a;
     }
+    partials[(int64_t)p * n_cols + c] = tot;
+}
+
+__global__ __launch_bounds__(256)
+void channel_final_kernel(const double* __restrict__ partials, int32_t P, int32_t n_cols, double* __restrict__ out) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= n_cols) return;
+    double tot = 0.0;
+    for (int p = 0; p < P; ++p) tot += partials[(int64_t)p * n_cols + c];
     out[c] = tot;
 }
 #pragma clang fp contract(fast)
@@ -1918,16 +1964,24 @@ int smt_row_scatter(void* weight, int64_t ld_weight, int32_t elem_bytes, int64_t
     return row_copy(true, weight, ld_weight, elem_bytes, n_cols, rows_dev, n_rows, const_cast<void*>(rows), ld_rows, stream);
 }
 
-int smt_column_gather(const void* x, int64_t ld_x, int64_t T, const int32_t* cols_dev, int32_t n_cols,
+int smt_column_gather(const void* x, int64_t ld_x, int64_t n_in, int64_t T, const int32_t* cols_dev, int32_t n_cols,
                       void* out, int64_t ld_out, hipStream_t stream) {
-    if (T < 0 || n_cols < 0 || ld_out < n_cols) return fail(SMT_E_INVALID, "smt_column_gather: bad sizes");
+    if (T < 0 || n_cols < 0 || ld_out < n_cols || n_in < 0) return fail(SMT_E_INVALID, "smt_column_gather: bad sizes");
     if (T == 0 || ld_out == 0) return SMT_OK;
     if (!x || !out || (n_cols > 0 && !cols_dev)) return fail(SMT_E_INVALID, "smt_column_gather: null pointer");
     if (!aligned16(out) || (ld_out & 7)) return fail(SMT_E_ALIGN, "smt_column_gather: out rows must be 16-byte aligned (ld_out %% 8 == 0)");
-    const int64_t blocks = (T * (ld_out >> 3) + 255) / 256;
+    if (!aligned16(x) || (ld_x & 7) || n_in > ld_x)
+        return fail(SMT_E_ALIGN, "smt_column_gather: x rows must be 16-byte aligned (ld_x %% 8 == 0) and n_in <= ld_x");
+    // rows staged per workgroup: up to 4, within a 64 KiB LDS stage
+    const int64_t row_bytes = ((n_in + 7) & ~(int64_t)7) * 2;
+    const int rows = row_bytes * 4 <= 65536 ? 4 : row_bytes * 2 <= 65536 ? 2 : 1;
+    if (row_bytes > 65536) return fail(SMT_E_INVALID, "smt_column_gather: rows of %lld elements exceed the LDS stage", (long long)n_in);
+    if (n_cols > 0 && ((uintptr_t)cols_dev & 15)) return fail(SMT_E_ALIGN, "smt_column_gather: cols not 16-byte aligned");
+    const int64_t blocks = (T + rows - 1) / rows;
     if (blocks > 0x7fffffffLL) return fail(SMT_E_INVALID, "smt_column_gather: too large");
-    hipLaunchKernelGGL(column_gather_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, static_cast<const uint16_t*>(x),
-                       ld_x, T, cols_dev, n_cols, static_cast<uint16_t*>(out), ld_out);
+    hipLaunchKernelGGL(column_gather_kernel, dim3((unsigned)blocks), dim3(256), (size_t)(rows * row_bytes), stream,
+                       static_cast<const uint16_t*>(x), ld_x, n_in, T, cols_dev, n_cols, static_cast<uint16_t*>(out), ld_out,
+                       rows);
     return check_launch("column_gather_kernel");
 }
 
@@ -1978,15 +2032,32 @@ int smt_act_accumulate(const void* x, int32_t x_dtype, int64_t ld_x, int64_t bat
     return check_launch("act_accumulate_kernel");
 }
 
-int smt_channel_score(const float* acc, int32_t B, int32_t S, int32_t n_cols, int32_t strategy, double* out,
-                      hipStream_t stream) {
+size_t smt_channel_score_workspace_bytes(int32_t S, int32_t n_cols) {
+    if (S <= 0 || n_cols <= 0) return 0;
+    return (size_t)((S + kChanRows - 1) / kChanRows) * (size_t)n_cols * sizeof(double);
+}
+
+int smt_channel_score(const float* acc, int32_t B, int32_t S, int32_t n_cols, int32_t strategy, double* partials,
+                      size_t partial_bytes, double* out, hipStream_t stream) {
     if (B < 0 || S < 0 || n_cols < 0) return fail(SMT_E_INVALID, "smt_channel_score: negative size");
     if (strategy < SMT_SCORE_MEAN_ABS || strategy > SMT_SCORE_L2) return fail(SMT_E_INVALID, "smt_channel_score: strategy %d", strategy);
     if (n_cols == 0) return SMT_OK;
     if (!out || (B > 0 && S > 0 && !acc)) return fail(SMT_E_INVALID, "smt_channel_score: null pointer");
-    hipLaunchKernelGGL(channel_score_kernel, dim3((n_cols + 255) / 256), dim3(256), 0, stream, acc, B, S, n_cols,
-                       (int32_t)(strategy == SMT_SCORE_L2), out);
-    return check_launch("channel_score_kernel");
+    if (S == 0) {
+        hipError_t e = hipMemsetAsync(out, 0, (size_t)n_cols * sizeof(double), stream);
+        return e == hipSuccess ? SMT_OK : fail(SMT_E_LAUNCH, "smt_channel_score: memset: %s", hipGetErrorString(e));
+    }
+    const size_t need = smt_channel_score_workspace_bytes(S, n_cols);
+    if (!partials || partial_bytes < need)
+        return fail(SMT_E_WORKSPACE, "smt_channel_score: workspace %zu < %zu bytes", partial_bytes, need);
+    const int P = (S + kChanRows - 1) / kChanRows;
+    if (P > 65535) return fail(SMT_E_INVALID, "smt_channel_score: S too large");
+    hipLaunchKernelGGL(channel_partial_kernel, dim3((n_cols + 255) / 256, P), dim3(256), 0, stream, acc, B, S, n_cols,
+                       (int32_t)(strategy == SMT_SCORE_L2), partials);
+    int rc = check_launch("channel_partial_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(channel_final_kernel, dim3((n_cols + 255) / 256), dim3(256), 0, stream, partials, P, n_cols, out);
+    return check_launch("channel_final_kernel");
 }
 
 }  // extern "C"

@@ -632,9 +632,7 @@ class linearChannel(torch.autograd.Function):
         ctx.shape = input.shape
         partial = None
         if ctx.needs_input_grad[1] and len(ch):
-            x2 = input.reshape(-1, input.shape[-1])
-            if x2.stride(1) != 1:
-                x2 = x2.contiguous()
+            x2 = _rows_ready(input.reshape(-1, input.shape[-1]))
             partial = _hip.column_gather(x2, ch.device_table(x2.device), len(ch), ch.padded)
         ctx.save_for_backward(partial, weight)
         return torch.matmul(input, weight.t())

@@ -75,11 +75,12 @@ def test_validation_errors_without_gpu():
     assert lib.smt_row_gather(None, 256, 2, 256, None, 4, None, 256, None) == -1
     assert lib.smt_row_gather(None, 256, 2, 256, None, 0, None, 256, None) == 0       # no rows: no-op
     assert lib.smt_row_scatter(None, 256, 8, 256, None, 4, None, 256, None) == -1
-    assert lib.smt_column_gather(None, 256, 16, None, 300, None, 256, None) == -1      # ld_out < n_cols
+    assert lib.smt_column_gather(None, 256, 256, 16, None, 300, None, 256, None) == -1      # ld_out < n_cols
     assert lib.smt_act_accumulate(None, 0, 256, 0, 1, 4, 256, None, 1, None) == -1
     assert lib.smt_act_accumulate(None, 7, 256, 0, 1, 4, 256, None, 1, None) == -1     # bad dtype / null acc
     assert lib.smt_act_accumulate(None, 0, 256, 0, 0, 4, 256, None, 1, None) == 0      # empty batch: no-op
-    assert lib.smt_channel_score(None, 1, 4, 256, 9, None, None) == -1
+    assert lib.smt_channel_score(None, 1, 4, 256, 9, None, 0, None, None) == -1
+    assert lib.smt_channel_score_workspace_bytes(2048, 5120) == 64 * 5120 * 8
     assert b"strategy" in lib.smt_last_error()
 
 

@@ -51,11 +51,12 @@ def test_row_gather_scatter_bit_exact(dtype):
     assert torch.equal(W.cpu(), expect)
 
 
-@pytest.mark.parametrize("T,k", [(80, 37), (1000, 256), (33, 300), (7, 1)])
-def test_column_gather_bit_exact_and_zero_pad(T, k):
+@pytest.mark.parametrize("T,k,in_f", [(80, 37, 512), (1000, 256, 512), (33, 300, 512), (7, 1, 512),
+                                      (67, 1713, 5120), (9, 500, 13824), (5, 3, 20000)])   # 4, 2, 1 rows per workgroup
+def test_column_gather_bit_exact_and_zero_pad(T, k, in_f):
     torch.manual_seed(1)
-    x = torch.randn(T, 512).bfloat16().to(DEV)
-    idx = torch.randperm(512)[:k].tolist()
+    x = torch.randn(T, in_f).bfloat16().to(DEV)
+    idx = torch.randperm(in_f)[:k].tolist()
     pad = -(-k // 256) * 256
     out = _hip.column_gather(x, _hip.index_table(idx, DEV), k, pad)
     assert torch.equal(out[:, :k].cpu(), x.cpu()[:, idx])
