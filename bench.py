@@ -95,6 +95,9 @@ def parse():
     ap.add_argument("--fp8", action="store_true",
                     help="BASELINE config 5 (DeepSeek-R1-Distill-LLaMA-8B = the LLaMA-3-8B architecture, "
                          "SMT(0.86%%)): the decoder layers' frozen linears run as rowwise-scaled e4m3 GEMMs")
+    ap.add_argument("--wgrad-batch-tiles", type=int, default=48,
+                    help="the engine launches the tile wgrad of consecutive modules together once they hold "
+                         "this many tiles (smt_tile_wgrad_batch); 0 = one launch per module")
     ap.add_argument("--no-overlap-wgrad", action="store_true",
                     help="run the tile weight gradients on the current stream (default: their own stream, "
                          "overlapped with the data-gradient GEMMs)")
@@ -120,13 +123,26 @@ def log(*a):
 
 
 class WgradTimer:
-    """HIP events around every smt_tile_wgrad call (on the stream it is launched on)."""
+    """HIP events around every tile-wgrad launch (smt_tile_wgrad per module, smt_tile_wgrad_batch
+    for the engine's batches, smt_tile_wgrad_mx on the fp8 path), on the stream it is launched on,
+    with its algorithmic bytes counted two ways: per tile (2 operand slices + the output tile), and
+    per DISTINCT operand slice (a g row-block or x column-block slice that several tiles of the
+    launch read counts once: the least HBM traffic the launch can have)."""
 
     def __init__(self):
         self.enabled = False
-        self.records = []      # (start, end, algorithmic bytes, flops)
+        self.records = []      # (start, end, bytes per tile, unique-slice bytes, flops)
+        self._host_tabs = {}
 
-    def hook(self, T, n_tiles, out_bytes, stream_fn, operand_bytes=2):
+    def host_rows(self, tab):
+        """Host copy of a (cached, never rewritten) device tile table."""
+        key = (tab.data_ptr(), tuple(tab.shape))
+        rows = self._host_tabs.get(key)
+        if rows is None:
+            rows = self._host_tabs[key] = tab.cpu().tolist()
+        return rows
+
+    def hook(self, T, n_tiles, out_bytes, stream_fn, operand_bytes=2, slices=None):
         if not self.enabled:
             return stream_fn()
         s = torch.cuda.current_stream()
@@ -135,18 +151,26 @@ class WgradTimer:
         e0.record(s)
         r = stream_fn()
         e1.record(s)
-        self.records.append((e0, e1, n_tiles * (T * 256 * operand_bytes * 2 + 65536 * out_bytes),
-                             2.0 * T * 65536 * n_tiles))
+        per_tile = n_tiles * (T * 256 * operand_bytes * 2 + 65536 * out_bytes)
+        n_slices = 2 * n_tiles if slices is None else slices
+        unique = n_slices * T * 256 * operand_bytes + n_tiles * 65536 * out_bytes
+        self.records.append((e0, e1, per_tile, unique, 2.0 * T * 65536 * n_tiles))
         return r
 
     def summary(self):
         if not self.records:
             return None
         torch.cuda.synchronize()
-        t = sum(a.elapsed_time(b) for a, b, _, _ in self.records) * 1e-3
-        by = sum(r[2] for r in self.records)
-        fl = sum(r[3] for r in self.records)
-        return dict(launches=len(self.records), seconds=t, bytes=by, flops=fl)
+        t = sum(a.elapsed_time(b) for a, b, *_ in self.records) * 1e-3
+        return dict(launches=len(self.records), seconds=t, bytes=sum(r[2] for r in self.records),
+                    unique_bytes=sum(r[3] for r in self.records), flops=sum(r[4] for r in self.records))
+
+
+def _slice_keys(g, x, rows):
+    """Distinct operand slices of one module's tiles: (address of the g row-block column slice),
+    (address of the x column block), from the (row_block, col_block) rows the kernel reads."""
+    xbs = 256 * x.shape[1] if x.dim() == 3 else 256
+    return ({g.data_ptr() + 512 * r for r, _c in rows} | {x.data_ptr() + 2 * xbs * c for _r, c in rows})
 
 
 def install_wgrad_timer(timer: WgradTimer):
@@ -154,9 +178,27 @@ def install_wgrad_timer(timer: WgradTimer):
     orig = _hip.tile_wgrad
 
     def timed(g2, x2, rc, out, accumulate=False, order=None):
+        n_slices = len(_slice_keys(g2, x2, timer.host_rows(rc))) if timer.enabled else None
         return timer.hook(g2.shape[0], rc.shape[0], out.element_size(),
-                          lambda: orig(g2, x2, rc, out, accumulate=accumulate, order=order))
+                          lambda: orig(g2, x2, rc, out, accumulate=accumulate, order=order), slices=n_slices)
     _hip.tile_wgrad = timed
+
+
+def install_wgrad_batch_timer(timer: WgradTimer):
+    """The engine's batched launches (smt_tile_wgrad_batch: the tiles of several modules at once)."""
+    from sparse_matrix_tuning_amd import _hip
+    orig = _hip.tile_wgrad_batch
+
+    def timed(items, tab, order=None):
+        n_slices = None
+        if timer.enabled:
+            keys, rows = set(), timer.host_rows(tab)
+            for m, (g2, x2, _out, _acc) in enumerate(items):
+                keys |= _slice_keys(g2, x2, [(r, c) for mm, r, c, _k in rows if mm == m])
+            n_slices = len(keys)
+        return timer.hook(items[0][0].shape[0], tab.shape[0], items[0][2].element_size(),
+                          lambda: orig(items, tab, order), slices=n_slices)
+    _hip.tile_wgrad_batch = timed
 
 
 def install_mx_wgrad_timer(timer: WgradTimer):
@@ -326,7 +368,9 @@ def pmc_traffic(args):
     """HBM bytes per wgrad launch from the committed rocprofv3 --pmc passes of this same bench
     configuration (scripts/pmc_traffic.py; FETCH_SIZE x2 + WRITE_SIZE), or None."""
     path = None
-    for cand in ("r02_wgrad_pmc.json", "r01_wgrad_pmc.json"):
+    # the counters of the launch pattern this run uses: batched (engine default) or one per module
+    cands = (("r02_wgrad_batch_pmc.json",) if args.wgrad_batch_tiles > 0 else ("r02_wgrad_pmc.json", "r01_wgrad_pmc.json"))
+    for cand in cands:
         if os.path.exists(os.path.join(ROOT, "profiles", cand)):
             path = os.path.join(ROOT, "profiles", cand)
             break
@@ -628,6 +672,7 @@ def main():
 
     timer = WgradTimer()
     install_wgrad_timer(timer)
+    install_wgrad_batch_timer(timer)
     mx_timer = WgradTimer()
     install_mx_wgrad_timer(mx_timer)
     atimer = AttnTimer()
@@ -658,7 +703,8 @@ def main():
 
     # ---- warm-up: full fine-tuning + gradient harvest (fine_tune.py:710-775) ----
     ds_config = {"gradient_clipping": 1.0, "train_micro_batch_size_per_gpu": B, "train_batch_size": B * world}
-    smt_config = dict(ds_config, fp8_linears=bool(args.fp8), overlap_wgrad=not args.no_overlap_wgrad)
+    smt_config = dict(ds_config, fp8_linears=bool(args.fp8), overlap_wgrad=not args.no_overlap_wgrad,
+                      wgrad_batch_tiles=args.wgrad_batch_tiles)
     from sparse_matrix_tuning_amd.smt.smt import _NO_DECAY
     groups = [{"params": [p for n, p in model.named_parameters() if not any(nd in n.lower() for nd in _NO_DECAY)],
                "weight_decay": 0.0},
@@ -791,19 +837,25 @@ def main():
             avg = w["seconds"] / w["launches"]
             tflops = w["flops"] / w["seconds"] / 1e12
             alg_bytes = w["bytes"] / w["launches"]
+            uniq_bytes = w["unique_bytes"] / w["launches"]
             alg_gbs = alg_bytes / avg / 1e9
+            uniq_gbs = uniq_bytes / avg / 1e9
             traffic, tsrc = (None, None) if mx else pmc_traffic(args)
             peak_mfma = PEAK_MXFP8_TFLOPS if mx else PEAK_BF16_TFLOPS
-            # The roof: HBM while the counter bytes are at least ~the algorithmic bytes (no operand slice
-            # is shared between the module's tiles, the bench's spread selection: intensity 128 F/B, below
-            # the 312 F/B ridge); MFMA when L2/MALL reuse brings the real bytes well below them.
-            hbm_bound = traffic is None or traffic >= 0.8 * alg_bytes
-            hbm = {"achieved": round(alg_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                   "frac": round(alg_gbs / PEAK_HBM_GBS, 4),
+            # The roof: the launch's intensity on its DISTINCT operand slices (each g row-block / x
+            # column-block slice once, however many tiles read it) against the ridge peak_mfma / HBM.
+            # The spread selection shares few slices: ~128-190 F/B, below the 312 F/B bf16 ridge.
+            intensity = w["flops"] / max(1.0, w["unique_bytes"])
+            ridge = peak_mfma * 1e12 / (PEAK_HBM_GBS * 1e9)
+            hbm_bound = intensity < ridge
+            hbm = {"achieved": round(uniq_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                   "frac": round(uniq_gbs / PEAK_HBM_GBS, 4),
+                   "on_per_tile_bytes": round(alg_gbs, 1), "frac_on_per_tile_bytes": round(alg_gbs / PEAK_HBM_GBS, 4),
                    "on_counter_bytes": None if traffic is None else round(traffic / avg / 1e9, 1),
                    "frac_on_counter_bytes": None if traffic is None else round(traffic / avg / 1e9 / PEAK_HBM_GBS, 4)}
             mfma = {"achieved": round(tflops, 1), "peak": peak_mfma, "unit": "TFLOP/s",
-                    "frac": round(tflops / peak_mfma, 4)}
+                    "frac": round(tflops / peak_mfma, 4), "intensity_flop_per_byte": round(intensity, 1),
+                    "ridge_flop_per_byte": round(ridge, 1)}
             roof = hbm if hbm_bound else mfma
             roofline = {"bound": "hbm" if hbm_bound else "mfma", "achieved": roof["achieved"], "peak": roof["peak"],
                         "unit": roof["unit"], "frac": roof["frac"], "traffic": traffic, "traffic_source": tsrc,
@@ -820,15 +872,20 @@ def main():
                                               "the MFMA-bound data-gradient GEMM: its launches stretch over the "
                                               "GEMM's duration while the step gets shorter"
                                               if engine.wgrad_stream is not None else None),
-                        "algorithmic_bytes_per_launch": round(alg_bytes),
+                        "algorithmic_bytes_per_launch": round(uniq_bytes),
+                        "per_tile_bytes_per_launch": round(alg_bytes),
+                        "tiles_per_launch": round(w["flops"] / w["launches"] / (2.0 * 65536 * B * S), 1),
                         "flops_per_launch": round(w["flops"] / w["launches"]),
                         "hbm": hbm, "mfma": mfma,
-                        "bytes_note": (("algorithmic bytes per launch = tiles x (2 operand slices T x 256 x 1 B + the "
-                                        "fp32 tile); the MX quantisation of the operands is a separate launch")
+                        "bytes_note": (("algorithmic bytes per launch = distinct operand slices (T x 256 x 1 B each: "
+                                        "a g row-block or x column-block slice several tiles read counts once) + the "
+                                        "fp32 tiles; the MX quantisation of the operands is a separate launch")
                                        if mx else
-                                       ("algorithmic bytes per launch = tiles x (2 operand slices T x 256 x 2 B + the "
-                                        "fp32 tile); traffic = FETCH_SIZE x2 + WRITE_SIZE (rocprofv3 --pmc) per call, "
-                                        "including the split-K slabs and their reduce"))}
+                                       ("algorithmic bytes per launch = distinct operand slices (T x 256 x 2 B each: a g "
+                                        "row-block or x column-block slice several tiles of the launch read counts once) "
+                                        "+ the fp32 tiles; per_tile_bytes counts both slices of every tile; traffic = "
+                                        "FETCH_SIZE x2 + WRITE_SIZE (rocprofv3 --pmc) per launch, including the split-K "
+                                        "slabs and their reduce"))}
         tiles_by_module = {}
         for (m, _l), v in list(sel_mlp.items()) + list(sel_att.items()):
             tiles_by_module.setdefault(m, []).extend(v)

@@ -12,6 +12,7 @@
  *   smt_tile_scatter      deepspeed/smt/smt.py:332-341   per-forward write-back tiles -> W
  *                         (also smt.py:429-439, the merge in convert_matrix_sparsity_to_linear_layer)
  *   smt_tile_wgrad        deepspeed/smt/smt.py:382-404   per-tile sum_b g[b,:,rows]^T x[b,:,cols]
+ *   smt_tile_wgrad_batch  the same, for the tiles of several modules in one launch (ABI v6)
  *   smt_tile_scatter_t    deepspeed/smt/smt.py:332-341 / 406   write-back into the transposed copy W^T
  *                         that the data-gradient GEMM grad_input = g @ W reads (as g @ (W^T)^T)
  *   smt_colblock_gather   deepspeed/smt/smt.py:351-358   ctx.list1: the input column slices linearZ keeps
@@ -143,6 +144,40 @@ int smt_tile_wgrad(const void* grad_out, int64_t ld_grad_out,
                    const int32_t* tile_rc_dev, const int32_t* order_dev, int32_t n_tiles,
                    void* grad_tiles, int32_t out_dtype, int32_t accumulate,
                    void* workspace, size_t workspace_bytes, hipStream_t stream);
+
+/*
+ * One module of a batched tile wgrad (smt_tile_wgrad_batch): the operands and output of one
+ * smt_tile_wgrad call (same meaning as its arguments), plus the module's accumulate flag.
+ */
+#define SMT_WGRAD_MAX_MODULES 16
+typedef struct smt_wgrad_module {
+    const void* grad_out;           /* bf16 [T, ld_grad_out]                                       */
+    const void* x;                  /* bf16; block c at x + c * x_block_stride, rows of ld_x        */
+    int64_t ld_grad_out;
+    int64_t ld_x;
+    int64_t x_block_stride;
+    void* grad_tiles;               /* this module's [n_m*256, 256] output of out_dtype            */
+    int32_t accumulate;             /* add to grad_tiles instead of overwriting                     */
+    int32_t reserved;
+} smt_wgrad_module;                 /* 56 bytes                                                     */
+
+/* Workspace bytes smt_tile_wgrad_batch needs for T rows and n_tiles tiles over all its modules. */
+size_t smt_wgrad_batch_workspace_bytes(int64_t T, int32_t n_tiles);
+
+/*
+ * The tile weight gradients of up to SMT_WGRAD_MAX_MODULES SMT modules that share T (every linear of
+ * a decoder sees the same B*S rows) in ONE launch: for tile i of tile_tab_dev (device int32
+ * [n_tiles][4] = (module m, row_block r, col_block c, tile index k in module m's output)),
+ *   modules[m].grad_tiles[k] (+)= sum_{t<T} grad_out_m[t, r*256 : r*256+256]^T  X_{m,c}[t, 0:256]
+ * exactly as smt_tile_wgrad computes it per module (smt.py:382-404; same kernels, same split and
+ * summation order for the same T and total tile count). `modules` is a HOST array of n_modules
+ * entries, passed to the kernels by value. Batching makes one launch of the ~8 tiles a module of a
+ * spread selection carries plus those of its neighbours: fewer split-K slabs per tile and one launch
+ * instead of several (the engine batches consecutive backward calls).
+ */
+int smt_tile_wgrad_batch(const smt_wgrad_module* modules, int32_t n_modules, int64_t T,
+                         const int32_t* tile_tab_dev, const int32_t* order_dev, int32_t n_tiles,
+                         int32_t out_dtype, void* workspace, size_t workspace_bytes, hipStream_t stream);
 
 /*
  * out[j, t, 0:256] = x[t, c_j*256 : c_j*256+256] for the n_cb column blocks c_j of col_blocks_dev

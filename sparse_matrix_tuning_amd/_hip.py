@@ -28,7 +28,8 @@ _DT = {torch.bfloat16: DTYPE_BF16, torch.float32: DTYPE_FP32, torch.float16: DTY
 # Every function the headers declare (include/smt_hip.h, smt_model_ops.h, smt_attention.h); tests check the
 # library exports each of them.
 ABI_FUNCTIONS = (
-    "smt_last_error", "smt_abi_version", "smt_wgrad_workspace_bytes", "smt_tile_wgrad", "smt_colblock_gather", "smt_tile_scatter_t",
+    "smt_last_error", "smt_abi_version", "smt_wgrad_workspace_bytes", "smt_tile_wgrad", "smt_wgrad_batch_workspace_bytes",
+    "smt_tile_wgrad_batch", "smt_colblock_gather", "smt_tile_scatter_t",
     "smt_tile_gather", "smt_tile_scatter", "smt_grad_accumulate", "smt_block_score",
     "smt_sq_norm", "smt_adamw_step", "smt_adamw_multi",
     "smt_mx_quant_cols", "smt_wgrad_mx_workspace_bytes", "smt_tile_wgrad_mx",
@@ -48,6 +49,16 @@ class TileDesc(ctypes.Structure):
     _fields_ = [("weight", ctypes.c_void_p), ("ld_weight", ctypes.c_int64),
                 ("row_block", ctypes.c_int32), ("col_block", ctypes.c_int32),
                 ("flat_offset", ctypes.c_int64)]
+
+
+class WgradModule(ctypes.Structure):
+    """smt_wgrad_module (include/smt_hip.h): one module of a batched tile wgrad."""
+    _fields_ = [("grad_out", ctypes.c_void_p), ("x", ctypes.c_void_p), ("ld_grad_out", ctypes.c_int64),
+                ("ld_x", ctypes.c_int64), ("x_block_stride", ctypes.c_int64), ("grad_tiles", ctypes.c_void_p),
+                ("accumulate", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+WGRAD_MAX_MODULES = 16
 
 
 class AccumEntry(ctypes.Structure):
@@ -104,6 +115,8 @@ _SIGS = {
     "smt_abi_version": (ctypes.c_int, []),
     "smt_wgrad_workspace_bytes": (_SZ, [_I64, _I32]),
     "smt_tile_wgrad": (ctypes.c_int, [_P, _I64, _P, _I64, _I64, _I64, _P, _P, _I32, _P, _I32, _I32, _P, _SZ, _P]),
+    "smt_wgrad_batch_workspace_bytes": (_SZ, [_I64, _I32]),
+    "smt_tile_wgrad_batch": (ctypes.c_int, [ctypes.POINTER(WgradModule), _I32, _I64, _P, _P, _I32, _I32, _P, _SZ, _P]),
     "smt_colblock_gather": (ctypes.c_int, [_P, _I64, _I64, _P, _I32, _P, _P]),
     "smt_tile_scatter_t": (ctypes.c_int, [_P, _I32, _P, _P]),
     "smt_tile_gather": (ctypes.c_int, [_P, _I64, _I32, _P, _I32, _P, _P]),
@@ -289,6 +302,70 @@ def tile_wgrad(grad_out2d: torch.Tensor, x: torch.Tensor, tile_rc: torch.Tensor,
                                _ptr(ws), ws_bytes, _stream(dev))
     _check(rc, "smt_tile_wgrad")
     return out
+
+
+def _wgrad_x_layout(x: torch.Tensor, T: int, what: str):
+    """(ld_x, x_block_stride) of a row-major [T, in] input or a block-major [n_cb, T, 256] copy."""
+    if x.dim() == 3:
+        if not x.is_contiguous() or x.shape[1:] != (T, BLOCK):
+            raise ValueError(f"{what}: a block-major x must be a contiguous [n_cb, T, 256] tensor")
+        return BLOCK, T * BLOCK
+    if x.dim() != 2 or x.shape[0] != T or x.stride(1) != 1:
+        raise ValueError(f"{what}: x must be [T, features] with unit feature stride")
+    return x.stride(0), BLOCK
+
+
+def tile_wgrad_batch(items: Sequence[tuple], tile_tab: torch.Tensor, order: Optional[torch.Tensor] = None) -> None:
+    """One launch of the tile weight gradients of several modules sharing T (``smt_tile_wgrad_batch``).
+
+    ``items``: per module ``(grad_out2d, x, out, accumulate)`` with the meaning of :func:`tile_wgrad`
+    (``out``: that module's contiguous [n_m*256, 256] output; all outputs one dtype). ``tile_tab``:
+    device int32 [n, 4] of (module, row_block, col_block, tile index in the module's output), e.g.
+    from :func:`wgrad_batch_table`; ``order``: optional int32 [n] schedule permutation (speed only).
+    Each tile's result is bit-identical to what :func:`tile_wgrad` gives for the same tile at the
+    same T and the same total tile count."""
+    if not items:
+        return
+    if len(items) > WGRAD_MAX_MODULES:
+        raise ValueError(f"tile_wgrad_batch: {len(items)} modules > {WGRAD_MAX_MODULES}")
+    dev = _require_device(tile_tab, order, *[t for it in items for t in it[:3]])
+    T = items[0][0].shape[0]
+    out_dtype = items[0][2].dtype
+    mods = (WgradModule * len(items))()
+    for i, (g, x, out, acc) in enumerate(items):
+        if g.dtype != torch.bfloat16 or x.dtype != torch.bfloat16:
+            raise NotImplementedError("tile_wgrad_batch: bf16 operands only")
+        if g.dim() != 2 or g.shape[0] != T or g.stride(1) != 1:
+            raise ValueError("tile_wgrad_batch: every grad_out must be [T, features] with the same T")
+        if out.dtype != out_dtype or out.dtype not in (torch.bfloat16, torch.float32) or not out.is_contiguous():
+            raise ValueError("tile_wgrad_batch: outputs must be contiguous and all bf16 or all fp32")
+        ld_x, xbs = _wgrad_x_layout(x, T, "tile_wgrad_batch")
+        mods[i] = WgradModule(_ptr(g), _ptr(x), g.stride(0), ld_x, xbs, _ptr(out), int(bool(acc)), 0)
+    if tile_tab.dtype != torch.int32 or tile_tab.dim() != 2 or tile_tab.shape[1] != 4:
+        raise ValueError("tile_wgrad_batch: tile_tab must be int32 [n, 4]")
+    n = tile_tab.shape[0]
+    if order is not None and (order.dtype != torch.int32 or order.numel() != n):
+        raise ValueError("tile_wgrad_batch: order must be int32 [n_tiles]")
+    ws_bytes = int(load().smt_wgrad_batch_workspace_bytes(T, n))
+    ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=dev)
+    rc = load().smt_tile_wgrad_batch(mods, len(items), T, _ptr(tile_tab), _ptr(order), n, _DT[out_dtype],
+                                     _ptr(ws), ws_bytes, _stream(dev))
+    _check(rc, "smt_tile_wgrad_batch")
+
+
+def wgrad_batch_table(module_tiles: Sequence[Sequence[Sequence[int]]], device: torch.device):
+    """Device tables of a batch: int32 [n, 4] (module, row_block, col_block, tile index) over the
+    modules' tile lists (``(row_block, col_block)`` as the kernel sees them: for a block-major input
+    the column block is the position in it), and the int32 [n] schedule (tiles of one module stay in
+    :func:`schedule_order`'s order, modules in batch order)."""
+    rows, order = [], []
+    for m, tl in enumerate(module_tiles):
+        base = len(rows)
+        rows.extend((m, int(r), int(c), k) for k, (r, c) in enumerate(tl))
+        order.extend(base + i for i in schedule_order(tl))
+    flat = [v for row in rows for v in row]
+    tab = torch.tensor(flat, dtype=torch.int32).view(-1, 4).to(device)
+    return tab, torch.tensor(order, dtype=torch.int32).to(device)
 
 
 def colblock_gather(x2d: torch.Tensor, col_blocks: torch.Tensor) -> torch.Tensor:

@@ -103,63 +103,83 @@ __device__ __forceinline__ bf16x8_t tr_frag(const uint8_t* img, uint32_t k, uint
 // Epilogue modes: partial slab (S > 1), or the final tile written directly (S == 1).
 enum WgradOut { kOutSlab = 0, kOutF32 = 1, kOutBF16 = 2 };
 
-// Epilogue: C/D map of 32x32x16 (col = lane&31, row = (i&3) + 8*(i>>2) + 4*(lane>>5)) to the fp32
-// partial slab of (tile, s), or straight to the fp32 / bf16 output tile when S == 1.
+// Where a workgroup's accumulators go: the fp32 partial slab (tile, s) of a split tile (S > 1), or
+// the final tile itself (S == 1; fp32 or bf16 per OUT).
 template <int OUT>
-__device__ __forceinline__ void wgrad_store(f32x16_t (&acc)[4][2], void* __restrict__ out_ptr, int tile, int s, int S,
+__device__ __forceinline__ void* wgrad_dst(void* out_ptr, int tile, int s, int S) {
+    if (OUT == kOutSlab) return static_cast<float*>(out_ptr) + (int64_t)(tile * S + s) * kTileElems;
+    if (OUT == kOutF32) return static_cast<float*>(out_ptr) + (int64_t)tile * kTileElems;
+    return static_cast<uint16_t*>(out_ptr) + (int64_t)tile * kTileElems;
+}
+
+// Epilogue: C/D map of 32x32x16 (col = lane&31, row = (i&3) + 8*(i>>2) + 4*(lane>>5)) into the
+// 256x256 destination `dst` (wgrad_dst): an fp32 slab, or the fp32 / bf16 output tile.
+template <int OUT>
+__device__ __forceinline__ void wgrad_store(f32x16_t (&acc)[4][2], void* __restrict__ dst,
                                             int wm, int wn, int lane, int accumulate) {
     const int col = lane & 31;
     const int h = lane >> 5;
-    if (OUT == kOutSlab) {
-        float* out = static_cast<float*>(out_ptr) + (int64_t)(tile * S + s) * kTileElems;
 #pragma unroll
-        for (int mb = 0; mb < 4; ++mb)
+    for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
-            for (int nb = 0; nb < 2; ++nb)
+        for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const int m = wm * 128 + mb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-                    const int n = wn * 64 + nb * 32 + col;
-                    out[m * kTile + n] = acc[mb][nb][i];
-                }
-    } else if (OUT == kOutF32) {
-        float* out = static_cast<float*>(out_ptr) + (int64_t)tile * kTileElems;
-#pragma unroll
-        for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const int m = wm * 128 + mb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-                    const int n = wn * 64 + nb * 32 + col;
-                    float v = acc[mb][nb][i];
+            for (int i = 0; i < 16; ++i) {
+                const int m = wm * 128 + mb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                const int n = wn * 64 + nb * 32 + col;
+                float v = acc[mb][nb][i];
+                if (OUT == kOutSlab) {
+                    static_cast<float*>(dst)[m * kTile + n] = v;
+                } else if (OUT == kOutF32) {
+                    float* out = static_cast<float*>(dst);
                     if (accumulate) v += out[m * kTile + n];
                     out[m * kTile + n] = v;
-                }
-    } else {
-        uint16_t* out = static_cast<uint16_t*>(out_ptr) + (int64_t)tile * kTileElems;
-#pragma unroll
-        for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const int m = wm * 128 + mb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-                    const int n = wn * 64 + nb * 32 + col;
-                    float v = acc[mb][nb][i];
+                } else {
+                    uint16_t* out = static_cast<uint16_t*>(dst);
                     if (accumulate) v += bf16_bits_to_f32(out[m * kTile + n]);
                     out[m * kTile + n] = f32_to_bf16_bits(v);
                 }
-    }
+            }
 }
 
-template <int OUT>
+// One tile of a wgrad launch: its operand column slices and its output. A launch covers the tiles
+// of one module (BATCH = false: int32 [n][2] table of (row_block, col_block), module m[0]) or of up
+// to SMT_WGRAD_MAX_MODULES modules that share T (BATCH = true: int32 [n][4] table of (module,
+// row_block, col_block, tile index in that module's output)). Everything here is workgroup-uniform.
+struct WgradModules { smt_wgrad_module m[SMT_WGRAD_MAX_MODULES]; };
+
+struct WgradTile {
+    const uint16_t* g;       // grad_out column slice r: element (t, j) at g[t * ldg + j]
+    const uint16_t* x;       // input column block c: element (t, j) at x[t * ldx + j]
+    int64_t ldg, ldx;
+    void* out;               // the final tile (S == 1 epilogue and the reduce)
+    int accumulate;
+};
+
+template <bool BATCH, int OUT_BYTES>
+__device__ __forceinline__ WgradTile wgrad_tile(const WgradModules& mods, const int32_t* __restrict__ tab, int tile) {
+    WgradTile t;
+    int mi = 0, r, c, ti;
+    if (BATCH) {
+        mi = tab[4 * tile]; r = tab[4 * tile + 1]; c = tab[4 * tile + 2]; ti = tab[4 * tile + 3];
+    } else {
+        r = tab[2 * tile]; c = tab[2 * tile + 1]; ti = tile;
+    }
+    const smt_wgrad_module& m = mods.m[mi];
+    t.ldg = m.ld_grad_out;
+    t.ldx = m.ld_x;
+    t.g = static_cast<const uint16_t*>(m.grad_out) + (int64_t)r * kTile;
+    t.x = static_cast<const uint16_t*>(m.x) + (int64_t)c * m.x_block_stride;
+    t.out = static_cast<uint8_t*>(m.grad_tiles) + (int64_t)ti * kTileElems * OUT_BYTES;
+    t.accumulate = m.accumulate;
+    return t;
+}
+
+template <int OUT, bool BATCH>
 __global__ __launch_bounds__(kWgThreads, 2)
-void wgrad_partial_kernel(const uint16_t* __restrict__ g, int64_t ldg,
-                          const uint16_t* __restrict__ x, int64_t ldx, int64_t xbs,
-                          int64_t T, int64_t chunk, int S, int n_tiles,
-                          const int32_t* __restrict__ tile_rc, const int32_t* __restrict__ order,
-                          void* __restrict__ out_ptr, int accumulate) {
+void wgrad_partial_kernel(const WgradModules mods, int64_t T, int64_t chunk, int S, int n_tiles,
+                          const int32_t* __restrict__ tile_tab, const int32_t* __restrict__ order,
+                          float* __restrict__ slab) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * 2 * kImgBytes];   // 128 KiB, one array
 
     // XCD-aware, chunk-major schedule. Workgroups are dealt round-robin over the 8 XCDs (b and b+8
@@ -175,14 +195,14 @@ void wgrad_partial_kernel(const uint16_t* __restrict__ g, int64_t ldg,
     const int s = L / n_tiles;
     const int li = L - s * n_tiles;
     const int tile = order != nullptr ? order[li] : li;
-    const int r = tile_rc[2 * tile];
-    const int c = tile_rc[2 * tile + 1];
+    const WgradTile tt = wgrad_tile<BATCH, OUT == kOutBF16 ? 2 : 4>(mods, tile_tab, tile);
     const int64_t t_begin = (int64_t)s * chunk;
     const int64_t t_end = (t_begin + chunk < T) ? (t_begin + chunk) : T;
     const int nst = (t_end > t_begin) ? (int)((t_end - t_begin + kBK - 1) / kBK) : 0;
 
-    const uint16_t* gb = g + (int64_t)r * kTile;
-    const uint16_t* xb = x + (int64_t)c * xbs;
+    const uint16_t* gb = tt.g;
+    const uint16_t* xb = tt.x;
+    const int64_t ldg = tt.ldg, ldx = tt.ldx;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -277,7 +297,7 @@ void wgrad_partial_kernel(const uint16_t* __restrict__ g, int64_t ldg,
         __syncthreads();
     }
 
-    wgrad_store<OUT>(acc, out_ptr, tile, s, S, wm, wn, lane, accumulate);
+    wgrad_store<OUT>(acc, OUT == kOutSlab ? wgrad_dst<kOutSlab>(slab, tile, s, S) : tt.out, wm, wn, lane, tt.accumulate);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -336,13 +356,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base,
     return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
 }
 
-template <int OUT, int SLOTS>
+template <int OUT, int SLOTS, bool BATCH>
 __global__ __launch_bounds__(kWgThreads, 1)
-void wgrad_dma_kernel(const uint16_t* __restrict__ g, int64_t ldg,
-                      const uint16_t* __restrict__ x, int64_t ldx, int64_t xbs,
-                      int64_t T, int64_t chunk, int S, int n_tiles,
-                      const int32_t* __restrict__ tile_rc, const int32_t* __restrict__ order,
-                      void* __restrict__ out_ptr, int accumulate) {
+void wgrad_dma_kernel(const WgradModules mods, int64_t T, int64_t chunk, int S, int n_tiles,
+                      const int32_t* __restrict__ tile_tab, const int32_t* __restrict__ order,
+                      float* __restrict__ slab) {
     static_assert(SLOTS >= 3 && SLOTS <= 5, "ring depth");
     constexpr int AHEAD = SLOTS - 2;                       // stages in flight beside the one computed
     __shared__ __attribute__((aligned(16))) uint8_t lds[SLOTS * kDmaSlotBytes];   // one array (T-trap 4a)
@@ -354,16 +372,16 @@ void wgrad_dma_kernel(const uint16_t* __restrict__ g, int64_t ldg,
     const int s = L / n_tiles;
     const int li = L - s * n_tiles;
     const int tile = order != nullptr ? order[li] : li;
-    const int r = tile_rc[2 * tile];
-    const int c = tile_rc[2 * tile + 1];
+    const WgradTile tt = wgrad_tile<BATCH, OUT == kOutBF16 ? 2 : 4>(mods, tile_tab, tile);
+    const int64_t ldg = tt.ldg, ldx = tt.ldx;
     const int64_t t_begin = (int64_t)s * chunk;
     const int64_t t_end = (t_begin + chunk < T) ? (t_begin + chunk) : T;
     const int rows = (t_end > t_begin) ? (int)(t_end - t_begin) : 0;
     const int nst = (rows + kDmaBK - 1) / kDmaBK;
 
     // descriptors over this chunk's rows of the two column slices (host guarantees rows*ld*2 < 2^31)
-    const __amdgpu_buffer_rsrc_t rg = uniform_rsrc(g + t_begin * ldg + (int64_t)r * kTile, (int64_t)rows * ldg * 2);
-    const __amdgpu_buffer_rsrc_t rx = uniform_rsrc(x + t_begin * ldx + (int64_t)c * xbs, (int64_t)rows * ldx * 2);
+    const __amdgpu_buffer_rsrc_t rg = uniform_rsrc(tt.g + t_begin * ldg, (int64_t)rows * ldg * 2);
+    const __amdgpu_buffer_rsrc_t rx = uniform_rsrc(tt.x + t_begin * ldx, (int64_t)rows * ldx * 2);
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -441,7 +459,7 @@ void wgrad_dma_kernel(const uint16_t* __restrict__ g, int64_t ldg,
                     acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mb], bfr[nb], acc[mb][nb], 0, 0, 0);
         }
     }
-    wgrad_store<OUT>(acc, out_ptr, tile, s, S, wm, wn, lane, accumulate);
+    wgrad_store<OUT>(acc, OUT == kOutSlab ? wgrad_dst<kOutSlab>(slab, tile, s, S) : tt.out, wm, wn, lane, tt.accumulate);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -473,7 +491,7 @@ __device__ __forceinline__ bf16x8_t qtr_frag(const uint8_t* img, uint32_t k, uin
 }
 
 template <int OUT>
-__device__ __forceinline__ void wgrad_store_q(f32x16_t (&acc)[2][2], void* __restrict__ out_ptr, int tile, int s, int S,
+__device__ __forceinline__ void wgrad_store_q(f32x16_t (&acc)[2][2], void* __restrict__ dst,
                                               int m0, int n0, int lane, int accumulate) {
     const int col = lane & 31;
     const int h = lane >> 5;
@@ -487,26 +505,24 @@ __device__ __forceinline__ void wgrad_store_q(f32x16_t (&acc)[2][2], void* __res
                 const int n = n0 + nb * 32 + col;
                 float v = acc[mb][nb][i];
                 if (OUT == kOutSlab) {
-                    static_cast<float*>(out_ptr)[(int64_t)(tile * S + s) * kTileElems + m * kTile + n] = v;
+                    static_cast<float*>(dst)[m * kTile + n] = v;
                 } else if (OUT == kOutF32) {
-                    float* out = static_cast<float*>(out_ptr) + (int64_t)tile * kTileElems;
+                    float* out = static_cast<float*>(dst);
                     if (accumulate) v += out[m * kTile + n];
                     out[m * kTile + n] = v;
                 } else {
-                    uint16_t* out = static_cast<uint16_t*>(out_ptr) + (int64_t)tile * kTileElems;
+                    uint16_t* out = static_cast<uint16_t*>(dst);
                     if (accumulate) v += bf16_bits_to_f32(out[m * kTile + n]);
                     out[m * kTile + n] = f32_to_bf16_bits(v);
                 }
             }
 }
 
-template <int OUT, int QS = kQSlots>
+template <int OUT, int QS, bool BATCH>
 __global__ __launch_bounds__(kQThreads, 2)
-void wgrad_quarter_kernel(const uint16_t* __restrict__ g, int64_t ldg,
-                          const uint16_t* __restrict__ x, int64_t ldx, int64_t xbs,
-                          int64_t T, int64_t chunk, int S, int n_tiles,
-                          const int32_t* __restrict__ tile_rc, const int32_t* __restrict__ order,
-                          void* __restrict__ out_ptr, int accumulate) {
+void wgrad_quarter_kernel(const WgradModules mods, int64_t T, int64_t chunk, int S, int n_tiles,
+                          const int32_t* __restrict__ tile_tab, const int32_t* __restrict__ order,
+                          float* __restrict__ slab) {
     static_assert(QS >= 3 && QS <= 5, "ring depth");
     constexpr int AHEAD = QS - 2;                          // stages in flight beside the one computed
     __shared__ __attribute__((aligned(16))) uint8_t lds[QS * kQSlotBytes];          // 64 KiB (4 slots), one array
@@ -522,15 +538,15 @@ void wgrad_quarter_kernel(const uint16_t* __restrict__ g, int64_t ldg,
     const int li = ts - s * n_tiles;
     const int tile = order != nullptr ? order[li] : li;
     const int qm = qd >> 1, qn = qd & 1;
-    const int r = tile_rc[2 * tile];
-    const int c = tile_rc[2 * tile + 1];
+    const WgradTile tt = wgrad_tile<BATCH, OUT == kOutBF16 ? 2 : 4>(mods, tile_tab, tile);
+    const int64_t ldg = tt.ldg, ldx = tt.ldx;
     const int64_t t_begin = (int64_t)s * chunk;
     const int64_t t_end = (t_begin + chunk < T) ? (t_begin + chunk) : T;
     const int rows = (t_end > t_begin) ? (int)(t_end - t_begin) : 0;
     const int nst = (rows + kDmaBK - 1) / kDmaBK;
 
-    const __amdgpu_buffer_rsrc_t rg = uniform_rsrc(g + t_begin * ldg + (int64_t)r * kTile + qm * 128, (int64_t)rows * ldg * 2);
-    const __amdgpu_buffer_rsrc_t rx = uniform_rsrc(x + t_begin * ldx + (int64_t)c * xbs + qn * 128, (int64_t)rows * ldx * 2);
+    const __amdgpu_buffer_rsrc_t rg = uniform_rsrc(tt.g + t_begin * ldg + qm * 128, (int64_t)rows * ldg * 2);
+    const __amdgpu_buffer_rsrc_t rx = uniform_rsrc(tt.x + t_begin * ldx + qn * 128, (int64_t)rows * ldx * 2);
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -607,15 +623,15 @@ void wgrad_quarter_kernel(const uint16_t* __restrict__ g, int64_t ldg,
                     acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mb], bfr[nb], acc[mb][nb], 0, 0, 0);
         }
     }
-    wgrad_store_q<OUT>(acc, out_ptr, tile, s, S, qm * 128 + wm * 64, qn * 128 + wn * 64, lane, accumulate);
+    wgrad_store_q<OUT>(acc, OUT == kOutSlab ? wgrad_dst<kOutSlab>(slab, tile, s, S) : tt.out,
+                       qm * 128 + wm * 64, qn * 128 + wn * 64, lane, tt.accumulate);
 }
 
-// Sum the S partial slabs of each tile in order s = 0..S-1 (deterministic) and write the tile.
-// 64 workgroups x 256 threads x 4 elements per tile.
+// Sum the S partial slabs of one tile in order s = 0..S-1 (deterministic) and write the tile (this
+// workgroup's 1024 of its elements).
 template <bool OUT_F32>
-__global__ __launch_bounds__(256)
-void wgrad_reduce_kernel(const float* __restrict__ slab, int S, void* __restrict__ out, int accumulate) {
-    const int tile = blockIdx.x >> 6;
+__device__ __forceinline__ void wgrad_reduce_tile(const float* __restrict__ slab, int S, int tile, void* __restrict__ tile_out,
+                                                  int accumulate) {
     const int e = (((blockIdx.x & 63) << 8) + threadIdx.x) * 4;
     const float* src = slab + (int64_t)tile * S * kTileElems + e;
     float4 sum = *reinterpret_cast<const float4*>(src);
@@ -623,7 +639,8 @@ void wgrad_reduce_kernel(const float* __restrict__ slab, int S, void* __restrict
         const float4 v = *reinterpret_cast<const float4*>(src + (int64_t)s * kTileElems);
         sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
     }
-    const int64_t o = (int64_t)tile * kTileElems + e;
+    const int64_t o = e;
+    void* out = tile_out;
     if (OUT_F32) {
         float4* dst = reinterpret_cast<float4*>(static_cast<float*>(out) + o);
         if (accumulate) {
@@ -645,6 +662,25 @@ void wgrad_reduce_kernel(const float* __restrict__ slab, int S, void* __restrict
         w.y = (uint32_t)f32_to_bf16_bits(sum.z) | ((uint32_t)f32_to_bf16_bits(sum.w) << 16);
         *dst = w;
     }
+}
+
+// 64 workgroups x 256 threads x 4 elements per tile; tile i's output = out + i tiles
+template <bool OUT_F32>
+__global__ __launch_bounds__(256)
+void wgrad_reduce_kernel(const float* __restrict__ slab, int S, void* __restrict__ out, int accumulate) {
+    const int tile = blockIdx.x >> 6;
+    wgrad_reduce_tile<OUT_F32>(slab, S, tile, static_cast<uint8_t*>(out) + (int64_t)tile * kTileElems * (OUT_F32 ? 4 : 2),
+                               accumulate);
+}
+
+// the same over a batch: each tile's output and accumulate flag from its module (wgrad_tile)
+template <bool OUT_F32>
+__global__ __launch_bounds__(256)
+void wgrad_reduce_batch_kernel(const float* __restrict__ slab, int S, const WgradModules mods,
+                               const int32_t* __restrict__ tile_tab) {
+    const int tile = blockIdx.x >> 6;
+    const WgradTile tt = wgrad_tile<true, OUT_F32 ? 4 : 2>(mods, tile_tab, tile);
+    wgrad_reduce_tile<OUT_F32>(slab, S, tile, tt.out, tt.accumulate);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -887,7 +923,7 @@ void wgrad_mx_kernel(const uint8_t* __restrict__ qa, const uint8_t* __restrict__
                 acc[mb][nb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af[mb], bfr[nb], acc[mb][nb],
                                                                                0, 0, 0, as[mb], 0, bs[nb]);
     }
-    wgrad_store<OUT>(acc, out_ptr, tile, s, S, wm, wn, lane, accumulate);
+    wgrad_store<OUT>(acc, wgrad_dst<OUT>(out_ptr, tile, s, S), wm, wn, lane, accumulate);
 }
 
 // Quarter-tile MX variant for modules with few tiles (the fill-bound regime, as wgrad_quarter_kernel):
@@ -1014,7 +1050,8 @@ void wgrad_mx_quarter_kernel(const uint8_t* __restrict__ qa, const uint8_t* __re
                 acc[mb][nb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af[mb], bfr[nb], acc[mb][nb],
                                                                                0, 0, 0, as[mb], 0, bs[nb]);
     }
-    wgrad_store_q<OUT>(acc, out_ptr, tile, s, S, qm * 128 + wm * 64, qn * 128 + wn * 64, lane, accumulate);
+    wgrad_store_q<OUT>(acc, wgrad_dst<OUT>(out_ptr, tile, s, S), qm * 128 + wm * 64, qn * 128 + wn * 64, lane,
+                       accumulate);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1631,7 +1668,7 @@ extern "C" {
 
 const char* smt_last_error(void) { return g_err; }
 
-int smt_abi_version(void) { return 5; }
+int smt_abi_version(void) { return 6; }
 
 size_t smt_wgrad_workspace_bytes(int64_t T, int32_t n_tiles) {
     if (T <= 0 || n_tiles <= 0) return 0;
@@ -1639,6 +1676,89 @@ size_t smt_wgrad_workspace_bytes(int64_t T, int32_t n_tiles) {
     if (sp.S == 1) return 0;                      // written straight from the accumulators
     return (size_t)n_tiles * (size_t)sp.S * (size_t)kTileElems * sizeof(float);
 }
+
+}  // extern "C"
+
+namespace {
+
+// Launch the tile wgrad of `n_tiles` tiles (one module, or a batch) and, when split, its reduce.
+// max_ld: the largest leading dimension of any operand (the LDS-DMA kernels' 32-bit buffer offsets
+// need chunk * ld * 2 < 2^31, otherwise the register-staged kernel, which addresses with 64 bits).
+template <bool BATCH>
+int wgrad_launch(const WgradModules& mods, int64_t T, int64_t max_ld, const int32_t* tab, const int32_t* order,
+                 int32_t n_tiles, int32_t out_dtype, void* workspace, size_t workspace_bytes, hipStream_t stream) {
+    const WgradSplit sp = wgrad_split(T, n_tiles);
+    const dim3 grid(n_tiles * sp.S), block(kWgThreads);
+    const dim3 qgrid(n_tiles * sp.S * 4), qblock(kQThreads);
+    static const bool force_reg = [] { const char* e = getenv("SMT_WGRAD_IMPL"); return e && strcmp(e, "reg") == 0; }();
+    // SMT_WGRAD_SLOTS=5: the 3-in-flight ring (A/B runs); default 4 (2 stages in flight)
+    static const int slots = [] { const char* e = getenv("SMT_WGRAD_SLOTS"); return (e && atoi(e) == 5) ? 5 : kDmaSlotsDefault; }();
+    // SMT_WGRAD_QSLOTS=5: the quarter kernel with 3 stages in flight (80 KiB LDS per workgroup)
+    static const int qslots = [] { const char* e = getenv("SMT_WGRAD_QSLOTS"); return (e && atoi(e) == 5) ? 5 : kQSlots; }();
+    const bool dma = !force_reg && sp.chunk * max_ld * 2 < (int64_t)0x7fffffff;
+    const bool quarter = dma && sp.quarter;
+    float* slab = nullptr;
+    if (sp.S > 1) {
+        const size_t need = (size_t)n_tiles * sp.S * kTileElems * sizeof(float);
+        if (!workspace || workspace_bytes < need)
+            return fail(SMT_E_WORKSPACE, "smt_tile_wgrad: workspace %zu < %zu bytes", workspace_bytes, need);
+        if (!aligned16(workspace)) return fail(SMT_E_ALIGN, "smt_tile_wgrad: workspace not 16-byte aligned");
+        slab = static_cast<float*>(workspace);
+    }
+#define SMT_WGRAD_LAUNCH(OUT)                                                                                     \
+    do {                                                                                                          \
+        if (!dma) hipLaunchKernelGGL((wgrad_partial_kernel<OUT, BATCH>), grid, block, 0, stream, mods, T, sp.chunk, \
+                                     sp.S, n_tiles, tab, order, slab);                                           \
+        else if (quarter && qslots == 5) hipLaunchKernelGGL((wgrad_quarter_kernel<OUT, 5, BATCH>), qgrid, qblock, 0, \
+                                     stream, mods, T, sp.chunk, sp.S, n_tiles, tab, order, slab);                \
+        else if (quarter) hipLaunchKernelGGL((wgrad_quarter_kernel<OUT, kQSlots, BATCH>), qgrid, qblock, 0, stream,  \
+                                     mods, T, sp.chunk, sp.S, n_tiles, tab, order, slab);                        \
+        else if (slots == 5) hipLaunchKernelGGL((wgrad_dma_kernel<OUT, 5, BATCH>), grid, block, 0, stream, mods, T,  \
+                                     sp.chunk, sp.S, n_tiles, tab, order, slab);                                 \
+        else hipLaunchKernelGGL((wgrad_dma_kernel<OUT, kDmaSlotsDefault, BATCH>), grid, block, 0, stream, mods, T,   \
+                                sp.chunk, sp.S, n_tiles, tab, order, slab);                                      \
+    } while (0)
+    if (sp.S == 1) {
+        if (out_dtype == SMT_DTYPE_FP32) SMT_WGRAD_LAUNCH(kOutF32);
+        else SMT_WGRAD_LAUNCH(kOutBF16);
+        return check_launch("wgrad kernel");
+    }
+    SMT_WGRAD_LAUNCH(kOutSlab);
+#undef SMT_WGRAD_LAUNCH
+    int rc = check_launch("wgrad kernel");
+    if (rc) return rc;
+    const dim3 rgrid(n_tiles * 64), rblock(256);
+    if (BATCH) {
+        if (out_dtype == SMT_DTYPE_FP32)
+            hipLaunchKernelGGL(wgrad_reduce_batch_kernel<true>, rgrid, rblock, 0, stream, slab, sp.S, mods, tab);
+        else
+            hipLaunchKernelGGL(wgrad_reduce_batch_kernel<false>, rgrid, rblock, 0, stream, slab, sp.S, mods, tab);
+    } else {
+        const smt_wgrad_module& m = mods.m[0];
+        if (out_dtype == SMT_DTYPE_FP32)
+            hipLaunchKernelGGL(wgrad_reduce_kernel<true>, rgrid, rblock, 0, stream, slab, sp.S, m.grad_tiles, m.accumulate);
+        else
+            hipLaunchKernelGGL(wgrad_reduce_kernel<false>, rgrid, rblock, 0, stream, slab, sp.S, m.grad_tiles, m.accumulate);
+    }
+    return check_launch("wgrad_reduce_kernel");
+}
+
+// argument checks shared by the single-module and batched entry points
+int check_wgrad_module(const char* fn, const smt_wgrad_module& m) {
+    if (!m.grad_out || !m.x || !m.grad_tiles) return fail(SMT_E_INVALID, "%s: null operand or output", fn);
+    if (!aligned16(m.grad_out) || !aligned16(m.x) || (m.ld_grad_out & 7) || (m.ld_x & 7) || !aligned16(m.grad_tiles))
+        return fail(SMT_E_ALIGN, "%s: operands need 16-byte aligned rows (ld %% 8 == 0) and a 16-byte aligned output", fn);
+    if (m.ld_grad_out < kTile || m.ld_x < kTile)
+        return fail(SMT_E_INVALID, "%s: leading dimensions %lld / %lld below 256", fn, (long long)m.ld_grad_out,
+                    (long long)m.ld_x);
+    if (m.x_block_stride < kTile || (m.x_block_stride & 7))
+        return fail(SMT_E_INVALID, "%s: x_block_stride %lld (>= 256, %% 8 == 0)", fn, (long long)m.x_block_stride);
+    return SMT_OK;
+}
+
+}  // namespace
+
+extern "C" {
 
 int smt_tile_wgrad(const void* grad_out, int64_t ld_grad_out, const void* x, int64_t ld_x, int64_t x_block_stride, int64_t T,
                    const int32_t* tile_rc_dev, const int32_t* order_dev, int32_t n_tiles, void* grad_tiles,
@@ -1658,66 +1778,40 @@ int smt_tile_wgrad(const void* grad_out, int64_t ld_grad_out, const void* x, int
     if (!grad_out || !x) return fail(SMT_E_INVALID, "smt_tile_wgrad: null operand");
     if (!aligned16(grad_out) || !aligned16(x) || (ld_grad_out & 7) || (ld_x & 7))
         return fail(SMT_E_ALIGN, "smt_tile_wgrad: operands need 16-byte aligned rows (ld %% 8 == 0)");
-    const int64_t xbs = x_block_stride;
-    if (xbs < kTile || (xbs & 7)) return fail(SMT_E_INVALID, "smt_tile_wgrad: x_block_stride %lld (>= 256, %% 8 == 0)",
-                                              (long long)xbs);
-    const WgradSplit sp = wgrad_split(T, n_tiles);
-    const uint16_t* gp = static_cast<const uint16_t*>(grad_out);
-    const uint16_t* xp = static_cast<const uint16_t*>(x);
-    const dim3 grid(n_tiles * sp.S), block(kWgThreads);
-    const dim3 qgrid(n_tiles * sp.S * 4), qblock(kQThreads);
-    // LDS-DMA kernel by default; its 32-bit buffer offsets need chunk * ld * 2 < 2^31, otherwise (and
-    // with SMT_WGRAD_IMPL=reg) the register-staged kernel, which addresses with 64 bits.
+    if (x_block_stride < kTile || (x_block_stride & 7))
+        return fail(SMT_E_INVALID, "smt_tile_wgrad: x_block_stride %lld (>= 256, %% 8 == 0)", (long long)x_block_stride);
+    WgradModules mods{};
+    mods.m[0] = smt_wgrad_module{grad_out, x, ld_grad_out, ld_x, x_block_stride, grad_tiles, accumulate ? 1 : 0, 0};
     const int64_t max_ld = ld_grad_out > ld_x ? ld_grad_out : ld_x;
-    static const bool force_reg = [] { const char* e = getenv("SMT_WGRAD_IMPL"); return e && strcmp(e, "reg") == 0; }();
-    // SMT_WGRAD_SLOTS=5: the 3-in-flight ring (A/B runs); default 4 (2 stages in flight)
-    static const int slots = [] { const char* e = getenv("SMT_WGRAD_SLOTS"); return (e && atoi(e) == 5) ? 5 : kDmaSlotsDefault; }();
-    // SMT_WGRAD_QSLOTS=5: the quarter kernel with 3 stages in flight (80 KiB LDS per workgroup)
-    static const int qslots = [] { const char* e = getenv("SMT_WGRAD_QSLOTS"); return (e && atoi(e) == 5) ? 5 : kQSlots; }();
-    const bool dma = !force_reg && sp.chunk * max_ld * 2 < (int64_t)0x7fffffff;
-    const bool quarter = dma && sp.quarter;
-#define SMT_WGRAD_DMA(OUT, S_, DST, ACC)                                                                        \
-    do {                                                                                                        \
-        if (quarter && qslots == 5) hipLaunchKernelGGL((wgrad_quarter_kernel<OUT, 5>), qgrid, qblock, 0, stream, gp,  \
-                                        ld_grad_out, xp, ld_x, xbs, T, sp.chunk, S_, n_tiles, tile_rc_dev, order_dev, DST, ACC); \
-        else if (quarter) hipLaunchKernelGGL((wgrad_quarter_kernel<OUT>), qgrid, qblock, 0, stream, gp, ld_grad_out, xp, \
-                                        ld_x, xbs, T, sp.chunk, S_, n_tiles, tile_rc_dev, order_dev, DST, ACC); \
-        else if (slots == 5) hipLaunchKernelGGL((wgrad_dma_kernel<OUT, 5>), grid, block, 0, stream, gp, ld_grad_out, xp, \
-                                           ld_x, xbs, T, sp.chunk, S_, n_tiles, tile_rc_dev, order_dev, DST, ACC); \
-        else hipLaunchKernelGGL((wgrad_dma_kernel<OUT, 4>), grid, block, 0, stream, gp, ld_grad_out, xp, ld_x, xbs,     \
-                                T, sp.chunk, S_, n_tiles, tile_rc_dev, order_dev, DST, ACC);                    \
-    } while (0)
-    if (sp.S == 1) {
-        if (out_dtype == SMT_DTYPE_FP32) {
-            if (dma) SMT_WGRAD_DMA(kOutF32, 1, grad_tiles, accumulate);
-            else hipLaunchKernelGGL(wgrad_partial_kernel<kOutF32>, grid, block, 0, stream, gp, ld_grad_out, xp, ld_x, xbs,
-                                    T, sp.chunk, 1, n_tiles, tile_rc_dev, order_dev, grad_tiles, accumulate);
-        } else {
-            if (dma) SMT_WGRAD_DMA(kOutBF16, 1, grad_tiles, accumulate);
-            else hipLaunchKernelGGL(wgrad_partial_kernel<kOutBF16>, grid, block, 0, stream, gp, ld_grad_out, xp, ld_x, xbs,
-                                    T, sp.chunk, 1, n_tiles, tile_rc_dev, order_dev, grad_tiles, accumulate);
-        }
-        return check_launch("wgrad_partial_kernel");
-    }
-    const size_t need = (size_t)n_tiles * sp.S * kTileElems * sizeof(float);
-    if (!workspace || workspace_bytes < need)
-        return fail(SMT_E_WORKSPACE, "smt_tile_wgrad: workspace %zu < %zu bytes", workspace_bytes, need);
-    if (!aligned16(workspace)) return fail(SMT_E_ALIGN, "smt_tile_wgrad: workspace not 16-byte aligned");
-    float* slab = static_cast<float*>(workspace);
-    if (dma)
-        SMT_WGRAD_DMA(kOutSlab, sp.S, slab, 0);
-    else
-        hipLaunchKernelGGL(wgrad_partial_kernel<kOutSlab>, grid, block, 0, stream, gp, ld_grad_out, xp, ld_x, xbs,
-                           T, sp.chunk, sp.S, n_tiles, tile_rc_dev, order_dev, slab, 0);
-    int rc = check_launch("wgrad_partial_kernel");
-    if (rc) return rc;
-    if (out_dtype == SMT_DTYPE_FP32)
-        hipLaunchKernelGGL(wgrad_reduce_kernel<true>, dim3(n_tiles * 64), dim3(256), 0, stream, slab, sp.S, grad_tiles, accumulate);
-    else
-        hipLaunchKernelGGL(wgrad_reduce_kernel<false>, dim3(n_tiles * 64), dim3(256), 0, stream, slab, sp.S, grad_tiles, accumulate);
-    return check_launch("wgrad_reduce_kernel");
+    return wgrad_launch<false>(mods, T, max_ld, tile_rc_dev, order_dev, n_tiles, out_dtype, workspace, workspace_bytes, stream);
 }
-#undef SMT_WGRAD_DMA
+
+size_t smt_wgrad_batch_workspace_bytes(int64_t T, int32_t n_tiles) { return smt_wgrad_workspace_bytes(T, n_tiles); }
+
+int smt_tile_wgrad_batch(const smt_wgrad_module* modules, int32_t n_modules, int64_t T, const int32_t* tile_tab_dev,
+                         const int32_t* order_dev, int32_t n_tiles, int32_t out_dtype, void* workspace,
+                         size_t workspace_bytes, hipStream_t stream) {
+    static const char* fn = "smt_tile_wgrad_batch";
+    if (n_tiles < 0 || T < 0 || n_modules < 0)
+        return fail(SMT_E_INVALID, "%s: negative size (T=%lld, n_tiles=%d, n_modules=%d)", fn, (long long)T, n_tiles, n_modules);
+    if (n_tiles == 0) return SMT_OK;
+    if (n_modules == 0 || n_modules > SMT_WGRAD_MAX_MODULES || !modules)
+        return fail(SMT_E_INVALID, "%s: %d modules (1..%d)", fn, n_modules, SMT_WGRAD_MAX_MODULES);
+    if (out_dtype != SMT_DTYPE_BF16 && out_dtype != SMT_DTYPE_FP32)
+        return fail(SMT_E_INVALID, "%s: out_dtype %d not supported", fn, out_dtype);
+    if (!tile_tab_dev) return fail(SMT_E_INVALID, "%s: null tile table", fn);
+    if (T == 0) return fail(SMT_E_INVALID, "%s: T = 0 (use smt_tile_wgrad per module)", fn);
+    WgradModules mods{};
+    int64_t max_ld = 0;
+    for (int i = 0; i < n_modules; ++i) {
+        const int rc = check_wgrad_module(fn, modules[i]);
+        if (rc) return rc;
+        mods.m[i] = modules[i];
+        mods.m[i].accumulate = modules[i].accumulate ? 1 : 0;
+        max_ld = std::max(max_ld, std::max(modules[i].ld_grad_out, modules[i].ld_x));
+    }
+    return wgrad_launch<true>(mods, T, max_ld, tile_tab_dev, order_dev, n_tiles, out_dtype, workspace, workspace_bytes, stream);
+}
 
 size_t smt_wgrad_mx_workspace_bytes(int64_t ldq, int32_t n_tiles) {
     if (ldq <= 0 || n_tiles <= 0) return 0;

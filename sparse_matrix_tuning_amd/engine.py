@@ -208,6 +208,9 @@ class _GradSink:
 
     __slots__ = ("buffer", "engine", "group", "buckets", "index")
 
+    def batcher(self) -> Optional["WgradBatcher"]:
+        return self.engine.wgrad_batcher if self.engine is not None else None
+
     def __init__(self, buffer: torch.Tensor, engine: "SMTEngine", group: "_TileGroup" = None,
                  buckets: "TileGradBuckets" = None, index: int = 0):
         self.buffer = buffer
@@ -242,6 +245,64 @@ class _GradSink:
             self.group.reported[self.index] = True
         if self.buckets is not None:
             self.buckets.ready(self.index)
+
+
+class WgradBatcher:
+    """Runs the tile weight gradients of consecutive SMT modules as ONE ``smt_tile_wgrad_batch``
+    launch (bf16 engine path).
+
+    A spread selection gives a module ~8 tiles: alone, its launch needs ~16-way split-K slabs (or
+    quarter tiles) to fill 256 CUs, and runs at half the HBM roofline. ``linearZ.backward`` hands
+    each module's operands here instead; once the pending modules hold ``min_tiles`` tiles (or
+    SMT_WGRAD_MAX_MODULES modules, or the same module comes back), they go out in one launch on the
+    engine's wgrad stream, and only then are they reported to the gradient buckets. A callback queued
+    on the autograd engine flushes what is left when the backward pass ends, so every launch is
+    enqueued before ``backward`` returns. The pending modules' output gradients stay allocated until
+    their launch (a few GB at the 8B point). Results are deterministic: the same modules batch the
+    same way every step (the split over T follows the batch's tile count)."""
+
+    def __init__(self, engine: "SMTEngine", min_tiles: int):
+        self.engine = engine
+        self.min_tiles = int(min_tiles)
+        self.pending: list = []        # (sink, g2, x2, TileIndex, packed, accumulate)
+        self.n_tiles = 0
+        self.callback_queued = False
+        self._tables = {}
+
+    def add(self, sink: "_GradSink", g2: torch.Tensor, x2: torch.Tensor, tiles, packed: bool) -> None:
+        if any(p[0] is sink for p in self.pending):
+            self.flush()                         # a second backward through one module: in order
+        if not self.callback_queued:
+            torch.autograd.Variable._execution_engine.queue_callback(self._end_of_backward)
+            self.callback_queued = True
+        self.pending.append((sink, g2, x2, tiles, bool(packed), sink.take_accumulate()))
+        self.n_tiles += len(tiles)
+        if self.n_tiles >= self.min_tiles or len(self.pending) >= _hip.WGRAD_MAX_MODULES:
+            self.flush()
+
+    def _end_of_backward(self) -> None:
+        self.callback_queued = False
+        self.flush()
+
+    def flush(self) -> None:
+        if not self.pending:
+            return
+        pending, self.pending, self.n_tiles = self.pending, [], 0
+        dev = pending[0][1].device
+        key = tuple((id(p[3]), p[4]) for p in pending) + (dev.index,)
+        tabs = self._tables.get(key)
+        if tabs is None:
+            if len(self._tables) >= 1024:
+                self._tables.clear()
+            tabs = _hip.wgrad_batch_table([p[3].kernel_tiles(p[4]) for p in pending], dev)
+            # hold the TileIndex objects: the key uses their ids
+            self._tables[key] = tabs = (tabs, [p[3] for p in pending])
+        (tab, order), _ = tabs
+        items = [(p[1], p[2], p[0].buffer, p[5]) for p in pending]
+        keep = [t for p in pending for t in (p[1], p[2])]
+        pending[0][0].run(lambda: _hip.tile_wgrad_batch(items, tab, order), *keep)
+        for p in pending:
+            p[0].mark_ready()
 
 
 class TileGradBuckets:
@@ -515,6 +576,10 @@ class SMTEngine:
         # every collective over the tile buffer and at the end of backward
         self.wgrad_stream = (torch.cuda.Stream(self.device) if self.tile_groups and self.device.type == "cuda"
                              and cfg.get("overlap_wgrad", True) else None)
+        # tile gradients of consecutive modules in one launch (wgrad_batch_tiles <= 0: one per module)
+        batch_tiles = int(cfg.get("wgrad_batch_tiles", 48))
+        self.wgrad_batcher = (WgradBatcher(self, batch_tiles) if self.tile_groups and batch_tiles > 0
+                              and self.device.type == "cuda" else None)
         for tg in self.tile_groups:
             if tg.buckets is not None:
                 tg.buckets.side_stream = self.wgrad_stream
@@ -559,6 +624,9 @@ class SMTEngine:
             if self.dense_buckets is not None:
                 self.dense_buckets.arm()
         loss.backward()
+        if self.wgrad_batcher is not None:
+            self.wgrad_batcher.callback_queued = False
+            self.wgrad_batcher.flush()          # (the end-of-backward callback already did, normally)
         if self.wgrad_stream is not None:
             torch.cuda.current_stream(self.device).wait_stream(self.wgrad_stream)
         if boundary:
@@ -662,6 +730,9 @@ class SMTEngine:
         if self.dense_buckets is not None:
             self.dense_buckets.remove()
             self.dense_buckets = None
+        if self.wgrad_batcher is not None:
+            self.wgrad_batcher.flush()
+            self.wgrad_batcher = None
         for tg in self.tile_groups:
             for m in tg.modules:
                 if hasattr(m.selected_weight, "_smt_grad_sink"):

@@ -121,6 +121,20 @@ class TileIndex:
             self._dev[key] = t
         return t
 
+    def kernel_tiles(self, packed: bool) -> List[Tuple[int, int]]:
+        """The ``(row_block, col_block)`` list as the wgrad kernel addresses the input: for the
+        block-major packed input of ``colblock_gather`` the column block is its position there."""
+        key = ("ktiles", packed)
+        t = self._dev.get(key)
+        if t is None:
+            if packed:
+                pos = {c: i for i, c in enumerate(self.column_blocks())}
+                t = [(r, pos[c]) for r, c in self.index_list]
+            else:
+                t = list(self.index_list)
+            self._dev[key] = t
+        return t
+
     def block_tables(self, device: torch.device):
         """Device int32 tables of the distinct row blocks and column blocks the tiles touch."""
         key = ("blocks", device.type, device.index)
@@ -346,7 +360,11 @@ class linearZ(torch.autograd.Function):
             else:
                 x2, table = _rows_ready(saved.reshape(-1, weight.shape[1])), tiles.device_table(dev)
             sink = ctx.sink
-            if sink is not None:
+            if sink is not None and sink.batcher() is not None:
+                # the engine launches this module's tiles together with those of the modules whose
+                # backward runs next (one smt_tile_wgrad_batch launch, deterministic)
+                sink.batcher().add(sink, g2, x2, tiles, ctx.packed)
+            elif sink is not None:
                 acc, order = sink.take_accumulate(), tiles.schedule(dev)
                 sink.run(lambda: _hip.tile_wgrad(g2, x2, table, sink.buffer, accumulate=acc, order=order), g2, x2)
                 sink.mark_ready()

@@ -1,0 +1,198 @@
+"""Batched tile weight gradient (``smt_tile_wgrad_batch``): the tiles of several SMT modules that
+share T in one launch, as the engine's WgradBatcher issues them in backward.
+
+Each module's tiles must equal what ``smt_tile_wgrad`` computes for that module (smt.py:397-404):
+- bit-exact where the split is the same (one module in the batch, or modules that are column
+  slices of one operand pair, so the batch IS one module's tile list);
+- otherwise against fp64 truth at the fp32 sink bar (1e-5), since the split over T follows the
+  batch's tile count.
+Shapes: LLaMA-3-8B modules at the bench's T = 32768 (q, k, gate, down; packed and row-major inputs;
+quarter-tile, slab and direct paths), plus the engine end to end against the unbatched engine.
+"""
+import pytest
+import torch
+
+from sparse_matrix_tuning_amd import _hip
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+T = 32768
+SHAPES = {"q_proj": (4096, 4096), "k_proj": (1024, 4096), "gate_proj": (14336, 4096), "down_proj": (4096, 14336)}
+
+
+def _rel(a, b):
+    return ((a.double() - b.double()).norm() / b.double().norm()).item()
+
+
+def _tiles(out_f, in_f, n, seed):
+    rb, cb = out_f // 256, in_f // 256
+    g = torch.Generator().manual_seed(seed)
+    flat = torch.randperm(rb * cb, generator=g)[:n].tolist()
+    return [(f // cb, f % cb) for f in flat]
+
+
+def _operands(out_f, in_f, seed, t=T):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    x = torch.randn(t, in_f, generator=g, device=DEV).bfloat16()
+    go = (torch.randn(t, out_f, generator=g, device=DEV) * 1e-2).bfloat16()
+    return go, x
+
+
+def _truth(go, x, r, c):
+    return go[:, r * 256:(r + 1) * 256].double().t() @ x[:, c * 256:(c + 1) * 256].double()
+
+
+def _packed(x, tiles):
+    cbs = []
+    for _r, c in tiles:
+        if c not in cbs:
+            cbs.append(c)
+    xp = _hip.colblock_gather(x, torch.tensor(cbs, dtype=torch.int32, device=DEV))
+    pos = {c: i for i, c in enumerate(cbs)}
+    return xp, [(r, pos[c]) for r, c in tiles]
+
+
+@pytest.mark.parametrize("n", [5, 27, 300])
+@pytest.mark.parametrize("out_dtype", [torch.bfloat16, torch.float32])
+def test_single_module_batch_bit_exact(n, out_dtype):
+    """A batch of one module runs the same kernels with the same split as smt_tile_wgrad."""
+    out_f, in_f = SHAPES["gate_proj"]
+    go, x = _operands(out_f, in_f, seed=n)
+    tiles = _tiles(out_f, in_f, n, seed=n)
+    ref = torch.empty(n * 256, 256, dtype=out_dtype, device=DEV)
+    _hip.tile_wgrad(go, x, _hip.tile_table(tiles, DEV), ref, order=_hip.order_table(tiles, DEV))
+    out = torch.empty_like(ref)
+    tab, order = _hip.wgrad_batch_table([tiles], DEV)
+    _hip.tile_wgrad_batch([(go, x, out, False)], tab, order)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+
+
+def test_batch_of_slices_equals_one_module():
+    """Modules that read one (g, x) pair: the batch equals smt_tile_wgrad over their concatenated
+    tile list bit for bit, whatever the order the schedule visits them in."""
+    out_f, in_f = SHAPES["q_proj"]
+    go, x = _operands(out_f, in_f, seed=3)
+    tiles = _tiles(out_f, in_f, 36, seed=3)
+    parts = [tiles[:9], tiles[9:17], tiles[17:30], tiles[30:]]
+    ref = torch.empty(36 * 256, 256, dtype=torch.float32, device=DEV)
+    _hip.tile_wgrad(go, x, _hip.tile_table(tiles, DEV), ref)
+    outs = [torch.empty(len(p) * 256, 256, dtype=torch.float32, device=DEV) for p in parts]
+    tab, order = _hip.wgrad_batch_table(parts, DEV)
+    _hip.tile_wgrad_batch([(go, x, o, False) for o in outs], tab, order)
+    torch.cuda.synchronize()
+    assert torch.equal(torch.cat(outs), ref)
+
+
+@pytest.mark.parametrize("total", [8, 24, 48])
+def test_mixed_modules_vs_fp64(total):
+    """q, k, gate (row-major input) and down (packed block-major input) in one launch, with
+    accumulation on two of them, fp32 outputs: every tile within 1e-5 of fp64 truth."""
+    per = {"q_proj": total // 4, "k_proj": total // 4, "gate_proj": total // 4, "down_proj": total - 3 * (total // 4)}
+    items, tile_lists, checks = [], [], []
+    for k, (name, n) in enumerate(per.items()):
+        out_f, in_f = SHAPES[name]
+        go, x = _operands(out_f, in_f, seed=10 + k)
+        tiles = _tiles(out_f, in_f, n, seed=20 + k)
+        acc = k % 2 == 1
+        out = (torch.randn(n * 256, 256, device=DEV) * 1e-3) if acc else torch.empty(n * 256, 256, device=DEV)
+        prior = out.clone()
+        if name == "down_proj":
+            xk, ktiles = _packed(x, tiles)
+        else:
+            xk, ktiles = x, tiles
+        items.append((go, xk, out, acc))
+        tile_lists.append(ktiles)
+        checks.append((go, x, tiles, out, prior, acc))
+    tab, order = _hip.wgrad_batch_table(tile_lists, DEV)
+    _hip.tile_wgrad_batch(items, tab, order)
+    torch.cuda.synchronize()
+    for go, x, tiles, out, prior, acc in checks:
+        for i in (0, len(tiles) // 2, len(tiles) - 1):
+            r, c = tiles[i]
+            truth = _truth(go, x, r, c) + (prior[i * 256:(i + 1) * 256].double() if acc else 0)
+            err = _rel(out[i * 256:(i + 1) * 256], truth)
+            assert err < 1e-5, (r, c, acc, err)
+
+
+def test_batch_rejects_bad_arguments():
+    go, x = _operands(1024, 1024, seed=1, t=512)
+    out = torch.empty(256, 256, device=DEV)
+    tab, order = _hip.wgrad_batch_table([[(0, 0)]], DEV)
+    with pytest.raises(ValueError):
+        _hip.tile_wgrad_batch([(go, x, out, False)], tab.view(-1)[:2].view(1, 2), None)
+    with pytest.raises(ValueError):
+        _hip.tile_wgrad_batch([(go, x, out, False)] * (_hip.WGRAD_MAX_MODULES + 1), tab, order)
+    go2, _ = _operands(1024, 1024, seed=2, t=256)
+    with pytest.raises(ValueError):          # modules with different T
+        _hip.tile_wgrad_batch([(go, x, out, False), (go2, x, out, False)], tab, order)
+
+
+def _mini_engine(batch_tiles, seed=0):
+    from sparse_matrix_tuning_amd import engine as eng
+    from sparse_matrix_tuning_amd.smt import smt
+
+    torch.manual_seed(seed)
+    layers = torch.nn.ModuleList()
+    for _ in range(3):
+        layers.append(torch.nn.ModuleDict({
+            "q_proj": torch.nn.Linear(1024, 1024, bias=False),
+            "k_proj": torch.nn.Linear(1024, 512, bias=False),
+            "up_proj": torch.nn.Linear(1024, 2048, bias=False),
+            "down_proj": torch.nn.Linear(2048, 1024, bias=False)}))
+    model = torch.nn.Module()
+    model.layers = layers
+    model = model.to(DEV).bfloat16()
+    sel = {}
+    for li, layer in enumerate(model.layers):
+        for name, lin in layer.items():
+            rb, cb = lin.weight.shape[0] // 256, lin.weight.shape[1] // 256
+            sel[f"layers.{li}.{name}"] = _tiles(rb * 256, cb * 256, min(3 + li, rb * cb), seed=li * 7 + len(name))
+    for name, tl in sel.items():
+        smt._replace(model, name, tl)
+    params = [m.selected_weight for m in model.modules() if isinstance(m, smt.LinearLayer_MatrixSparsity)]
+    opt = eng.SMTFusedAdam(params, lr=1e-3)
+    engine, *_ = eng.initialize(model=model, optimizer=opt,
+                                config={"gradient_clipping": 1.0, "wgrad_batch_tiles": batch_tiles})
+
+    def fwd(x):
+        for layer in model.layers:
+            h = layer["q_proj"](x) + torch.nn.functional.pad(layer["k_proj"](x), (0, 512))
+            x = x + layer["down_proj"](torch.nn.functional.silu(layer["up_proj"](h)))
+        return x
+    return engine, fwd
+
+
+def test_engine_batched_equals_unbatched():
+    """The engine with batched tile launches gives the same tile gradients (fp32, within the sink
+    bar) and, through the same AdamW, the same tiles as one launch per module; two steps."""
+    x = torch.randn(4, 512, 1024, device=DEV).bfloat16()
+    res = {}
+    for bt in (0, 10, 48):
+        engine, fwd = _mini_engine(bt)
+        for _ in range(2):
+            loss = fwd(x).float().pow(2).mean()
+            engine.backward(loss)
+            grads = [tg.grad.clone() for tg in engine.tile_groups]
+            engine.step()
+        res[bt] = (grads, [tg.master.clone() for tg in engine.tile_groups])
+    for bt in (10, 48):
+        for a, b in zip(res[bt][0], res[0][0]):
+            assert _rel(a, b) < 1e-6
+        for a, b in zip(res[bt][1], res[0][1]):
+            assert _rel(a, b) < 1e-6
+    assert engine.wgrad_batcher is not None and not engine.wgrad_batcher.pending
+
+
+def test_engine_batcher_module_used_twice():
+    """A module whose backward runs twice in one pass accumulates (the batcher launches the first
+    use before queueing the second)."""
+    x = torch.randn(2, 256, 1024, device=DEV).bfloat16()
+    out = {}
+    for bt in (0, 48):
+        engine, _fwd = _mini_engine(bt, seed=1)
+        q = engine.module.layers[0]["q_proj"]
+        loss = (q(q(x)).float().pow(2).mean())
+        engine.backward(loss)
+        out[bt] = engine.tile_groups[0].grad.clone()
+    assert _rel(out[48], out[0]) < 1e-6
