@@ -24,9 +24,11 @@ One process per GPU (RCCL over xGMI for N > 1, weak scaling: B=16 x S=2048 per G
    The reference's memory policy (per-layer recompute) is then timed over as many steps
    (``grad_ckpt_mode``).
 
-Rank 0 prints ONE JSON line. ``roofline`` is for the dominant hand-written kernel (the grouped
-tile-wgrad, smt_tile_wgrad = wgrad_dma + wgrad_reduce), timed with HIP events on its launch
-stream over the timed region, against the MFMA roof (its HBM rate on counter bytes beside it).
+Rank 0 prints ONE JSON line. ``roofline`` is for the dominant hand-written kernel (the tile
+wgrad: smt_tile_wgrad_batch / smt_tile_wgrad = wgrad_dma | wgrad_quarter + wgrad_reduce), timed
+with HIP events on its launch stream over extra steps with the wgrad stream joined (the kernel
+alone); its algorithmic bytes count each distinct operand slice of a launch once, and the roof
+(HBM or MFMA) follows the launch's intensity on those bytes; counter bytes beside it.
 ``cpu_baseline`` times the oracle's restatement of the reference path (oracle/smt_oracle.py) on this
 host's cores for BASELINE.md's four units, each beside the same unit on the GPU.
 """
