@@ -203,6 +203,27 @@ def install_wgrad_batch_timer(timer: WgradTimer):
     _hip.tile_wgrad_batch = timed
 
 
+def install_mx_wgrad_batch_timer(timer: WgradTimer):
+    """The engine's batched MX launches (smt_tile_wgrad_mx_batch; the quantisation of the output
+    gradients is a launch of its own, as on the per-module path)."""
+    from sparse_matrix_tuning_amd import _hip
+    orig = _hip.tile_wgrad_mx_batch
+
+    def timed(items, tab, order=None):
+        n_slices = None
+        if timer.enabled:
+            keys, rows = set(), timer.host_rows(tab)
+            for m, (g, x, _out, _acc) in enumerate(items):
+                for mm, r, c, _k in rows:
+                    if mm == m:
+                        keys.add((g.q.data_ptr(), r))
+                        keys.add((x.q.data_ptr(), c))
+            n_slices = len(keys)
+        return timer.hook(items[0][0].ldq, tab.shape[0], items[0][2].element_size(),
+                          lambda: orig(items, tab, order), operand_bytes=1, slices=n_slices)
+    _hip.tile_wgrad_mx_batch = timed
+
+
 def install_mx_wgrad_timer(timer: WgradTimer):
     """The fp8 path's smt_tile_wgrad_mx (1-byte operands; T = the MX blocks' padded rows)."""
     from sparse_matrix_tuning_amd import _hip
@@ -677,6 +698,7 @@ def main():
     install_wgrad_batch_timer(timer)
     mx_timer = WgradTimer()
     install_mx_wgrad_timer(mx_timer)
+    install_mx_wgrad_batch_timer(mx_timer)
     atimer = AttnTimer()
     if not (args.eager_ops or args.sdpa_attention):
         install_attn_timer(atimer)

@@ -26,7 +26,8 @@
  *                         (deepspeed/fine_tune.py:352,361-363,773; DeepSpeed 0.16.5, external),
  *                         fused with clip, bf16 cast and the tile -> W scatter
  *   smt_mx_quant_cols,    MX-fp8 (e4m3 + e8m0 per 32 tokens) column blocks and the tile weight
- *   smt_tile_wgrad_mx     gradient over them (config 5's fp8 tiles; no reference counterpart)
+ *   smt_tile_wgrad_mx     gradient over them (config 5's fp8 tiles; no reference counterpart);
+ *   smt_tile_wgrad_mx_batch  the same for several modules in one launch (ABI v6)
  *   smt_adamw_multi       the same step over many dense parameters in one launch (the warm-up
  *                         full fine-tune's FusedAdam multi_tensor_apply, fine_tune.py:352-363)
  *   Channel path (activation-selected rows; SURVEY §8(f) row 1, ABI v3):
@@ -265,6 +266,27 @@ int smt_tile_wgrad_mx(const void* qg, const void* sg, const void* qx, const void
                       const int32_t* tile_rc_dev, const int32_t* order_dev, int32_t n_tiles, void* grad_tiles,
                       int32_t out_dtype, int32_t accumulate, void* workspace, size_t workspace_bytes,
                       hipStream_t stream);
+
+/* One module of a batched MX tile wgrad: its MX blocks of g and x and its output. */
+typedef struct smt_wgrad_mx_module {
+    const void* qg;                 /* MX row blocks of the output gradient (e4m3 panels)          */
+    const void* sg;                 /* their e8m0 exponents                                         */
+    const void* qx;                 /* MX column blocks of the input                                */
+    const void* sx;
+    void* grad_tiles;               /* this module's [n_m*256, 256] output of out_dtype            */
+    int32_t accumulate;
+    int32_t reserved;
+} smt_wgrad_mx_module;              /* 48 bytes                                                     */
+
+/*
+ * smt_tile_wgrad_mx over up to SMT_WGRAD_MAX_MODULES modules sharing ldq in one launch (as
+ * smt_tile_wgrad_batch: HOST module array, device int32 [n_tiles][4] table of (module, index into
+ * the module's g blocks, index into its x blocks, tile index in its output)). Workspace:
+ * smt_wgrad_mx_workspace_bytes(ldq, n_tiles) over all tiles.
+ */
+int smt_tile_wgrad_mx_batch(const smt_wgrad_mx_module* modules, int32_t n_modules, int64_t ldq,
+                            const int32_t* tile_tab_dev, const int32_t* order_dev, int32_t n_tiles,
+                            int32_t out_dtype, void* workspace, size_t workspace_bytes, hipStream_t stream);
 
 /* ---- channel path (ABI v3) ------------------------------------------------------------------- */
 

@@ -32,7 +32,7 @@ ABI_FUNCTIONS = (
     "smt_tile_wgrad_batch", "smt_colblock_gather", "smt_tile_scatter_t",
     "smt_tile_gather", "smt_tile_scatter", "smt_grad_accumulate", "smt_block_score",
     "smt_sq_norm", "smt_adamw_step", "smt_adamw_multi",
-    "smt_mx_quant_cols", "smt_wgrad_mx_workspace_bytes", "smt_tile_wgrad_mx",
+    "smt_mx_quant_cols", "smt_wgrad_mx_workspace_bytes", "smt_tile_wgrad_mx", "smt_tile_wgrad_mx_batch",
     "smt_row_gather", "smt_row_scatter", "smt_column_gather", "smt_act_accumulate",
     "smt_channel_score_workspace_bytes", "smt_channel_score",
     "smt_model_ops_last_error", "smt_rmsnorm_fwd", "smt_rmsnorm_bwd_waves", "smt_rmsnorm_bwd",
@@ -56,6 +56,12 @@ class WgradModule(ctypes.Structure):
     _fields_ = [("grad_out", ctypes.c_void_p), ("x", ctypes.c_void_p), ("ld_grad_out", ctypes.c_int64),
                 ("ld_x", ctypes.c_int64), ("x_block_stride", ctypes.c_int64), ("grad_tiles", ctypes.c_void_p),
                 ("accumulate", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class WgradMxModule(ctypes.Structure):
+    """smt_wgrad_mx_module (include/smt_hip.h): one module of a batched MX tile wgrad."""
+    _fields_ = [("qg", ctypes.c_void_p), ("sg", ctypes.c_void_p), ("qx", ctypes.c_void_p), ("sx", ctypes.c_void_p),
+                ("grad_tiles", ctypes.c_void_p), ("accumulate", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 WGRAD_MAX_MODULES = 16
@@ -129,6 +135,7 @@ _SIGS = {
     "smt_mx_quant_cols": (ctypes.c_int, [_P, _I64, _I64, _P, _I32, _I64, _P, _P, _P]),
     "smt_wgrad_mx_workspace_bytes": (_SZ, [_I64, _I32]),
     "smt_tile_wgrad_mx": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _P, _I32, _P, _I32, _I32, _P, _SZ, _P]),
+    "smt_tile_wgrad_mx_batch": (ctypes.c_int, [ctypes.POINTER(WgradMxModule), _I32, _I64, _P, _P, _I32, _I32, _P, _SZ, _P]),
     "smt_row_gather": (ctypes.c_int, [_P, _I64, _I32, _I64, _P, _I32, _P, _I64, _P]),
     "smt_row_scatter": (ctypes.c_int, [_P, _I64, _I32, _I64, _P, _I32, _P, _I64, _P]),
     "smt_column_gather": (ctypes.c_int, [_P, _I64, _I64, _I64, _P, _I32, _P, _I64, _P]),
@@ -437,6 +444,36 @@ def tile_wgrad_mx(g: MxBlocks, x: MxBlocks, tile_rc: torch.Tensor, out: torch.Te
                                   ws_bytes, _stream(dev))
     _check(rc, "smt_tile_wgrad_mx")
     return out
+
+
+def tile_wgrad_mx_batch(items: Sequence[tuple], tile_tab: torch.Tensor, order: Optional[torch.Tensor] = None) -> None:
+    """One launch of the MX tile weight gradients of several modules (``smt_tile_wgrad_mx_batch``):
+    ``items`` per module ``(g: MxBlocks, x: MxBlocks, out, accumulate)`` as :func:`tile_wgrad_mx`,
+    all with the same ldq; ``tile_tab`` int32 [n, 4] of (module, block of its g, block of its x,
+    tile index in its output), e.g. :func:`wgrad_batch_table` over the modules' mx tables."""
+    if not items:
+        return
+    if len(items) > WGRAD_MAX_MODULES:
+        raise ValueError(f"tile_wgrad_mx_batch: {len(items)} modules > {WGRAD_MAX_MODULES}")
+    dev = _require_device(tile_tab, order, *[t for g, x, out, _a in items for t in (g.q, x.q, out)])
+    ldq, out_dtype = items[0][0].ldq, items[0][2].dtype
+    mods = (WgradMxModule * len(items))()
+    for i, (g, x, out, acc) in enumerate(items):
+        if g.ldq != ldq or x.ldq != ldq or g.T != x.T:
+            raise ValueError("tile_wgrad_mx_batch: every module's MX blocks must cover the same rows")
+        if out.dtype != out_dtype or out.dtype not in (torch.bfloat16, torch.float32) or not out.is_contiguous():
+            raise ValueError("tile_wgrad_mx_batch: outputs must be contiguous and all bf16 or all fp32")
+        mods[i] = WgradMxModule(_ptr(g.q), _ptr(g.scales), _ptr(x.q), _ptr(x.scales), _ptr(out), int(bool(acc)), 0)
+    if tile_tab.dtype != torch.int32 or tile_tab.dim() != 2 or tile_tab.shape[1] != 4:
+        raise ValueError("tile_wgrad_mx_batch: tile_tab must be int32 [n, 4]")
+    n = tile_tab.shape[0]
+    if order is not None and (order.dtype != torch.int32 or order.numel() != n):
+        raise ValueError("tile_wgrad_mx_batch: order must be int32 [n_tiles]")
+    ws_bytes = int(load().smt_wgrad_mx_workspace_bytes(ldq, n))
+    ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=dev)
+    rc = load().smt_tile_wgrad_mx_batch(mods, len(items), ldq, _ptr(tile_tab), _ptr(order), n, _DT[out_dtype],
+                                        _ptr(ws), ws_bytes, _stream(dev))
+    _check(rc, "smt_tile_wgrad_mx_batch")
 
 
 def tile_gather(weight: torch.Tensor, tile_rc: torch.Tensor, out: torch.Tensor) -> torch.Tensor:

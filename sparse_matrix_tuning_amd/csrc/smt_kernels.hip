@@ -147,6 +147,7 @@ __device__ __forceinline__ void wgrad_store(f32x16_t (&acc)[4][2], void* __restr
 // to SMT_WGRAD_MAX_MODULES modules that share T (BATCH = true: int32 [n][4] table of (module,
 // row_block, col_block, tile index in that module's output)). Everything here is workgroup-uniform.
 struct WgradModules { smt_wgrad_module m[SMT_WGRAD_MAX_MODULES]; };
+struct WgradMxModules { smt_wgrad_mx_module m[SMT_WGRAD_MAX_MODULES]; };   // the MX-fp8 kernels
 
 struct WgradTile {
     const uint16_t* g;       // grad_out column slice r: element (t, j) at g[t * ldg + j]
@@ -673,6 +674,19 @@ void wgrad_reduce_kernel(const float* __restrict__ slab, int S, void* __restrict
                                accumulate);
 }
 
+// the same over an MX batch
+template <bool OUT_F32>
+__global__ __launch_bounds__(256)
+void wgrad_reduce_mx_batch_kernel(const float* __restrict__ slab, int S, const WgradMxModules mods,
+                                  const int32_t* __restrict__ tile_tab) {
+    const int tile = blockIdx.x >> 6;
+    const int m = tile_tab[4 * tile];
+    const int ti = tile_tab[4 * tile + 3];
+    wgrad_reduce_tile<OUT_F32>(slab, S, tile,
+                               static_cast<uint8_t*>(mods.m[m].grad_tiles) + (int64_t)ti * kTileElems * (OUT_F32 ? 4 : 2),
+                               mods.m[m].accumulate);
+}
+
 // the same over a batch: each tile's output and accumulate flag from its module (wgrad_tile)
 template <bool OUT_F32>
 __global__ __launch_bounds__(256)
@@ -812,12 +826,40 @@ __device__ __forceinline__ i32x8_t mx_frag(const uint8_t* img, int row, int h) {
     return f;
 }
 
-template <int OUT>
+// One tile of an MX wgrad launch (one module, or a batch: as WgradTile). The operands are the
+// module's MX row blocks of g (qa/sa, block r) and column blocks of x (qb/sb, block c).
+
+struct WgradMxTile {
+    const uint8_t *qa, *sa, *qb, *sb;    // this tile's blocks
+    void* out;
+    int accumulate;
+};
+
+template <bool BATCH, int OUT_BYTES>
+__device__ __forceinline__ WgradMxTile wgrad_mx_tile(const WgradMxModules& mods, const int32_t* __restrict__ tab,
+                                                     int tile, int64_t ldq) {
+    int mi = 0, r, c, ti;
+    if (BATCH) {
+        mi = tab[4 * tile]; r = tab[4 * tile + 1]; c = tab[4 * tile + 2]; ti = tab[4 * tile + 3];
+    } else {
+        r = tab[2 * tile]; c = tab[2 * tile + 1]; ti = tile;
+    }
+    const smt_wgrad_mx_module& m = mods.m[mi];
+    const int64_t blk_bytes = (int64_t)kTile * ldq, sc_bytes = (ldq >> 5) * kTile;
+    WgradMxTile t;
+    t.qa = static_cast<const uint8_t*>(m.qg) + r * blk_bytes;
+    t.sa = static_cast<const uint8_t*>(m.sg) + r * sc_bytes;
+    t.qb = static_cast<const uint8_t*>(m.qx) + c * blk_bytes;
+    t.sb = static_cast<const uint8_t*>(m.sx) + c * sc_bytes;
+    t.out = static_cast<uint8_t*>(m.grad_tiles) + (int64_t)ti * kTileElems * OUT_BYTES;
+    t.accumulate = m.accumulate;
+    return t;
+}
+
+template <int OUT, bool BATCH>
 __global__ __launch_bounds__(kWgThreads, 1)
-void wgrad_mx_kernel(const uint8_t* __restrict__ qa, const uint8_t* __restrict__ sa,
-                     const uint8_t* __restrict__ qb, const uint8_t* __restrict__ sb, int64_t ldq,
-                     int64_t chunk, int S, int n_tiles, const int32_t* __restrict__ tile_rc,
-                     const int32_t* __restrict__ order, void* __restrict__ out_ptr, int accumulate) {
+void wgrad_mx_kernel(const WgradMxModules mods, int64_t ldq, int64_t chunk, int S, int n_tiles,
+                     const int32_t* __restrict__ tile_tab, const int32_t* __restrict__ order, float* __restrict__ slab) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kMxSlots * kMxSlotBytes];   // 132 KiB, one array
 
     const int total = n_tiles * S;
@@ -827,18 +869,17 @@ void wgrad_mx_kernel(const uint8_t* __restrict__ qa, const uint8_t* __restrict__
     const int s = L / n_tiles;
     const int li = L - s * n_tiles;
     const int tile = order != nullptr ? order[li] : li;
-    const int r = tile_rc[2 * tile];
-    const int c = tile_rc[2 * tile + 1];
+    const WgradMxTile tt = wgrad_mx_tile<BATCH, OUT == kOutBF16 ? 2 : 4>(mods, tile_tab, tile, ldq);
     const int64_t t_begin = (int64_t)s * chunk;
     const int64_t t_end = (t_begin + chunk < ldq) ? (t_begin + chunk) : ldq;
     const int nst = (t_end > t_begin) ? (int)((t_end - t_begin) / kMxBK) : 0;   // ldq, chunk % 64 == 0
 
     const int64_t blk_bytes = (int64_t)kTile * ldq;       // = (ldq / 64) panels of 16 KiB
     const int64_t sc_bytes = (ldq >> 5) * kTile;
-    const __amdgpu_buffer_rsrc_t rqa = uniform_rsrc(qa + r * blk_bytes + t_begin * kTile, blk_bytes - t_begin * kTile);
-    const __amdgpu_buffer_rsrc_t rqb = uniform_rsrc(qb + c * blk_bytes + t_begin * kTile, blk_bytes - t_begin * kTile);
-    const __amdgpu_buffer_rsrc_t rsa = uniform_rsrc(sa + r * sc_bytes + (t_begin >> 5) * kTile, sc_bytes - (t_begin >> 5) * kTile);
-    const __amdgpu_buffer_rsrc_t rsb = uniform_rsrc(sb + c * sc_bytes + (t_begin >> 5) * kTile, sc_bytes - (t_begin >> 5) * kTile);
+    const __amdgpu_buffer_rsrc_t rqa = uniform_rsrc(tt.qa + t_begin * kTile, blk_bytes - t_begin * kTile);
+    const __amdgpu_buffer_rsrc_t rqb = uniform_rsrc(tt.qb + t_begin * kTile, blk_bytes - t_begin * kTile);
+    const __amdgpu_buffer_rsrc_t rsa = uniform_rsrc(tt.sa + (t_begin >> 5) * kTile, sc_bytes - (t_begin >> 5) * kTile);
+    const __amdgpu_buffer_rsrc_t rsb = uniform_rsrc(tt.sb + (t_begin >> 5) * kTile, sc_bytes - (t_begin >> 5) * kTile);
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -923,7 +964,7 @@ void wgrad_mx_kernel(const uint8_t* __restrict__ qa, const uint8_t* __restrict__
                 acc[mb][nb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af[mb], bfr[nb], acc[mb][nb],
                                                                                0, 0, 0, as[mb], 0, bs[nb]);
     }
-    wgrad_store<OUT>(acc, wgrad_dst<OUT>(out_ptr, tile, s, S), wm, wn, lane, accumulate);
+    wgrad_store<OUT>(acc, OUT == kOutSlab ? wgrad_dst<kOutSlab>(slab, tile, s, S) : tt.out, wm, wn, lane, tt.accumulate);
 }
 
 // Quarter-tile MX variant for modules with few tiles (the fill-bound regime, as wgrad_quarter_kernel):
@@ -934,12 +975,11 @@ void wgrad_mx_kernel(const uint8_t* __restrict__ qa, const uint8_t* __restrict__
 constexpr int kMxQImg = 128 * kMxBK;                        // 8 KiB per operand per stage
 constexpr int kMxQSlotBytes = 2 * kMxQImg + 2 * 256;
 
-template <int OUT>
+template <int OUT, bool BATCH>
 __global__ __launch_bounds__(kQThreads, 2)
-void wgrad_mx_quarter_kernel(const uint8_t* __restrict__ qa, const uint8_t* __restrict__ sa,
-                             const uint8_t* __restrict__ qb, const uint8_t* __restrict__ sb, int64_t ldq,
-                             int64_t chunk, int S, int n_tiles, const int32_t* __restrict__ tile_rc,
-                             const int32_t* __restrict__ order, void* __restrict__ out_ptr, int accumulate) {
+void wgrad_mx_quarter_kernel(const WgradMxModules mods, int64_t ldq, int64_t chunk, int S, int n_tiles,
+                             const int32_t* __restrict__ tile_tab, const int32_t* __restrict__ order,
+                             float* __restrict__ slab) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kMxSlots * kMxQSlotBytes];  // 66 KiB, one array
 
     const int total = n_tiles * S * 4;
@@ -952,8 +992,7 @@ void wgrad_mx_quarter_kernel(const uint8_t* __restrict__ qa, const uint8_t* __re
     const int li = ts - s * n_tiles;
     const int tile = order != nullptr ? order[li] : li;
     const int qm = qd >> 1, qn = qd & 1;
-    const int r = tile_rc[2 * tile];
-    const int c = tile_rc[2 * tile + 1];
+    const WgradMxTile tt = wgrad_mx_tile<BATCH, OUT == kOutBF16 ? 2 : 4>(mods, tile_tab, tile, ldq);
     const int64_t t_begin = (int64_t)s * chunk;
     const int64_t t_end = (t_begin + chunk < ldq) ? (t_begin + chunk) : ldq;
     const int nst = (t_end > t_begin) ? (int)((t_end - t_begin) / kMxBK) : 0;
@@ -961,12 +1000,12 @@ void wgrad_mx_quarter_kernel(const uint8_t* __restrict__ qa, const uint8_t* __re
     const int64_t blk_bytes = (int64_t)kTile * ldq;
     const int64_t sc_bytes = (ldq >> 5) * kTile;
     // this quarter's 128 rows of the A / B blocks
-    const __amdgpu_buffer_rsrc_t rqa = uniform_rsrc(qa + r * blk_bytes + t_begin * kTile + qm * 128 * kMxBK,
+    const __amdgpu_buffer_rsrc_t rqa = uniform_rsrc(tt.qa + t_begin * kTile + qm * 128 * kMxBK,
                                                     blk_bytes - t_begin * kTile - qm * 128 * kMxBK);
-    const __amdgpu_buffer_rsrc_t rqb = uniform_rsrc(qb + c * blk_bytes + t_begin * kTile + qn * 128 * kMxBK,
+    const __amdgpu_buffer_rsrc_t rqb = uniform_rsrc(tt.qb + t_begin * kTile + qn * 128 * kMxBK,
                                                     blk_bytes - t_begin * kTile - qn * 128 * kMxBK);
-    const __amdgpu_buffer_rsrc_t rsa = uniform_rsrc(sa + r * sc_bytes + (t_begin >> 5) * kTile, sc_bytes - (t_begin >> 5) * kTile);
-    const __amdgpu_buffer_rsrc_t rsb = uniform_rsrc(sb + c * sc_bytes + (t_begin >> 5) * kTile, sc_bytes - (t_begin >> 5) * kTile);
+    const __amdgpu_buffer_rsrc_t rsa = uniform_rsrc(tt.sa + (t_begin >> 5) * kTile, sc_bytes - (t_begin >> 5) * kTile);
+    const __amdgpu_buffer_rsrc_t rsb = uniform_rsrc(tt.sb + (t_begin >> 5) * kTile, sc_bytes - (t_begin >> 5) * kTile);
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1050,8 +1089,8 @@ void wgrad_mx_quarter_kernel(const uint8_t* __restrict__ qa, const uint8_t* __re
                 acc[mb][nb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af[mb], bfr[nb], acc[mb][nb],
                                                                                0, 0, 0, as[mb], 0, bs[nb]);
     }
-    wgrad_store_q<OUT>(acc, wgrad_dst<OUT>(out_ptr, tile, s, S), qm * 128 + wm * 64, qn * 128 + wn * 64, lane,
-                       accumulate);
+    wgrad_store_q<OUT>(acc, OUT == kOutSlab ? wgrad_dst<kOutSlab>(slab, tile, s, S) : tt.out,
+                       qm * 128 + wm * 64, qn * 128 + wn * 64, lane, tt.accumulate);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1849,6 +1888,67 @@ int smt_mx_quant_cols(const void* x, int64_t ld_x, int64_t T, const int32_t* blo
     return check_launch("mx_quant_cols_kernel");
 }
 
+}  // extern "C"
+
+namespace {
+
+template <bool BATCH>
+int wgrad_mx_launch(const WgradMxModules& mods, int64_t ldq, const int32_t* tab, const int32_t* order, int32_t n_tiles,
+                    int32_t out_dtype, void* workspace, size_t workspace_bytes, hipStream_t stream) {
+    const WgradSplit sp = wgrad_split(ldq, n_tiles, true, 512.0);
+    const dim3 grid(n_tiles * sp.S), block(kWgThreads);
+    const dim3 qgrid(n_tiles * sp.S * 4), qblock(kQThreads);
+    float* slab = nullptr;
+    if (sp.S > 1) {
+        const size_t need = (size_t)n_tiles * sp.S * kTileElems * sizeof(float);
+        if (!workspace || workspace_bytes < need)
+            return fail(SMT_E_WORKSPACE, "smt_tile_wgrad_mx: workspace %zu < %zu bytes", workspace_bytes, need);
+        if (!aligned16(workspace)) return fail(SMT_E_ALIGN, "smt_tile_wgrad_mx: workspace not 16-byte aligned");
+        slab = static_cast<float*>(workspace);
+    }
+#define SMT_WGRAD_MX(OUT)                                                                                       \
+    do {                                                                                                        \
+        if (sp.quarter) hipLaunchKernelGGL((wgrad_mx_quarter_kernel<OUT, BATCH>), qgrid, qblock, 0, stream, mods, ldq, \
+                                           sp.chunk, sp.S, n_tiles, tab, order, slab);                          \
+        else hipLaunchKernelGGL((wgrad_mx_kernel<OUT, BATCH>), grid, block, 0, stream, mods, ldq, sp.chunk, sp.S,     \
+                                n_tiles, tab, order, slab);                                                     \
+    } while (0)
+    if (sp.S == 1) {
+        if (out_dtype == SMT_DTYPE_FP32) SMT_WGRAD_MX(kOutF32);
+        else SMT_WGRAD_MX(kOutBF16);
+        return check_launch("wgrad_mx_kernel");
+    }
+    SMT_WGRAD_MX(kOutSlab);
+#undef SMT_WGRAD_MX
+    int rc = check_launch("wgrad_mx_kernel");
+    if (rc) return rc;
+    const dim3 rgrid(n_tiles * 64), rblock(256);
+    if (BATCH) {
+        if (out_dtype == SMT_DTYPE_FP32)
+            hipLaunchKernelGGL(wgrad_reduce_mx_batch_kernel<true>, rgrid, rblock, 0, stream, slab, sp.S, mods, tab);
+        else
+            hipLaunchKernelGGL(wgrad_reduce_mx_batch_kernel<false>, rgrid, rblock, 0, stream, slab, sp.S, mods, tab);
+    } else {
+        const smt_wgrad_mx_module& m = mods.m[0];
+        if (out_dtype == SMT_DTYPE_FP32)
+            hipLaunchKernelGGL(wgrad_reduce_kernel<true>, rgrid, rblock, 0, stream, slab, sp.S, m.grad_tiles, m.accumulate);
+        else
+            hipLaunchKernelGGL(wgrad_reduce_kernel<false>, rgrid, rblock, 0, stream, slab, sp.S, m.grad_tiles, m.accumulate);
+    }
+    return check_launch("wgrad_reduce_kernel");
+}
+
+int check_mx_module(const char* fn, const smt_wgrad_mx_module& m) {
+    if (!m.qg || !m.sg || !m.qx || !m.sx || !m.grad_tiles) return fail(SMT_E_INVALID, "%s: null operand or output", fn);
+    if (!aligned16(m.qg) || !aligned16(m.qx) || !aligned16(m.sg) || !aligned16(m.sx) || !aligned16(m.grad_tiles))
+        return fail(SMT_E_ALIGN, "%s: operands / output not 16-byte aligned", fn);
+    return SMT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
 int smt_tile_wgrad_mx(const void* qg, const void* sg, const void* qx, const void* sx, int64_t ldq,
                       const int32_t* tile_rc_dev, const int32_t* order_dev, int32_t n_tiles, void* grad_tiles,
                       int32_t out_dtype, int32_t accumulate, void* workspace, size_t workspace_bytes,
@@ -1870,37 +1970,32 @@ int smt_tile_wgrad_mx(const void* qg, const void* sg, const void* qx, const void
     if (!aligned16(qg) || !aligned16(qx) || !aligned16(sg) || !aligned16(sx))
         return fail(SMT_E_ALIGN, "smt_tile_wgrad_mx: operands not 16-byte aligned");
     if ((int64_t)kTile * ldq >= (int64_t)0x7fffffff) return fail(SMT_E_INVALID, "smt_tile_wgrad_mx: T too large for 32-bit offsets");
-    const WgradSplit sp = wgrad_split(ldq, n_tiles, true, 512.0);
-    const uint8_t *a = static_cast<const uint8_t*>(qg), *as = static_cast<const uint8_t*>(sg);
-    const uint8_t *b = static_cast<const uint8_t*>(qx), *bs = static_cast<const uint8_t*>(sx);
-    const dim3 grid(n_tiles * sp.S), block(kWgThreads);
-    const dim3 qgrid(n_tiles * sp.S * 4), qblock(kQThreads);
-#define SMT_WGRAD_MX(OUT, S_, DST, ACC)                                                                         \
-    do {                                                                                                        \
-        if (sp.quarter) hipLaunchKernelGGL((wgrad_mx_quarter_kernel<OUT>), qgrid, qblock, 0, stream, a, as, b, bs,  \
-                                           ldq, sp.chunk, S_, n_tiles, tile_rc_dev, order_dev, DST, ACC);       \
-        else hipLaunchKernelGGL((wgrad_mx_kernel<OUT>), grid, block, 0, stream, a, as, b, bs, ldq, sp.chunk, S_,    \
-                                n_tiles, tile_rc_dev, order_dev, DST, ACC);                                     \
-    } while (0)
-    if (sp.S == 1) {
-        if (out_dtype == SMT_DTYPE_FP32) SMT_WGRAD_MX(kOutF32, 1, grad_tiles, accumulate);
-        else SMT_WGRAD_MX(kOutBF16, 1, grad_tiles, accumulate);
-        return check_launch("wgrad_mx_kernel");
+    WgradMxModules mods{};
+    mods.m[0] = smt_wgrad_mx_module{qg, sg, qx, sx, grad_tiles, accumulate ? 1 : 0, 0};
+    return wgrad_mx_launch<false>(mods, ldq, tile_rc_dev, order_dev, n_tiles, out_dtype, workspace, workspace_bytes, stream);
+}
+
+int smt_tile_wgrad_mx_batch(const smt_wgrad_mx_module* modules, int32_t n_modules, int64_t ldq,
+                            const int32_t* tile_tab_dev, const int32_t* order_dev, int32_t n_tiles,
+                            int32_t out_dtype, void* workspace, size_t workspace_bytes, hipStream_t stream) {
+    static const char* fn = "smt_tile_wgrad_mx_batch";
+    if (n_tiles < 0 || ldq < 0 || n_modules < 0) return fail(SMT_E_INVALID, "%s: negative size", fn);
+    if (n_tiles == 0) return SMT_OK;
+    if (n_modules == 0 || n_modules > SMT_WGRAD_MAX_MODULES || !modules)
+        return fail(SMT_E_INVALID, "%s: %d modules (1..%d)", fn, n_modules, SMT_WGRAD_MAX_MODULES);
+    if (ldq <= 0 || ldq % 64) return fail(SMT_E_INVALID, "%s: ldq %lld (a positive multiple of 64)", fn, (long long)ldq);
+    if ((int64_t)kTile * ldq >= (int64_t)0x7fffffff) return fail(SMT_E_INVALID, "%s: T too large for 32-bit offsets", fn);
+    if (out_dtype != SMT_DTYPE_BF16 && out_dtype != SMT_DTYPE_FP32)
+        return fail(SMT_E_INVALID, "%s: out_dtype %d not supported", fn, out_dtype);
+    if (!tile_tab_dev) return fail(SMT_E_INVALID, "%s: null tile table", fn);
+    WgradMxModules mods{};
+    for (int i = 0; i < n_modules; ++i) {
+        const int rc = check_mx_module(fn, modules[i]);
+        if (rc) return rc;
+        mods.m[i] = modules[i];
+        mods.m[i].accumulate = modules[i].accumulate ? 1 : 0;
     }
-    const size_t need = (size_t)n_tiles * sp.S * kTileElems * sizeof(float);
-    if (!workspace || workspace_bytes < need)
-        return fail(SMT_E_WORKSPACE, "smt_tile_wgrad_mx: workspace %zu < %zu bytes", workspace_bytes, need);
-    if (!aligned16(workspace)) return fail(SMT_E_ALIGN, "smt_tile_wgrad_mx: workspace not 16-byte aligned");
-    float* slab = static_cast<float*>(workspace);
-    SMT_WGRAD_MX(kOutSlab, sp.S, slab, 0);
-#undef SMT_WGRAD_MX
-    int rc = check_launch("wgrad_mx_kernel");
-    if (rc) return rc;
-    if (out_dtype == SMT_DTYPE_FP32)
-        hipLaunchKernelGGL(wgrad_reduce_kernel<true>, dim3(n_tiles * 64), dim3(256), 0, stream, slab, sp.S, grad_tiles, accumulate);
-    else
-        hipLaunchKernelGGL(wgrad_reduce_kernel<false>, dim3(n_tiles * 64), dim3(256), 0, stream, slab, sp.S, grad_tiles, accumulate);
-    return check_launch("wgrad_reduce_kernel");
+    return wgrad_mx_launch<true>(mods, ldq, tile_tab_dev, order_dev, n_tiles, out_dtype, workspace, workspace_bytes, stream);
 }
 
 static int tile_copy(bool scatter, void* weight, int64_t ld_weight, int32_t elem_bytes, const int32_t* tile_rc_dev,

@@ -249,7 +249,8 @@ class _GradSink:
 
 class WgradBatcher:
     """Runs the tile weight gradients of consecutive SMT modules as ONE ``smt_tile_wgrad_batch``
-    launch (bf16 engine path).
+    launch (bf16 operands) or ``smt_tile_wgrad_mx_batch`` launch (the fp8 path's MX operands; the
+    output gradients are quantised into their MX row blocks just before it).
 
     A spread selection gives a module ~8 tiles: alone, its launch needs ~16-way split-K slabs (or
     quarter tiles) to fill 256 CUs, and runs at half the HBM roofline. ``linearZ.backward`` hands
@@ -270,13 +271,23 @@ class WgradBatcher:
         self._tables = {}
 
     def add(self, sink: "_GradSink", g2: torch.Tensor, x2: torch.Tensor, tiles, packed: bool) -> None:
-        if any(p[0] is sink for p in self.pending):
+        """bf16 path: ``g2`` the output gradient [T, out], ``x2`` the saved input (row-major, or the
+        block-major packed copy when ``packed``)."""
+        self._add(sink, "bf16", (g2, x2, tiles, bool(packed)), (g2, x2), len(tiles))
+
+    def add_mx(self, sink: "_GradSink", g2: torch.Tensor, rb_dev: torch.Tensor, mx, tiles) -> None:
+        """fp8 path: ``g2`` is quantised into its MX row blocks ``rb_dev`` at launch time; ``mx`` is
+        the input's MX column blocks saved by the forward."""
+        self._add(sink, "mx", (g2, rb_dev, mx, tiles), (g2, mx.q, mx.scales), len(tiles))
+
+    def _add(self, sink, kind, args, keep, n) -> None:
+        if any(p[0] is sink for p in self.pending) or (self.pending and self.pending[0][1] != kind):
             self.flush()                         # a second backward through one module: in order
         if not self.callback_queued:
             torch.autograd.Variable._execution_engine.queue_callback(self._end_of_backward)
             self.callback_queued = True
-        self.pending.append((sink, g2, x2, tiles, bool(packed), sink.take_accumulate()))
-        self.n_tiles += len(tiles)
+        self.pending.append((sink, kind, args, keep, sink.take_accumulate()))
+        self.n_tiles += n
         if self.n_tiles >= self.min_tiles or len(self.pending) >= _hip.WGRAD_MAX_MODULES:
             self.flush()
 
@@ -288,19 +299,31 @@ class WgradBatcher:
         if not self.pending:
             return
         pending, self.pending, self.n_tiles = self.pending, [], 0
-        dev = pending[0][1].device
-        key = tuple((id(p[3]), p[4]) for p in pending) + (dev.index,)
+        kind = pending[0][1]
+        dev = pending[0][2][0].device
+        if kind == "bf16":
+            key = ("bf16", dev.index) + tuple((id(p[2][2]), p[2][3]) for p in pending)
+            ktiles = lambda: [p[2][2].kernel_tiles(p[2][3]) for p in pending]
+        else:
+            key = ("mx", dev.index) + tuple(id(p[2][3]) for p in pending)
+            ktiles = lambda: [p[2][3].mx_kernel_tiles() for p in pending]
         tabs = self._tables.get(key)
         if tabs is None:
             if len(self._tables) >= 1024:
                 self._tables.clear()
-            tabs = _hip.wgrad_batch_table([p[3].kernel_tiles(p[4]) for p in pending], dev)
             # hold the TileIndex objects: the key uses their ids
-            self._tables[key] = tabs = (tabs, [p[3] for p in pending])
+            tabs = self._tables[key] = (_hip.wgrad_batch_table(ktiles(), dev), [p[2] for p in pending])
         (tab, order), _ = tabs
-        items = [(p[1], p[2], p[0].buffer, p[5]) for p in pending]
-        keep = [t for p in pending for t in (p[1], p[2])]
-        pending[0][0].run(lambda: _hip.tile_wgrad_batch(items, tab, order), *keep)
+        keep = [t for p in pending for t in p[3]]
+        if kind == "bf16":
+            items = [(p[2][0], p[2][1], p[0].buffer, p[4]) for p in pending]
+            launch = lambda: _hip.tile_wgrad_batch(items, tab, order)
+        else:
+            def launch():
+                items = [(_hip.mx_quant_cols(g2, rb), mx, p[0].buffer, p[4])
+                         for p, (g2, rb, mx, _t) in ((p, p[2]) for p in pending)]
+                _hip.tile_wgrad_mx_batch(items, tab, order)
+        pending[0][0].run(launch, *keep)
         for p in pending:
             p[0].mark_ready()
 

@@ -135,6 +135,17 @@ class TileIndex:
             self._dev[key] = t
         return t
 
+    def mx_kernel_tiles(self) -> List[Tuple[int, int]]:
+        """Host ``(row-block position, column-block position)`` list of :meth:`mx_tables`."""
+        t = self._dev.get("mx_ktiles")
+        if t is None:
+            rbs = {}
+            for r, _c in self.index_list:
+                rbs.setdefault(r, len(rbs))
+            pos = {c: i for i, c in enumerate(self.column_blocks())}
+            t = self._dev["mx_ktiles"] = [(rbs[r], pos[c]) for r, c in self.index_list]
+        return t
+
     def block_tables(self, device: torch.device):
         """Device int32 tables of the distinct row blocks and column blocks the tiles touch."""
         key = ("blocks", device.type, device.index)
@@ -339,7 +350,11 @@ class linearZ(torch.autograd.Function):
             g2 = _rows_ready(grad_output.reshape(-1, weight.shape[0]))
             rb_dev, _cb, table = tiles.mx_tables(g2.device)
             sink = ctx.sink
-            if sink is not None:
+            if sink is not None and sink.batcher() is not None:
+                # quantised and launched with the modules whose backward runs next (one
+                # smt_tile_wgrad_mx_batch launch)
+                sink.batcher().add_mx(sink, g2, rb_dev, ctx.mx, tiles)
+            elif sink is not None:
                 acc, mx, order = sink.take_accumulate(), ctx.mx, tiles.schedule(g2.device)
                 sink.run(lambda: _hip.tile_wgrad_mx(_hip.mx_quant_cols(g2, rb_dev), mx, table, sink.buffer,
                                                     accumulate=acc, order=order),

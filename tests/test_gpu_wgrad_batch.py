@@ -196,3 +196,92 @@ def test_engine_batcher_module_used_twice():
         engine.backward(loss)
         out[bt] = engine.tile_groups[0].grad.clone()
     assert _rel(out[48], out[0]) < 1e-6
+
+
+# ---- MX-fp8 operands (config 5) -----------------------------------------------------------------
+def _mx_module(out_f, in_f, n, seed, t=T):
+    go, x = _operands(out_f, in_f, seed, t)
+    tiles = _tiles(out_f, in_f, n, seed)
+    rbs, cbs = [], []
+    for r, c in tiles:
+        if r not in rbs:
+            rbs.append(r)
+        if c not in cbs:
+            cbs.append(c)
+    gq = _hip.mx_quant_cols(go, torch.tensor(rbs, dtype=torch.int32, device=DEV))
+    xq = _hip.mx_quant_cols(x, torch.tensor(cbs, dtype=torch.int32, device=DEV))
+    ktiles = [(rbs.index(r), cbs.index(c)) for r, c in tiles]
+    return gq, xq, ktiles
+
+
+@pytest.mark.parametrize("n", [6, 40])
+def test_mx_single_module_batch_bit_exact(n):
+    gq, xq, kt = _mx_module(*SHAPES["gate_proj"], n, seed=n)
+    ref = torch.empty(n * 256, 256, device=DEV)
+    _hip.tile_wgrad_mx(gq, xq, _hip.tile_table(kt, DEV), ref, order=_hip.order_table(kt, DEV))
+    out = torch.empty_like(ref)
+    tab, order = _hip.wgrad_batch_table([kt], DEV)
+    _hip.tile_wgrad_mx_batch([(gq, xq, out, False)], tab, order)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("total", [8, 44])
+def test_mx_mixed_modules_vs_per_module(total):
+    """q, k, gate, down MX operands in one launch (two of them accumulating): each module's tiles
+    equal its own smt_tile_wgrad_mx launch to fp32 rounding (1e-5; only the split over T differs)."""
+    per = {"q_proj": total // 4, "k_proj": total // 4, "gate_proj": total // 4, "down_proj": total - 3 * (total // 4)}
+    items, kts, refs = [], [], []
+    for k, (name, n) in enumerate(per.items()):
+        gq, xq, kt = _mx_module(*SHAPES[name], n, seed=30 + k)
+        acc = k % 2 == 0
+        prior = torch.randn(n * 256, 256, device=DEV) * 1e-3
+        ref = prior.clone()
+        _hip.tile_wgrad_mx(gq, xq, _hip.tile_table(kt, DEV), ref, accumulate=acc)
+        out = prior.clone()
+        items.append((gq, xq, out, acc))
+        kts.append(kt)
+        refs.append(ref)
+    tab, order = _hip.wgrad_batch_table(kts, DEV)
+    _hip.tile_wgrad_mx_batch(items, tab, order)
+    torch.cuda.synchronize()
+    for (_g, _x, out, _a), ref in zip(items, refs):
+        assert _rel(out, ref) < 1e-5
+
+
+def test_engine_fp8_batched_equals_unbatched():
+    """The fp8 engine (MX tile wgrad) with batched launches: the same tile gradients as one launch
+    per module (fp32 rounding), over two steps of the mini LLaMA."""
+    import bench
+    from collections import defaultdict
+    from sparse_matrix_tuning_amd.engine import SMTFusedAdam, initialize
+    from sparse_matrix_tuning_amd.smt import smt
+
+    def run(bt):
+        cfg = dict(bench.MODELS["mini"], num_hidden_layers=2)
+        bench.MODELS["_b"] = cfg
+        try:
+            model = bench.build_model("_b", DEV)
+        finally:
+            del bench.MODELS["_b"]
+        sel_mlp = defaultdict(list, {("up_proj", 1): [(2, 1), (0, 0)], ("down_proj", 0): [(1, 0), (0, 1)],
+                                     ("gate_proj", 1): [(1, 1)]})
+        sel_att = defaultdict(list, {("q_proj", 0): [(1, 1)], ("k_proj", 1): [(0, 0)], ("v_proj", 1): [(0, 1)]})
+        smt.freeze_unselected_matrix_layer(model, sel_mlp, sel_att)
+        smt.convert_linear_layer_to_matrix_sparsity(model, sel_mlp, sel_att)
+        opt = SMTFusedAdam(smt.get_optimizer_sparse_grouped_parameters(model, 0.0, 1e-3), lr=1e-3, betas=(0.9, 0.95))
+        engine, *_ = initialize(model=model, optimizer=opt, config={"gradient_clipping": 1.0, "fp8_linears": True,
+                                                                    "wgrad_batch_tiles": bt})
+        ids = torch.randint(0, 4096, (2, 256), generator=torch.Generator().manual_seed(0)).to(DEV)
+        grads = []
+        for _ in range(2):
+            loss = engine(input_ids=ids, labels=ids, use_cache=False).loss
+            engine.backward(loss)
+            grads.append([tg.grad.clone() for tg in engine.tile_groups])
+            engine.step()
+        return grads
+
+    a, b = run(0), run(48)
+    for ga, gb in zip(a, b):
+        for x, y in zip(ga, gb):
+            assert _rel(y, x) < 1e-5
