@@ -230,8 +230,13 @@ def install_mx_wgrad_timer(timer: WgradTimer):
     orig = _hip.tile_wgrad_mx
 
     def timed(g, x, rc, out, accumulate=False, order=None):
+        n_slices = None
+        if timer.enabled:
+            rows = timer.host_rows(rc)
+            n_slices = len({r for r, _c in rows}) + len({c for _r, c in rows})
         return timer.hook(g.ldq, rc.shape[0], out.element_size(),
-                          lambda: orig(g, x, rc, out, accumulate=accumulate, order=order), operand_bytes=1)
+                          lambda: orig(g, x, rc, out, accumulate=accumulate, order=order), operand_bytes=1,
+                          slices=n_slices)
     _hip.tile_wgrad_mx = timed
 
 
