@@ -38,6 +38,8 @@
  *                         accumulator `feat[key] (+)= |x|` over steps)
  *   smt_channel_score     deepspeed/smt/smt_helper.py:167-184   per-channel statistic (batch sum of
  *                         smt_helper.py:170, then the sequence reduction) in fp64
+ *   smt_channel_mean_aten deepspeed/smt/smt_helper.py:167-176   the mean statistic in ATen's own CPU
+ *                         summation order (bit-identical values; ABI v6)
  */
 #ifndef SMT_HIP_H
 #define SMT_HIP_H
@@ -326,6 +328,18 @@ int smt_act_accumulate(const void* x, int32_t x_dtype, int64_t ld_x, int64_t bat
 size_t smt_channel_score_workspace_bytes(int32_t S, int32_t n_cols);
 int smt_channel_score(const float* acc, int32_t B, int32_t S, int32_t n_cols, int32_t strategy, double* partials,
                       size_t partial_bytes, double* out, hipStream_t stream);
+
+/*
+ * The mean_abs / abs_mean channel statistic of smt_helper.py:167-176 with the reference's own fp32
+ * rounding: out[c] = torch.mean(torch.sum(act.abs(), dim=0).abs(), dim=0)[c] as ATen's CPU kernels
+ * compute it (cascade_sum: 4 accumulator levels of 2^p rows, p = max(4, ceil_log2(n)/4), per output
+ * column; then div_ by S), for a contiguous fp32 [B, S, n_cols] accumulator (ABI v6). The caller
+ * confirms it against the reference expression on the host once per shape. Workspace:
+ * smt_channel_mean_aten_workspace_bytes(S, n_cols) bytes of fp32 chunk sums.
+ */
+size_t smt_channel_mean_aten_workspace_bytes(int32_t S, int32_t n_cols);
+int smt_channel_mean_aten(const float* acc, int32_t B, int32_t S, int32_t n_cols, float* workspace,
+                          size_t workspace_bytes, float* out, hipStream_t stream);
 
 #ifdef __cplusplus
 }

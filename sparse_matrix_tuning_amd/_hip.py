@@ -35,6 +35,7 @@ ABI_FUNCTIONS = (
     "smt_mx_quant_cols", "smt_wgrad_mx_workspace_bytes", "smt_tile_wgrad_mx", "smt_tile_wgrad_mx_batch",
     "smt_row_gather", "smt_row_scatter", "smt_column_gather", "smt_act_accumulate",
     "smt_channel_score_workspace_bytes", "smt_channel_score",
+    "smt_channel_mean_aten_workspace_bytes", "smt_channel_mean_aten",
     "smt_model_ops_last_error", "smt_rmsnorm_fwd", "smt_rmsnorm_bwd_waves", "smt_rmsnorm_bwd",
     "smt_add_rmsnorm_fwd", "smt_rmsnorm_bwd_add",
     "smt_rope_fwd", "smt_rope_bwd", "smt_swiglu_fwd", "smt_swiglu_bwd", "smt_ce_fwd", "smt_ce_bwd",
@@ -142,6 +143,8 @@ _SIGS = {
     "smt_act_accumulate": (ctypes.c_int, [_P, _I32, _I64, _I64, _I32, _I32, _I32, _P, _I32, _P]),
     "smt_channel_score_workspace_bytes": (_SZ, [_I32, _I32]),
     "smt_channel_score": (ctypes.c_int, [_P, _I32, _I32, _I32, _I32, _P, _SZ, _P, _P]),
+    "smt_channel_mean_aten_workspace_bytes": (_SZ, [_I32, _I32]),
+    "smt_channel_mean_aten": (ctypes.c_int, [_P, _I32, _I32, _I32, _P, _SZ, _P, _P]),
     "smt_attn_last_error": (ctypes.c_char_p, []),
     "smt_attn_fwd": (ctypes.c_int, [ctypes.POINTER(AttnTensor)] * 4 + [_P, ctypes.POINTER(AttnShape), _P]),
     "smt_attn_bwd": (ctypes.c_int, [ctypes.POINTER(AttnTensor)] * 5 + [_P, _P] + [ctypes.POINTER(AttnTensor)] * 3
@@ -689,6 +692,21 @@ def act_accumulate(x3d: torch.Tensor, acc: torch.Tensor, assign: bool) -> None:
     rc = load().smt_act_accumulate(_ptr(x3d), _DT[x3d.dtype], x3d.stride(1), x3d.stride(0), B, S, C, _ptr(acc),
                                    int(bool(assign)), _stream(dev))
     _check(rc, "smt_act_accumulate")
+
+
+def channel_mean_aten(acc: torch.Tensor) -> torch.Tensor:
+    """fp32 [C]: torch.mean(torch.sum(acc.abs(), 0).abs(), 0) in ATen's CPU summation order
+    (``smt_channel_mean_aten``) for a contiguous fp32 [B, S, C] accumulator."""
+    dev = _require_device(acc)
+    if acc.dtype != torch.float32 or not acc.is_contiguous() or acc.dim() != 3:
+        raise ValueError("channel_mean_aten: contiguous fp32 [B, S, C] accumulator expected")
+    B, S, C = acc.shape
+    out = torch.empty(C, dtype=torch.float32, device=dev)
+    ws_bytes = int(load().smt_channel_mean_aten_workspace_bytes(S, C))
+    ws = torch.empty(max(ws_bytes // 4, 4), dtype=torch.float32, device=dev)
+    rc = load().smt_channel_mean_aten(_ptr(acc), B, S, C, _ptr(ws), ws_bytes, _ptr(out), _stream(dev))
+    _check(rc, "smt_channel_mean_aten")
+    return out
 
 
 def channel_scores(acc: torch.Tensor, strategy: int) -> torch.Tensor:

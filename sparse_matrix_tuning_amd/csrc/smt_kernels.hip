@@ -1656,6 +1656,95 @@ void channel_final_kernel(const double* __restrict__ partials, int32_t P, int32_
 // n = 27 -> S = 9 (243 workgroups, one round); n = 436 -> S = 4 (7 rounds of T/4 instead of 2 rounds
 // of T). S == 1: the tile is written straight from the accumulators.
 constexpr int kCUs = 256;
+// ------------------------------------------------------------------------------------------------
+// Channel mean in ATen's CPU summation order (smt_helper.py:167-176 as the reference computes it:
+// torch.sum(act.abs(), dim=0) then torch.mean(., dim=0), i.e. sum then div_ by S on the CPU).
+// Both are outer reductions of a contiguous fp32 tensor, which ATen's cascade_sum (SumKernel.cpp,
+// multi_row_sum) computes per output column with 4 accumulator levels of 2^p rows,
+// p = max(4, ceil_log2(n) / 4): rows are added one by one into level 0 from 0.0f; after every full
+// chunk of 2^p rows level j-1 is added into level j and cleared, climbing while the row count is a
+// multiple of 2^(p*j); the tail rows go into level 0; finally level 0 += level 1, += level 2,
+// += level 3. Each output column is reduced by one thread in that order whatever the thread count
+// (parallel_dim_reduction splits the columns). The host checks the result against the reference
+// expression once per shape before trusting it (smt_helper.channel_scores_exact).
+// Pass 1: one thread per (chunk of the S reduction, column): the chunk's row sum, each row value
+// itself the cascade over B. Pass 2: one thread per column replays the levels over the chunks.
+// ------------------------------------------------------------------------------------------------
+__host__ __device__ inline int cascade_level_power(int64_t n) {
+    int lg = 0;
+    while (((int64_t)1 << lg) < n) ++lg;                  // ceil_log2 (0 for n <= 1)
+    return (lg / 4) > 4 ? (lg / 4) : 4;
+}
+
+// the cascade of ATen over n strided values (fp32, no contraction: additions only)
+__device__ __forceinline__ float cascade_sum_strided(const float* __restrict__ p, int64_t stride, int64_t n, int lp,
+                                                     bool absval) {
+    const int64_t step = (int64_t)1 << lp;
+    const int64_t mask = step - 1;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    int64_t i = 0;
+    while (i + step <= n) {
+        for (int64_t j = 0; j < step; ++j, ++i) {
+            const float v = p[i * stride];
+            acc[0] = __fadd_rn(acc[0], absval ? fabsf(v) : v);
+        }
+        for (int j = 1; j < 4; ++j) {
+            acc[j] = __fadd_rn(acc[j], acc[j - 1]);
+            acc[j - 1] = 0.f;
+            if ((i & (mask << (j * lp))) != 0) break;
+        }
+    }
+    for (; i < n; ++i) {
+        const float v = p[i * stride];
+        acc[0] = __fadd_rn(acc[0], absval ? fabsf(v) : v);
+    }
+    for (int j = 1; j < 4; ++j) acc[0] = __fadd_rn(acc[0], acc[j]);
+    return acc[0];
+}
+
+// pass 1: chunk q < n_full of the S reduction is rows [q*2^lpS, (q+1)*2^lpS); chunk n_full is the tail
+__global__ __launch_bounds__(256)
+void channel_aten_chunks_kernel(const float* __restrict__ acc, int B, int S, int C, int lpS, int lpB,
+                                float* __restrict__ chunks) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= C) return;
+    const int q = blockIdx.y;
+    const int64_t step = (int64_t)1 << lpS;
+    const int64_t r0 = (int64_t)q * step;
+    const int64_t r1 = r0 + step < S ? r0 + step : S;
+    const int64_t bs = (int64_t)S * C;
+    float sum = 0.f;
+    for (int64_t r = r0; r < r1; ++r) {
+        const float v = cascade_sum_strided(acc + r * C + c, bs, B, lpB, true);   // torch.sum(act.abs(), 0)
+        sum = __fadd_rn(sum, v);                           // .abs() of a non-negative sum: the same value
+    }
+    chunks[(int64_t)q * C + c] = sum;
+}
+
+// pass 2: the level replay over the chunks, then the mean's division by S
+__global__ __launch_bounds__(256)
+void channel_aten_levels_kernel(const float* __restrict__ chunks, int S, int C, int lpS, float* __restrict__ out) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= C) return;
+    const int64_t step = (int64_t)1 << lpS;
+    const int64_t mask = step - 1;
+    const int64_t n_full = S / step;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    int64_t i = 0;
+    for (int64_t q = 0; q < n_full; ++q) {
+        i += step;
+        acc[0] = chunks[q * C + c];                        // the chunk summed from 0.0f into level 0
+        for (int j = 1; j < 4; ++j) {
+            acc[j] = __fadd_rn(acc[j], acc[j - 1]);
+            acc[j - 1] = 0.f;
+            if ((i & (mask << (j * lpS))) != 0) break;
+        }
+    }
+    if (S % step) acc[0] = chunks[n_full * C + c];         // the tail rows, from 0.0f
+    for (int j = 1; j < 4; ++j) acc[0] = __fadd_rn(acc[0], acc[j]);
+    out[c] = __fdiv_rn(acc[0], (float)S);                  // sum(...).div_(S)
+}
+
 struct WgradSplit { int S; int64_t chunk; bool quarter; };
 
 // Quarter-tile kernel for modules with at most this many tiles (SMT_WGRAD_QUARTER_MAX; 0 disables).
@@ -2247,6 +2336,30 @@ int smt_channel_score(const float* acc, int32_t B, int32_t S, int32_t n_cols, in
     if (rc) return rc;
     hipLaunchKernelGGL(channel_final_kernel, dim3((n_cols + 255) / 256), dim3(256), 0, stream, partials, P, n_cols, out);
     return check_launch("channel_final_kernel");
+}
+
+size_t smt_channel_mean_aten_workspace_bytes(int32_t S, int32_t n_cols) {
+    if (S <= 0 || n_cols <= 0) return 0;
+    const int64_t step = (int64_t)1 << cascade_level_power(S);
+    return (size_t)(S / step + 1) * (size_t)n_cols * sizeof(float);
+}
+
+int smt_channel_mean_aten(const float* acc, int32_t B, int32_t S, int32_t n_cols, float* workspace,
+                          size_t workspace_bytes, float* out, hipStream_t stream) {
+    static const char* fn = "smt_channel_mean_aten";
+    if (B <= 0 || S <= 0 || n_cols <= 0) return fail(SMT_E_INVALID, "%s: sizes must be positive", fn);
+    if (!acc || !out || !workspace) return fail(SMT_E_INVALID, "%s: null pointer", fn);
+    const size_t need = smt_channel_mean_aten_workspace_bytes(S, n_cols);
+    if (workspace_bytes < need) return fail(SMT_E_WORKSPACE, "%s: workspace %zu < %zu bytes", fn, workspace_bytes, need);
+    const int lpS = cascade_level_power(S), lpB = cascade_level_power(B);
+    const int64_t n_chunks = S / ((int64_t)1 << lpS) + ((S % ((int64_t)1 << lpS)) ? 1 : 0);
+    if (n_chunks > 65535) return fail(SMT_E_INVALID, "%s: S too large", fn);
+    const dim3 g1((n_cols + 255) / 256, (unsigned)n_chunks), g2((n_cols + 255) / 256);
+    hipLaunchKernelGGL(channel_aten_chunks_kernel, g1, dim3(256), 0, stream, acc, B, S, n_cols, lpS, lpB, workspace);
+    int rc = check_launch("channel_aten_chunks_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(channel_aten_levels_kernel, g2, dim3(256), 0, stream, workspace, S, n_cols, lpS, out);
+    return check_launch("channel_aten_levels_kernel");
 }
 
 }  // extern "C"

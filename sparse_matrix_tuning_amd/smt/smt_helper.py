@@ -344,8 +344,84 @@ def reference_channel_stat(act: torch.Tensor, strategy: str) -> np.ndarray:
     return s.numpy().reshape(-1)
 
 
+# Whether ATen's value of a channel equals its value computed over just the channel's aligned
+# 256-channel window of the [B, S, in] state: checked once per strategy and process against the whole
+# key (as _ROW_SLICE_OK for blocks). On this host ATen's outer reductions agree on windows of >= 32
+# aligned channels and differ on arbitrary column subsets, so a window, never a gather, is re-scored.
+_CHANNEL_WINDOW = 256
+_CHANNEL_WINDOW_OK: Dict[str, bool] = {}
+
+
+def channel_rescorer(src: torch.Tensor, strategy: str):
+    """``rescore(flat)`` for the channel keys: the reference's values (reference_channel_stat) of the
+    aligned 256-channel windows holding the requested channels, 1/(in/256) of the key's bytes to copy
+    and reduce each; the whole key when a window is partial, when more than a quarter of the key's
+    windows are asked for, from the third call on one key, or when the window check failed."""
+    C = src.shape[2]
+    W = _CHANNEL_WINDOW
+
+    def window(w):
+        return reference_channel_stat(src[:, :, w * W:(w + 1) * W].contiguous(), strategy)
+
+    calls = [0]
+
+    def rescore(flat):
+        wins = np.unique(np.asarray(flat, dtype=np.int64) // W)
+        calls[0] += 1
+        # a partial last window, or a key the ranking keeps coming back to (the order of its selected
+        # channels is a chain of close values): the whole key at once, in one copy
+        if (C % W and int(wins[-1]) == C // W) or calls[0] > 2 or 4 * wins.size > -(-C // W):
+            return np.arange(C), reference_channel_stat(src, strategy)
+        ok = _CHANNEL_WINDOW_OK.get(strategy)
+        if ok is None:
+            full = reference_channel_stat(src, strategy)
+            w0 = int(wins[0])
+            ok = _CHANNEL_WINDOW_OK[strategy] = bool(np.array_equal(window(w0), full[w0 * W:(w0 + 1) * W]))
+            if not ok:
+                return np.arange(C), full
+        if not ok:
+            return np.arange(C), reference_channel_stat(src, strategy)
+        covered, vals = [], []
+        for w in wins:
+            w = int(w)
+            covered.append(np.arange(w * W, (w + 1) * W))
+            vals.append(window(w))
+        return np.concatenate(covered), np.concatenate(vals)
+    return rescore
+
+
+# Whether smt_channel_mean_aten (ATen's CPU summation order replayed on the GPU) reproduces the
+# reference expression on this host, per accumulator shape: checked once per shape and process
+# against reference_channel_stat on the host; a mismatch falls back to the interval ranking.
+_ATEN_MEAN_OK: Dict[tuple, bool] = {}
+ATEN_MEAN_REPORT: dict = {"exact_keys": 0, "checked_shapes": [], "fallback_shapes": []}
+
+
+def _exact_channel_means(dev_acc: torch.Tensor, src, C: int, strategy: str) -> Optional[np.ndarray]:
+    """The reference's fp32 mean_abs / abs_mean values of one key, computed on the GPU in ATen's
+    order, or None when that does not hold on this host for the shape (or for L1 / L2)."""
+    if strategy not in ("mean_abs", "abs_mean"):
+        return None
+    shape = tuple(dev_acc.shape)
+    ok = _ATEN_MEAN_OK.get(shape)
+    if ok is False:
+        return None
+    vals = _hip.channel_mean_aten(dev_acc).cpu().numpy()[:C]
+    if ok is None:
+        ref = reference_channel_stat(src, strategy)
+        ok = _ATEN_MEAN_OK[shape] = bool(np.array_equal(vals, ref))
+        ATEN_MEAN_REPORT["checked_shapes" if ok else "fallback_shapes"].append(shape)
+        if not ok:
+            return None
+    ATEN_MEAN_REPORT["exact_keys"] += 1
+    return vals
+
+
 def score_channel_entries(activation: Dict[Hashable, object], calculate_strategy: str = "mean_abs") -> List[ranking.KeyScores]:
     """smt_helper.py:167-184 on the GPU: per key, the channel statistics as :class:`ranking.KeyScores`.
+    mean_abs / abs_mean (the harvested |x| sums are non-negative: the same values) come out exact,
+    in ATen's own summation order (smt_channel_mean_aten, checked on the host once per shape); L1 / L2
+    (and a shape whose check failed) as fp64 sums with intervals and the window re-score.
     Keys with an unknown strategy are skipped as in the reference (no branch assigns them)."""
     if calculate_strategy not in _STRATEGY:
         return []
@@ -353,11 +429,17 @@ def score_channel_entries(activation: Dict[Hashable, object], calculate_strategy
     for key, act in activation.items():
         dev_acc, src = _channel_sources(act)
         B, S, C = src.shape
+        exact = _exact_channel_means(dev_acc, src, C, calculate_strategy)
+        if exact is not None:
+            e64 = exact.astype(np.float64)
+            entries.append(ranking.KeyScores(key, (C,), exact, e64, e64.copy(),
+                                             rescore=channel_rescorer(src, calculate_strategy)))
+            continue
         raw = _hip.channel_scores(dev_acc, _STRATEGY[calculate_strategy]).cpu().numpy()[:C]
         nominal, lo, hi = ranking.channel_intervals(raw, B, S, calculate_strategy)
         entries.append(ranking.KeyScores(
             key, (C,), nominal, lo, hi,
-            rescore=ranking.whole_key(lambda src=src: reference_channel_stat(src, calculate_strategy)),
+            rescore=channel_rescorer(src, calculate_strategy),
             bounds=lambda worst, raw=raw, B=B, S=S: ranking.channel_intervals(raw, B, S, calculate_strategy,
                                                                                worst)[1:]))
     return entries

@@ -46,7 +46,8 @@ def _sdpa_bf16(q, k, v, g):
 
 
 @pytest.mark.parametrize("B,Hq,Hkv,S,layout", [
-    (2, 8, 2, 256, "hf"), (1, 4, 4, 200, "hf"), (1, 8, 1, 384, "contig"), (2, 4, 2, 1024, "hf"), (1, 2, 2, 4, "hf")])
+    (2, 8, 2, 256, "hf"), (1, 4, 4, 200, "hf"), (1, 8, 1, 384, "contig"), (2, 4, 2, 1024, "hf"), (1, 2, 2, 4, "hf"),
+    (1, 40, 40, 512, "hf")])                                   # LLaMA-2-13B heads (config 4)
 def test_flash_attention_matches_fp32_reference(B, Hq, Hkv, S, layout):
     torch.manual_seed(S + Hq)
     D = 128

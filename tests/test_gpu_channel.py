@@ -307,3 +307,30 @@ def test_channel_path_at_config4_geometry():
     rows = torch.tensor(idx[:64], device=DEV)
     truth = x.view(-1, H)[:, rows].double().t() @ g.view(-1, H).double()          # [64, H]
     assert _rel(gw[:64], truth) < 2e-3
+
+
+@pytest.mark.parametrize("B,S,C", [(16, 2048, 5120), (4, 2048, 256), (2, 100, 512), (3, 4096, 768), (1, 17, 256)])
+def test_channel_mean_aten_bit_identical_to_reference_expression(B, S, C):
+    """smt_channel_mean_aten replays ATen's CPU cascade_sum order: every channel's fp32 value equals
+    the reference expression (smt_helper.py:167-176: torch.sum(act.abs(), 0) then torch.mean(., 0),
+    run here on the host CPU), including S not a multiple of the 16-row chunk and config 4's
+    [16, 2048, 5120] state; mean_abs and abs_mean agree on the non-negative harvest."""
+    gen = torch.Generator(device=DEV).manual_seed(B * S + C)
+    acc = torch.rand(B, S, C, generator=gen, device=DEV) * torch.rand(C, generator=gen, device=DEV) * 3.0
+    got = _hip.channel_mean_aten(acc).cpu().numpy()
+    for strategy in ("mean_abs", "abs_mean"):
+        assert np.array_equal(got, smt_helper.reference_channel_stat(acc, strategy))
+
+
+def test_exact_channel_scores_skip_the_host_rescore():
+    """With the ATen-order means the ranking has nothing undecided: no key is re-scored, and the
+    selection equals the oracle's on the same state (near-tie fixture values included)."""
+    gen = torch.Generator(device=DEV).manual_seed(5)
+    acts = {("q_proj", i): torch.rand(2, 256, 512, generator=gen, device=DEV) for i in range(3)}
+    acts[("k_proj", 0)] = acts[("q_proj", 0)] * (1 + 1e-7)          # values a few ulps apart
+    from sparse_matrix_tuning_amd.smt import ranking
+    got = smt_helper.select_channel_based_on_activation(acts, 40)
+    assert ranking.LAST_REPORT["rescored_keys"] == []
+    want = ref.select_channel({k: v.cpu() for k, v in acts.items()}, 40)
+    assert {k: list(v) for k, v in got.items()} == {k: list(v) for k, v in want.items()}
+    assert list(got) == list(want)

@@ -200,3 +200,22 @@ def test_block_row_rescore_equals_whole_key(strategy):
         assert np.array_equal(vals, full[covered])
         assert covered.size == 3 * d2
     assert smt_helper._ROW_SLICE_OK[strategy]
+
+
+@pytest.mark.parametrize("strategy", ["mean_abs", "abs_mean", "L1", "L2"])
+def test_channel_window_rescore_equals_whole_key(strategy):
+    """The channel re-score reads only the aligned 256-channel windows holding the undecided channels:
+    ATen's value of a channel over its window of the fp32 [B, S, in] state equals its value in the
+    whole key (config 4's q/k/v width, a reduced batch; checked once per strategy at run time too)."""
+    gen = torch.Generator().manual_seed(9)
+    act = torch.rand(4, 2048, 5120, generator=gen) * torch.rand(5120, generator=gen)
+    full = smt_helper.reference_channel_stat(act, strategy)
+    smt_helper._CHANNEL_WINDOW_OK.pop(strategy, None)
+    covered, vals = smt_helper.channel_rescorer(act, strategy)(np.array([3, 700, 5119]))
+    assert np.array_equal(vals, full[covered])
+    assert covered.size == 3 * 256
+    assert smt_helper._CHANNEL_WINDOW_OK[strategy]
+    # a partial last window (width not a multiple of 256) re-scores the whole key
+    part = act[:, :, :1000].contiguous()
+    covered, vals = smt_helper.channel_rescorer(part, strategy)(np.array([999]))
+    assert covered.size == 1000 and np.array_equal(vals, smt_helper.reference_channel_stat(part, strategy))
