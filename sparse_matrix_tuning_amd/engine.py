@@ -275,14 +275,19 @@ class WgradBatcher:
         block-major packed copy when ``packed``)."""
         self._add(sink, "bf16", (g2, x2, tiles, bool(packed)), (g2, x2), len(tiles))
 
-    def add_mx(self, sink: "_GradSink", g2: torch.Tensor, rb_dev: torch.Tensor, mx, tiles) -> None:
+    def add_mx(self, sink: "_GradSink", g2: torch.Tensor, rb_dev: torch.Tensor, mx, tiles, col_pos=None) -> None:
         """fp8 path: ``g2`` is quantised into its MX row blocks ``rb_dev`` at launch time; ``mx`` is
-        the input's MX column blocks saved by the forward."""
-        self._add(sink, "mx", (g2, rb_dev, mx, tiles), (g2, mx.q, mx.scales), len(tiles))
+        the input's MX column blocks saved by the forward (the module's own, or its group's shared
+        blocks with ``col_pos`` mapping column block -> position)."""
+        self._add(sink, "mx", (g2, rb_dev, mx, tiles, col_pos), (g2, mx.q, mx.scales), len(tiles))
 
     def _add(self, sink, kind, args, keep, n) -> None:
-        if any(p[0] is sink for p in self.pending) or (self.pending and self.pending[0][1] != kind):
-            self.flush()                         # a second backward through one module: in order
+        rows = args[0].shape[0]
+        if self.pending and (any(p[0] is sink for p in self.pending) or self.pending[0][1] != kind
+                             or self.pending[0][2][0].shape[0] != rows):
+            # a second backward through one module (in order), or operands one launch cannot share
+            # (the other operand kind, another T)
+            self.flush()
         if not self.callback_queued:
             torch.autograd.Variable._execution_engine.queue_callback(self._end_of_backward)
             self.callback_queued = True
@@ -305,8 +310,8 @@ class WgradBatcher:
             key = ("bf16", dev.index) + tuple((id(p[2][2]), p[2][3]) for p in pending)
             ktiles = lambda: [p[2][2].kernel_tiles(p[2][3]) for p in pending]
         else:
-            key = ("mx", dev.index) + tuple(id(p[2][3]) for p in pending)
-            ktiles = lambda: [p[2][3].mx_kernel_tiles() for p in pending]
+            key = ("mx", dev.index) + tuple((id(p[2][3]), id(p[2][4])) for p in pending)
+            ktiles = lambda: [p[2][3].mx_kernel_tiles(p[2][4]) for p in pending]
         tabs = self._tables.get(key)
         if tabs is None:
             if len(self._tables) >= 1024:
@@ -321,7 +326,7 @@ class WgradBatcher:
         else:
             def launch():
                 items = [(_hip.mx_quant_cols(g2, rb), mx, p[0].buffer, p[4])
-                         for p, (g2, rb, mx, _t) in ((p, p[2]) for p in pending)]
+                         for p, (g2, rb, mx, _t, _c) in ((p, p[2]) for p in pending)]
                 _hip.tile_wgrad_mx_batch(items, tab, order)
         pending[0][0].run(launch, *keep)
         for p in pending:
@@ -529,6 +534,11 @@ class _TileGroup:
             if fw.group is not None:
                 union.setdefault(id(fw.group), (fw.group, set()))[1].update(m.tiles.column_blocks())
         self.fp8_groups = [(g, torch.tensor(sorted(cbs), dtype=torch.int32).to(device)) for g, cbs in union.values()]
+        for g, cbs in union.values():
+            if any(getattr(m.weight, "_smt_fp8", None) is not None and m.weight._smt_fp8.mx_wgrad
+                   for m in modules if getattr(m.weight, "_smt_fp8", None) is not None
+                   and m.weight._smt_fp8.group is g):
+                g.set_mx_union(cbs, device)
         self.step = 0
 
     def begin_window(self) -> None:
@@ -650,6 +660,9 @@ class SMTEngine:
         if self.wgrad_batcher is not None:
             self.wgrad_batcher.callback_queued = False
             self.wgrad_batcher.flush()          # (the end-of-backward callback already did, normally)
+        for tg in self.tile_groups:
+            for g, _cb in tg.fp8_groups:
+                g.clear_mx_cache()              # the shared MX input blocks live until their backward
         if self.wgrad_stream is not None:
             torch.cuda.current_stream(self.device).wait_stream(self.wgrad_stream)
         if boundary:

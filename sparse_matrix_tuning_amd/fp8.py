@@ -119,6 +119,29 @@ class Fp8Group:
         self.offsets = [sum(self.outs[:i]) for i in range(len(self.outs))]
         self.wt8, self.swt = quant_cols_t(self._cat())           # [in, sum(out)]
         self.swt_row = self.swt.view(1, -1)
+        # the MX column blocks of the members' shared input, quantised once per forward for the union
+        # of the column blocks the members' tiles read (set by the engine: set_mx_union)
+        self.mx_union = None            # (device int32 blocks, {block: position})
+        self._mx_cache = None           # (weakref to the input, its version, MxBlocks)
+
+    def set_mx_union(self, col_blocks, device) -> None:
+        cbs = sorted(int(c) for c in col_blocks)
+        self.mx_union = (torch.tensor(cbs, dtype=torch.int32).to(device), {c: i for i, c in enumerate(cbs)})
+        self._mx_cache = None
+
+    def mx_input_blocks(self, x: torch.Tensor, x2d: torch.Tensor):
+        """The MX column blocks (union order) of the input ``x`` the members read: quantised by the
+        first member's forward, shared by the others (same tensor object and version)."""
+        import weakref
+        c = self._mx_cache
+        if c is not None and c[0]() is x and c[1] == x._version:
+            return c[2]
+        mx = _hip.mx_quant_cols(x2d, self.mx_union[0])
+        self._mx_cache = (weakref.ref(x), x._version, mx)
+        return mx
+
+    def clear_mx_cache(self) -> None:
+        self._mx_cache = None
 
     def _cat(self) -> torch.Tensor:
         return torch.cat([w.detach() for w in self.weights], 0)

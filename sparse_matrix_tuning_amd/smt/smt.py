@@ -135,15 +135,25 @@ class TileIndex:
             self._dev[key] = t
         return t
 
-    def mx_kernel_tiles(self) -> List[Tuple[int, int]]:
-        """Host ``(row-block position, column-block position)`` list of :meth:`mx_tables`."""
-        t = self._dev.get("mx_ktiles")
+    def mx_kernel_tiles(self, col_pos: Optional[dict] = None) -> List[Tuple[int, int]]:
+        """Host ``(row-block position, column-block position)`` list of :meth:`mx_tables`; with
+        ``col_pos`` the column positions in a group's shared MX input blocks instead of this module's."""
+        key = ("mx_ktiles", id(col_pos))
+        t = self._dev.get(key)
         if t is None:
             rbs = {}
             for r, _c in self.index_list:
                 rbs.setdefault(r, len(rbs))
-            pos = {c: i for i, c in enumerate(self.column_blocks())}
-            t = self._dev["mx_ktiles"] = [(rbs[r], pos[c]) for r, c in self.index_list]
+            pos = col_pos if col_pos is not None else {c: i for i, c in enumerate(self.column_blocks())}
+            t = self._dev[key] = [(rbs[r], pos[c]) for r, c in self.index_list]
+        return t
+
+    def mx_group_table(self, col_pos: dict, device: torch.device) -> torch.Tensor:
+        """Device int32 [n, 2] table of :meth:`mx_kernel_tiles` against a group's shared blocks."""
+        key = ("mx_group", id(col_pos), device.type, device.index)
+        t = self._dev.get(key)
+        if t is None:
+            t = self._dev[key] = _hip.tile_table(self.mx_kernel_tiles(col_pos), device)
         return t
 
     def block_tables(self, device: torch.device):
@@ -313,6 +323,7 @@ class linearZ(torch.autograd.Function):
         ctx.sink = getattr(selected_weight, "_smt_grad_sink", None)
         ctx.packed = False
         ctx.mx = None
+        ctx.mx_pos = None
         saved = input
         in_blocks = weight.shape[1] // Block_dimension
         fw = getattr(weight, "_smt_fp8", None)
@@ -320,8 +331,16 @@ class linearZ(torch.autograd.Function):
                 and input.device.type == "cuda"):
             # fp8 path: the tile weight gradient runs on MX-fp8 operands; keep only the input's
             # column blocks, quantised (half the bytes of the bf16 blocks)
-            _rb, cb_dev, _table = tiles.mx_tables(input.device)
-            ctx.mx = _hip.mx_quant_cols(_rows_ready(input.reshape(-1, weight.shape[1])), cb_dev)
+            grp = fw.group
+            if grp is not None and grp.mx_union is not None:
+                # q/k/v (gate/up) read one input: its MX blocks are quantised once for the group's
+                # union of column blocks and shared
+                ctx.mx = grp.mx_input_blocks(input, _rows_ready(input.reshape(-1, weight.shape[1])))
+                ctx.mx_pos = grp.mx_union[1]
+            else:
+                _rb, cb_dev, _table = tiles.mx_tables(input.device)
+                ctx.mx = _hip.mx_quant_cols(_rows_ready(input.reshape(-1, weight.shape[1])), cb_dev)
+                ctx.mx_pos = None
             saved = None
         elif (ctx.needs_input_grad[1] and len(tiles) and input.device.type == "cuda"
                 and 2 * len(tiles.column_blocks()) <= in_blocks):
@@ -349,11 +368,13 @@ class linearZ(torch.autograd.Function):
         if ctx.needs_input_grad[1] and ctx.mx is not None:
             g2 = _rows_ready(grad_output.reshape(-1, weight.shape[0]))
             rb_dev, _cb, table = tiles.mx_tables(g2.device)
+            if ctx.mx_pos is not None:
+                table = tiles.mx_group_table(ctx.mx_pos, g2.device)
             sink = ctx.sink
             if sink is not None and sink.batcher() is not None:
                 # quantised and launched with the modules whose backward runs next (one
                 # smt_tile_wgrad_mx_batch launch)
-                sink.batcher().add_mx(sink, g2, rb_dev, ctx.mx, tiles)
+                sink.batcher().add_mx(sink, g2, rb_dev, ctx.mx, tiles, ctx.mx_pos)
             elif sink is not None:
                 acc, mx, order = sink.take_accumulate(), ctx.mx, tiles.schedule(g2.device)
                 sink.run(lambda: _hip.tile_wgrad_mx(_hip.mx_quant_cols(g2, rb_dev), mx, table, sink.buffer,

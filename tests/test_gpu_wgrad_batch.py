@@ -285,3 +285,63 @@ def test_engine_fp8_batched_equals_unbatched():
     for ga, gb in zip(a, b):
         for x, y in zip(ga, gb):
             assert _rel(y, x) < 1e-5
+
+
+def test_engine_batcher_flushes_on_a_different_T():
+    """Modules whose inputs have different row counts in one backward (here two separate inputs
+    through different modules) go out in separate launches, each exact."""
+    out = {}
+    for bt in (0, 48):
+        engine, _fwd = _mini_engine(bt, seed=2)
+        l0 = engine.module.layers[0]
+        xa = torch.randn(2, 256, 1024, device=DEV).bfloat16()
+        xb = torch.randn(1, 384, 1024, device=DEV).bfloat16()
+        loss = l0["q_proj"](xa).float().pow(2).mean() + l0["up_proj"](xb).float().pow(2).mean()
+        engine.backward(loss)
+        out[bt] = engine.tile_groups[0].grad.clone()
+    assert _rel(out[48], out[0]) < 1e-6
+
+
+def test_fp8_group_shares_mx_input_blocks():
+    """q/k/v (gate/up) of one layer quantise their shared input's MX column blocks once, for the
+    union of the blocks their tiles read; the tile gradients equal the per-module quantisation's
+    (the MX values of a block do not depend on which other blocks are quantised with it)."""
+    import bench
+    from collections import defaultdict
+    from sparse_matrix_tuning_amd import engine as eng
+    from sparse_matrix_tuning_amd.smt import smt
+
+    def run(share):
+        cfg = dict(bench.MODELS["mini"], num_hidden_layers=1)
+        bench.MODELS["_s"] = cfg
+        try:
+            model = bench.build_model("_s", DEV)
+        finally:
+            del bench.MODELS["_s"]
+        sel_att = defaultdict(list, {("q_proj", 0): [(1, 1), (0, 0)], ("k_proj", 0): [(0, 1)], ("v_proj", 0): [(0, 0)]})
+        sel_mlp = defaultdict(list, {("gate_proj", 0): [(2, 1)], ("up_proj", 0): [(1, 0), (0, 1)]})
+        smt.freeze_unselected_matrix_layer(model, sel_mlp, sel_att)
+        smt.convert_linear_layer_to_matrix_sparsity(model, sel_mlp, sel_att)
+        opt = eng.SMTFusedAdam(smt.get_optimizer_sparse_grouped_parameters(model, 0.0, 1e-3), lr=1e-3)
+        engine, *_ = eng.initialize(model=model, optimizer=opt, config={"fp8_linears": True})
+        if not share:
+            for tg in engine.tile_groups:
+                for g, _cb in tg.fp8_groups:
+                    g.mx_union = None
+        calls = []
+        orig = smt._hip.mx_quant_cols
+        smt._hip.mx_quant_cols = lambda x, b: (calls.append(b.numel()), orig(x, b))[1]
+        try:
+            ids = torch.randint(0, 4096, (2, 256), generator=torch.Generator().manual_seed(0)).to(DEV)
+            loss = engine(input_ids=ids, labels=ids, use_cache=False).loss
+            engine.backward(loss)
+        finally:
+            smt._hip.mx_quant_cols = orig
+        return [tg.grad.clone() for tg in engine.tile_groups], calls
+
+    shared, c_shared = run(True)
+    alone, c_alone = run(False)
+    # forward input quantisations: 2 groups once each vs 5 modules (backward: one per module either way)
+    assert len(c_shared) == len(c_alone) - 3
+    for a, b in zip(shared, alone):
+        assert torch.equal(a, b)
