@@ -35,6 +35,8 @@ at 288 GB per GPU the 57 M-parameter tile optimizer state is simply replicated (
 """
 from __future__ import annotations
 
+import collections
+import os
 from typing import List, Optional
 
 import torch
@@ -233,11 +235,13 @@ class _GradSink:
         if side is None:
             launch()
             return
-        side.wait_stream(torch.cuda.current_stream(side.device))
+        cur = torch.cuda.current_stream(side.device)
+        side.wait_stream(cur)
         with torch.cuda.stream(side):
             launch()
         for t in keep:
             t.record_stream(side)
+        self.engine.bound_wgrad_lag(cur)
 
     def mark_ready(self) -> None:
         """Called by ``linearZ.backward`` once this module's tile-gradient kernels are enqueued."""
@@ -309,15 +313,18 @@ class WgradBatcher:
         if kind == "bf16":
             key = ("bf16", dev.index) + tuple((id(p[2][2]), p[2][3]) for p in pending)
             ktiles = lambda: [p[2][2].kernel_tiles(p[2][3]) for p in pending]
+            ids = [p[2][2] for p in pending]
         else:
             key = ("mx", dev.index) + tuple((id(p[2][3]), id(p[2][4])) for p in pending)
             ktiles = lambda: [p[2][3].mx_kernel_tiles(p[2][4]) for p in pending]
+            ids = [(p[2][3], p[2][4]) for p in pending]
         tabs = self._tables.get(key)
         if tabs is None:
             if len(self._tables) >= 1024:
                 self._tables.clear()
-            # hold the TileIndex objects: the key uses their ids
-            tabs = self._tables[key] = (_hip.wgrad_batch_table(ktiles(), dev), [p[2] for p in pending])
+            # hold the objects whose ids make the key (TileIndex, the group's column-position map)
+            # and NOTHING else: a cached operand tensor would stay allocated for the whole run
+            tabs = self._tables[key] = (_hip.wgrad_batch_table(ktiles(), dev), ids)
         (tab, order), _ = tabs
         keep = [t for p in pending for t in p[3]]
         if kind == "bf16":
@@ -609,6 +616,12 @@ class SMTEngine:
         # every collective over the tile buffer and at the end of backward
         self.wgrad_stream = (torch.cuda.Stream(self.device) if self.tile_groups and self.device.type == "cuda"
                              and cfg.get("overlap_wgrad", True) else None)
+        # at most this many wgrad launches may be pending behind the current stream: the operands
+        # they hold (output gradients, saved inputs) stay allocated until the wgrad stream passes
+        # them, and a wgrad stream starved of CUs by the data-gradient GEMMs would otherwise keep
+        # every SMT module's output gradient of the step alive (~50 GB at the 8B point)
+        self.wgrad_max_lag = int(cfg.get("wgrad_max_lag", os.environ.get("SMT_WGRAD_MAX_LAG", 2)))
+        self._wgrad_events = collections.deque()
         # tile gradients of consecutive modules in one launch (wgrad_batch_tiles <= 0: one per module)
         batch_tiles = int(cfg.get("wgrad_batch_tiles", 48))
         self.wgrad_batcher = (WgradBatcher(self, batch_tiles) if self.tile_groups and batch_tiles > 0
@@ -636,6 +649,17 @@ class SMTEngine:
     def eval(self):
         self.module.eval()
         return self
+
+    def bound_wgrad_lag(self, cur) -> None:
+        """After a launch on the wgrad stream: when more than ``wgrad_max_lag`` launches are
+        outstanding, the current stream waits for the oldest (``<= 0``: no bound)."""
+        if self.wgrad_max_lag <= 0:
+            return
+        ev = torch.cuda.Event()
+        ev.record(self.wgrad_stream)
+        self._wgrad_events.append(ev)
+        if len(self._wgrad_events) > self.wgrad_max_lag:
+            cur.wait_event(self._wgrad_events.popleft())
 
     def is_gradient_accumulation_boundary(self) -> bool:
         return (self.micro_steps + 1) % self.gradient_accumulation_steps == 0
@@ -665,6 +689,7 @@ class SMTEngine:
                 g.clear_mx_cache()              # the shared MX input blocks live until their backward
         if self.wgrad_stream is not None:
             torch.cuda.current_stream(self.device).wait_stream(self.wgrad_stream)
+            self._wgrad_events.clear()
         if boundary:
             for tg in self.tile_groups:
                 tg.zero_unreported()

@@ -10,7 +10,7 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
 
 
-def _run(overlap: bool):
+def _run(overlap: bool, max_lag: int = 2):
     import bench
     from sparse_matrix_tuning_amd.engine import SMTFusedAdam, initialize
     from sparse_matrix_tuning_amd.smt import smt
@@ -27,7 +27,8 @@ def _run(overlap: bool):
     smt.freeze_unselected_matrix_layer(model, sel_mlp, sel_att)
     smt.convert_linear_layer_to_matrix_sparsity(model, sel_mlp, sel_att)
     opt = SMTFusedAdam(smt.get_optimizer_sparse_grouped_parameters(model, 0.0, 1e-3), lr=1e-3, betas=(0.9, 0.95))
-    engine, *_ = initialize(model=model, optimizer=opt, config={"gradient_clipping": 1.0, "overlap_wgrad": overlap})
+    engine, *_ = initialize(model=model, optimizer=opt, config={"gradient_clipping": 1.0, "overlap_wgrad": overlap,
+                                                                  "wgrad_max_lag": max_lag})
     assert (engine.wgrad_stream is not None) == overlap
     gen = torch.Generator().manual_seed(1)
     losses = []
@@ -41,9 +42,12 @@ def _run(overlap: bool):
     return losses, [(tg.master.clone(), tg.grad.clone()) for tg in engine.tile_groups]
 
 
-def test_overlapped_wgrad_bit_identical():
+@pytest.mark.parametrize("max_lag", [0, 1, 2])
+def test_overlapped_wgrad_bit_identical(max_lag):
+    """0: the wgrad stream may run arbitrarily far behind; 1, 2: the current stream waits for all
+    but the last 1 (2) wgrad launches (the bound on the operands held for the wgrad stream)."""
     l0, s0 = _run(False)
-    l1, s1 = _run(True)
+    l1, s1 = _run(True, max_lag)
     assert l0 == l1
     for (m0, g0), (m1, g1) in zip(s0, s1):
         assert torch.equal(m0, m1) and torch.equal(g0, g1)
