@@ -57,6 +57,14 @@ int smt_rmsnorm_bwd(const void* dy, int64_t ld_dy, const void* x, int64_t ld_x, 
                     void* dx, int64_t ld_dx, float* dw_partial, void* dw, int64_t rows, int32_t hidden,
                     hipStream_t stream);
 
+/* smt_rmsnorm_bwd with the weight gradient AND the residual-path gradient (the full fine-tuning
+ * warm-up's LlamaDecoderLayer norms): dx = bf16(bf16(dx_norm) + dres), dw = bf16(sum_rows bf16(dy *
+ * bf16(x * rstd))) via dw_partial[smt_rmsnorm_bwd_waves(rows)][hidden] fp32 (overwritten).
+ * hidden % 512 == 0, <= 8192. (ABI 7) */
+int smt_rmsnorm_bwd_add_dw(const void* dy, int64_t ld_dy, const void* x, int64_t ld_x, const void* weight,
+                           const float* rstd, const void* dres, int64_t ld_dres, void* dx, int64_t ld_dx,
+                           float* dw_partial, void* dw, int64_t rows, int32_t hidden, hipStream_t stream);
+
 /* q/k rotary embedding (one launch for both); cos/sin [B, S, D] with strides (cos_sb, cos_ss, 1). */
 int smt_rope_fwd(const smt_rope_tensor* q, const smt_rope_tensor* k, const void* cos, const void* sin,
                  int64_t cos_sb, int64_t cos_ss, int64_t B, int32_t S, int32_t D, hipStream_t stream);

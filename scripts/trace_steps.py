@@ -1,7 +1,10 @@
 """Per-category kernel time of the SMT steps from a rocprofv3 kernel-trace CSV.
 
 SMT steps are delimited by adamw_tiles_kernel dispatches (one per step): the region between two
-consecutive ones is one step. Prints per-step wall (first start .. last end) and kernel-time by category."""
+consecutive ones is one step. Prints per-step wall (first start .. last end) and kernel-time by category.
+``python scripts/trace_steps.py trace.csv adamw_multi_kernel``: the full fine-tuning warm-up steps
+instead (one dense multi-tensor AdamW launch per parameter group and step: the first of each step's
+burst delimits)."""
 import collections
 import csv
 import sys
@@ -11,6 +14,10 @@ def cat(name):
     n = name
     if "wgrad_" in n or "colblock_gather" in n:
         return "smt_wgrad"
+    if "grad_accumulate" in n or "block_score" in n:
+        return "smt_harvest"
+    if "adamw_multi" in n:
+        return "dense_adamw"
     if "adamw" in n or "sq_norm" in n or "tile_copy" in n or "tile_scatter_t" in n:
         return "smt_optimizer"
     if "ce_fwd_kernel" in n or "ce_bwd_kernel" in n:
@@ -32,10 +39,12 @@ def cat(name):
     return "other"
 
 
-def main(path):
+def main(path, delim="adamw_tiles_kernel"):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    idx = [i for i, r in enumerate(rows) if "adamw_tiles_kernel" in r["Kernel_Name"]]
+    idx = [i for i, r in enumerate(rows) if delim in r["Kernel_Name"]]
+    # a burst of delimiter launches (one per parameter group) counts once: keep the last of each
+    idx = [i for k, i in enumerate(idx) if k + 1 == len(idx) or idx[k + 1] - i > 8]
     if len(idx) < 2:
         print("need >= 2 SMT steps")
         return
@@ -67,4 +76,4 @@ def main(path):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(*sys.argv[1:3])

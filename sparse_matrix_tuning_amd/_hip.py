@@ -36,7 +36,7 @@ ABI_FUNCTIONS = (
     "smt_row_gather", "smt_row_scatter", "smt_column_gather", "smt_act_accumulate",
     "smt_channel_score_workspace_bytes", "smt_channel_score",
     "smt_channel_mean_aten_workspace_bytes", "smt_channel_mean_aten",
-    "smt_model_ops_last_error", "smt_rmsnorm_fwd", "smt_rmsnorm_bwd_waves", "smt_rmsnorm_bwd",
+    "smt_model_ops_last_error", "smt_rmsnorm_fwd", "smt_rmsnorm_bwd_waves", "smt_rmsnorm_bwd", "smt_rmsnorm_bwd_add_dw",
     "smt_add_rmsnorm_fwd", "smt_rmsnorm_bwd_add",
     "smt_rope_fwd", "smt_rope_bwd", "smt_swiglu_fwd", "smt_swiglu_bwd", "smt_ce_fwd", "smt_ce_bwd",
     "smt_attn_last_error", "smt_attn_fwd", "smt_attn_bwd",
@@ -155,6 +155,7 @@ _SIGS = {
     "smt_add_rmsnorm_fwd": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _P, _I64, _P, _I64, _P, _I64, _I32, ctypes.c_float, _P]),
     "smt_rmsnorm_bwd_add": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _P, _P, _I64, _P, _I64, _I64, _I32, _P]),
     "smt_rmsnorm_bwd": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _P, _P, _I64, _P, _P, _I64, _I32, _P]),
+    "smt_rmsnorm_bwd_add_dw": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _P, _P, _I64, _P, _I64, _P, _P, _I64, _I32, _P]),
     "smt_rope_fwd": (ctypes.c_int, [ctypes.POINTER(RopeTensor), ctypes.POINTER(RopeTensor), _P, _P, _I64, _I64, _I64, _I32, _I32, _P]),
     "smt_rope_bwd": (ctypes.c_int, [ctypes.POINTER(RopeTensor), ctypes.POINTER(RopeTensor), _P, _P, _I64, _I64, _I64, _I32, _I32, _P]),
     "smt_swiglu_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _P]),

@@ -105,24 +105,17 @@ void rmsnorm_fwd_kernel(const uint16_t* __restrict__ x, int64_t ldx, const uint1
     }
 }
 
-// Backward of the eager chain: dn = bf16(dy * w); dx = bf16(r*dn - xf * r^3 * sum(dn*xf) / H);
-// optional weight grad: dw = bf16(sum_rows float(bf16(dy * bf16(xf*r)))) as per-wave fp32 partials
-// [n_waves][H] summed in a fixed order by rmsnorm_dw_kernel. Waves stride over rows.
-template <bool DW, int CPL>
+// Backward of the eager chain: dn = bf16(dy * w); dx = bf16(r*dn - xf * r^3 * sum(dn*xf) / H), for
+// any hidden % 8 == 0 (the register-resident kernels below cover hidden % 512 == 0). Waves stride
+// over rows.
 __global__ __launch_bounds__(256)
 void rmsnorm_bwd_kernel(const uint16_t* __restrict__ dy, int64_t lddy, const uint16_t* __restrict__ x, int64_t ldx,
                         const uint16_t* __restrict__ w, const float* __restrict__ rstd,
-                        uint16_t* __restrict__ dx, int64_t lddx, float* __restrict__ dw_partial,
-                        int64_t rows, int H) {
+                        uint16_t* __restrict__ dx, int64_t lddx, int64_t rows, int H) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int64_t n_waves = (int64_t)gridDim.x * 4;
     const int nch = H >> 3;
-    float acc[DW ? CPL * 8 : 1];
-    if (DW) {
-#pragma unroll
-        for (int i = 0; i < CPL * 8; ++i) acc[i] = 0.f;
-    }
     for (int64_t row = wave; row < rows; row += n_waves) {
         const float r = rstd[row];
         const uint16_t* xr = x + row * ldx;
@@ -136,28 +129,31 @@ void rmsnorm_bwd_kernel(const uint16_t* __restrict__ dy, int64_t lddy, const uin
         dot = wave_sum_f(dot);
         const float coef = r * r * r * dot / (float)H;
         uint16_t* dxr = dx + row * lddx;
-        int k = 0;
-        for (int c = lane; c < nch; c += 64, ++k) {
+        for (int c = lane; c < nch; c += 64) {
             const F8 xv = ld8(xr + c * 8), gv = ld8(dyr + c * 8), wv = ld8(w + c * 8);
             F8 o;
 #pragma unroll
             for (int j = 0; j < 8; ++j) o.v[j] = r * rbf(gv.v[j] * wv.v[j]) - xv.v[j] * coef;
             st8(dxr + c * 8, o);
-            if (DW) {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) acc[k * 8 + j] += rbf(gv.v[j] * rbf(xv.v[j] * r));
-            }
         }
     }
-    if (DW) {
-        float* pr = dw_partial + wave * H;
-        int k = 0;
-        for (int c = lane; c < nch; c += 64, ++k) {
-            float4* d = reinterpret_cast<float4*>(pr + c * 8);
-            d[0] = make_float4(acc[k * 8 + 0], acc[k * 8 + 1], acc[k * 8 + 2], acc[k * 8 + 3]);
-            d[1] = make_float4(acc[k * 8 + 4], acc[k * 8 + 5], acc[k * 8 + 6], acc[k * 8 + 7]);
-        }
-    }
+}
+
+// dw = bf16(sum over the waves' partials), in a fixed order: stage 1 sums each chunk of kDwChunk
+// partial rows (in row order) into the chunk's first row, stage 2 the chunk sums in chunk order.
+// (One thread per column over all 4096 partial rows took 1.1 ms per call: 16 workgroups of
+// serial loads.)
+constexpr int kDwChunk = 64;
+
+__global__ __launch_bounds__(256)
+void rmsnorm_dw_chunk_kernel(float* __restrict__ partial, int64_t n_waves, int H) {
+    const int col = blockIdx.x * 256 + threadIdx.x;
+    if (col >= H) return;
+    const int64_t r0 = (int64_t)blockIdx.y * kDwChunk;
+    const int64_t r1 = r0 + kDwChunk < n_waves ? r0 + kDwChunk : n_waves;
+    float s = 0.f;
+    for (int64_t i = r0; i < r1; ++i) s += partial[i * H + col];
+    partial[r0 * H + col] = s;
 }
 
 __global__ __launch_bounds__(256)
@@ -165,7 +161,7 @@ void rmsnorm_dw_kernel(const float* __restrict__ partial, int64_t n_waves, int H
     const int col = blockIdx.x * 256 + threadIdx.x;
     if (col >= H) return;
     float s = 0.f;
-    for (int64_t i = 0; i < n_waves; ++i) s += partial[i * H + col];
+    for (int64_t i = 0; i < n_waves; i += kDwChunk) s += partial[i * H + col];
     dw[col] = (uint16_t)tobf(s);
 }
 
@@ -307,6 +303,35 @@ void rmsnorm_bwd_reg_kernel(const uint16_t* __restrict__ dy, int64_t lddy, const
             *reinterpret_cast<uint2*>(q8 + row * ldq + c * 8) = q;
         }
     }
+}
+
+// The weight gradient of the full fine-tuning warm-up: dw = bf16(sum_rows bf16(dy * bf16(x * r))),
+// the eager chain's terms. Its own pass over x and dy (the dx pass stays the register-resident
+// kernel, one row per wave): a thread owns 8 columns of one chunk of `rows_per_chunk` rows and adds
+// that chunk's terms in row order into dw_partial[chunk]; the chunks are then summed in chunk order.
+// (Fusing the column sums into the dx kernel needs 8 * CPL fp32 accumulators per lane beside the
+// row: ~390 registers at hidden 4096, one wave per SIMD, 2.9 TB/s.)
+__global__ __launch_bounds__(256)
+void rmsnorm_dw_rows_kernel(const uint16_t* __restrict__ dy, int64_t lddy, const uint16_t* __restrict__ x,
+                            int64_t ldx, const float* __restrict__ rstd, float* __restrict__ dw_partial,
+                            int64_t rows, int64_t rows_per_chunk, int H) {
+    const int c = (blockIdx.x * 256 + threadIdx.x) * 8;
+    if (c >= H) return;
+    const int64_t r0 = (int64_t)blockIdx.y * rows_per_chunk;
+    const int64_t r1 = r0 + rows_per_chunk < rows ? r0 + rows_per_chunk : rows;
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+#pragma unroll 4
+    for (int64_t row = r0; row < r1; ++row) {
+        const float r = rstd[row];
+        const F8 xv = ld8(x + row * ldx + c), gv = ld8(dy + row * lddy + c);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += rbf(gv.v[j] * rbf(xv.v[j] * r));
+    }
+    float4* d = reinterpret_cast<float4*>(dw_partial + (int64_t)blockIdx.y * H + c);
+    d[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    d[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -569,6 +594,35 @@ int launch_bwd_reg(bool add, const void* dy, int64_t lddy, const void* x, int64_
                                    (const uint16_t*)w, rstd, nullptr, 0, (uint16_t*)dx, lddx, rows, H);
 }
 
+// dx (with dres: + the residual-path gradient) by the register-resident kernel, then dw: chunk
+// partials over rows (at most smt_rmsnorm_bwd_waves(rows) chunks: the caller's partial buffer)
+// and the fixed-order reduction.
+int launch_bwd_dw(const void* dres, int64_t lddr, const void* dy, int64_t lddy, const void* x, int64_t ldx,
+                  const void* w, const float* rstd, void* dx, int64_t lddx, float* dw_partial, void* dw, int64_t rows,
+                  int H, hipStream_t stream) {
+    if (!dw_partial || !dw || (H % 512) || H > 8192)
+        return fail(-1, "smt_rmsnorm_bwd: weight grad needs hidden %% 512 == 0, <= 8192 and a partial buffer");
+    int rc = launch_bwd_reg(dres != nullptr, dy, lddy, x, ldx, w, rstd, dres, lddr, dx, lddx, rows, H, stream);
+    if (rc) return rc;
+    const int64_t cap = smt_rmsnorm_bwd_waves(rows);
+    int64_t per = (rows + cap - 1) / cap;
+    if (per < 64) per = 64;
+    const int64_t n_chunks = (rows + per - 1) / per;
+    const unsigned col_blocks = (unsigned)((H / 8 + 255) / 256);
+    hipLaunchKernelGGL(rmsnorm_dw_rows_kernel, dim3(col_blocks, (unsigned)n_chunks), dim3(256), 0, stream,
+                       (const uint16_t*)dy, lddy, (const uint16_t*)x, ldx, rstd, dw_partial, rows, per, H);
+    rc = check_launch("rmsnorm_dw_rows_kernel");
+    if (rc) return rc;
+    const unsigned out_blocks = (unsigned)((H + 255) / 256);
+    hipLaunchKernelGGL(rmsnorm_dw_chunk_kernel, dim3(out_blocks, (unsigned)((n_chunks + kDwChunk - 1) / kDwChunk)),
+                       dim3(256), 0, stream, dw_partial, n_chunks, H);
+    rc = check_launch("rmsnorm_dw_chunk_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(rmsnorm_dw_kernel, dim3(out_blocks), dim3(256), 0, stream, (const float*)dw_partial, n_chunks, H,
+                       (uint16_t*)dw);
+    return check_launch("rmsnorm_dw_kernel");
+}
+
 }  // namespace
 
 extern "C" {
@@ -725,25 +779,23 @@ int smt_rmsnorm_bwd(const void* dy, int64_t ld_dy, const void* x, int64_t ld_x, 
     if (dw == nullptr) {
         if (hidden % 512 == 0 && hidden <= 8192)
             return launch_bwd_reg(false, dy, ld_dy, x, ld_x, weight, rstd, nullptr, 0, dx, ld_dx, rows, hidden, stream);
-        hipLaunchKernelGGL((rmsnorm_bwd_kernel<false, 1>), grid, block, 0, stream, pdy, ld_dy, px, ld_x, pw, rstd, pdx, ld_dx,
-                           nullptr, rows, hidden);
+        hipLaunchKernelGGL(rmsnorm_bwd_kernel, grid, block, 0, stream, pdy, ld_dy, px, ld_x, pw, rstd, pdx, ld_dx, rows,
+                           hidden);
         return check_launch("rmsnorm_bwd_kernel");
     }
-    if (!dw_partial || (hidden % 512) || hidden > 8192)
-        return fail(-1, "smt_rmsnorm_bwd: weight grad needs hidden %% 512 == 0, <= 8192 and a partial buffer");
-    const int cpl = hidden / 512;
-#define RMS_DW(C) case C: hipLaunchKernelGGL((rmsnorm_bwd_kernel<true, C>), grid, block, 0, stream, pdy, ld_dy, px, ld_x, pw, rstd, pdx, ld_dx, dw_partial, rows, hidden); break;
-    switch (cpl) {
-        RMS_DW(1) RMS_DW(2) RMS_DW(3) RMS_DW(4) RMS_DW(5) RMS_DW(6) RMS_DW(7) RMS_DW(8)
-        RMS_DW(9) RMS_DW(10) RMS_DW(11) RMS_DW(12) RMS_DW(13) RMS_DW(14) RMS_DW(15) RMS_DW(16)
-        default: return fail(-1, "smt_rmsnorm_bwd: hidden %d", hidden);
-    }
-#undef RMS_DW
-    int rc = check_launch("rmsnorm_bwd_kernel");
-    if (rc) return rc;
-    hipLaunchKernelGGL(rmsnorm_dw_kernel, dim3((hidden + 255) / 256), dim3(256), 0, stream, dw_partial, (int64_t)n_waves,
-                       hidden, (uint16_t*)dw);
-    return check_launch("rmsnorm_dw_kernel");
+    return launch_bwd_dw(nullptr, 0, dy, ld_dy, x, ld_x, weight, rstd, dx, ld_dx, dw_partial, dw, rows, hidden, stream);
+}
+
+int smt_rmsnorm_bwd_add_dw(const void* dy, int64_t ld_dy, const void* x, int64_t ld_x, const void* weight,
+                           const float* rstd, const void* dres, int64_t ld_dres, void* dx, int64_t ld_dx,
+                           float* dw_partial, void* dw, int64_t rows, int32_t hidden, hipStream_t stream) {
+    if (rows < 0 || hidden <= 0 || (hidden & 7)) return fail(-1, "smt_rmsnorm_bwd_add_dw: bad sizes");
+    if (rows == 0) return 0;
+    if (!dy || !x || !weight || !rstd || !dx || !dres) return fail(-1, "smt_rmsnorm_bwd_add_dw: null pointer");
+    if (!aligned16(dy) || !aligned16(x) || !aligned16(weight) || !aligned16(dx) || !aligned16(dres) || (ld_dy & 7) ||
+        (ld_x & 7) || (ld_dx & 7) || (ld_dres & 7))
+        return fail(-2, "smt_rmsnorm_bwd_add_dw: 16-byte aligned rows required");
+    return launch_bwd_dw(dres, ld_dres, dy, ld_dy, x, ld_x, weight, rstd, dx, ld_dx, dw_partial, dw, rows, hidden, stream);
 }
 
 static int rope(bool bwd, const smt_rope_tensor* q, const smt_rope_tensor* k, const void* cos, const void* sin,

@@ -73,7 +73,10 @@ class FusedRMSNormFn(torch.autograd.Function):
         return dx.view(ctx.shape), dw, None
 
 
-def _rmsnorm_bwd(x2, w, rstd, dy, need_dw: bool):
+def _rmsnorm_bwd(x2, w, rstd, dy, need_dw: bool, dres=None):
+    """dx (+ ``dres``, the gradient reaching the same input by the residual path) and, with
+    ``need_dw``, the weight gradient. With both (the full fine-tuning warm-up) one
+    ``smt_rmsnorm_bwd_add_dw`` pass; returns ``(dx 2-D, dw or None)``."""
     rows, H = x2.shape
     dy2 = _rows2d(dy)
     dx = torch.empty_like(x2)
@@ -83,11 +86,20 @@ def _rmsnorm_bwd(x2, w, rstd, dy, need_dw: bool):
         waves = lib.smt_rmsnorm_bwd_waves(rows)
         partial = torch.empty(waves, H, dtype=torch.float32, device=x2.device)
         dw = torch.empty(H, dtype=w.dtype, device=w.device)
+    if dres is not None and need_dw and H % 512 == 0 and H <= 8192:
+        dr2 = _rows2d(dres)
+        rc = lib.smt_rmsnorm_bwd_add_dw(dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0), w.data_ptr(),
+                                        rstd.data_ptr(), dr2.data_ptr(), dr2.stride(0), dx.data_ptr(), dx.stride(0),
+                                        partial.data_ptr(), dw.data_ptr(), rows, H, _stream(x2))
+        _hip._check(rc, "smt_rmsnorm_bwd_add_dw")
+        return dx, dw
     rc = lib.smt_rmsnorm_bwd(dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0), w.data_ptr(),
                              rstd.data_ptr(), dx.data_ptr(), dx.stride(0),
                              None if partial is None else partial.data_ptr(),
                              None if dw is None else dw.data_ptr(), rows, H, _stream(x2))
     _hip._check(rc, "smt_rmsnorm_bwd")
+    if dres is not None:
+        dx = dx + _rows2d(dres)
     return dx, dw
 
 
@@ -123,9 +135,8 @@ class FusedRMSNormResFn(torch.autograd.Function):
     def backward(ctx, dy, dres):
         x2, w, rstd = ctx.saved_tensors              # unpacked once (activation checkpointing)
         if dres is None or ctx.needs_input_grad[1] or x2.shape[1] % 512 or x2.shape[1] > 8192:
-            dx, dw = _rmsnorm_bwd(x2, w, rstd, dy, ctx.needs_input_grad[1])
-            dx = dx.view(ctx.shape)
-            return (dx if dres is None else dx + dres), dw, None, None, None
+            dx, dw = _rmsnorm_bwd(x2, w, rstd, dy, ctx.needs_input_grad[1], dres)
+            return dx.view(ctx.shape), dw, None, None, None
         rows, H = x2.shape
         dy2, dr2 = _rows2d(dy), _rows2d(dres)
         if getattr(ctx, "quant_grad", False):
@@ -185,20 +196,10 @@ class FusedAddRMSNormFn(torch.autograd.Function):
         if dy is None:
             dx = dh
         elif ctx.needs_input_grad[2] or dh is None:
-            # weight grad (full fine-tuning warm-up) or no residual gradient: the plain norm backward
-            dy2 = _rows2d(dy)
-            dx = torch.empty_like(h)
-            partial = None
-            if ctx.needs_input_grad[2]:
-                partial = torch.empty(lib.smt_rmsnorm_bwd_waves(rows), H, dtype=torch.float32, device=h.device)
-                dw = torch.empty(H, dtype=w.dtype, device=w.device)
-            rc = lib.smt_rmsnorm_bwd(dy2.data_ptr(), dy2.stride(0), h.data_ptr(), H, w.data_ptr(), rstd.data_ptr(),
-                                     dx.data_ptr(), H, None if partial is None else partial.data_ptr(),
-                                     None if dw is None else dw.data_ptr(), rows, H, _stream(h))
-            _hip._check(rc, "smt_rmsnorm_bwd")
+            # weight grad (full fine-tuning warm-up; the residual gradient added in the same pass)
+            # or no residual gradient: the plain norm backward
+            dx, dw = _rmsnorm_bwd(h, w, rstd, dy, ctx.needs_input_grad[2], dh)
             dx = dx.view(ctx.shape)
-            if dh is not None:
-                dx = dx + dh
         elif getattr(ctx, "quant_grad", False):
             from .fp8 import rmsnorm_bwd_add_quant
             dx, q, sq = rmsnorm_bwd_add_quant(_rows2d(dy), h, w, rstd, _rows2d(dh))

@@ -154,3 +154,26 @@ def test_fused_add_rmsnorm_vs_eager(H, weight_grad):
     if weight_grad:
         relw = ((norm.weight.grad.float() - dw_e.float()).norm() / dw_e.float().norm()).item()
         assert relw < 5e-3, relw
+
+
+@pytest.mark.parametrize("H", [512, 4096, 5120])
+@pytest.mark.parametrize("rows", [133, 4133])
+def test_rmsnorm_bwd_add_dw_equals_separate_passes(H, rows):
+    """smt_rmsnorm_bwd_add_dw (the warm-up's norm backward: weight gradient and residual-path add in
+    one pass) gives bit for bit the dx of smt_rmsnorm_bwd followed by autograd's bf16 add, and the
+    same dw; dw within bf16 rounding of the fp64 sum of the reference chain's per-row terms."""
+    torch.manual_seed(rows + H)
+    x = (torch.randn(rows, H, device=DEV) * 2).bfloat16()
+    w = (torch.randn(H, device=DEV) * 0.2 + 1.0).bfloat16()
+    dy = torch.randn(rows, H, device=DEV).bfloat16()
+    dres = torch.randn(rows, H, device=DEV).bfloat16()
+    rstd = torch.rsqrt(x.float().pow(2).mean(-1) + 1e-5)
+    dx0, dw0 = fl._rmsnorm_bwd(x, w, rstd, dy, True)
+    dx1, dw1 = fl._rmsnorm_bwd(x, w, rstd, dy, True, dres)
+    torch.cuda.synchronize()
+    assert torch.equal(dx1, dx0 + dres)
+    assert torch.equal(dw1, dw0)
+    terms = (dy.float() * (x.float() * rstd[:, None]).bfloat16().float()).bfloat16().double()
+    truth = terms.sum(0)
+    rel = ((dw1.double() - truth).norm() / truth.norm()).item()
+    assert rel < 4e-3, rel
