@@ -717,7 +717,9 @@ class SMTEngine:
                 self._norm_sq += _hip.sq_norm(tg.grad) * (gs * gs)
             dense_grads = [p.grad for _g, ps in self.dense_groups for p in ps if p.grad is not None]
             if dense_grads:
-                norms = torch._foreach_norm(dense_grads, 2.0)
+                # fp32-accumulated per-tensor norms (DeepSpeed takes fp32 norms of the gradients): the
+                # default for bf16 inputs returns each norm ROUNDED TO bf16 (~0.2 % off the clip)
+                norms = torch._foreach_norm(dense_grads, 2.0, dtype=torch.float32)
                 self._norm_sq += torch.stack([n.double() for n in norms]).pow(2).sum()
             norm = self._norm_sq
         for tg in self.tile_groups:

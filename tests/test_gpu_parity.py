@@ -239,6 +239,37 @@ def test_engine_sparse_adamw_step_matches_oracle():
     assert torch.equal(W1._smt_weight_t, W1.detach().t()) and torch.equal(W2._smt_weight_t, W2.detach().t())
 
 
+def test_engine_dense_warmup_step_matches_oracle():
+    """The full fine-tuning warm-up's dense step (DeepSpeed gradient_clipping + FusedAdam over every
+    parameter, fine_tune.py:160-190, 352-363): clip coefficient from the fp32 norms of the bf16
+    gradients (the oracle: fp64), then AdamW; several parameters, the clip active, 3 steps. With
+    per-tensor norms rounded to bf16 (torch._foreach_norm's default for bf16) the clip is off by up to
+    ~0.4 %, far outside this bar."""
+    torch.manual_seed(11)
+    net = nn.Sequential(nn.Linear(512, 768, bias=True), nn.Linear(768, 256, bias=False)).to(DEV).bfloat16()
+    p0 = [p.detach().float().cpu().clone() for p in net.parameters()]
+    opt = SMTFusedAdam([{"params": list(net.parameters()), "weight_decay": 0.01, "lr": 1e-3}], lr=1e-3, betas=(0.9, 0.95))
+    engine, _, _, _ = initialize(model=net, optimizer=opt, config={"gradient_clipping": 1.0})
+    masters = [t.clone() for t in p0]
+    ms = [torch.zeros_like(t) for t in masters]
+    vs = [torch.zeros_like(t) for t in masters]
+    for step in range(1, 4):
+        x = torch.randn(64, 512, device=DEV).bfloat16()
+        loss = (engine(x).float() ** 2).mean() * 1000.0
+        engine.backward(loss)
+        grads = [p.grad.detach().float().cpu().clone() for p in net.parameters()]
+        engine.step()
+        coef = ref.clip_coef(grads, 1.0)
+        assert coef < 0.5                                   # the clip is active
+        for t, g, m, v in zip(masters, grads, ms, vs):
+            ref.fused_adam_step(t, g * coef, m, v, step, 1e-3, (0.9, 0.95), 1e-8, 0.01)
+    torch.cuda.synchronize()
+    for p, t in zip(net.parameters(), masters):
+        st = engine._dense_state[id(p)]
+        assert _rel(st["master"].cpu(), t) < 1e-5
+        assert torch.equal(p.detach().cpu(), st["master"].cpu().bfloat16())
+
+
 def test_transposed_dgrad_matches_plain_dgrad():
     """The TN data gradient on W^T (SMT modules and frozen nn.Linear) vs g @ W."""
     from sparse_matrix_tuning_amd.engine import attach_transposed_weights, detach_transposed_weights
