@@ -188,7 +188,21 @@ __device__ __forceinline__ void dma_rows(__amdgpu_buffer_rsrc_t rsrc, int64_t ss
 // Forward: a workgroup = 4 waves x 32 query rows of one (b, q head); K/V tiles of 64 keys staged
 // through registers into a double-buffered LDS ring (issue-early / write-late), one barrier per tile.
 // ------------------------------------------------------------------------------------------------
-constexpr int kFwdQW = 32, kFwdWaves = 4, kFwdQB = kFwdQW * kFwdWaves, kKV = 64;
+// SMT_FWD_WAVES / SMT_DQ_WAVES: waves (x 32 query rows) per workgroup of the forward / dQ kernels.
+// Every workgroup stages its own K/V tiles, so 8 waves (256 query rows, one workgroup per CU) halve
+// the LDS-fill bytes per MFMA; measured at B16 Hq32 Hkv8 S2048 (profiles/r02_attn_waves.jsonl) the
+// 8-wave forward ran 7 % slower (0.89 vs 0.83 ms) and the 8-wave dQ the same: these loops are not
+// bound by the K/V fill, so 4 stays the default.
+#ifndef SMT_FWD_WAVES
+#define SMT_FWD_WAVES 4
+#endif
+#ifndef SMT_DQ_WAVES
+#define SMT_DQ_WAVES 4
+#endif
+constexpr int kFwdQW = 32, kFwdWaves = SMT_FWD_WAVES, kFwdQB = kFwdQW * kFwdWaves, kKV = 64;
+constexpr int kDqWaves = SMT_DQ_WAVES, kDqQB = kFwdQW * kDqWaves;
+static_assert(kFwdWaves == 4 || kFwdWaves == 8, "forward: 4 or 8 waves");
+static_assert(kDqWaves == 4 || kDqWaves == 8, "dQ: 4 or 8 waves");
 constexpr int kTileB = kKV * kRowB;        // 16 KiB per operand tile
 
 struct FwdArgs {
@@ -375,7 +389,7 @@ __device__ __forceinline__ void fwd_block(const FwdArgs& a, uint8_t* lds, int b,
     }
 }
 
-__global__ __launch_bounds__(256, 2)
+__global__ __launch_bounds__(64 * kFwdWaves, 8 / kFwdWaves)
 void attn_fwd_kernel(FwdArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kFRing * 2 * kFTileB];      // 64 KiB
     const int nqb = (a.S + kFwdQB - 1) / kFwdQB;
@@ -442,7 +456,7 @@ __device__ __forceinline__ void dq_block(const DqArgs& a, uint8_t* lds, int b, i
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int hi = lane >> 5, l32 = lane & 31;
-    const int q0 = qb * kFwdQB, qw = q0 + wave * kFwdQW;
+    const int q0 = qb * kDqQB, qw = q0 + wave * kFwdQW;
     const uint16_t* qp = a.q.p + b * a.q.sb + h * a.q.sh;
     const uint16_t* dop = a.dout.p + b * a.dout.sb + h * a.dout.sh;
     const uint16_t* kp = a.k.p + b * a.k.sb + hk * a.k.sh;
@@ -485,15 +499,16 @@ __device__ __forceinline__ void dq_block(const DqArgs& a, uint8_t* lds, int b, i
         dlt = qvalid ? a.delta[srow] : 0.f;
     }
 
-    const int kv_end = min(a.S, q0 + kFwdQB);
+    const int kv_end = min(a.S, q0 + kDqQB);
     const int nt = (kv_end + kKV - 1) / kKV;
     const __amdgpu_buffer_rsrc_t rk = uniform_rsrc(kp, (int64_t)a.S * a.k.ss * 2);
     const __amdgpu_buffer_rsrc_t rv = uniform_rsrc(vp, (int64_t)a.S * a.v.ss * 2);
     const uint32_t lds0 = lds_addr(lds);
     auto issue = [&](int t) {
         const uint32_t slot = lds0 + (uint32_t)((t & 1) * 2 * kTileB);
-        dma_rows(rk, a.k.ss, slot, t * kKV, t * kKV + 16 * wave, 4, lane);
-        dma_rows(rv, a.v.ss, slot + kTileB, t * kKV, t * kKV + 16 * wave, 4, lane);
+        constexpr int rows_w = kKV / kDqWaves;                 // rows of each operand tile one wave brings
+        dma_rows(rk, a.k.ss, slot, t * kKV, t * kKV + rows_w * wave, rows_w / 4, lane);
+        dma_rows(rv, a.v.ss, slot + kTileB, t * kKV, t * kKV + rows_w * wave, rows_w / 4, lane);
     };
 
     const TrLane tl = tr_lane(lane);
@@ -564,10 +579,10 @@ __device__ __forceinline__ void dq_block(const DqArgs& a, uint8_t* lds, int b, i
     }
 }
 
-__global__ __launch_bounds__(256, 2)
+__global__ __launch_bounds__(64 * kDqWaves, 8 / kDqWaves)
 void attn_dq_kernel(DqArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * 2 * kTileB];      // 64 KiB
-    const int nqb = (a.S + kFwdQB - 1) / kFwdQB;
+    const int nqb = (a.S + kDqQB - 1) / kDqQB;
     const int G = a.Hq / a.Hkv;
     const int total = nqb * a.Hq * a.B;
     // consecutive ids: the G heads of one (b, kv head) at one q block, heaviest (longest causal row)
@@ -802,7 +817,7 @@ int smt_attn_fwd(const smt_attn_tensor* q, const smt_attn_tensor* k, const smt_a
     const int64_t nqb = (shape->S + kFwdQB - 1) / kFwdQB;
     const int64_t blocks = nqb * shape->Hq * shape->B;
     if (blocks > 0x7fffffffLL) return fail(-1, "smt_attn_fwd: too many blocks");
-    hipLaunchKernelGGL(attn_fwd_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(attn_fwd_kernel, dim3((unsigned)blocks), dim3(64 * kFwdWaves), 0, stream, a);
     return check_launch("attn_fwd_kernel");
 }
 
@@ -833,8 +848,8 @@ int smt_attn_bwd(const smt_attn_tensor* q, const smt_attn_tensor* k, const smt_a
     qa.dq = static_cast<uint16_t*>(dq->ptr); qa.dq_sb = dq->sb; qa.dq_sh = dq->sh; qa.dq_ss = dq->ss;
     qa.lse = lse; qa.delta = delta_ws;
     qa.B = B; qa.Hq = Hq; qa.Hkv = Hkv; qa.S = S; qa.sl2 = sl2; qa.scale = shape->scale;
-    const int64_t nqb = (S + kFwdQB - 1) / kFwdQB;
-    hipLaunchKernelGGL(attn_dq_kernel, dim3((unsigned)(nqb * Hq * B)), dim3(256), 0, stream, qa);
+    const int64_t nqb = (S + kDqQB - 1) / kDqQB;
+    hipLaunchKernelGGL(attn_dq_kernel, dim3((unsigned)(nqb * Hq * B)), dim3(64 * kDqWaves), 0, stream, qa);
     if ((rc = check_launch("attn_dq_kernel"))) return rc;
 
     DkvArgs ka;
