@@ -151,6 +151,86 @@ def make_gradient_checkpointing_compatible(model) -> bool:
     return False
 
 
+def checkpointed_layers(model) -> List[torch.nn.Module]:
+    """The modules transformers' gradient checkpointing wraps (the decoder layers), in order."""
+    try:
+        from transformers.modeling_layers import GradientCheckpointingLayer
+    except ImportError:                       # older transformers: no per-layer switch
+        return []
+    return [m for m in model.modules() if isinstance(m, GradientCheckpointingLayer)
+            and hasattr(m, "_gradient_checkpointing_func")]
+
+
+def set_resident_layers(model, n_resident: int) -> int:
+    """MI355X memory policy for a model under per-layer recompute (fine_tune.py:192): keep the
+    activations of the LAST ``n_resident`` checkpointed layers resident (no recompute), recompute
+    the others. The reference recomputes every layer to fit its GPUs; with 288 GB of HBM the full
+    fine-tuning warm-up has room for most layers' activations beside the fp32 optimizer state.
+    Returns the number of layers left resident. Numerics are those of full recompute (the
+    recomputed forward is the same code on the same inputs)."""
+    layers = checkpointed_layers(model)
+    n = max(0, min(int(n_resident), len(layers)))
+    for i, m in enumerate(layers):
+        m.gradient_checkpointing = i < len(layers) - n
+    return n
+
+
+@torch.no_grad()
+def _rope_for(model, x: torch.Tensor):
+    rot = getattr(getattr(model, "model", model), "rotary_emb", None)
+    if rot is None:
+        return None
+    pos = torch.arange(x.shape[1], device=x.device).unsqueeze(0).expand(x.shape[0], -1)
+    return rot(x, pos)
+
+
+def layer_activation_bytes(model, batch: int, seq: int) -> int:
+    """HBM one decoder layer's saved activations take beyond its input (which recompute keeps
+    anyway) at ``batch`` x ``seq`` tokens, measured: one forward of the first checkpointed layer on a
+    random input with autograd recording (its weights' gradient state as it is), then freed."""
+    layers = checkpointed_layers(model)
+    if not layers:
+        return 0
+    layer = layers[0]
+    p = next(layer.parameters())
+    hidden = getattr(getattr(model, "config", None), "hidden_size", None) or p.shape[-1]
+    x = torch.randn(batch, seq, hidden, device=p.device, dtype=p.dtype, requires_grad=True)
+    pe = _rope_for(model, x)
+    was = layer.gradient_checkpointing
+    layer.gradient_checkpointing = False
+    torch.cuda.synchronize(p.device)
+    m0 = torch.cuda.memory_allocated(p.device)
+    try:
+        with torch.enable_grad():
+            out = layer(x, position_embeddings=pe)
+            out = out[0] if isinstance(out, tuple) else out
+            torch.cuda.synchronize(p.device)
+            used = torch.cuda.memory_allocated(p.device) - m0 - out.numel() * out.element_size()
+        del out
+    finally:
+        layer.gradient_checkpointing = was
+    del x
+    return max(0, int(used))
+
+
+def resident_layers_for(model, batch: int, seq: int, peak_bytes: int, reserve_frac: float = 0.25) -> int:
+    """How many checkpointed layers can keep their activations resident: the HBM left above
+    ``peak_bytes`` (a step's peak with every layer recomputed) minus ``reserve_frac`` of the device
+    for allocator fragmentation and backward transients, over :func:`layer_activation_bytes`. (At
+    the LLaMA-3-8B warm-up, B 16 x S 2048: 3.7 GB per layer; a 12 % reserve put the step's peak at
+    280 GB of 309, hence 25 %.)"""
+    layers = checkpointed_layers(model)
+    if not layers:
+        return 0
+    dev = next(layers[0].parameters()).device
+    total = torch.cuda.get_device_properties(dev).total_memory
+    per = layer_activation_bytes(model, batch, seq)
+    room = total * (1.0 - reserve_frac) - peak_bytes
+    if per <= 0 or room <= 0:
+        return 0
+    return min(len(layers), int(room // per))
+
+
 def select_and_convert(engine, harvester: GradHarvester, targeted_module_dims: dict,
                        num_attention_blocks: int, num_mlp_blocks: int, *, selection_strategy="no_restriction",
                        calculate_strategy="mean_abs", no_limit_mixture=False, w_decay=0.0, smt_lr=9.865e-6,
