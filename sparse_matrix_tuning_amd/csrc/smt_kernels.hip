@@ -337,10 +337,20 @@ typedef __attribute__((address_space(3))) uint8_t lds_u8_t;
 // (with the builtin it puts s_waitcnt vmcnt(0) before every ds_read, draining the 2-deep pipeline);
 // completion is tracked by the hand-counted vmcnt in the loop. M0 is saved / restored inside the
 // statement (cdna_hip_programming §5.7).
+// SMT_DMA_NT=1: the operand stream with the non-temporal cache policy (A/B builds; measured the same
+// as the default policy on the bench's batched launches: profiles/r02_wgrad_nt_ab.jsonl)
+#ifndef SMT_DMA_NT
+#define SMT_DMA_NT 0
+#endif
+#if SMT_DMA_NT
+#define SMT_DMA_POLICY " nt lds"
+#else
+#define SMT_DMA_POLICY " lds"
+#endif
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, uint32_t lds_base, int voff) {
     uint32_t keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
-                 "buffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                 "buffer_load_dwordx4 %1, %2, 0 offen" SMT_DMA_POLICY "\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(lds_base) : "memory");
 }
 
