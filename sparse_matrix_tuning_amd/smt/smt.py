@@ -689,6 +689,8 @@ class linearChannel(torch.autograd.Function):
             x2 = _rows_ready(input.reshape(-1, input.shape[-1]))
             partial = _hip.column_gather(x2, ch.device_table(x2.device), len(ch), ch.padded)
         ctx.save_for_backward(partial, weight)
+        # q/k/v share their input: their data gradients accumulate in one buffer (dgrad.py)
+        ctx.acc = dgrad.register(input, ctx)
         return torch.matmul(input, weight.t())
 
     @staticmethod
@@ -719,7 +721,7 @@ class linearChannel(torch.autograd.Function):
                 _hip.tile_scatter(dense, table, tiles)
                 grad_weight = dense[:k]
         if ctx.needs_input_grad[0]:
-            grad_input = torch.matmul(grad_output, weight)
+            grad_input = dgrad.input_grad(ctx.acc, grad_output, weight)
         return grad_input, grad_weight, None, None
 
 

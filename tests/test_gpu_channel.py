@@ -334,3 +334,20 @@ def test_exact_channel_scores_skip_the_host_rescore():
     want = ref.select_channel({k: v.cpu() for k, v in acts.items()}, 40)
     assert {k: list(v) for k, v in got.items()} == {k: list(v) for k, v in want.items()}
     assert list(got) == list(want)
+
+
+def test_channel_modules_share_input_gradient_accumulation():
+    """q/k/v channel modules reading one input accumulate their data gradients in one buffer
+    (dgrad.py), also when one of them does not reach the loss: the input gradient equals the fp64
+    sum over the consumers that ran."""
+    torch.manual_seed(21)
+    Ws = [nn.Parameter((torch.randn(512, 512) * 0.05).bfloat16().to(DEV), requires_grad=False) for _ in range(3)]
+    mods = [smt.LinearLayer_ChannelSparsity(W, index_list=idx) for W, idx in zip(Ws, ([3, 100, 7], [0, 511], [42]))]
+    x = torch.randn(2, 96, 512).bfloat16().to(DEV)
+    gs = [torch.randn(2, 96, 512).bfloat16().to(DEV) for _ in mods]
+    for used in ((0, 1, 2), (0, 2)):
+        xi = x.clone().requires_grad_(True)
+        outs = [m(xi) for m in mods]
+        torch.autograd.backward([outs[i] for i in used], [gs[i] for i in used])
+        truth = sum(gs[i].double() @ mods[i].weight.detach().double() for i in used)
+        assert ((xi.grad.double() - truth).norm() / truth.norm()).item() < 5e-3, used
