@@ -43,7 +43,7 @@ import torch
 import torch.distributed as dist
 
 from . import _hip, dgrad
-from .smt.smt import LinearLayer_MatrixSparsity
+from .smt.smt import LinearLayer_ChannelSparsity, LinearLayer_MatrixSparsity
 
 TILE_ELEMS = _hip.TILE_ELEMS
 
@@ -182,11 +182,13 @@ def attach_transposed_weights(model: torch.nn.Module) -> int:
     copies are skipped. Returns the bytes added."""
     added = 0
     for m in model.modules():
-        if isinstance(m, LinearLayer_MatrixSparsity) or type(m) is torch.nn.Linear:
+        if isinstance(m, (LinearLayer_MatrixSparsity, LinearLayer_ChannelSparsity)) or type(m) is torch.nn.Linear:
             w = m.weight
             if (not _transposable(w) or getattr(w, "_smt_weight_t", None) is not None
                     or getattr(w, "_smt_fp8", None) is not None):
                 continue
+            if isinstance(m, LinearLayer_ChannelSparsity):
+                m.sync_weight()                 # W^T is taken from W with the current rows in it
             w._smt_weight_t = w.detach().t().contiguous()
             added += w.numel() * w.element_size()
             if type(m) is torch.nn.Linear:
@@ -592,14 +594,19 @@ class SMTEngine:
         self.fp8_bytes = 0
         if optimizer is not None:
             owner = {}
+            channel_rows = False
             for m in model.modules():
                 if isinstance(m, LinearLayer_MatrixSparsity) and m.selected_weight.requires_grad and len(m.tiles):
                     owner[id(m.selected_weight)] = m
+                if isinstance(m, LinearLayer_ChannelSparsity) and m.selected_weight.requires_grad:
+                    channel_rows = True
             if owner and cfg.get("fp8_linears", False):
                 # config 5: e4m3 copies of the decoder-layer weights (re-quantised after each step)
                 self.fp8_bytes = attach_fp8_weights(model)
-            if owner and cfg.get("transposed_dgrad", True):
-                # SMT phase: every linear weight is frozen (tiles change only through the epilogue)
+            if (owner or channel_rows) and cfg.get("transposed_dgrad", True):
+                # SMT phase: every linear weight is frozen (tiles change only through the epilogue;
+                # the channel path's rows through LinearLayer_ChannelSparsity.sync_weight, which keeps
+                # W^T in step)
                 self.transposed_bytes = attach_transposed_weights(model)
             for group in optimizer.param_groups:
                 mods = [owner[id(p)] for p in group["params"] if id(p) in owner]

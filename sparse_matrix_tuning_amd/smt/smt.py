@@ -592,6 +592,14 @@ class ChannelIndex:
             self._dev[key] = t
         return t
 
+    def long_index(self, device: torch.device) -> torch.Tensor:
+        """int64 device index (torch indexing ops: the column write into a transposed W copy)."""
+        key = ("long", device.type, device.index)
+        t = self._dev.get(key)
+        if t is None:
+            t = self._dev[key] = torch.tensor(self.index_list, dtype=torch.int64).to(device)
+        return t
+
     def wgrad_tiles(self, out_features: int, device: torch.device) -> torch.Tensor:
         """int32 [(k_pad/256) * (out/256), 2] table covering the [k_pad, out] channel gradient."""
         key = ("tiles", out_features, device.type, device.index)
@@ -649,10 +657,15 @@ class LinearLayer_ChannelSparsity(torch.nn.Module):
         self.fn = linearChannel.apply
 
     def sync_weight(self) -> None:
-        """Scatter the rows into W (smt.py:208-213) with one launch."""
+        """Scatter the rows into W (smt.py:208-213) with one launch, and into the columns of the
+        transposed copy W^T when the engine attached one (the data gradient's TN operand)."""
         w = self.weight.data
         if len(self.channels) and w.device.type == "cuda":
-            _hip.row_scatter(w, self.channels.device_table(w.device), self.selected_weight.data)
+            table = self.channels.device_table(w.device)
+            _hip.row_scatter(w, table, self.selected_weight.data)
+            wt = getattr(self.weight, "_smt_weight_t", None)
+            if wt is not None:
+                wt.index_copy_(1, self.channels.long_index(w.device), self.selected_weight.data.t())
 
     def forward(self, x):
         if self.writeback_on_forward:
@@ -721,7 +734,9 @@ class linearChannel(torch.autograd.Function):
                 _hip.tile_scatter(dense, table, tiles)
                 grad_weight = dense[:k]
         if ctx.needs_input_grad[0]:
-            grad_input = dgrad.input_grad(ctx.acc, grad_output, weight)
+            # g @ W, as the TN product g @ (W^T)^T when the engine attached the transposed copy
+            wt = getattr(weight, "_smt_weight_t", None)
+            grad_input = dgrad.input_grad(ctx.acc, grad_output, weight if wt is None else wt.t())
         return grad_input, grad_weight, None, None
 
 

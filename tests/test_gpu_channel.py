@@ -351,3 +351,38 @@ def test_channel_modules_share_input_gradient_accumulation():
         torch.autograd.backward([outs[i] for i in used], [gs[i] for i in used])
         truth = sum(gs[i].double() @ mods[i].weight.detach().double() for i in used)
         assert ((xi.grad.double() - truth).norm() / truth.norm()).item() < 5e-3, used
+
+
+def test_channel_engine_transposed_copies_follow_the_rows():
+    """Under the engine the channel path's frozen weights get transposed copies (the TN data-gradient
+    layout): every row update reaches W^T's columns through sync_weight, the data gradient through
+    W^T equals the plain one to GEMM rounding, and the rows' training matches the run without copies."""
+    from sparse_matrix_tuning_amd.engine import SMTFusedAdam, initialize
+
+    def run(transposed):
+        torch.manual_seed(23)
+        net = nn.Module()
+        W = nn.Parameter((torch.randn(512, 512) * 0.05).bfloat16().to(DEV), requires_grad=False)
+        net.q = smt.LinearLayer_ChannelSparsity(W, index_list=[5, 300, 17])
+        net.o = nn.Linear(512, 512, bias=False).to(DEV).bfloat16().requires_grad_(False)
+        opt = SMTFusedAdam([net.q.selected_weight], lr=1e-2)
+        engine, *_ = initialize(model=net, optimizer=opt, config={"transposed_dgrad": transposed})
+        assert (getattr(W, "_smt_weight_t", None) is not None) == transposed
+        x = torch.randn(2, 64, 512).bfloat16().to(DEV)
+        grads = []
+        for _ in range(3):
+            xi = x.clone().requires_grad_(True)
+            loss = net.o(net.q(xi)).float().pow(2).mean()
+            engine.backward(loss)
+            grads.append(xi.grad.clone())
+            engine.step()
+            net.q.sync_weight()
+            if transposed:
+                assert torch.equal(W._smt_weight_t, W.detach().t())
+        return grads, net.q.selected_weight.detach().clone()
+
+    g0, r0 = run(False)
+    g1, r1 = run(True)
+    for a, b in zip(g1, g0):
+        assert _rel(a, b) < 1e-2
+    assert _rel(r1, r0) < 1e-2
