@@ -53,6 +53,22 @@ __device__ __forceinline__ F8 ld8(const uint16_t* p) {
     return r;
 }
 
+// bf16 bits of 8 floats (RNE; exact for values that are bf16 already) and back
+__device__ __forceinline__ uint4 pack8(const F8& r) {
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = tobf(r.v[2 * j]) | (tobf(r.v[2 * j + 1]) << 16);
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__device__ __forceinline__ F8 unpack8(const uint4 a) {
+    F8 r;
+    const uint32_t w[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { r.v[2 * j] = bf(w[j] & 0xffffu); r.v[2 * j + 1] = bf(w[j] >> 16); }
+    return r;
+}
+
 __device__ __forceinline__ void st8(uint16_t* p, const F8& r) {
     uint32_t w[4];
 #pragma unroll
@@ -241,7 +257,7 @@ void rmsnorm_fwd_reg_kernel(const uint16_t* __restrict__ x, int64_t ldx, const u
 // Backward without weight grad; with ADD the gradient reaching the norm's input by the residual path
 // is added as autograd would: dx = bf16(bf16(dx_norm) + dres).
 template <int CPL, bool ADD, bool QUANT = false>
-__global__ __launch_bounds__(256)
+__global__ __launch_bounds__(256, CPL <= 10 ? 2 : 1)        // two waves per SIMD up to hidden 5120
 void rmsnorm_bwd_reg_kernel(const uint16_t* __restrict__ dy, int64_t lddy, const uint16_t* __restrict__ x, int64_t ldx,
                             const uint16_t* __restrict__ w, const float* __restrict__ rstd,
                             const uint16_t* __restrict__ dres, int64_t lddr, uint16_t* __restrict__ dx, int64_t lddx,
@@ -251,55 +267,61 @@ void rmsnorm_bwd_reg_kernel(const uint16_t* __restrict__ dy, int64_t lddy, const
     const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= rows) return;
     const float r = rstd[row];
-    F8 gw[CPL], xv[CPL];
+    // the row's x and bf16(dy * w) stay in registers as packed bf16 (both are bf16 values, so this is
+    // exact): half the registers of fp32 copies, two waves per SIMD at CPL 8 and 10
+    uint4 xr[CPL], gr[CPL];
     float dot = 0.f;
 #pragma unroll
     for (int k = 0; k < CPL; ++k) {
         const int c = lane + 64 * k;
-        xv[k] = ld8(x + row * ldx + c * 8);
-        const F8 gv = ld8(dy + row * lddy + c * 8), wv = ld8(w + c * 8);
+        xr[k] = *reinterpret_cast<const uint4*>(x + row * ldx + c * 8);
+        const F8 xv = unpack8(xr[k]), gv = ld8(dy + row * lddy + c * 8), wv = ld8(w + c * 8);
+        F8 gw;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            gw[k].v[j] = rbf(gv.v[j] * wv.v[j]);
-            dot += gw[k].v[j] * xv[k].v[j];
+            gw.v[j] = rbf(gv.v[j] * wv.v[j]);
+            dot += gw.v[j] * xv.v[j];
         }
+        gr[k] = pack8(gw);
     }
     dot = wave_sum_f(dot);
     const float coef = r * r * r * dot / (float)H;
+    asm volatile("" ::: "memory");                 // the residual-gradient loads stay in this pass
 #pragma unroll
     for (int k = 0; k < CPL; ++k) {
         const int c = lane + 64 * k;
+        const F8 xv = unpack8(xr[k]), gw = unpack8(gr[k]);
         F8 o;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o.v[j] = r * gw[k].v[j] - xv[k].v[j] * coef;
+        for (int j = 0; j < 8; ++j) o.v[j] = r * gw.v[j] - xv.v[j] * coef;
         if (ADD) {
             const F8 dr = ld8(dres + row * lddr + c * 8);
 #pragma unroll
             for (int j = 0; j < 8; ++j) o.v[j] = rbf(o.v[j]) + dr.v[j];
         }
         st8(dx + row * lddx + c * 8, o);
-        if (QUANT) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) gw[k].v[j] = rbf(o.v[j]);     // the stored bf16 dx, kept for the e4m3 pass
-        }
+        if (QUANT) gr[k] = pack8(o);                  // the stored bf16 dx, kept for the e4m3 pass
     }
     if (QUANT) {
         // dx also as one e4m3 row + scale (the data-gradient GEMM operand of the fp8 linear that
         // consumes this gradient), exactly as smt_quant_rows_e4m3 would quantise the stored dx
         float amax = 0.f;
 #pragma unroll
-        for (int k = 0; k < CPL; ++k)
+        for (int k = 0; k < CPL; ++k) {
+            const F8 d = unpack8(gr[k]);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(gw[k].v[j]));
+            for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(d.v[j]));
+        }
         amax = wave_max_f(amax);
         const float scale = e4m3_scale(amax);
         if (lane == 0) qscale[row] = scale;
 #pragma unroll
         for (int k = 0; k < CPL; ++k) {
             const int c = lane + 64 * k;
+            const F8 d = unpack8(gr[k]);
             uint2 q;
-            q.x = pack4(qv(gw[k].v[0], scale), qv(gw[k].v[1], scale), qv(gw[k].v[2], scale), qv(gw[k].v[3], scale));
-            q.y = pack4(qv(gw[k].v[4], scale), qv(gw[k].v[5], scale), qv(gw[k].v[6], scale), qv(gw[k].v[7], scale));
+            q.x = pack4(qv(d.v[0], scale), qv(d.v[1], scale), qv(d.v[2], scale), qv(d.v[3], scale));
+            q.y = pack4(qv(d.v[4], scale), qv(d.v[5], scale), qv(d.v[6], scale), qv(d.v[7], scale));
             *reinterpret_cast<uint2*>(q8 + row * ldq + c * 8) = q;
         }
     }
