@@ -69,6 +69,28 @@ __device__ __forceinline__ F8 unpack8(const uint4 a) {
     return r;
 }
 
+// Row values kept in registers by the register-resident kernels: fp32 (PACK = false) or packed
+// bf16 bits (PACK = true; exact for values that are bf16 already).
+__device__ __forceinline__ F8 rbf8(const F8& v) {
+    F8 r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r.v[j] = rbf(v.v[j]);
+    return r;
+}
+template <bool PACK> struct RowReg;
+template <> struct RowReg<false> {
+    typedef F8 T;
+    static __device__ __forceinline__ T keep(const uint4 raw) { return unpack8(raw); }
+    static __device__ __forceinline__ T put(const F8& v) { return v; }
+    static __device__ __forceinline__ F8 get(const T& v) { return v; }
+};
+template <> struct RowReg<true> {
+    typedef uint4 T;
+    static __device__ __forceinline__ T keep(const uint4 raw) { return raw; }
+    static __device__ __forceinline__ T put(const F8& v) { return pack8(v); }
+    static __device__ __forceinline__ F8 get(const T& v) { return unpack8(v); }
+};
+
 __device__ __forceinline__ void st8(uint16_t* p, const F8& r) {
     uint32_t w[4];
 #pragma unroll
@@ -267,30 +289,33 @@ void rmsnorm_bwd_reg_kernel(const uint16_t* __restrict__ dy, int64_t lddy, const
     const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= rows) return;
     const float r = rstd[row];
-    // the row's x and bf16(dy * w) stay in registers as packed bf16 (both are bf16 values, so this is
-    // exact): half the registers of fp32 copies, two waves per SIMD at CPL 8 and 10
-    uint4 xr[CPL], gr[CPL];
+    // the row's x and bf16(dy * w) stay in registers; above CPL 8 as packed bf16 (both are bf16
+    // values, so this is exact): half the registers of fp32 copies, two waves per SIMD at CPL 10
+    // instead of one (at CPL 8 the fp32 copies fit two waves, and the packing only adds ALU work)
+    constexpr bool PACK = CPL > 8;
+    typename RowReg<PACK>::T xr[CPL], gr[CPL];
     float dot = 0.f;
 #pragma unroll
     for (int k = 0; k < CPL; ++k) {
         const int c = lane + 64 * k;
-        xr[k] = *reinterpret_cast<const uint4*>(x + row * ldx + c * 8);
-        const F8 xv = unpack8(xr[k]), gv = ld8(dy + row * lddy + c * 8), wv = ld8(w + c * 8);
+        const uint4 xraw = *reinterpret_cast<const uint4*>(x + row * ldx + c * 8);
+        xr[k] = RowReg<PACK>::keep(xraw);
+        const F8 xv = unpack8(xraw), gv = ld8(dy + row * lddy + c * 8), wv = ld8(w + c * 8);
         F8 gw;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             gw.v[j] = rbf(gv.v[j] * wv.v[j]);
             dot += gw.v[j] * xv.v[j];
         }
-        gr[k] = pack8(gw);
+        gr[k] = RowReg<PACK>::put(gw);
     }
     dot = wave_sum_f(dot);
     const float coef = r * r * r * dot / (float)H;
-    asm volatile("" ::: "memory");                 // the residual-gradient loads stay in this pass
+    if constexpr (PACK) asm volatile("" ::: "memory");   // the residual-gradient loads stay in this pass
 #pragma unroll
     for (int k = 0; k < CPL; ++k) {
         const int c = lane + 64 * k;
-        const F8 xv = unpack8(xr[k]), gw = unpack8(gr[k]);
+        const F8 xv = RowReg<PACK>::get(xr[k]), gw = RowReg<PACK>::get(gr[k]);
         F8 o;
 #pragma unroll
         for (int j = 0; j < 8; ++j) o.v[j] = r * gw.v[j] - xv.v[j] * coef;
@@ -300,7 +325,7 @@ void rmsnorm_bwd_reg_kernel(const uint16_t* __restrict__ dy, int64_t lddy, const
             for (int j = 0; j < 8; ++j) o.v[j] = rbf(o.v[j]) + dr.v[j];
         }
         st8(dx + row * lddx + c * 8, o);
-        if (QUANT) gr[k] = pack8(o);                  // the stored bf16 dx, kept for the e4m3 pass
+        if (QUANT) gr[k] = RowReg<PACK>::put(rbf8(o));   // the stored bf16 dx, kept for the e4m3 pass
     }
     if (QUANT) {
         // dx also as one e4m3 row + scale (the data-gradient GEMM operand of the fp8 linear that
@@ -308,7 +333,7 @@ void rmsnorm_bwd_reg_kernel(const uint16_t* __restrict__ dy, int64_t lddy, const
         float amax = 0.f;
 #pragma unroll
         for (int k = 0; k < CPL; ++k) {
-            const F8 d = unpack8(gr[k]);
+            const F8 d = RowReg<PACK>::get(gr[k]);
 #pragma unroll
             for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(d.v[j]));
         }
@@ -318,7 +343,7 @@ void rmsnorm_bwd_reg_kernel(const uint16_t* __restrict__ dy, int64_t lddy, const
 #pragma unroll
         for (int k = 0; k < CPL; ++k) {
             const int c = lane + 64 * k;
-            const F8 d = unpack8(gr[k]);
+            const F8 d = RowReg<PACK>::get(gr[k]);
             uint2 q;
             q.x = pack4(qv(d.v[0], scale), qv(d.v[1], scale), qv(d.v[2], scale), qv(d.v[3], scale));
             q.y = pack4(qv(d.v[4], scale), qv(d.v[5], scale), qv(d.v[6], scale), qv(d.v[7], scale));
@@ -371,17 +396,17 @@ struct RopeT {
     int H;
 };
 
+// One (b, head) row block per blockIdx.y (q heads first, then k heads: wave-uniform), the
+// (s, 8-pair chunk) index on blockIdx.x * 256 + tid with 32-bit arithmetic (the flat 64-bit
+// div / mod chain of a 1-D grid cost more than the bytes).
 template <bool BWD>
-__device__ __forceinline__ void rope_one(const RopeT& t, const uint16_t* cos, const uint16_t* sin, int64_t cb,
-                                         int64_t cs, int64_t idx, int S, int D) {
+__device__ __forceinline__ void rope_row(const RopeT& t, const uint16_t* cos, const uint16_t* sin, int64_t cb,
+                                         int64_t cs, int64_t b, int h, int idx, int S, int D) {
     const int half = D >> 1;
     const int cpr = half >> 3;                        // 8-pair chunks per head row
-    const int c = (int)(idx % cpr);
-    int64_t rest = idx / cpr;
-    const int s = (int)(rest % S); rest /= S;
-    const int h = (int)(rest % t.H);
-    const int64_t b = rest / t.H;
-    const int d = c * 8;
+    const int s = idx / cpr;
+    if (s >= S) return;
+    const int d = (idx - s * cpr) * 8;
     const uint16_t* ip = t.in + b * t.sb + h * t.sh + (int64_t)s * t.ss;
     uint16_t* op = t.out + b * t.ob + h * t.oh + (int64_t)s * t.os;
     const uint16_t* cp = cos + b * cb + (int64_t)s * cs;
@@ -407,12 +432,13 @@ template <bool BWD>
 __global__ __launch_bounds__(256)
 void rope_kernel(RopeT q, RopeT k, const uint16_t* __restrict__ cos, const uint16_t* __restrict__ sin,
                  int64_t cb, int64_t cs, int64_t B, int S, int D) {
-    const int64_t cpr = D >> 4;
-    const int64_t nq = B * q.H * (int64_t)S * cpr;
-    const int64_t nk = B * k.H * (int64_t)S * cpr;
-    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (idx < nq) rope_one<BWD>(q, cos, sin, cb, cs, idx, S, D);
-    else if (idx < nq + nk) rope_one<BWD>(k, cos, sin, cb, cs, idx - nq, S, D);
+    const int heads = q.H + k.H;
+    const int y = blockIdx.y;                         // b * heads + head
+    const int64_t b = y / heads;
+    const int hh = y - (int)b * heads;
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (hh < q.H) rope_row<BWD>(q, cos, sin, cb, cs, b, hh, idx, S, D);
+    else rope_row<BWD>(k, cos, sin, cb, cs, b, hh - q.H, idx, S, D);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -831,14 +857,18 @@ static int rope(bool bwd, const smt_rope_tensor* q, const smt_rope_tensor* k, co
     const int64_t strides[] = {q->in_sb, q->in_sh, q->in_ss, q->out_sb, q->out_sh, q->out_ss,
                                k->in_sb, k->in_sh, k->in_ss, k->out_sb, k->out_sh, k->out_ss, cos_sb, cos_ss};
     for (int64_t s : strides) if (s & 7) return fail(-2, "smt_rope: strides must be multiples of 8 elements");
-    const int64_t total = B * (int64_t)(q->heads + k->heads) * S * (D / 16);
-    if (total == 0) return 0;
-    const int64_t blocks = (total + 255) / 256;
+    const int64_t rows = B * (int64_t)(q->heads + k->heads);
+    const int64_t per_row = (int64_t)S * (D / 16);
+    if (rows == 0 || per_row == 0) return 0;
+    if (rows > 65535 || per_row > 0x7fffffffLL - 255)
+        return fail(-1, "smt_rope: %lld (batch x heads) rows of %lld chunks exceed the grid", (long long)rows,
+                    (long long)per_row);
+    const dim3 grid((unsigned)((per_row + 255) / 256), (unsigned)rows);
     if (bwd)
-        hipLaunchKernelGGL(rope_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, stream, tq, tk, (const uint16_t*)cos,
+        hipLaunchKernelGGL(rope_kernel<true>, grid, dim3(256), 0, stream, tq, tk, (const uint16_t*)cos,
                            (const uint16_t*)sin, cos_sb, cos_ss, B, S, D);
     else
-        hipLaunchKernelGGL(rope_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, stream, tq, tk, (const uint16_t*)cos,
+        hipLaunchKernelGGL(rope_kernel<false>, grid, dim3(256), 0, stream, tq, tk, (const uint16_t*)cos,
                            (const uint16_t*)sin, cos_sb, cos_ss, B, S, D);
     return check_launch("rope_kernel");
 }
