@@ -341,3 +341,24 @@ def test_top_level_smt_package_serves_fine_tune_imports():
     assert select_submatrix_based_on_grads is smt_helper.select_submatrix_based_on_grads
     import torch.distributed as dist
     assert not dist.is_initialized()                 # no process group at import (smt.py:20 does one)
+
+
+def test_resident_layers_policy_host_logic():
+    """trainer.checkpointed_layers / set_resident_layers on a meta-device LLaMA with transformers'
+    gradient checkpointing: the LAST n decoder layers stop recomputing, n is clamped, 0 restores the
+    reference's recompute-everything policy."""
+    from transformers import LlamaConfig, LlamaForCausalLM
+    cfg = LlamaConfig(vocab_size=512, hidden_size=256, intermediate_size=512, num_hidden_layers=5,
+                      num_attention_heads=4, num_key_value_heads=2)
+    with torch.device("meta"):
+        model = LlamaForCausalLM(cfg)
+    assert trainer.checkpointed_layers(model) == []          # not checkpointing: nothing to switch
+    model.gradient_checkpointing_enable()
+    layers = trainer.checkpointed_layers(model)
+    assert len(layers) == 5 and all(m.gradient_checkpointing for m in layers)
+    assert trainer.set_resident_layers(model, 2) == 2
+    assert [m.gradient_checkpointing for m in layers] == [True, True, True, False, False]
+    assert trainer.set_resident_layers(model, 99) == 5
+    assert not any(m.gradient_checkpointing for m in layers)
+    assert trainer.set_resident_layers(model, 0) == 0
+    assert all(m.gradient_checkpointing for m in layers)
