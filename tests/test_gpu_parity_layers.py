@@ -1,5 +1,6 @@
 """End-to-end parity at the LLaMA-3-8B LAYER geometry (hidden 4096, intermediate 14336, 32 query /
-8 key-value heads of 128, one sequence of S = 2048): one decoder layer of the product path (fused
+8 key-value heads of 128, one sequence of S = 2048), and at LLaMA-2-13B's (hidden 5120, 40 heads, two
+sequences of 1024, so the reference's per-sample bf16 rounding is exercised): one decoder layer of the product path (fused
 RMSNorm / RoPE / SwiGLU, smt_flash attention, smt_ce loss: fused_llama.patch_llama; SMT modules on
 q/k/v/o/gate/up/down with tiles in every block row range) against the CPU restatement of the
 reference modules (oracle.ref_convert + transformers' eager LLaMA on the host). SURVEY §8(c):
@@ -19,6 +20,20 @@ DEV = torch.device("cuda", 0)
 CFG = dict(vocab_size=4096, hidden_size=4096, intermediate_size=14336, num_hidden_layers=1,
            num_attention_heads=32, num_key_value_heads=8, rope_theta=500000.0, rms_norm_eps=1e-5,
            tie_word_embeddings=False, max_position_embeddings=4096)
+# LLaMA-2-13B's layer (config 4's model, here on the matrix path): 40 heads without GQA, 13824 wide MLP
+CFG_13B = dict(CFG, hidden_size=5120, intermediate_size=13824, num_attention_heads=40, num_key_value_heads=40,
+               rope_theta=10000.0)
+CASES = {
+    "llama3-8b layer, B1 S2048": (CFG, 1, 2048,
+                                  {("q_proj", 0): [(15, 3), (0, 0), (7, 12)], ("k_proj", 0): [(3, 15), (0, 1)],
+                                   ("v_proj", 0): [(2, 2)]},
+                                  {("gate_proj", 0): [(55, 0), (10, 9)], ("up_proj", 0): [(0, 15), (31, 4), (12, 12)],
+                                   ("down_proj", 0): [(15, 55), (4, 20)]}),
+    "llama2-13b layer, B2 S1024": (CFG_13B, 2, 1024,
+                                   {("q_proj", 0): [(19, 0), (3, 7)], ("k_proj", 0): [(0, 19)], ("v_proj", 0): [(10, 10)]},
+                                   {("gate_proj", 0): [(53, 19), (0, 0)], ("up_proj", 0): [(20, 5)],
+                                    ("down_proj", 0): [(19, 53), (2, 30)]}),
+}
 
 
 def _rel(a, b):
@@ -26,9 +41,9 @@ def _rel(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-300)).item()
 
 
-def _build(device):
+def _build(device, cfg_dict):
     from transformers import LlamaConfig, LlamaForCausalLM
-    cfg = LlamaConfig(**CFG)
+    cfg = LlamaConfig(**cfg_dict)
     cfg._attn_implementation = "sdpa" if device.type == "cuda" else "eager"
     torch.manual_seed(2024)
     prev = torch.get_default_dtype()
@@ -40,24 +55,24 @@ def _build(device):
         torch.set_default_dtype(prev)
 
 
-def test_llama3_8b_layer_loss_and_tile_grads_vs_reference_restatement():
+@pytest.mark.parametrize("case", list(CASES))
+def test_layer_loss_and_tile_grads_vs_reference_restatement(case):
     from sparse_matrix_tuning_amd.fused_llama import patch_llama, unpatch_llama
-    model = _build(DEV)
+    cfg, B, S, att, mlp = CASES[case]
+    model = _build(DEV, cfg)
     sd = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
-    sel_att = defaultdict(list, {("q_proj", 0): [(15, 3), (0, 0), (7, 12)], ("k_proj", 0): [(3, 15), (0, 1)],
-                                 ("v_proj", 0): [(2, 2)]})
-    sel_mlp = defaultdict(list, {("gate_proj", 0): [(55, 0), (10, 9)], ("up_proj", 0): [(0, 15), (31, 4), (12, 12)],
-                                 ("down_proj", 0): [(15, 55), (4, 20)]})
+    sel_att = defaultdict(list, att)
+    sel_mlp = defaultdict(list, mlp)
     smt.freeze_unselected_matrix_layer(model, sel_mlp, sel_att)
     smt.convert_linear_layer_to_matrix_sparsity(model, sel_mlp, sel_att)
     patch_llama(model)
     try:
-        _gpu_and_host(model, sd, sel_mlp, sel_att, unpatch_llama)
+        _gpu_and_host(model, sd, sel_mlp, sel_att, unpatch_llama, cfg, B, S)
     finally:
         unpatch_llama()
 
 
-def _gpu_and_host(model, sd, sel_mlp, sel_att, unpatch_llama):
+def _gpu_and_host(model, sd, sel_mlp, sel_att, unpatch_llama, cfg, B, S):
     gpu_mods = {n: m for n, m in model.named_modules() if isinstance(m, smt.LinearLayer_MatrixSparsity)}
     assert len(gpu_mods) == 6
     seen_x, seen_g = {}, {}
@@ -68,7 +83,7 @@ def _gpu_and_host(model, sd, sel_mlp, sel_att, unpatch_llama):
             out.register_hook(lambda g: seen_g.__setitem__(name, g.detach().clone()))
         return hook
     handles = [m.register_forward_hook(capture(n)) for n, m in gpu_mods.items()]
-    ids = torch.randint(0, CFG["vocab_size"], (1, 2048), generator=torch.Generator().manual_seed(5))
+    ids = torch.randint(0, cfg["vocab_size"], (B, S), generator=torch.Generator().manual_seed(5))
     out = model(input_ids=ids.to(DEV), labels=ids.to(DEV), use_cache=False)
     out.loss.backward()
     torch.cuda.synchronize()
@@ -76,7 +91,7 @@ def _gpu_and_host(model, sd, sel_mlp, sel_att, unpatch_llama):
         h.remove()
 
     unpatch_llama()                     # the host model runs transformers' own modules
-    cpu = _build(torch.device("cpu"))
+    cpu = _build(torch.device("cpu"), cfg)
     cpu.load_state_dict(sd)
     smt.freeze_unselected_matrix_layer(cpu, sel_mlp, sel_att)
     ref.ref_convert(cpu, sel_mlp, sel_att)
