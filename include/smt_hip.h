@@ -13,6 +13,8 @@
  *                         (also smt.py:429-439, the merge in convert_matrix_sparsity_to_linear_layer)
  *   smt_tile_wgrad        deepspeed/smt/smt.py:382-404   per-tile sum_b g[b,:,rows]^T x[b,:,cols]
  *   smt_tile_wgrad_batch  the same, for the tiles of several modules in one launch (ABI v6)
+ *   smt_tile_wgrad_batch_seq  the same with the reference's rounding: every per-sample [256, 256]
+ *                         partial rounded to bf16, then the batch sum (smt.py:397-404, ABI v8)
  *   smt_tile_scatter_t    deepspeed/smt/smt.py:332-341 / 406   write-back into the transposed copy W^T
  *                         that the data-gradient GEMM grad_input = g @ W reads (as g @ (W^T)^T)
  *   smt_colblock_gather   deepspeed/smt/smt.py:351-358   ctx.list1: the input column slices linearZ keeps
@@ -181,6 +183,23 @@ size_t smt_wgrad_batch_workspace_bytes(int64_t T, int32_t n_tiles);
 int smt_tile_wgrad_batch(const smt_wgrad_module* modules, int32_t n_modules, int64_t T,
                          const int32_t* tile_tab_dev, const int32_t* order_dev, int32_t n_tiles,
                          int32_t out_dtype, void* workspace, size_t workspace_bytes, hipStream_t stream);
+
+/* Workspace bytes smt_tile_wgrad_batch_seq needs (T = n_samples * seq_len rows, n_tiles tiles). */
+size_t smt_wgrad_seq_workspace_bytes(int64_t T, int64_t seq_len, int32_t n_tiles);
+
+/*
+ * smt_tile_wgrad_batch with the reference's rounding (ABI v8; opt-in parity mode). The T rows are
+ * T / seq_len samples of seq_len rows (linearZ's 3-D input [B, S, in] flattened, so seq_len = S), and
+ * each tile's gradient is computed exactly as smt.py:397-404 rounds it: one [256, 256] product per
+ * sample accumulated in fp32 and rounded to bf16 (torch.matmul of bf16), the B bf16 partials summed in
+ * fp32 in sample order and rounded to bf16 (torch.sum(dim=0)), then, with accumulate, added to the
+ * output (autograd's accumulation into .grad). An fp32 output holds that bf16 value exactly. T must be
+ * a whole number of samples (SMT_E_INVALID otherwise). Deterministic; about n_samples / S times the
+ * default mode's fp32 slab traffic.
+ */
+int smt_tile_wgrad_batch_seq(const smt_wgrad_module* modules, int32_t n_modules, int64_t T, int64_t seq_len,
+                             const int32_t* tile_tab_dev, const int32_t* order_dev, int32_t n_tiles,
+                             int32_t out_dtype, void* workspace, size_t workspace_bytes, hipStream_t stream);
 
 /*
  * out[j, t, 0:256] = x[t, c_j*256 : c_j*256+256] for the n_cb column blocks c_j of col_blocks_dev

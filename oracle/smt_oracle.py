@@ -48,15 +48,21 @@ def linearz_forward(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
     return torch.matmul(x, weight.t())
 
 
-def linearz_backward(grad_output: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, index_list):
-    """smt.py:382-406: per tile, a batched [B,256,S]x[B,S,256] matmul in the input dtype (each
-    per-sample partial rounded to that dtype), summed over the batch; ``grad_input = g @ W``."""
+def linearz_tile_grads(grad_output: torch.Tensor, x: torch.Tensor, index_list) -> torch.Tensor:
+    """smt.py:382-404: per tile, a batched [B,256,S]x[B,S,256] matmul in the input dtype (each
+    per-sample partial rounded to that dtype), summed over the batch (``torch.sum(dim=0)``)."""
     B = Block_dimension
     grad_weight = torch.empty(len(index_list) * B, B, dtype=grad_output.dtype)
     for i, index in enumerate(index_list):
         grad_weight[i * B:(i + 1) * B, :] = torch.sum(torch.matmul(
             grad_output.permute(0, 2, 1)[:, index[0] * B:(index[0] + 1) * B, :],
             x[:, :, index[1] * B:(index[1] + 1) * B]), dim=0)
+    return grad_weight
+
+
+def linearz_backward(grad_output: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, index_list):
+    """smt.py:382-406: the tile gradients of :func:`linearz_tile_grads`; ``grad_input = g @ W``."""
+    grad_weight = linearz_tile_grads(grad_output, x, index_list)
     grad_input = torch.matmul(grad_output, weight)
     return grad_input, grad_weight
 

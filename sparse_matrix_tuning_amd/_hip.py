@@ -29,7 +29,7 @@ _DT = {torch.bfloat16: DTYPE_BF16, torch.float32: DTYPE_FP32, torch.float16: DTY
 # library exports each of them.
 ABI_FUNCTIONS = (
     "smt_last_error", "smt_abi_version", "smt_wgrad_workspace_bytes", "smt_tile_wgrad", "smt_wgrad_batch_workspace_bytes",
-    "smt_tile_wgrad_batch", "smt_colblock_gather", "smt_tile_scatter_t",
+    "smt_tile_wgrad_batch", "smt_wgrad_seq_workspace_bytes", "smt_tile_wgrad_batch_seq", "smt_colblock_gather", "smt_tile_scatter_t",
     "smt_tile_gather", "smt_tile_scatter", "smt_grad_accumulate", "smt_block_score",
     "smt_sq_norm", "smt_adamw_step", "smt_adamw_multi",
     "smt_mx_quant_cols", "smt_wgrad_mx_workspace_bytes", "smt_tile_wgrad_mx", "smt_tile_wgrad_mx_batch",
@@ -124,6 +124,9 @@ _SIGS = {
     "smt_tile_wgrad": (ctypes.c_int, [_P, _I64, _P, _I64, _I64, _I64, _P, _P, _I32, _P, _I32, _I32, _P, _SZ, _P]),
     "smt_wgrad_batch_workspace_bytes": (_SZ, [_I64, _I32]),
     "smt_tile_wgrad_batch": (ctypes.c_int, [ctypes.POINTER(WgradModule), _I32, _I64, _P, _P, _I32, _I32, _P, _SZ, _P]),
+    "smt_wgrad_seq_workspace_bytes": (_SZ, [_I64, _I64, _I32]),
+    "smt_tile_wgrad_batch_seq": (ctypes.c_int, [ctypes.POINTER(WgradModule), _I32, _I64, _I64, _P, _P, _I32, _I32, _P,
+                                                _SZ, _P]),
     "smt_colblock_gather": (ctypes.c_int, [_P, _I64, _I64, _P, _I32, _P, _P]),
     "smt_tile_scatter_t": (ctypes.c_int, [_P, _I32, _P, _P]),
     "smt_tile_gather": (ctypes.c_int, [_P, _I64, _I32, _P, _I32, _P, _P]),
@@ -280,11 +283,20 @@ def wgrad_workspace_bytes(T: int, n_tiles: int) -> int:
 
 
 def tile_wgrad(grad_out2d: torch.Tensor, x: torch.Tensor, tile_rc: torch.Tensor, out: torch.Tensor,
-               accumulate: bool = False, order: Optional[torch.Tensor] = None) -> torch.Tensor:
+               accumulate: bool = False, order: Optional[torch.Tensor] = None,
+               seq_len: Optional[int] = None) -> torch.Tensor:
     """out[i] (+)= grad_out2d[:, r_i-block]^T @ X_{c_i} for every tile (smt.py:397-404): ``x`` is the
     input, row-major [T, in] (X_c = its c-th 256-column block), or the block-major [n_cb, T, 256]
     copy of ``colblock_gather`` (X_c = x[c]). ``order``: optional device int32 schedule permutation
-    (speed only)."""
+    (speed only). ``seq_len``: the reference's rounding (``smt_tile_wgrad_batch_seq``): T is
+    T / seq_len samples, each sample's partial rounded to bf16 before the batch sum."""
+    if seq_len:
+        n = tile_rc.shape[0]
+        tab = torch.zeros(n, 4, dtype=torch.int32, device=tile_rc.device)
+        tab[:, 1:3] = tile_rc
+        tab[:, 3] = torch.arange(n, dtype=torch.int32, device=tile_rc.device)
+        tile_wgrad_batch([(grad_out2d, x, out, accumulate)], tab, order, seq_len=seq_len)
+        return out
     dev = _require_device(grad_out2d, x, tile_rc, out, order)
     if grad_out2d.dtype != torch.bfloat16 or x.dtype != torch.bfloat16:
         raise NotImplementedError(f"tile_wgrad: bf16 operands only (got {grad_out2d.dtype}, {x.dtype})")
@@ -326,7 +338,8 @@ def _wgrad_x_layout(x: torch.Tensor, T: int, what: str):
     return x.stride(0), BLOCK
 
 
-def tile_wgrad_batch(items: Sequence[tuple], tile_tab: torch.Tensor, order: Optional[torch.Tensor] = None) -> None:
+def tile_wgrad_batch(items: Sequence[tuple], tile_tab: torch.Tensor, order: Optional[torch.Tensor] = None,
+                     seq_len: Optional[int] = None) -> None:
     """One launch of the tile weight gradients of several modules sharing T (``smt_tile_wgrad_batch``).
 
     ``items``: per module ``(grad_out2d, x, out, accumulate)`` with the meaning of :func:`tile_wgrad`
@@ -334,7 +347,8 @@ def tile_wgrad_batch(items: Sequence[tuple], tile_tab: torch.Tensor, order: Opti
     device int32 [n, 4] of (module, row_block, col_block, tile index in the module's output), e.g.
     from :func:`wgrad_batch_table`; ``order``: optional int32 [n] schedule permutation (speed only).
     Each tile's result is bit-identical to what :func:`tile_wgrad` gives for the same tile at the
-    same T and the same total tile count."""
+    same T and the same total tile count. ``seq_len``: the reference's per-sample bf16 rounding
+    (``smt_tile_wgrad_batch_seq``, include/smt_hip.h)."""
     if not items:
         return
     if len(items) > WGRAD_MAX_MODULES:
@@ -357,6 +371,15 @@ def tile_wgrad_batch(items: Sequence[tuple], tile_tab: torch.Tensor, order: Opti
     n = tile_tab.shape[0]
     if order is not None and (order.dtype != torch.int32 or order.numel() != n):
         raise ValueError("tile_wgrad_batch: order must be int32 [n_tiles]")
+    if seq_len:
+        if T % int(seq_len):
+            raise ValueError(f"tile_wgrad_batch: T = {T} is not a whole number of {seq_len}-row samples")
+        ws_bytes = int(load().smt_wgrad_seq_workspace_bytes(T, int(seq_len), n))
+        ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=dev)
+        rc = load().smt_tile_wgrad_batch_seq(mods, len(items), T, int(seq_len), _ptr(tile_tab), _ptr(order), n,
+                                             _DT[out_dtype], _ptr(ws), ws_bytes, _stream(dev))
+        _check(rc, "smt_tile_wgrad_batch_seq")
+        return
     ws_bytes = int(load().smt_wgrad_batch_workspace_bytes(T, n))
     ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=dev)
     rc = load().smt_tile_wgrad_batch(mods, len(items), T, _ptr(tile_tab), _ptr(order), n, _DT[out_dtype],

@@ -18,7 +18,10 @@ base model:
   a mismatch instead of resuming on the wrong weights.
 
 Only rank 0 writes (the tiles and the optimizer state are replicated), each file to a temporary
-name first and then renamed; every rank waits at a barrier before returning.
+name first and then renamed; rank 0 then broadcasts whether the save succeeded, so a failed write
+raises on every rank instead of leaving the others waiting. Every file carries the save's random id
+(safetensors metadata, and ``save_id`` in the meta file written last): a directory overwritten by a
+save that crashed half-way, holding files of two saves, is refused on load.
 
 :func:`save_merged_model` writes the plain HF-style state dict with the tiles merged into W and
 no ``selected_weight`` keys (``convert_matrix_sparsity_to_linear_layer`` semantics, smt.py:416-457).
@@ -28,10 +31,12 @@ from __future__ import annotations
 
 import json
 import os
+import uuid
 from collections import defaultdict
 from typing import Dict, Optional, Tuple
 
 import torch
+from safetensors import safe_open
 from safetensors.torch import load_file, save_file
 
 from .smt.smt import (LinearLayer_MatrixSparsity, _attn_module_name, _layer_number, _mlp_module_name,
@@ -91,14 +96,30 @@ def _atomic(path: str, write) -> None:
 def save_checkpoint(engine, save_dir: str, client_state: Optional[dict] = None, include_frozen: bool = True) -> str:
     """Write selection + tiles + optimizer state of an :class:`SMTEngine` (DeepSpeed
     ``engine.save_checkpoint`` counterpart), and with ``include_frozen`` every frozen weight.
-    Returns the directory."""
+    Returns the directory. Raises on every rank if rank 0's write failed."""
     dist = _dist()
     rank = dist.get_rank() if dist is not None else 0
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    err = None
+    if rank == 0:
+        try:
+            _write_checkpoint(engine, save_dir, client_state, include_frozen)
+        except Exception as e:          # reported to every rank below, then re-raised here
+            err = e
+    if dist is not None:
+        msg = [None if err is None else f"{type(err).__name__}: {err}"]
+        dist.broadcast_object_list(msg, src=0)
+        if err is None and msg[0] is not None:
+            raise RuntimeError(f"save_checkpoint failed on rank 0: {msg[0]}")
+    if err is not None:
+        raise err
+    return save_dir
+
+
+def _write_checkpoint(engine, save_dir: str, client_state: Optional[dict], include_frozen: bool) -> None:
     model = engine.module
-    torch.cuda.synchronize()
-    if rank != 0:
-        dist.barrier()
-        return save_dir
+    save_id = uuid.uuid4().hex
     os.makedirs(save_dir, exist_ok=True)
     tensors: Dict[str, torch.Tensor] = {}
     modules = []
@@ -118,20 +139,30 @@ def save_checkpoint(engine, save_dir: str, client_state: Optional[dict] = None, 
             "micro_steps": engine.micro_steps,
             "lr_scheduler": engine.lr_scheduler.state_dict() if engine.lr_scheduler is not None else None,
             "client_state": client_state or {}, "frozen_fingerprints": _frozen_fingerprints(model),
-            "includes_frozen": bool(include_frozen)}
-    _atomic(os.path.join(save_dir, STATE), lambda p: save_file(tensors, p))
+            "includes_frozen": bool(include_frozen), "save_id": save_id}
+    tag = {"smt_save_id": save_id}
+    _atomic(os.path.join(save_dir, STATE), lambda p: save_file(tensors, p, metadata=tag))
     if include_frozen:
         frozen = {n: p.detach().contiguous().cpu() for n, p in model.named_parameters()
                   if not n.endswith("selected_weight")}
-        _atomic(os.path.join(save_dir, FROZEN), lambda p: save_file(frozen, p))
+        _atomic(os.path.join(save_dir, FROZEN), lambda p: save_file(frozen, p, metadata=tag))
 
     def write_meta(p):
         with open(p, "w") as f:
             json.dump(meta, f, indent=1, default=_json_default)
     _atomic(os.path.join(save_dir, META), write_meta)          # last: its presence marks a complete save
-    if dist is not None:
-        dist.barrier()
-    return save_dir
+
+
+def _load_checked(path: str, meta: dict) -> Dict[str, torch.Tensor]:
+    """load_file, after checking that the file belongs to the save ``meta`` describes."""
+    want = meta.get("save_id")
+    if want is not None:
+        with safe_open(path, framework="pt") as f:
+            got = (f.metadata() or {}).get("smt_save_id")
+        if got != want:
+            raise ValueError(f"{os.path.basename(path)} is from another save ({got}) than {META} ({want}): "
+                             "the checkpoint directory was overwritten by an incomplete save")
+    return load_file(path)
 
 
 def _json_default(o):
@@ -169,7 +200,7 @@ def restore_model(model, load_dir: str):
     sel_mlp, sel_att = read_selection(load_dir)
     frozen_path = os.path.join(load_dir, FROZEN)
     if meta.get("includes_frozen") and os.path.exists(frozen_path):
-        frozen = load_file(frozen_path)
+        frozen = _load_checked(frozen_path, meta)
         params = dict(model.named_parameters())
         missing = [n for n in frozen if n not in params]
         if missing:
@@ -179,7 +210,7 @@ def restore_model(model, load_dir: str):
                 params[n].data.copy_(t.to(params[n].device))
     freeze_unselected_matrix_layer(model, sel_mlp, sel_att)
     convert_linear_layer_to_matrix_sparsity(model, sel_mlp, sel_att)
-    state = load_file(os.path.join(load_dir, STATE))
+    state = _load_checked(os.path.join(load_dir, STATE), meta)
     for name, m in _smt_modules(model):
         t = state.get(f"tiles/{name}")
         if t is None:
@@ -202,7 +233,7 @@ def load_optimizer_state(engine, load_dir: str) -> dict:
     (same param-group order as at save time). Returns the saved ``client_state``."""
     with open(os.path.join(load_dir, META)) as f:
         meta = json.load(f)
-    state = load_file(os.path.join(load_dir, STATE))
+    state = _load_checked(os.path.join(load_dir, STATE), meta)
     if len(meta["groups"]) != len(engine.tile_groups):
         raise ValueError(f"checkpoint has {len(meta['groups'])} tile groups, engine {len(engine.tile_groups)}")
     for gi, (g, tg) in enumerate(zip(meta["groups"], engine.tile_groups)):

@@ -176,9 +176,26 @@ __device__ __forceinline__ WgradTile wgrad_tile(const WgradModules& mods, const 
     return t;
 }
 
+// Rows [t_begin, t_end) of split s. Default (seq == 0): contiguous chunks of T. Reference rounding
+// (seq > 0, smt.py:397-404 rounds every per-sample [256, 256] partial to bf16): split s = sample *
+// kps + j covers piece j (chunk rows) of one seq-row sample, so no split crosses a sample boundary
+// and the reduce can rebuild each sample's partial before rounding it.
+__device__ __forceinline__ void wgrad_span(int s, int64_t T, int64_t chunk, int64_t seq, int kps,
+                                           int64_t& t_begin, int64_t& t_end) {
+    if (seq > 0) {
+        const int smp = s / kps, j = s - smp * kps;
+        const int64_t lim = (int64_t)(smp + 1) * seq;
+        t_begin = (int64_t)smp * seq + (int64_t)j * chunk;
+        t_end = (t_begin + chunk < lim) ? (t_begin + chunk) : lim;
+    } else {
+        t_begin = (int64_t)s * chunk;
+        t_end = (t_begin + chunk < T) ? (t_begin + chunk) : T;
+    }
+}
+
 template <int OUT, bool BATCH>
 __global__ __launch_bounds__(kWgThreads, 2)
-void wgrad_partial_kernel(const WgradModules mods, int64_t T, int64_t chunk, int S, int n_tiles,
+void wgrad_partial_kernel(const WgradModules mods, int64_t T, int64_t chunk, int S, int64_t seq, int kps, int n_tiles,
                           const int32_t* __restrict__ tile_tab, const int32_t* __restrict__ order,
                           float* __restrict__ slab) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * 2 * kImgBytes];   // 128 KiB, one array
@@ -197,8 +214,8 @@ void wgrad_partial_kernel(const WgradModules mods, int64_t T, int64_t chunk, int
     const int li = L - s * n_tiles;
     const int tile = order != nullptr ? order[li] : li;
     const WgradTile tt = wgrad_tile<BATCH, OUT == kOutBF16 ? 2 : 4>(mods, tile_tab, tile);
-    const int64_t t_begin = (int64_t)s * chunk;
-    const int64_t t_end = (t_begin + chunk < T) ? (t_begin + chunk) : T;
+    int64_t t_begin, t_end;
+    wgrad_span(s, T, chunk, seq, kps, t_begin, t_end);
     const int nst = (t_end > t_begin) ? (int)((t_end - t_begin + kBK - 1) / kBK) : 0;
 
     const uint16_t* gb = tt.g;
@@ -369,7 +386,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base,
 
 template <int OUT, int SLOTS, bool BATCH>
 __global__ __launch_bounds__(kWgThreads, 1)
-void wgrad_dma_kernel(const WgradModules mods, int64_t T, int64_t chunk, int S, int n_tiles,
+void wgrad_dma_kernel(const WgradModules mods, int64_t T, int64_t chunk, int S, int64_t seq, int kps, int n_tiles,
                       const int32_t* __restrict__ tile_tab, const int32_t* __restrict__ order,
                       float* __restrict__ slab) {
     static_assert(SLOTS >= 3 && SLOTS <= 5, "ring depth");
@@ -385,8 +402,8 @@ void wgrad_dma_kernel(const WgradModules mods, int64_t T, int64_t chunk, int S, 
     const int tile = order != nullptr ? order[li] : li;
     const WgradTile tt = wgrad_tile<BATCH, OUT == kOutBF16 ? 2 : 4>(mods, tile_tab, tile);
     const int64_t ldg = tt.ldg, ldx = tt.ldx;
-    const int64_t t_begin = (int64_t)s * chunk;
-    const int64_t t_end = (t_begin + chunk < T) ? (t_begin + chunk) : T;
+    int64_t t_begin, t_end;
+    wgrad_span(s, T, chunk, seq, kps, t_begin, t_end);
     const int rows = (t_end > t_begin) ? (int)(t_end - t_begin) : 0;
     const int nst = (rows + kDmaBK - 1) / kDmaBK;
 
@@ -531,7 +548,7 @@ __device__ __forceinline__ void wgrad_store_q(f32x16_t (&acc)[2][2], void* __res
 
 template <int OUT, int QS, bool BATCH>
 __global__ __launch_bounds__(kQThreads, 2)
-void wgrad_quarter_kernel(const WgradModules mods, int64_t T, int64_t chunk, int S, int n_tiles,
+void wgrad_quarter_kernel(const WgradModules mods, int64_t T, int64_t chunk, int S, int64_t seq, int kps, int n_tiles,
                           const int32_t* __restrict__ tile_tab, const int32_t* __restrict__ order,
                           float* __restrict__ slab) {
     static_assert(QS >= 3 && QS <= 5, "ring depth");
@@ -551,8 +568,8 @@ void wgrad_quarter_kernel(const WgradModules mods, int64_t T, int64_t chunk, int
     const int qm = qd >> 1, qn = qd & 1;
     const WgradTile tt = wgrad_tile<BATCH, OUT == kOutBF16 ? 2 : 4>(mods, tile_tab, tile);
     const int64_t ldg = tt.ldg, ldx = tt.ldx;
-    const int64_t t_begin = (int64_t)s * chunk;
-    const int64_t t_end = (t_begin + chunk < T) ? (t_begin + chunk) : T;
+    int64_t t_begin, t_end;
+    wgrad_span(s, T, chunk, seq, kps, t_begin, t_end);
     const int rows = (t_end > t_begin) ? (int)(t_end - t_begin) : 0;
     const int nst = (rows + kDmaBK - 1) / kDmaBK;
 
@@ -638,17 +655,39 @@ void wgrad_quarter_kernel(const WgradModules mods, int64_t T, int64_t chunk, int
                        qm * 128 + wm * 64, qn * 128 + wn * 64, lane, tt.accumulate);
 }
 
+__device__ __forceinline__ float bf16_round(float v) { return bf16_bits_to_f32(f32_to_bf16_bits(v)); }
+
 // Sum the S partial slabs of one tile in order s = 0..S-1 (deterministic) and write the tile (this
-// workgroup's 1024 of its elements).
+// workgroup's 1024 of its elements). kps > 0 (reference rounding, wgrad_span): the slabs come in
+// groups of kps per sample; each sample's partial (its kps slabs summed in fp32) is rounded to bf16,
+// the samples are summed in order in fp32 and the sum is rounded to bf16 once more (smt.py:397-404:
+// bf16 matmul per sample, then torch.sum(dim=0) of the bf16 partials, accumulated in fp32), before
+// the optional accumulation into the output (autograd's add into .grad).
 template <bool OUT_F32>
-__device__ __forceinline__ void wgrad_reduce_tile(const float* __restrict__ slab, int S, int tile, void* __restrict__ tile_out,
-                                                  int accumulate) {
+__device__ __forceinline__ void wgrad_reduce_tile(const float* __restrict__ slab, int S, int kps, int tile,
+                                                  void* __restrict__ tile_out, int accumulate) {
     const int e = (((blockIdx.x & 63) << 8) + threadIdx.x) * 4;
     const float* src = slab + (int64_t)tile * S * kTileElems + e;
-    float4 sum = *reinterpret_cast<const float4*>(src);
-    for (int s = 1; s < S; ++s) {
-        const float4 v = *reinterpret_cast<const float4*>(src + (int64_t)s * kTileElems);
-        sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
+    float4 sum;
+    if (kps <= 0) {
+        sum = *reinterpret_cast<const float4*>(src);
+        for (int s = 1; s < S; ++s) {
+            const float4 v = *reinterpret_cast<const float4*>(src + (int64_t)s * kTileElems);
+            sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
+        }
+    } else {
+        sum = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int s0 = 0; s0 < S; s0 += kps) {
+            float4 part = *reinterpret_cast<const float4*>(src + (int64_t)s0 * kTileElems);
+            for (int j = 1; j < kps; ++j) {
+                const float4 v = *reinterpret_cast<const float4*>(src + (int64_t)(s0 + j) * kTileElems);
+                part.x += v.x; part.y += v.y; part.z += v.z; part.w += v.w;
+            }
+            sum.x += bf16_round(part.x); sum.y += bf16_round(part.y);
+            sum.z += bf16_round(part.z); sum.w += bf16_round(part.w);
+        }
+        sum.x = bf16_round(sum.x); sum.y = bf16_round(sum.y);
+        sum.z = bf16_round(sum.z); sum.w = bf16_round(sum.w);
     }
     const int64_t o = e;
     void* out = tile_out;
@@ -678,9 +717,9 @@ __device__ __forceinline__ void wgrad_reduce_tile(const float* __restrict__ slab
 // 64 workgroups x 256 threads x 4 elements per tile; tile i's output = out + i tiles
 template <bool OUT_F32>
 __global__ __launch_bounds__(256)
-void wgrad_reduce_kernel(const float* __restrict__ slab, int S, void* __restrict__ out, int accumulate) {
+void wgrad_reduce_kernel(const float* __restrict__ slab, int S, int kps, void* __restrict__ out, int accumulate) {
     const int tile = blockIdx.x >> 6;
-    wgrad_reduce_tile<OUT_F32>(slab, S, tile, static_cast<uint8_t*>(out) + (int64_t)tile * kTileElems * (OUT_F32 ? 4 : 2),
+    wgrad_reduce_tile<OUT_F32>(slab, S, kps, tile, static_cast<uint8_t*>(out) + (int64_t)tile * kTileElems * (OUT_F32 ? 4 : 2),
                                accumulate);
 }
 
@@ -692,7 +731,7 @@ void wgrad_reduce_mx_batch_kernel(const float* __restrict__ slab, int S, const W
     const int tile = blockIdx.x >> 6;
     const int m = tile_tab[4 * tile];
     const int ti = tile_tab[4 * tile + 3];
-    wgrad_reduce_tile<OUT_F32>(slab, S, tile,
+    wgrad_reduce_tile<OUT_F32>(slab, S, 0, tile,
                                static_cast<uint8_t*>(mods.m[m].grad_tiles) + (int64_t)ti * kTileElems * (OUT_F32 ? 4 : 2),
                                mods.m[m].accumulate);
 }
@@ -700,11 +739,11 @@ void wgrad_reduce_mx_batch_kernel(const float* __restrict__ slab, int S, const W
 // the same over a batch: each tile's output and accumulate flag from its module (wgrad_tile)
 template <bool OUT_F32>
 __global__ __launch_bounds__(256)
-void wgrad_reduce_batch_kernel(const float* __restrict__ slab, int S, const WgradModules mods,
+void wgrad_reduce_batch_kernel(const float* __restrict__ slab, int S, int kps, const WgradModules mods,
                                const int32_t* __restrict__ tile_tab) {
     const int tile = blockIdx.x >> 6;
     const WgradTile tt = wgrad_tile<true, OUT_F32 ? 4 : 2>(mods, tile_tab, tile);
-    wgrad_reduce_tile<OUT_F32>(slab, S, tile, tt.out, tt.accumulate);
+    wgrad_reduce_tile<OUT_F32>(slab, S, kps, tile, tt.out, tt.accumulate);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1755,7 +1794,8 @@ void channel_aten_levels_kernel(const float* __restrict__ chunks, int S, int C, 
     out[c] = __fdiv_rn(acc[0], (float)S);                  // sum(...).div_(S)
 }
 
-struct WgradSplit { int S; int64_t chunk; bool quarter; };
+// S splits of `chunk` rows each; seq > 0: the reference-rounding split (kps pieces per seq-row sample)
+struct WgradSplit { int S; int64_t chunk; bool quarter; int64_t seq; int kps; };
 
 // Quarter-tile kernel for modules with at most this many tiles (SMT_WGRAD_QUARTER_MAX; 0 disables).
 // Measured at T = 32768 (profiles/r02_wgrad_quarter.jsonl): 1.1-1.2x faster than the full-tile
@@ -1767,7 +1807,7 @@ int quarter_max_tiles() {
 
 // row_bytes: operand bytes per T row of one tile (1 KiB bf16, 512 B MX-fp8)
 WgradSplit wgrad_split(int64_t T, int32_t n_tiles, bool allow_quarter = true, double row_bytes = 1024.0) {
-    WgradSplit sp{1, kBK, false};
+    WgradSplit sp{1, kBK, false, 0, 0};
     if (T <= 0 || n_tiles <= 0) return sp;
     const int64_t s_max = std::max<int64_t>(1, std::min<int64_t>(64, (T + 511) / 512));
     int64_t S = 1;
@@ -1797,6 +1837,27 @@ WgradSplit wgrad_split(int64_t T, int32_t n_tiles, bool allow_quarter = true, do
     return sp;
 }
 
+// Reference-rounding split (T = n_samples * seq): every sample is cut into kps pieces of `chunk`
+// rows (a multiple of 32, the LDS-DMA stage), kps doubled until the launch fills the chip (256
+// full-tile or 512 quarter-tile workgroup slots) or a piece would drop below 64 rows. Always the
+// slab path (S = n_samples * kps >= 1): the reduce rebuilds and rounds each sample's partial.
+WgradSplit wgrad_split_seq(int64_t T, int64_t seq, int32_t n_tiles) {
+    WgradSplit sp{1, seq, false, seq, 1};
+    if (T <= 0 || n_tiles <= 0 || seq <= 0 || T % seq) return sp;
+    const int64_t n_samples = T / seq;
+    sp.quarter = n_tiles <= quarter_max_tiles();
+    const int64_t slots = sp.quarter ? 2 * kCUs : kCUs;
+    const int64_t per_split = sp.quarter ? 4 : 1;
+    int64_t k = 1;
+    while ((int64_t)n_tiles * n_samples * k * per_split < slots && seq / (2 * k) >= 64) k *= 2;
+    int64_t chunk = (seq + k - 1) / k;
+    chunk = (chunk + 31) / 32 * 32;
+    sp.chunk = chunk;
+    sp.kps = (int)((seq + chunk - 1) / chunk);
+    sp.S = (int)(n_samples * sp.kps);
+    return sp;
+}
+
 }  // namespace
 
 // ================================================================================================
@@ -1806,7 +1867,7 @@ extern "C" {
 
 const char* smt_last_error(void) { return g_err; }
 
-int smt_abi_version(void) { return 7; }
+int smt_abi_version(void) { return 8; }
 
 size_t smt_wgrad_workspace_bytes(int64_t T, int32_t n_tiles) {
     if (T <= 0 || n_tiles <= 0) return 0;
@@ -1824,8 +1885,10 @@ namespace {
 // need chunk * ld * 2 < 2^31, otherwise the register-staged kernel, which addresses with 64 bits).
 template <bool BATCH>
 int wgrad_launch(const WgradModules& mods, int64_t T, int64_t max_ld, const int32_t* tab, const int32_t* order,
-                 int32_t n_tiles, int32_t out_dtype, void* workspace, size_t workspace_bytes, hipStream_t stream) {
-    const WgradSplit sp = wgrad_split(T, n_tiles);
+                 int32_t n_tiles, int32_t out_dtype, void* workspace, size_t workspace_bytes, hipStream_t stream,
+                 int64_t seq = 0) {
+    const WgradSplit sp = seq > 0 ? wgrad_split_seq(T, seq, n_tiles) : wgrad_split(T, n_tiles);
+    const bool use_slab = sp.S > 1 || sp.seq > 0;       // reference rounding always reduces
     const dim3 grid(n_tiles * sp.S), block(kWgThreads);
     const dim3 qgrid(n_tiles * sp.S * 4), qblock(kQThreads);
     static const bool force_reg = [] { const char* e = getenv("SMT_WGRAD_IMPL"); return e && strcmp(e, "reg") == 0; }();
@@ -1836,7 +1899,7 @@ int wgrad_launch(const WgradModules& mods, int64_t T, int64_t max_ld, const int3
     const bool dma = !force_reg && sp.chunk * max_ld * 2 < (int64_t)0x7fffffff;
     const bool quarter = dma && sp.quarter;
     float* slab = nullptr;
-    if (sp.S > 1) {
+    if (use_slab) {
         const size_t need = (size_t)n_tiles * sp.S * kTileElems * sizeof(float);
         if (!workspace || workspace_bytes < need)
             return fail(SMT_E_WORKSPACE, "smt_tile_wgrad: workspace %zu < %zu bytes", workspace_bytes, need);
@@ -1846,17 +1909,17 @@ int wgrad_launch(const WgradModules& mods, int64_t T, int64_t max_ld, const int3
 #define SMT_WGRAD_LAUNCH(OUT)                                                                                     \
     do {                                                                                                          \
         if (!dma) hipLaunchKernelGGL((wgrad_partial_kernel<OUT, BATCH>), grid, block, 0, stream, mods, T, sp.chunk, \
-                                     sp.S, n_tiles, tab, order, slab);                                           \
+                                     sp.S, sp.seq, sp.kps, n_tiles, tab, order, slab);                           \
         else if (quarter && qslots == 5) hipLaunchKernelGGL((wgrad_quarter_kernel<OUT, 5, BATCH>), qgrid, qblock, 0, \
-                                     stream, mods, T, sp.chunk, sp.S, n_tiles, tab, order, slab);                \
+                                     stream, mods, T, sp.chunk, sp.S, sp.seq, sp.kps, n_tiles, tab, order, slab);\
         else if (quarter) hipLaunchKernelGGL((wgrad_quarter_kernel<OUT, kQSlots, BATCH>), qgrid, qblock, 0, stream,  \
-                                     mods, T, sp.chunk, sp.S, n_tiles, tab, order, slab);                        \
+                                     mods, T, sp.chunk, sp.S, sp.seq, sp.kps, n_tiles, tab, order, slab);        \
         else if (slots == 5) hipLaunchKernelGGL((wgrad_dma_kernel<OUT, 5, BATCH>), grid, block, 0, stream, mods, T,  \
-                                     sp.chunk, sp.S, n_tiles, tab, order, slab);                                 \
+                                     sp.chunk, sp.S, sp.seq, sp.kps, n_tiles, tab, order, slab);                 \
         else hipLaunchKernelGGL((wgrad_dma_kernel<OUT, kDmaSlotsDefault, BATCH>), grid, block, 0, stream, mods, T,   \
-                                sp.chunk, sp.S, n_tiles, tab, order, slab);                                      \
+                                sp.chunk, sp.S, sp.seq, sp.kps, n_tiles, tab, order, slab);                      \
     } while (0)
-    if (sp.S == 1) {
+    if (!use_slab) {
         if (out_dtype == SMT_DTYPE_FP32) SMT_WGRAD_LAUNCH(kOutF32);
         else SMT_WGRAD_LAUNCH(kOutBF16);
         return check_launch("wgrad kernel");
@@ -1866,17 +1929,18 @@ int wgrad_launch(const WgradModules& mods, int64_t T, int64_t max_ld, const int3
     int rc = check_launch("wgrad kernel");
     if (rc) return rc;
     const dim3 rgrid(n_tiles * 64), rblock(256);
+    const int kps = sp.seq > 0 ? sp.kps : 0;
     if (BATCH) {
         if (out_dtype == SMT_DTYPE_FP32)
-            hipLaunchKernelGGL(wgrad_reduce_batch_kernel<true>, rgrid, rblock, 0, stream, slab, sp.S, mods, tab);
+            hipLaunchKernelGGL(wgrad_reduce_batch_kernel<true>, rgrid, rblock, 0, stream, slab, sp.S, kps, mods, tab);
         else
-            hipLaunchKernelGGL(wgrad_reduce_batch_kernel<false>, rgrid, rblock, 0, stream, slab, sp.S, mods, tab);
+            hipLaunchKernelGGL(wgrad_reduce_batch_kernel<false>, rgrid, rblock, 0, stream, slab, sp.S, kps, mods, tab);
     } else {
         const smt_wgrad_module& m = mods.m[0];
         if (out_dtype == SMT_DTYPE_FP32)
-            hipLaunchKernelGGL(wgrad_reduce_kernel<true>, rgrid, rblock, 0, stream, slab, sp.S, m.grad_tiles, m.accumulate);
+            hipLaunchKernelGGL(wgrad_reduce_kernel<true>, rgrid, rblock, 0, stream, slab, sp.S, kps, m.grad_tiles, m.accumulate);
         else
-            hipLaunchKernelGGL(wgrad_reduce_kernel<false>, rgrid, rblock, 0, stream, slab, sp.S, m.grad_tiles, m.accumulate);
+            hipLaunchKernelGGL(wgrad_reduce_kernel<false>, rgrid, rblock, 0, stream, slab, sp.S, kps, m.grad_tiles, m.accumulate);
     }
     return check_launch("wgrad_reduce_kernel");
 }
@@ -1926,10 +1990,13 @@ int smt_tile_wgrad(const void* grad_out, int64_t ld_grad_out, const void* x, int
 
 size_t smt_wgrad_batch_workspace_bytes(int64_t T, int32_t n_tiles) { return smt_wgrad_workspace_bytes(T, n_tiles); }
 
-int smt_tile_wgrad_batch(const smt_wgrad_module* modules, int32_t n_modules, int64_t T, const int32_t* tile_tab_dev,
-                         const int32_t* order_dev, int32_t n_tiles, int32_t out_dtype, void* workspace,
-                         size_t workspace_bytes, hipStream_t stream) {
-    static const char* fn = "smt_tile_wgrad_batch";
+}  // extern "C"
+
+namespace {
+
+int wgrad_batch_entry(const char* fn, const smt_wgrad_module* modules, int32_t n_modules, int64_t T, int64_t seq,
+                      const int32_t* tile_tab_dev, const int32_t* order_dev, int32_t n_tiles, int32_t out_dtype,
+                      void* workspace, size_t workspace_bytes, hipStream_t stream) {
     if (n_tiles < 0 || T < 0 || n_modules < 0)
         return fail(SMT_E_INVALID, "%s: negative size (T=%lld, n_tiles=%d, n_modules=%d)", fn, (long long)T, n_tiles, n_modules);
     if (n_tiles == 0) return SMT_OK;
@@ -1939,6 +2006,9 @@ int smt_tile_wgrad_batch(const smt_wgrad_module* modules, int32_t n_modules, int
         return fail(SMT_E_INVALID, "%s: out_dtype %d not supported", fn, out_dtype);
     if (!tile_tab_dev) return fail(SMT_E_INVALID, "%s: null tile table", fn);
     if (T == 0) return fail(SMT_E_INVALID, "%s: T = 0 (use smt_tile_wgrad per module)", fn);
+    if (seq < 0 || (seq > 0 && T % seq))
+        return fail(SMT_E_INVALID, "%s: T = %lld is not a whole number of %lld-row samples", fn, (long long)T,
+                    (long long)seq);
     WgradModules mods{};
     int64_t max_ld = 0;
     for (int i = 0; i < n_modules; ++i) {
@@ -1948,7 +2018,33 @@ int smt_tile_wgrad_batch(const smt_wgrad_module* modules, int32_t n_modules, int
         mods.m[i].accumulate = modules[i].accumulate ? 1 : 0;
         max_ld = std::max(max_ld, std::max(modules[i].ld_grad_out, modules[i].ld_x));
     }
-    return wgrad_launch<true>(mods, T, max_ld, tile_tab_dev, order_dev, n_tiles, out_dtype, workspace, workspace_bytes, stream);
+    return wgrad_launch<true>(mods, T, max_ld, tile_tab_dev, order_dev, n_tiles, out_dtype, workspace, workspace_bytes,
+                              stream, seq);
+}
+
+}  // namespace
+
+extern "C" {
+
+int smt_tile_wgrad_batch(const smt_wgrad_module* modules, int32_t n_modules, int64_t T, const int32_t* tile_tab_dev,
+                         const int32_t* order_dev, int32_t n_tiles, int32_t out_dtype, void* workspace,
+                         size_t workspace_bytes, hipStream_t stream) {
+    return wgrad_batch_entry("smt_tile_wgrad_batch", modules, n_modules, T, 0, tile_tab_dev, order_dev, n_tiles,
+                             out_dtype, workspace, workspace_bytes, stream);
+}
+
+size_t smt_wgrad_seq_workspace_bytes(int64_t T, int64_t seq_len, int32_t n_tiles) {
+    if (T <= 0 || n_tiles <= 0 || seq_len <= 0 || T % seq_len) return 0;
+    const WgradSplit sp = wgrad_split_seq(T, seq_len, n_tiles);
+    return (size_t)n_tiles * (size_t)sp.S * (size_t)kTileElems * sizeof(float);
+}
+
+int smt_tile_wgrad_batch_seq(const smt_wgrad_module* modules, int32_t n_modules, int64_t T, int64_t seq_len,
+                             const int32_t* tile_tab_dev, const int32_t* order_dev, int32_t n_tiles,
+                             int32_t out_dtype, void* workspace, size_t workspace_bytes, hipStream_t stream) {
+    if (seq_len <= 0) return fail(SMT_E_INVALID, "smt_tile_wgrad_batch_seq: seq_len %lld <= 0", (long long)seq_len);
+    return wgrad_batch_entry("smt_tile_wgrad_batch_seq", modules, n_modules, T, seq_len, tile_tab_dev, order_dev,
+                             n_tiles, out_dtype, workspace, workspace_bytes, stream);
 }
 
 size_t smt_wgrad_mx_workspace_bytes(int64_t ldq, int32_t n_tiles) {
@@ -2030,9 +2126,9 @@ int wgrad_mx_launch(const WgradMxModules& mods, int64_t ldq, const int32_t* tab,
     } else {
         const smt_wgrad_mx_module& m = mods.m[0];
         if (out_dtype == SMT_DTYPE_FP32)
-            hipLaunchKernelGGL(wgrad_reduce_kernel<true>, rgrid, rblock, 0, stream, slab, sp.S, m.grad_tiles, m.accumulate);
+            hipLaunchKernelGGL(wgrad_reduce_kernel<true>, rgrid, rblock, 0, stream, slab, sp.S, 0, m.grad_tiles, m.accumulate);
         else
-            hipLaunchKernelGGL(wgrad_reduce_kernel<false>, rgrid, rblock, 0, stream, slab, sp.S, m.grad_tiles, m.accumulate);
+            hipLaunchKernelGGL(wgrad_reduce_kernel<false>, rgrid, rblock, 0, stream, slab, sp.S, 0, m.grad_tiles, m.accumulate);
     }
     return check_launch("wgrad_reduce_kernel");
 }

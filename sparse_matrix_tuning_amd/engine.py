@@ -276,10 +276,12 @@ class WgradBatcher:
         self.callback_queued = False
         self._tables = {}
 
-    def add(self, sink: "_GradSink", g2: torch.Tensor, x2: torch.Tensor, tiles, packed: bool) -> None:
+    def add(self, sink: "_GradSink", g2: torch.Tensor, x2: torch.Tensor, tiles, packed: bool,
+            seq_len: Optional[int] = None) -> None:
         """bf16 path: ``g2`` the output gradient [T, out], ``x2`` the saved input (row-major, or the
-        block-major packed copy when ``packed``)."""
-        self._add(sink, "bf16", (g2, x2, tiles, bool(packed)), (g2, x2), len(tiles))
+        block-major packed copy when ``packed``); ``seq_len``: the reference's per-sample rounding
+        (smt.smt.set_wgrad_rounding)."""
+        self._add(sink, "bf16", (g2, x2, tiles, bool(packed), seq_len), (g2, x2), len(tiles))
 
     def add_mx(self, sink: "_GradSink", g2: torch.Tensor, rb_dev: torch.Tensor, mx, tiles, col_pos=None) -> None:
         """fp8 path: ``g2`` is quantised into its MX row blocks ``rb_dev`` at launch time; ``mx`` is
@@ -289,10 +291,12 @@ class WgradBatcher:
 
     def _add(self, sink, kind, args, keep, n) -> None:
         rows = args[0].shape[0]
+        seq = args[4] if kind == "bf16" else None
         if self.pending and (any(p[0] is sink for p in self.pending) or self.pending[0][1] != kind
-                             or self.pending[0][2][0].shape[0] != rows):
+                             or self.pending[0][2][0].shape[0] != rows
+                             or (kind == "bf16" and self.pending[0][2][4] != seq)):
             # a second backward through one module (in order), or operands one launch cannot share
-            # (the other operand kind, another T)
+            # (the other operand kind, another T or sample length)
             self.flush()
         if not self.callback_queued:
             torch.autograd.Variable._execution_engine.queue_callback(self._end_of_backward)
@@ -331,7 +335,8 @@ class WgradBatcher:
         keep = [t for p in pending for t in p[3]]
         if kind == "bf16":
             items = [(p[2][0], p[2][1], p[0].buffer, p[4]) for p in pending]
-            launch = lambda: _hip.tile_wgrad_batch(items, tab, order)
+            seq = pending[0][2][4]
+            launch = lambda: _hip.tile_wgrad_batch(items, tab, order, seq_len=seq)
         else:
             def launch():
                 items = [(_hip.mx_quant_cols(g2, rb), mx, p[0].buffer, p[4])
@@ -351,10 +356,13 @@ class TileGradBuckets:
     counts one module of its bucket. Buckets are issued as ``all_reduce(buffer[bucket],
     async_op=True)`` strictly from the last bucket to the first -- the order backward completes them
     in -- each as soon as it and every later bucket are complete, so all ranks issue the collectives
-    in the same order whatever the timing. A collective is enqueued on the process group's stream
-    behind the current stream's work (the tile-gradient kernels) and runs while backward continues.
-    :meth:`finish` issues what is left (buckets with a module that did not run backward in this
-    step: the engine zeroed such modules first) and makes the current stream wait for all of them."""
+    in the same order whatever the timing. A bucket's collective is issued from a communication
+    stream of its own that waits only for an event recorded behind the bucket's tile-gradient
+    kernels (on the engine's wgrad stream, or the current stream without one), so neither the
+    compute stream nor the wgrad stream waits at a bucket boundary; backward continues while the
+    collective runs. :meth:`finish` issues what is left (buckets with a module that did not run
+    backward in this step: the engine zeroed such modules first) behind the current stream and makes
+    the current stream wait for all of them."""
 
     def __init__(self, buffer: torch.Tensor, module_ranges: List[tuple], bucket_elems: int):
         self.buffer = buffer
@@ -374,7 +382,8 @@ class TileGradBuckets:
         self.seen: set = set()
         self.next = -1                         # next bucket to issue (descending)
         self.armed = False
-        self.side_stream = None                # the engine's wgrad stream: joined before a collective
+        self.side_stream = None                # the engine's wgrad stream (where the kernels run)
+        self.comm_stream = None                # the collectives are issued from here (device buffers)
 
     def arm(self) -> None:
         self.pending = [b[2] for b in self.buckets]
@@ -398,17 +407,30 @@ class TileGradBuckets:
             self._launch(self.next)
             self.next -= 1
 
-    def _launch(self, b: int) -> None:
+    def _launch(self, b: int, after=None) -> None:
+        """Issue bucket b's all-reduce once the work enqueued so far on ``after`` (default: the
+        stream that ran the bucket's tile-gradient kernels) is done."""
         start, end, _ = self.buckets[b]
-        if self.side_stream is not None:
-            torch.cuda.current_stream(self.side_stream.device).wait_stream(self.side_stream)
-        self.works[b] = dist.all_reduce(self.buffer[start:end], async_op=True)
+        flat = self.buffer[start:end]
+        if flat.device.type != "cuda":
+            self.works[b] = dist.all_reduce(flat, async_op=True)
+            return
+        if self.comm_stream is None:
+            self.comm_stream = torch.cuda.Stream(flat.device)
+        src = after if after is not None else (self.side_stream if self.side_stream is not None
+                                               else torch.cuda.current_stream(flat.device))
+        ev = torch.cuda.Event()
+        ev.record(src)
+        self.comm_stream.wait_event(ev)
+        with torch.cuda.stream(self.comm_stream):
+            self.works[b] = dist.all_reduce(flat, async_op=True)
 
     def finish(self) -> None:
         if not self.armed:
             return
+        cur = torch.cuda.current_stream(self.buffer.device) if self.buffer.device.type == "cuda" else None
         while self.next >= 0:
-            self._launch(self.next)
+            self._launch(self.next, after=cur)   # behind zero_unreported and the joined wgrad stream
             self.next -= 1
         for w in self.works:
             w.wait()
@@ -420,11 +442,15 @@ class DenseGradBuckets:
     warm-up (fine_tune.py:160-190; DeepSpeed's ``reduce_bucket_size`` buckets, deepspeed_helpers.py:73).
 
     Parameters are grouped in reverse registration order (the order backward produces their
-    gradients) into buckets of at least ``bucket_elems`` elements. A post-accumulate-grad hook counts
-    each parameter; buckets are issued in order, each as soon as it and every earlier bucket are
-    complete: the bucket's gradients are packed into one flat buffer (same dtype) and all-reduced
-    (sum) asynchronously. :meth:`finish` issues the rest (a parameter without a gradient contributes
-    zeros on every rank), waits, and writes the averaged values back into ``p.grad``."""
+    gradients) into buckets of at least ``bucket_elems`` elements. A post-accumulate-grad hook copies
+    each parameter's finished gradient ONCE into its bucket's flat buffer (allocated when the
+    bucket's first gradient arrives) and re-points ``p.grad`` at that slice, so the old gradient is
+    freed and nothing is copied back; buckets are issued in order, each as soon as it and every
+    earlier bucket are complete, as one asynchronous all-reduce (sum) of the flat buffer.
+    :meth:`finish` issues the rest (a parameter without a gradient contributes zeros on every rank),
+    waits, and divides each flat buffer by the world size in place: ``p.grad`` then holds the
+    DP-averaged value. A gradient accumulated into a parameter again after its bucket was issued
+    would be lost, so that raises (as :class:`TileGradBuckets` does)."""
 
     def __init__(self, params: List[torch.Tensor], bucket_elems: int, world: int):
         self.world = world
@@ -439,6 +465,12 @@ class DenseGradBuckets:
         if cur:
             self.buckets.append(cur)
         self.bucket_of = {id(p): i for i, b in enumerate(self.buckets) for p in b}
+        self.offset_of = {}
+        for b in self.buckets:
+            off = 0
+            for p in b:
+                self.offset_of[id(p)] = off
+                off += p.numel()
         self.handles = [p.register_post_accumulate_grad_hook(self._hook) for p in params]
         self.armed = False
         self.works: list = []
@@ -452,11 +484,39 @@ class DenseGradBuckets:
         self.next = 0
         self.armed = True
 
+    def _flat(self, b: int, like: torch.Tensor) -> torch.Tensor:
+        if self.flats[b] is None:
+            n = sum(p.numel() for p in self.buckets[b])
+            self.flats[b] = torch.empty(n, dtype=like.dtype, device=like.device)
+        return self.flats[b]
+
+    def _pack(self, p: torch.Tensor) -> None:
+        """Copy p.grad into its bucket slice (unless it already is that slice) and re-point it."""
+        b = self.bucket_of[id(p)]
+        off, n = self.offset_of[id(p)], p.numel()
+        flat = self._flat(b, p.grad if p.grad is not None else p)
+        view = flat[off:off + n].view_as(p)
+        if p.grad is None:
+            view.zero_()
+        elif p.grad.data_ptr() != view.data_ptr():
+            if p.grad.dtype != flat.dtype:
+                raise RuntimeError("DenseGradBuckets: gradients of one bucket must share a dtype")
+            view.copy_(p.grad)
+        p.grad = view
+
     def _hook(self, p: torch.Tensor) -> None:
-        if not self.armed or id(p) in self.seen:
+        if not self.armed:
+            return
+        b = self.bucket_of[id(p)]
+        if id(p) in self.seen:
+            if self.works[b] is not None:
+                raise RuntimeError("a dense gradient was accumulated again after its bucket was all-reduced "
+                                   "(a parameter used twice in one backward is not supported with DP buckets)")
+            self._pack(p)                       # a second accumulation before the launch: re-pack
             return
         self.seen.add(id(p))
-        self.pending[self.bucket_of[id(p)]] -= 1
+        self._pack(p)
+        self.pending[b] -= 1
         while self.next < len(self.buckets) and self.pending[self.next] == 0:
             self._launch(self.next)
             self.next += 1
@@ -464,11 +524,9 @@ class DenseGradBuckets:
     def _launch(self, b: int) -> None:
         params = self.buckets[b]
         for p in params:
-            if p.grad is None:
-                p.grad = torch.zeros_like(p)
-        flat = torch.cat([p.grad.reshape(-1) for p in params])
-        self.flats[b] = flat
-        self.works[b] = dist.all_reduce(flat, async_op=True)
+            if id(p) not in self.seen:          # no gradient on this rank in this step: zeros
+                self._pack(p)
+        self.works[b] = dist.all_reduce(self.flats[b], async_op=True)
 
     def finish(self) -> None:
         if not self.armed:
@@ -478,12 +536,7 @@ class DenseGradBuckets:
             self.next += 1
         for b, w in enumerate(self.works):
             w.wait()
-            flat = self.flats[b].div_(float(self.world))
-            off = 0
-            for p in self.buckets[b]:
-                n = p.numel()
-                p.grad.copy_(flat[off:off + n].view_as(p.grad))
-                off += n
+            self.flats[b].div_(float(self.world))          # p.grad are views of it
         self.works, self.flats = [], []
         self.armed = False
 
@@ -543,11 +596,6 @@ class _TileGroup:
             if fw.group is not None:
                 union.setdefault(id(fw.group), (fw.group, set()))[1].update(m.tiles.column_blocks())
         self.fp8_groups = [(g, torch.tensor(sorted(cbs), dtype=torch.int32).to(device)) for g, cbs in union.values()]
-        for g, cbs in union.values():
-            if any(getattr(m.weight, "_smt_fp8", None) is not None and m.weight._smt_fp8.mx_wgrad
-                   for m in modules if getattr(m.weight, "_smt_fp8", None) is not None
-                   and m.weight._smt_fp8.group is g):
-                g.set_mx_union(cbs, device)
         self.step = 0
 
     def begin_window(self) -> None:
@@ -581,6 +629,10 @@ class SMTEngine:
             gas = max(1, int(total) // (int(micro) * self.world)) if (micro and total) else 1
         self.gradient_accumulation_steps = int(gas)
         self.max_grad_norm = float(cfg.get("gradient_clipping", 0.0) or 0.0)
+        if "wgrad_rounding" in cfg:
+            # "reference": the tile gradients rounded as smt.py:397-404 does (per-sample bf16 partials)
+            from .smt import smt as _smt
+            _smt.set_wgrad_rounding(cfg["wgrad_rounding"])
         self.micro_steps = 0
         self.global_steps = 0
         self.device = next(model.parameters()).device
@@ -618,6 +670,7 @@ class SMTEngine:
                                                        self.reduce_bucket_size if self.world > 1 else None))
                 if dense:
                     self.dense_groups.append((group, dense))
+        self._set_mx_unions()
         self._norm_sq = torch.zeros(1, dtype=torch.float64, device=self.device)
         # tile-gradient kernels on a stream of their own (overlap_wgrad, default on): joined before
         # every collective over the tile buffer and at the end of backward
@@ -639,6 +692,18 @@ class SMTEngine:
         dense_params = [p for _g, ps in self.dense_groups for p in ps]
         self.dense_buckets = (DenseGradBuckets(dense_params, self.reduce_bucket_size, self.world)
                               if self.world > 1 and dense_params else None)
+
+    def _set_mx_unions(self) -> None:
+        """fp8 groups (q/k/v, gate/up) whose members run MX-fp8 tile gradients share one quantised
+        copy of their input's column blocks: the union over ALL members with tiles, whichever
+        optimizer parameter group (tile group) each member belongs to."""
+        union = {}
+        for tg in self.tile_groups:
+            for m, fw in tg.fp8_modules:
+                if fw.group is not None and fw.mx_wgrad:
+                    union.setdefault(id(fw.group), (fw.group, set()))[1].update(m.tiles.column_blocks())
+        for g, cbs in union.values():
+            g.set_mx_union(cbs, self.device)
 
     # -- DeepSpeed surface ----------------------------------------------------------------------
     def __call__(self, *args, **kwargs):

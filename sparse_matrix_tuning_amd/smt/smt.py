@@ -16,15 +16,18 @@ Differences from the reference, all deliberate:
 
 * no process-group initialisation or rank query at import (smt.py:20-21);
 * no ``print_rank_0`` spam;
-* the wgrad sums the whole batch in fp32 and rounds once, where the reference rounds every
-  per-sample ``[256, 256]`` partial to bf16 before summing (smt.py:397-404), so tile gradients
-  are closer to exact than the reference's (tolerance stated in tests/test_gpu_parity.py).
+* by default the wgrad sums the whole batch in fp32 and rounds once, where the reference rounds
+  every per-sample ``[256, 256]`` partial to bf16 before summing (smt.py:397-404), so tile
+  gradients are closer to exact than the reference's. :func:`set_wgrad_rounding("reference")`
+  (or ``SMT_WGRAD_ROUNDING=reference``, or the engine config key ``"wgrad_rounding"``) reproduces
+  the reference's rounding instead (``smt_tile_wgrad_batch_seq``; tests/test_gpu_wgrad_full.py).
 
 There is no CPU or eager-PyTorch path: a module built on CPU tensors raises. ``meta`` tensors are
 accepted for shape-only construction (used by the CPU tests of the conversion logic).
 """
 from __future__ import annotations
 
+import os
 import re
 from typing import Iterable, List, Optional, Sequence, Tuple
 
@@ -36,6 +39,26 @@ from .. import _hip, dgrad
 Block_dimension = 256
 
 _LAYER_PATTERN = re.compile(r'model\.layers\.(\d+)\.')
+
+# Tile-gradient rounding of linearZ.backward: "single" (fp32 over the whole batch, one rounding) or
+# "reference" (smt.py:397-404: every per-sample partial rounded to bf16, then the batch sum)
+WGRAD_ROUNDINGS = ("single", "reference")
+_wgrad_rounding = os.environ.get("SMT_WGRAD_ROUNDING", "single")
+if _wgrad_rounding not in WGRAD_ROUNDINGS:
+    raise ValueError(f"SMT_WGRAD_ROUNDING={_wgrad_rounding!r}: one of {WGRAD_ROUNDINGS}")
+
+
+def set_wgrad_rounding(mode: str) -> str:
+    """Select the tile-gradient rounding of every later ``linearZ`` forward; returns the old mode."""
+    global _wgrad_rounding
+    if mode not in WGRAD_ROUNDINGS:
+        raise ValueError(f"wgrad rounding {mode!r}: one of {WGRAD_ROUNDINGS}")
+    old, _wgrad_rounding = _wgrad_rounding, mode
+    return old
+
+
+def wgrad_rounding() -> str:
+    return _wgrad_rounding
 _NO_DECAY = ["bias", "layer_norm.weight", "layernorm.weight", "norm.weight", "ln_f.weight"]
 
 
@@ -138,23 +161,24 @@ class TileIndex:
     def mx_kernel_tiles(self, col_pos: Optional[dict] = None) -> List[Tuple[int, int]]:
         """Host ``(row-block position, column-block position)`` list of :meth:`mx_tables`; with
         ``col_pos`` the column positions in a group's shared MX input blocks instead of this module's."""
+        # the entry holds the map itself: an id() of a map that was dropped could be reused
         key = ("mx_ktiles", id(col_pos))
-        t = self._dev.get(key)
-        if t is None:
+        e = self._dev.get(key)
+        if e is None or e[0] is not col_pos:
             rbs = {}
             for r, _c in self.index_list:
                 rbs.setdefault(r, len(rbs))
             pos = col_pos if col_pos is not None else {c: i for i, c in enumerate(self.column_blocks())}
-            t = self._dev[key] = [(rbs[r], pos[c]) for r, c in self.index_list]
-        return t
+            e = self._dev[key] = (col_pos, [(rbs[r], pos[c]) for r, c in self.index_list])
+        return e[1]
 
     def mx_group_table(self, col_pos: dict, device: torch.device) -> torch.Tensor:
         """Device int32 [n, 2] table of :meth:`mx_kernel_tiles` against a group's shared blocks."""
         key = ("mx_group", id(col_pos), device.type, device.index)
-        t = self._dev.get(key)
-        if t is None:
-            t = self._dev[key] = _hip.tile_table(self.mx_kernel_tiles(col_pos), device)
-        return t
+        e = self._dev.get(key)
+        if e is None or e[0] is not col_pos:
+            e = self._dev[key] = (col_pos, _hip.tile_table(self.mx_kernel_tiles(col_pos), device))
+        return e[1]
 
     def block_tables(self, device: torch.device):
         """Device int32 tables of the distinct row blocks and column blocks the tiles touch."""
@@ -320,6 +344,8 @@ class linearZ(torch.autograd.Function):
             # smt.py:354-356 slices input[:, :, cols]; anything but 3-D fails there
             raise IndexError(f"too many indices for tensor of dimension {input.dim()}")
         ctx.tiles = tiles
+        # reference rounding: each of the input's B sequences (S rows) is one sample of smt.py:397-404
+        ctx.seq_len = int(input.shape[1]) if (_wgrad_rounding == "reference" and len(tiles)) else None
         ctx.sink = getattr(selected_weight, "_smt_grad_sink", None)
         ctx.packed = False
         ctx.mx = None
@@ -399,16 +425,17 @@ class linearZ(torch.autograd.Function):
             if sink is not None and sink.batcher() is not None:
                 # the engine launches this module's tiles together with those of the modules whose
                 # backward runs next (one smt_tile_wgrad_batch launch, deterministic)
-                sink.batcher().add(sink, g2, x2, tiles, ctx.packed)
+                sink.batcher().add(sink, g2, x2, tiles, ctx.packed, ctx.seq_len)
             elif sink is not None:
-                acc, order = sink.take_accumulate(), tiles.schedule(dev)
-                sink.run(lambda: _hip.tile_wgrad(g2, x2, table, sink.buffer, accumulate=acc, order=order), g2, x2)
+                acc, order, seq = sink.take_accumulate(), tiles.schedule(dev), ctx.seq_len
+                sink.run(lambda: _hip.tile_wgrad(g2, x2, table, sink.buffer, accumulate=acc, order=order,
+                                                 seq_len=seq), g2, x2)
                 sink.mark_ready()
             else:
                 grad_weight = torch.empty(n * Block_dimension, Block_dimension,
                                           dtype=grad_output.dtype, device=grad_output.device)
                 if n:
-                    _hip.tile_wgrad(g2, x2, table, grad_weight, order=tiles.schedule(dev))
+                    _hip.tile_wgrad(g2, x2, table, grad_weight, order=tiles.schedule(dev), seq_len=ctx.seq_len)
         if ctx.needs_input_grad[0]:
             wt = getattr(weight, "_smt_weight_t", None)
             fw = getattr(weight, "_smt_fp8", None)

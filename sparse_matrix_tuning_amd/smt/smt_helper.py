@@ -115,9 +115,10 @@ def reference_block_stat(grad: torch.Tensor, d1: int, d2: int, strategy: str) ->
 
 
 # Whether ATen's value of a block equals its value computed over just the block's row of blocks
-# (the per-output reduction order does not depend on the other rows): checked once per strategy and
-# process against the whole key; if it ever differed, whole keys would be re-scored.
-_ROW_SLICE_OK: Dict[str, bool] = {}
+# (the per-output reduction order does not depend on the other rows): checked against the whole key
+# once per (strategy, block grid, host thread count) and process, since ATen's split of a reduction
+# depends on the output count and the threads; if it ever differed, whole keys would be re-scored.
+_ROW_SLICE_OK: Dict[tuple, bool] = {}
 
 
 def block_rescorer(grad: torch.Tensor, d1: int, d2: int, strategy: str):
@@ -126,12 +127,13 @@ def block_rescorer(grad: torch.Tensor, d1: int, d2: int, strategy: str):
     expression over a slice, 1/d1 of the key's bytes to copy and reduce)."""
     def rescore(flat):
         rows = np.unique(np.asarray(flat, dtype=np.int64) // d2)
-        ok = _ROW_SLICE_OK.get(strategy)
+        key = (strategy, d1, d2, torch.get_num_threads())
+        ok = _ROW_SLICE_OK.get(key)
         if ok is None:
             full = reference_block_stat(grad, d1, d2, strategy)
             r0 = int(rows[0])
             part = reference_block_stat(grad[r0 * Block_dimension:(r0 + 1) * Block_dimension], 1, d2, strategy)
-            ok = _ROW_SLICE_OK[strategy] = bool(np.array_equal(part, full[r0 * d2:(r0 + 1) * d2]))
+            ok = _ROW_SLICE_OK[key] = bool(np.array_equal(part, full[r0 * d2:(r0 + 1) * d2]))
             if not ok:
                 return np.arange(d1 * d2), full
         if not ok:
@@ -345,11 +347,11 @@ def reference_channel_stat(act: torch.Tensor, strategy: str) -> np.ndarray:
 
 
 # Whether ATen's value of a channel equals its value computed over just the channel's aligned
-# 256-channel window of the [B, S, in] state: checked once per strategy and process against the whole
-# key (as _ROW_SLICE_OK for blocks). On this host ATen's outer reductions agree on windows of >= 32
+# 256-channel window of the [B, S, in] state: checked against the whole key once per (strategy, state
+# shape, host thread count) and process (as _ROW_SLICE_OK for blocks). On this host ATen's outer reductions agree on windows of >= 32
 # aligned channels and differ on arbitrary column subsets, so a window, never a gather, is re-scored.
 _CHANNEL_WINDOW = 256
-_CHANNEL_WINDOW_OK: Dict[str, bool] = {}
+_CHANNEL_WINDOW_OK: Dict[tuple, bool] = {}
 
 
 def channel_rescorer(src: torch.Tensor, strategy: str):
@@ -372,11 +374,12 @@ def channel_rescorer(src: torch.Tensor, strategy: str):
         # channels is a chain of close values): the whole key at once, in one copy
         if (C % W and int(wins[-1]) == C // W) or calls[0] > 2 or 4 * wins.size > -(-C // W):
             return np.arange(C), reference_channel_stat(src, strategy)
-        ok = _CHANNEL_WINDOW_OK.get(strategy)
+        key = (strategy, tuple(src.shape), torch.get_num_threads())
+        ok = _CHANNEL_WINDOW_OK.get(key)
         if ok is None:
             full = reference_channel_stat(src, strategy)
             w0 = int(wins[0])
-            ok = _CHANNEL_WINDOW_OK[strategy] = bool(np.array_equal(window(w0), full[w0 * W:(w0 + 1) * W]))
+            ok = _CHANNEL_WINDOW_OK[key] = bool(np.array_equal(window(w0), full[w0 * W:(w0 + 1) * W]))
             if not ok:
                 return np.arange(C), full
         if not ok:
@@ -402,7 +405,7 @@ def _exact_channel_means(dev_acc: torch.Tensor, src, C: int, strategy: str) -> O
     order, or None when that does not hold on this host for the shape (or for L1 / L2)."""
     if strategy not in ("mean_abs", "abs_mean"):
         return None
-    shape = tuple(dev_acc.shape)
+    shape = (tuple(dev_acc.shape), torch.get_num_threads())
     ok = _ATEN_MEAN_OK.get(shape)
     if ok is False:
         return None

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
     out = subprocess.run(["nm", "-D", "--defined-only", _hip.lib_path()], capture_output=True, text=True).stdout
     for name in declared_functions():
         assert re.search(rf"\bT {name}$", out, re.M), name
-    assert lib.smt_abi_version() == 7
+    assert lib.smt_abi_version() == 8
 
 
 def test_library_carries_gfx950_code_object():
@@ -45,6 +45,7 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(_hip.AdamWArgs) == 44
     assert ctypes.sizeof(_hip.RopeTensor) == 72
     assert ctypes.sizeof(_hip.AdamWTensor) == 48
+    assert ctypes.sizeof(_hip.WgradModule) == 56
 
 
 def test_validation_errors_without_gpu():
@@ -71,6 +72,18 @@ def test_validation_errors_without_gpu():
     assert lib.smt_wgrad_workspace_bytes(32768, 256) == 0          # S == 1: no slabs
     assert lib.smt_wgrad_workspace_bytes(32768, 128) == 128 * 2 * 65536 * 4
     assert lib.smt_wgrad_workspace_bytes(0, 27) == 0
+    # reference rounding (ABI v8): per-sample pieces, never crossing a sample boundary
+    assert lib.smt_wgrad_seq_workspace_bytes(32768, 2048, 51) == 51 * 16 * 65536 * 4        # 816 >= 256 splits
+    assert lib.smt_wgrad_seq_workspace_bytes(32768, 2048, 9) == 9 * 16 * 2 * 65536 * 4      # 9 tiles: 2 pieces
+    assert lib.smt_wgrad_seq_workspace_bytes(4096, 2048, 8) == 8 * 2 * 8 * 65536 * 4        # quarter: 8 x 2 x 8 x 4
+    assert lib.smt_wgrad_seq_workspace_bytes(4096, 3000, 8) == 0                            # not whole samples
+    mods = (_hip.WgradModule * 1)()
+    assert lib.smt_tile_wgrad_batch_seq(mods, 1, 4096, 3000, None, None, 8, 0, None, 0, None) == -1
+    assert b"null tile table" in lib.smt_last_error()
+    tab = ctypes.c_void_p(16)                           # never dereferenced: validation fails first
+    assert lib.smt_tile_wgrad_batch_seq(mods, 1, 4096, 3000, tab, None, 8, 0, None, 0, None) == -1
+    assert b"whole number" in lib.smt_last_error()
+    assert lib.smt_tile_wgrad_batch_seq(mods, 1, 4096, 0, tab, None, 8, 0, None, 0, None) == -1
     # channel path (ABI v3)
     assert lib.smt_row_gather(None, 256, 2, 256, None, 4, None, 256, None) == -1
     assert lib.smt_row_gather(None, 256, 2, 256, None, 0, None, 256, None) == 0       # no rows: no-op

@@ -114,18 +114,32 @@ def _dense_worker(rank, world, port, q):
     ok = [[p.numel() for p in b] for b in buckets.buckets] == [[4, 64], [16, 128], [3]]
     x = torch.randn(5, 8, generator=torch.Generator().manual_seed(10 + rank))
     for step in range(2):
+        # this rank's own gradients (p.grad becomes the bucket buffer, reduced in flight, once armed)
+        local = list(torch.autograd.grad(net(x).pow(2).sum(), list(net.parameters())))
         for p in params:
             p.grad = None
         buckets.arm()
         net(x).pow(2).sum().backward()
         ok &= buckets.next >= 1                         # the last layer's bucket went out during backward
-        local = [p.grad.clone() for p in net.parameters()]
         gathered = [[torch.zeros_like(g) for _ in range(world)] for g in local]
         buckets.finish()
         for g, bucket in zip(local, gathered):
             dist.all_gather(bucket, g)
         ok &= all(torch.allclose(p.grad, sum(b) / world) for p, b in zip(net.parameters(), gathered))
         ok &= torch.equal(unused.grad, torch.zeros(3))
+        # the averaged gradients ARE the bucket buffers (no copy back): p.grad views of one flat tensor
+        b0 = buckets.buckets[0]
+        ok &= b0[1].grad.data_ptr() == b0[0].grad.data_ptr() + 4 * b0[0].numel()
+    # a gradient accumulated again after its bucket went out would be lost: that raises
+    buckets.arm()
+    net(x).pow(2).sum().backward()
+    last = buckets.buckets[0][0]
+    try:
+        buckets._hook(last)
+        ok = False
+    except RuntimeError as e:
+        ok &= "again" in str(e)
+    buckets.finish()
     buckets.remove()
     q.put((rank, bool(ok)))
     dist.barrier()

@@ -55,8 +55,20 @@ def _build(device, cfg_dict):
         torch.set_default_dtype(prev)
 
 
+@pytest.mark.parametrize("rounding", ["single", "reference"])
 @pytest.mark.parametrize("case", list(CASES))
-def test_layer_loss_and_tile_grads_vs_reference_restatement(case):
+def test_layer_loss_and_tile_grads_vs_reference_restatement(case, rounding):
+    """Also the direct product-vs-restatement difference of every module's tile gradients
+    (oracle.linearz_backward on the module's own operands): <= 1e-3 with the reference-rounding mode
+    (smt.set_wgrad_rounding("reference")), <= 1.5 x the reference's own error by default."""
+    old = smt.set_wgrad_rounding(rounding)
+    try:
+        _layer_case(case, rounding)
+    finally:
+        smt.set_wgrad_rounding(old)
+
+
+def _layer_case(case, rounding):
     from sparse_matrix_tuning_amd.fused_llama import patch_llama, unpatch_llama
     cfg, B, S, att, mlp = CASES[case]
     model = _build(DEV, cfg)
@@ -67,12 +79,12 @@ def test_layer_loss_and_tile_grads_vs_reference_restatement(case):
     smt.convert_linear_layer_to_matrix_sparsity(model, sel_mlp, sel_att)
     patch_llama(model)
     try:
-        _gpu_and_host(model, sd, sel_mlp, sel_att, unpatch_llama, cfg, B, S)
+        _gpu_and_host(model, sd, sel_mlp, sel_att, unpatch_llama, cfg, B, S, rounding)
     finally:
         unpatch_llama()
 
 
-def _gpu_and_host(model, sd, sel_mlp, sel_att, unpatch_llama, cfg, B, S):
+def _gpu_and_host(model, sd, sel_mlp, sel_att, unpatch_llama, cfg, B, S, rounding):
     gpu_mods = {n: m for n, m in model.named_modules() if isinstance(m, smt.LinearLayer_MatrixSparsity)}
     assert len(gpu_mods) == 6
     seen_x, seen_g = {}, {}
@@ -105,5 +117,8 @@ def _gpu_and_host(model, sd, sel_mlp, sel_att, unpatch_llama, cfg, B, S):
         truth = ref.tile_grads_fp64(g, x, m.index_list)
         _gi, ref_gw = ref.linearz_backward(g, x, m.weight.detach().cpu(), m.index_list)
         err, ref_err = _rel(m.selected_weight.grad, truth), _rel(ref_gw, truth)
-        print(f"{n}: {len(m.index_list)} tiles, tile-grad rel err {err:.2e} (reference algorithm {ref_err:.2e})")
+        direct = _rel(m.selected_weight.grad, ref_gw)
+        print(f"{rounding}: {n}: {len(m.index_list)} tiles, vs oracle.linearz_backward {direct:.2e}; vs fp64 "
+              f"{err:.2e} (reference algorithm {ref_err:.2e})")
         assert err <= max(1e-3, 1.1 * ref_err), (n, err)
+        assert direct <= (1e-3 if rounding == "reference" else max(1e-3, 1.5 * ref_err)), (n, direct)

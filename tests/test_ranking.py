@@ -199,7 +199,23 @@ def test_block_row_rescore_equals_whole_key(strategy):
         covered, vals = smt_helper.block_rescorer(x, d1, d2, strategy)(np.array([0, d2 * (d1 // 2) + 3, d1 * d2 - 1]))
         assert np.array_equal(vals, full[covered])
         assert covered.size == 3 * d2
-    assert smt_helper._ROW_SLICE_OK[strategy]
+        assert smt_helper._ROW_SLICE_OK[(strategy, d1, d2, torch.get_num_threads())]
+
+
+@pytest.mark.parametrize("strategy", STRATEGIES)
+def test_row_slice_check_runs_per_shape(strategy):
+    """the row-slice assumption is checked for every new (block grid, thread count), not
+    once per strategy: a small-d2 key after a large-d2 key gets its own check against the whole key."""
+    gen = torch.Generator().manual_seed(10)
+    for r, c in ((1024, 14336), (1024, 512)):
+        x = torch.randn(r, c, generator=gen)
+        d1, d2 = r // 256, c // 256
+        key = (strategy, d1, d2, torch.get_num_threads())
+        smt_helper._ROW_SLICE_OK.pop(key, None)
+        full = smt_helper.reference_block_stat(x, d1, d2, strategy)
+        covered, vals = smt_helper.block_rescorer(x, d1, d2, strategy)(np.array([d2 + 1]))
+        assert key in smt_helper._ROW_SLICE_OK
+        assert np.array_equal(vals, full[covered])
 
 
 @pytest.mark.parametrize("strategy", ["mean_abs", "abs_mean", "L1", "L2"])
@@ -210,11 +226,12 @@ def test_channel_window_rescore_equals_whole_key(strategy):
     gen = torch.Generator().manual_seed(9)
     act = torch.rand(4, 2048, 5120, generator=gen) * torch.rand(5120, generator=gen)
     full = smt_helper.reference_channel_stat(act, strategy)
-    smt_helper._CHANNEL_WINDOW_OK.pop(strategy, None)
+    key = (strategy, tuple(act.shape), torch.get_num_threads())
+    smt_helper._CHANNEL_WINDOW_OK.pop(key, None)
     covered, vals = smt_helper.channel_rescorer(act, strategy)(np.array([3, 700, 5119]))
     assert np.array_equal(vals, full[covered])
     assert covered.size == 3 * 256
-    assert smt_helper._CHANNEL_WINDOW_OK[strategy]
+    assert smt_helper._CHANNEL_WINDOW_OK[key]
     # a partial last window (width not a multiple of 256) re-scores the whole key
     part = act[:, :, :1000].contiguous()
     covered, vals = smt_helper.channel_rescorer(part, strategy)(np.array([999]))
