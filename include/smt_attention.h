@@ -53,6 +53,24 @@ int smt_attn_bwd(const smt_attn_tensor* q, const smt_attn_tensor* k, const smt_a
                  const smt_attn_tensor* dq, const smt_attn_tensor* dk, const smt_attn_tensor* dv,
                  const smt_attn_shape* shape, hipStream_t stream);
 
+/*
+ * The same with a key mask (ABI v8): the attention of a padded batch, as transformers builds it from
+ * the 2-D attention_mask the reference's collator passes (input_ids != pad_token_id,
+ * deepspeed/helpers/helper.py:194-204), combined with the causal mask. key_mask: device uint64
+ * [B][key_mask_ld], key_mask_ld >= ceil(S / 64); bit (j & 63) of word b*key_mask_ld + (j >> 6) set =
+ * key j of batch b takes part. The mask may have holes anywhere (a pad id can occur inside a
+ * sequence). A query row whose visible keys are all masked gets o = 0, lse = +inf and zero
+ * gradients (torch's safe softmax). key_mask NULL = smt_attn_fwd / smt_attn_bwd.
+ */
+int smt_attn_fwd_kmask(const smt_attn_tensor* q, const smt_attn_tensor* k, const smt_attn_tensor* v,
+                       const smt_attn_tensor* o, float* lse, const uint64_t* key_mask, int64_t key_mask_ld,
+                       const smt_attn_shape* shape, hipStream_t stream);
+int smt_attn_bwd_kmask(const smt_attn_tensor* q, const smt_attn_tensor* k, const smt_attn_tensor* v,
+                       const smt_attn_tensor* o, const smt_attn_tensor* d_o, const float* lse, float* delta_ws,
+                       const smt_attn_tensor* dq, const smt_attn_tensor* dk, const smt_attn_tensor* dv,
+                       const uint64_t* key_mask, int64_t key_mask_ld, const smt_attn_shape* shape,
+                       hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -39,7 +39,7 @@ ABI_FUNCTIONS = (
     "smt_model_ops_last_error", "smt_rmsnorm_fwd", "smt_rmsnorm_bwd_waves", "smt_rmsnorm_bwd", "smt_rmsnorm_bwd_add_dw",
     "smt_add_rmsnorm_fwd", "smt_rmsnorm_bwd_add",
     "smt_rope_fwd", "smt_rope_bwd", "smt_swiglu_fwd", "smt_swiglu_bwd", "smt_ce_fwd", "smt_ce_bwd",
-    "smt_attn_last_error", "smt_attn_fwd", "smt_attn_bwd",
+    "smt_attn_last_error", "smt_attn_fwd", "smt_attn_bwd", "smt_attn_fwd_kmask", "smt_attn_bwd_kmask",
     "smt_fp8_last_error", "smt_quant_rows_e4m3", "smt_quant_cols_t_e4m3", "smt_quant_rows_cat_e4m3",
     "smt_swiglu_fwd_quant_e4m3", "smt_swiglu_bwd_quant_e4m3", "smt_rmsnorm_fwd_quant_e4m3",
     "smt_rmsnorm_bwd_add_quant_e4m3",
@@ -152,6 +152,9 @@ _SIGS = {
     "smt_attn_fwd": (ctypes.c_int, [ctypes.POINTER(AttnTensor)] * 4 + [_P, ctypes.POINTER(AttnShape), _P]),
     "smt_attn_bwd": (ctypes.c_int, [ctypes.POINTER(AttnTensor)] * 5 + [_P, _P] + [ctypes.POINTER(AttnTensor)] * 3
                      + [ctypes.POINTER(AttnShape), _P]),
+    "smt_attn_fwd_kmask": (ctypes.c_int, [ctypes.POINTER(AttnTensor)] * 4 + [_P, _P, _I64, ctypes.POINTER(AttnShape), _P]),
+    "smt_attn_bwd_kmask": (ctypes.c_int, [ctypes.POINTER(AttnTensor)] * 5 + [_P, _P] + [ctypes.POINTER(AttnTensor)] * 3
+                           + [_P, _I64, ctypes.POINTER(AttnShape), _P]),
     "smt_model_ops_last_error": (ctypes.c_char_p, []),
     "smt_rmsnorm_fwd": (ctypes.c_int, [_P, _I64, _P, _P, _I64, _P, _I64, _I32, ctypes.c_float, _P]),
     "smt_rmsnorm_bwd_waves": (ctypes.c_int, [_I64]),

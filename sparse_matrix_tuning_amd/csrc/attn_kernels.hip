@@ -205,11 +205,19 @@ static_assert(kFwdWaves == 4 || kFwdWaves == 8, "forward: 4 or 8 waves");
 static_assert(kDqWaves == 4 || kDqWaves == 8, "dQ: 4 or 8 waves");
 constexpr int kTileB = kKV * kRowB;        // 16 KiB per operand tile
 
+// Key mask (optional, smt_attn_*_kmask): bit (j & 63) of kmask[b * kmask_ld + (j >> 6)] set = key j
+// of batch b takes part (transformers' 2-D attention_mask of a padded batch, e.g. the reference's
+// collator mask input_ids != pad, deepspeed/helpers/helper.py:194-204). A query row whose every
+// visible key is masked gets a zero output, lse = +inf and zero gradients (torch's safe softmax).
+__device__ __forceinline__ bool key_bit(uint64_t w, int key) { return (w >> (key & 63)) & 1ull; }
+
 struct FwdArgs {
     Tns q, k, v;
     uint16_t* o;
     int64_t o_sb, o_sh, o_ss;
     float* lse;
+    const uint64_t* kmask;
+    int64_t kmask_ld;
     int B, Hq, Hkv, S;
     float sl2;                             // scale * log2(e)
 };
@@ -246,6 +254,7 @@ __device__ __forceinline__ PairTask pair_task(int L, int nblk, int G, int Hkv) {
 #endif
 constexpr int kFKV = SMT_FWD_KV, kFRing = SMT_FWD_RING, kFTileB = kFKV * kRowB, kFS = kFKV / 32;
 
+template <bool KMASK>
 __device__ __forceinline__ void fwd_block(const FwdArgs& a, uint8_t* lds, int b, int h, int hk, int qb) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -254,6 +263,7 @@ __device__ __forceinline__ void fwd_block(const FwdArgs& a, uint8_t* lds, int b,
     const uint16_t* qp = a.q.p + b * a.q.sb + h * a.q.sh;
     const uint16_t* kp = a.k.p + b * a.k.sb + hk * a.k.sh;
     const uint16_t* vp = a.v.p + b * a.v.sb + hk * a.v.sh;
+    const uint64_t* km = KMASK ? a.kmask + (int64_t)b * a.kmask_ld : nullptr;
 
     const int qrow = qw + l32;
     bf16x8_t qf[8];
@@ -328,6 +338,16 @@ __device__ __forceinline__ void fwd_block(const FwdArgs& a, uint8_t* lds, int b,
                     if (key > qrow) x[i] = kNegInf;
                 }
             }
+            if (KMASK) {
+                const uint64_t w = km[k0 >> 6];                    // workgroup-uniform
+                if (~w != 0ull) {
+#pragma unroll
+                    for (int i = 0; i < 16 * kFS; ++i) {
+                        const int key = k0 + 32 * (i >> 4) + (i & 3) + 8 * ((i & 15) >> 2) + 4 * hi;
+                        if (!key_bit(w, key)) x[i] = kNegInf;
+                    }
+                }
+            }
             float mloc = x[0];
 #pragma unroll
             for (int i = 1; i < 16 * kFS; ++i) mloc = fmaxf(mloc, x[i]);
@@ -336,20 +356,22 @@ __device__ __forceinline__ void fwd_block(const FwdArgs& a, uint8_t* lds, int b,
 #else
             const float m_new = fmaxf(m_run, other_half_max(mloc));
 #endif
+            // a row with no visible key so far (key mask only) keeps m = -inf: exponentiate against 0
+            const float m_use = (KMASK && m_new == kNegInf) ? 0.f : m_new;
             float p[16 * kFS];
             float sum = 0.f;
 #pragma unroll
             for (int i = 0; i < 16 * kFS; ++i) {
 #if SMT_ATTN_FASTSM
-                p[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(x[i], a.sl2, -m_new));
+                p[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(x[i], a.sl2, -m_use));
 #else
-                p[i] = __builtin_amdgcn_exp2f(x[i] - m_new);
+                p[i] = __builtin_amdgcn_exp2f(x[i] - m_use);
 #endif
                 sum += p[i];
             }
             // rescale only when some row's max grew (alpha = 1 exactly otherwise: skipping is exact)
             if (!SMT_ATTN_FASTSM || __builtin_amdgcn_ballot_w64(m_new != m_run) != 0) {   // wave-uniform
-                const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+                const float alpha = __builtin_amdgcn_exp2f(m_run - m_use);
                 l_run *= alpha;
 #pragma unroll
                 for (int dt = 0; dt < 4; ++dt)
@@ -373,7 +395,7 @@ __device__ __forceinline__ void fwd_block(const FwdArgs& a, uint8_t* lds, int b,
 
     const float l_tot = halves_sum(l_run);
     if (qrow < a.S) {
-        const float inv = 1.f / l_tot;
+        const float inv = (KMASK && !(l_tot > 0.f)) ? 0.f : 1.f / l_tot;
         uint16_t* op = a.o + b * a.o_sb + h * a.o_sh + (int64_t)qrow * a.o_ss;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt)
@@ -385,10 +407,13 @@ __device__ __forceinline__ void fwd_block(const FwdArgs& a, uint8_t* lds, int b,
                 w.y = pk_bf16(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
                 *reinterpret_cast<uint2*>(op + d) = w;
             }
-        if (hi == 0) a.lse[((int64_t)b * a.Hq + h) * a.S + qrow] = m_run + __log2f(l_tot);
+        if (hi == 0)
+            a.lse[((int64_t)b * a.Hq + h) * a.S + qrow] =
+                (KMASK && !(l_tot > 0.f)) ? __builtin_huge_valf() : m_run + __log2f(l_tot);
     }
 }
 
+template <bool KMASK>
 __global__ __launch_bounds__(64 * kFwdWaves, 8 / kFwdWaves)
 void attn_fwd_kernel(FwdArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kFRing * 2 * kFTileB];      // 64 KiB
@@ -402,7 +427,7 @@ void attn_fwd_kernel(FwdArgs a) {
     const int grp = L / per_group;
     const int rem = L - grp * per_group;
     const int hk = grp % a.Hkv;
-    fwd_block(a, lds, grp / a.Hkv, hk * G + rem % G, hk, nqb - 1 - rem / G);
+    fwd_block<KMASK>(a, lds, grp / a.Hkv, hk * G + rem % G, hk, nqb - 1 - rem / G);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -448,10 +473,13 @@ struct DqArgs {
     int64_t dq_sb, dq_sh, dq_ss;
     const float* lse;
     float* delta;
+    const uint64_t* kmask;
+    int64_t kmask_ld;
     int B, Hq, Hkv, S;
     float sl2, scale;
 };
 
+template <bool KMASK>
 __device__ __forceinline__ void dq_block(const DqArgs& a, uint8_t* lds, int b, int h, int hk, int qb) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -461,6 +489,7 @@ __device__ __forceinline__ void dq_block(const DqArgs& a, uint8_t* lds, int b, i
     const uint16_t* dop = a.dout.p + b * a.dout.sb + h * a.dout.sh;
     const uint16_t* kp = a.k.p + b * a.k.sb + hk * a.k.sh;
     const uint16_t* vp = a.v.p + b * a.v.sb + hk * a.v.sh;
+    const uint64_t* km = KMASK ? a.kmask + (int64_t)b * a.kmask_ld : nullptr;
 
     const int qrow = qw + l32;
     const bool qvalid = qrow < a.S;
@@ -541,15 +570,15 @@ __device__ __forceinline__ void dq_block(const DqArgs& a, uint8_t* lds, int b, i
                     dp[j] = mfma(row_frag(V, 32 * j + l32, 32 * ks + 16 * hi), df[ks], dp[j]);
                 }
             const bool diag = k0 + kKV - 1 > qw;
+            const uint64_t kw64 = KMASK ? km[k0 >> 6] : ~0ull;    // workgroup-uniform
             float ds[32];
 #pragma unroll
             for (int i = 0; i < 32; ++i) {
                 const int j = i >> 4, ii = i & 15;
                 float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(s[j][ii], a.sl2, -lse));
-                if (diag) {
-                    const int key = k0 + 32 * j + (ii & 3) + 8 * (ii >> 2) + 4 * hi;
-                    if (key > qrow) pv = 0.f;
-                }
+                const int key = k0 + 32 * j + (ii & 3) + 8 * (ii >> 2) + 4 * hi;
+                if (diag && key > qrow) pv = 0.f;
+                if (KMASK && !key_bit(kw64, key)) pv = 0.f;
                 ds[i] = pv * (dp[j][ii] - dlt);
             }
             bf16x8_t sf[4];
@@ -579,6 +608,7 @@ __device__ __forceinline__ void dq_block(const DqArgs& a, uint8_t* lds, int b, i
     }
 }
 
+template <bool KMASK>
 __global__ __launch_bounds__(64 * kDqWaves, 8 / kDqWaves)
 void attn_dq_kernel(DqArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * 2 * kTileB];      // 64 KiB
@@ -592,7 +622,7 @@ void attn_dq_kernel(DqArgs a) {
     const int grp = L / per_group;
     const int rem = L - grp * per_group;
     const int hk = grp % a.Hkv;
-    dq_block(a, lds, grp / a.Hkv, hk * G + rem % G, hk, nqb - 1 - rem / G);
+    dq_block<KMASK>(a, lds, grp / a.Hkv, hk * G + rem % G, hk, nqb - 1 - rem / G);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -625,10 +655,13 @@ struct DkvArgs {
     int64_t dv_sb, dv_sh, dv_ss;
     const float* lse;
     const float* delta;
+    const uint64_t* kmask;
+    int64_t kmask_ld;
     int B, Hq, Hkv, S;
     float sl2, scale;
 };
 
+template <bool KMASK>
 __device__ __forceinline__ void dkdv_block(const DkvArgs& a, uint8_t* lds, int b, int hk, int kb) {
     const int G = a.Hq / a.Hkv;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -636,6 +669,8 @@ __device__ __forceinline__ void dkdv_block(const DkvArgs& a, uint8_t* lds, int b
     const int hi = lane >> 5, l32 = lane & 31;
     const int k0 = kb * kKB, kw = k0 + wave * kKW;
     const int key = kw + l32;
+    // a masked key (key mask) has P = 0 for every query: zero dK / dV
+    const bool kvalid = !KMASK || (key < a.S && key_bit(a.kmask[(int64_t)b * a.kmask_ld + (key >> 6)], key));
     const uint16_t* kp = a.k.p + b * a.k.sb + hk * a.k.sh;
     const uint16_t* vp = a.v.p + b * a.v.sb + hk * a.v.sh;
     const uint32_t lds0 = lds_addr(lds);
@@ -720,6 +755,7 @@ __device__ __forceinline__ void dkdv_block(const DkvArgs& a, uint8_t* lds, int b
                     const int q = s0 + (i & 3) + 8 * (i >> 2) + 4 * hi;
                     if (key > q) pv = 0.f;
                 }
+                if (KMASK && !kvalid) pv = 0.f;
                 pr[i] = pv;
             }
             bf16x8_t pf[2], sf[2];
@@ -760,6 +796,7 @@ __device__ __forceinline__ void dkdv_block(const DkvArgs& a, uint8_t* lds, int b
     }
 }
 
+template <bool KMASK>
 __global__ __launch_bounds__(kDkvWaves * 64, 2)
 void attn_dkdv_kernel(DkvArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kVImg + kDkvRing * kSliceBuf];
@@ -771,7 +808,7 @@ void attn_dkdv_kernel(DkvArgs a) {
 #pragma nounroll
     for (int i = 0; i < t.n; ++i) {
         if (i) __syncthreads();
-        dkdv_block(a, lds, t.b, t.hk, t.blk[1 - i]);
+        dkdv_block<KMASK>(a, lds, t.b, t.hk, t.blk[1 - i]);
     }
 }
 
@@ -800,39 +837,52 @@ extern "C" {
 
 const char* smt_attn_last_error(void) { return g_err; }
 
-int smt_attn_fwd(const smt_attn_tensor* q, const smt_attn_tensor* k, const smt_attn_tensor* v,
-                 const smt_attn_tensor* o, float* lse, const smt_attn_shape* shape, hipStream_t stream) {
+int smt_attn_fwd_kmask(const smt_attn_tensor* q, const smt_attn_tensor* k, const smt_attn_tensor* v,
+                       const smt_attn_tensor* o, float* lse, const uint64_t* key_mask, int64_t key_mask_ld,
+                       const smt_attn_shape* shape, hipStream_t stream) {
     int rc;
-    if ((rc = check_shape(shape, "smt_attn_fwd")) || (rc = check_tensor(q, "q", "smt_attn_fwd")) ||
-        (rc = check_tensor(k, "k", "smt_attn_fwd")) || (rc = check_tensor(v, "v", "smt_attn_fwd")) ||
-        (rc = check_tensor(o, "o", "smt_attn_fwd")))
+    const char* fn = key_mask ? "smt_attn_fwd_kmask" : "smt_attn_fwd";
+    if ((rc = check_shape(shape, fn)) || (rc = check_tensor(q, "q", fn)) || (rc = check_tensor(k, "k", fn)) ||
+        (rc = check_tensor(v, "v", fn)) || (rc = check_tensor(o, "o", fn)))
         return rc;
-    if (!lse) return fail(-1, "smt_attn_fwd: null lse");
+    if (!lse) return fail(-1, "%s: null lse", fn);
+    if (key_mask && key_mask_ld < (shape->S + 63) / 64)
+        return fail(-1, "%s: key_mask_ld %lld < ceil(S / 64)", fn, (long long)key_mask_ld);
     FwdArgs a;
     a.q = tns(q); a.k = tns(k); a.v = tns(v);
     a.o = static_cast<uint16_t*>(o->ptr); a.o_sb = o->sb; a.o_sh = o->sh; a.o_ss = o->ss;
     a.lse = lse;
+    a.kmask = key_mask; a.kmask_ld = key_mask_ld;
     a.B = shape->B; a.Hq = shape->Hq; a.Hkv = shape->Hkv; a.S = shape->S;
     a.sl2 = shape->scale * 1.4426950408889634f;
     const int64_t nqb = (shape->S + kFwdQB - 1) / kFwdQB;
     const int64_t blocks = nqb * shape->Hq * shape->B;
-    if (blocks > 0x7fffffffLL) return fail(-1, "smt_attn_fwd: too many blocks");
-    hipLaunchKernelGGL(attn_fwd_kernel, dim3((unsigned)blocks), dim3(64 * kFwdWaves), 0, stream, a);
+    if (blocks > 0x7fffffffLL) return fail(-1, "%s: too many blocks", fn);
+    if (key_mask) hipLaunchKernelGGL(attn_fwd_kernel<true>, dim3((unsigned)blocks), dim3(64 * kFwdWaves), 0, stream, a);
+    else hipLaunchKernelGGL(attn_fwd_kernel<false>, dim3((unsigned)blocks), dim3(64 * kFwdWaves), 0, stream, a);
     return check_launch("attn_fwd_kernel");
 }
 
-int smt_attn_bwd(const smt_attn_tensor* q, const smt_attn_tensor* k, const smt_attn_tensor* v,
-                 const smt_attn_tensor* o, const smt_attn_tensor* d_o, const float* lse, float* delta_ws,
-                 const smt_attn_tensor* dq, const smt_attn_tensor* dk, const smt_attn_tensor* dv,
-                 const smt_attn_shape* shape, hipStream_t stream) {
+int smt_attn_fwd(const smt_attn_tensor* q, const smt_attn_tensor* k, const smt_attn_tensor* v,
+                 const smt_attn_tensor* o, float* lse, const smt_attn_shape* shape, hipStream_t stream) {
+    return smt_attn_fwd_kmask(q, k, v, o, lse, nullptr, 0, shape, stream);
+}
+
+int smt_attn_bwd_kmask(const smt_attn_tensor* q, const smt_attn_tensor* k, const smt_attn_tensor* v,
+                       const smt_attn_tensor* o, const smt_attn_tensor* d_o, const float* lse, float* delta_ws,
+                       const smt_attn_tensor* dq, const smt_attn_tensor* dk, const smt_attn_tensor* dv,
+                       const uint64_t* key_mask, int64_t key_mask_ld, const smt_attn_shape* shape,
+                       hipStream_t stream) {
     int rc;
-    const char* fn = "smt_attn_bwd";
+    const char* fn = key_mask ? "smt_attn_bwd_kmask" : "smt_attn_bwd";
     if ((rc = check_shape(shape, fn)) || (rc = check_tensor(q, "q", fn)) || (rc = check_tensor(k, "k", fn)) ||
         (rc = check_tensor(v, "v", fn)) || (rc = check_tensor(o, "o", fn)) || (rc = check_tensor(d_o, "do", fn)) ||
         (rc = check_tensor(dq, "dq", fn)) || (rc = check_tensor(dk, "dk", fn)) || (rc = check_tensor(dv, "dv", fn)))
         return rc;
     if (!lse || !delta_ws) return fail(-1, "%s: null lse / delta workspace", fn);
     if (!al16(lse) || !al16(delta_ws) || (shape->S & 3)) return fail(-2, "%s: lse / delta need 16-byte rows (S %% 4 == 0)", fn);
+    if (key_mask && key_mask_ld < (shape->S + 63) / 64)
+        return fail(-1, "%s: key_mask_ld %lld < ceil(S / 64)", fn, (long long)key_mask_ld);
     const int B = shape->B, Hq = shape->Hq, Hkv = shape->Hkv, S = shape->S;
     const float sl2 = shape->scale * 1.4426950408889634f;
 
@@ -847,9 +897,12 @@ int smt_attn_bwd(const smt_attn_tensor* q, const smt_attn_tensor* k, const smt_a
     qa.q = tns(q); qa.k = tns(k); qa.v = tns(v); qa.dout = tns(d_o); qa.o = tns(o);
     qa.dq = static_cast<uint16_t*>(dq->ptr); qa.dq_sb = dq->sb; qa.dq_sh = dq->sh; qa.dq_ss = dq->ss;
     qa.lse = lse; qa.delta = delta_ws;
+    qa.kmask = key_mask; qa.kmask_ld = key_mask_ld;
     qa.B = B; qa.Hq = Hq; qa.Hkv = Hkv; qa.S = S; qa.sl2 = sl2; qa.scale = shape->scale;
     const int64_t nqb = (S + kDqQB - 1) / kDqQB;
-    hipLaunchKernelGGL(attn_dq_kernel, dim3((unsigned)(nqb * Hq * B)), dim3(64 * kDqWaves), 0, stream, qa);
+    const dim3 qgrid((unsigned)(nqb * Hq * B)), qblock(64 * kDqWaves);
+    if (key_mask) hipLaunchKernelGGL(attn_dq_kernel<true>, qgrid, qblock, 0, stream, qa);
+    else hipLaunchKernelGGL(attn_dq_kernel<false>, qgrid, qblock, 0, stream, qa);
     if ((rc = check_launch("attn_dq_kernel"))) return rc;
 
     DkvArgs ka;
@@ -857,11 +910,20 @@ int smt_attn_bwd(const smt_attn_tensor* q, const smt_attn_tensor* k, const smt_a
     ka.dk = static_cast<uint16_t*>(dk->ptr); ka.dk_sb = dk->sb; ka.dk_sh = dk->sh; ka.dk_ss = dk->ss;
     ka.dv = static_cast<uint16_t*>(dv->ptr); ka.dv_sb = dv->sb; ka.dv_sh = dv->sh; ka.dv_ss = dv->ss;
     ka.lse = lse; ka.delta = delta_ws;
+    ka.kmask = key_mask; ka.kmask_ld = key_mask_ld;
     ka.B = B; ka.Hq = Hq; ka.Hkv = Hkv; ka.S = S; ka.sl2 = sl2; ka.scale = shape->scale;
     const int64_t nkb = (S + kKB - 1) / kKB;
     const dim3 grid((unsigned)(((nkb + 1) / 2) * Hkv * B));
-    hipLaunchKernelGGL(attn_dkdv_kernel, grid, dim3(kDkvWaves * 64), 0, stream, ka);
+    if (key_mask) hipLaunchKernelGGL(attn_dkdv_kernel<true>, grid, dim3(kDkvWaves * 64), 0, stream, ka);
+    else hipLaunchKernelGGL(attn_dkdv_kernel<false>, grid, dim3(kDkvWaves * 64), 0, stream, ka);
     return check_launch("attn_dkdv_kernel");
+}
+
+int smt_attn_bwd(const smt_attn_tensor* q, const smt_attn_tensor* k, const smt_attn_tensor* v,
+                 const smt_attn_tensor* o, const smt_attn_tensor* d_o, const float* lse, float* delta_ws,
+                 const smt_attn_tensor* dq, const smt_attn_tensor* dk, const smt_attn_tensor* dv,
+                 const smt_attn_shape* shape, hipStream_t stream) {
+    return smt_attn_bwd_kmask(q, k, v, o, d_o, lse, delta_ws, dq, dk, dv, nullptr, 0, shape, stream);
 }
 
 }  // extern "C"

@@ -453,12 +453,36 @@ def _attn_ready(t: torch.Tensor) -> torch.Tensor:
     return t.contiguous()
 
 
+class KeyMask:
+    """The key mask of a padded batch as the smt_flash kernels take it (include/smt_attention.h,
+    ``smt_attn_*_kmask``): ``bits`` int64 [B, ceil(S/64)] on the device, bit j%64 of word j/64 set =
+    key j takes part. Built by :func:`smt_flash_mask` from transformers' 2-D ``attention_mask``
+    (the reference's collator passes ``input_ids != pad_token_id``, helper.py:194-204)."""
+
+    __slots__ = ("bits", "S")
+
+    def __init__(self, bits: torch.Tensor, S: int):
+        self.bits, self.S = bits, int(S)
+
+    @classmethod
+    def from_padding_mask(cls, mask2d: torch.Tensor) -> "KeyMask":
+        B, S = mask2d.shape
+        W = -(-S // 64)
+        m = torch.zeros(B, W * 64, dtype=torch.int64, device=mask2d.device)
+        m[:, :S] = mask2d.to(torch.bool).to(torch.int64)
+        shifts = torch.arange(64, dtype=torch.int64, device=mask2d.device)
+        # distinct powers of two: the int64 sum is the bitwise OR (bit 63 wraps to the sign bit)
+        bits = (m.view(B, W, 64) << shifts).sum(-1)
+        return cls(bits.contiguous(), S)
+
+
 class FlashAttnFn(torch.autograd.Function):
     """Causal GQA attention: q [B, Hq, S, 128], k / v [B, Hkv, S, 128] (any strides with head_dim
-    innermost) -> o [B, S, Hq, 128] (the layout transformers' attention functions return)."""
+    innermost) -> o [B, S, Hq, 128] (the layout transformers' attention functions return).
+    ``key_mask``: optional :class:`KeyMask` (padded batches)."""
 
     @staticmethod
-    def forward(ctx, q, k, v, scale):
+    def forward(ctx, q, k, v, scale, key_mask=None):
         for t, n in ((q, "q"), (k, "k"), (v, "v")):
             _need(t, "flash attention " + n)
         B, Hq, S, D = q.shape
@@ -474,17 +498,23 @@ class FlashAttnFn(torch.autograd.Function):
         lse = torch.empty(B, Hq, S, dtype=torch.float32, device=q.device)
         ov = o.transpose(1, 2)
         shape = _hip.AttnShape(B, Hq, Hkv, S, float(scale), 0)
-        rc = _hip.load().smt_attn_fwd(ctypes.byref(_attn_tensor(q)), ctypes.byref(_attn_tensor(k)),
-                                      ctypes.byref(_attn_tensor(v)), ctypes.byref(_attn_tensor(ov)),
-                                      lse.data_ptr(), ctypes.byref(shape), _stream(q))
+        km, km_ld = None, 0
+        if key_mask is not None:
+            if key_mask.S != S or key_mask.bits.shape[0] != B or key_mask.bits.device != q.device:
+                raise ValueError(f"flash attention: key mask for [{key_mask.bits.shape[0]}, {key_mask.S}] keys, "
+                                 f"batch has [{B}, {S}]")
+            km, km_ld = key_mask.bits.data_ptr(), key_mask.bits.shape[1]
+        rc = _hip.load().smt_attn_fwd_kmask(ctypes.byref(_attn_tensor(q)), ctypes.byref(_attn_tensor(k)),
+                                            ctypes.byref(_attn_tensor(v)), ctypes.byref(_attn_tensor(ov)),
+                                            lse.data_ptr(), km, km_ld, ctypes.byref(shape), _stream(q))
         _hip._check(rc, "smt_attn_fwd")
-        ctx.save_for_backward(q, k, v, o, lse)
+        ctx.save_for_backward(q, k, v, o, lse, key_mask.bits if key_mask is not None else None)
         ctx.scale = float(scale)
         return o
 
     @staticmethod
     def backward(ctx, do):
-        q, k, v, o, lse = ctx.saved_tensors
+        q, k, v, o, lse, km = ctx.saved_tensors
         B, Hq, S, D = q.shape
         Hkv = k.shape[1]
         do = do if (do.stride(-1) == 1 and not any(s % 8 for s in do.stride()[:3]) and do.data_ptr() % 16 == 0) \
@@ -495,43 +525,69 @@ class FlashAttnFn(torch.autograd.Function):
         delta = torch.empty(B, Hq, S, dtype=torch.float32, device=q.device)
         shape = _hip.AttnShape(B, Hq, Hkv, S, ctx.scale, 0)
         T = _attn_tensor
-        rc = _hip.load().smt_attn_bwd(ctypes.byref(T(q)), ctypes.byref(T(k)), ctypes.byref(T(v)),
-                                      ctypes.byref(T(o.transpose(1, 2))), ctypes.byref(T(do.transpose(1, 2))),
-                                      lse.data_ptr(), delta.data_ptr(), ctypes.byref(T(dq)), ctypes.byref(T(dk)),
-                                      ctypes.byref(T(dv)), ctypes.byref(shape), _stream(q))
+        rc = _hip.load().smt_attn_bwd_kmask(ctypes.byref(T(q)), ctypes.byref(T(k)), ctypes.byref(T(v)),
+                                            ctypes.byref(T(o.transpose(1, 2))), ctypes.byref(T(do.transpose(1, 2))),
+                                            lse.data_ptr(), delta.data_ptr(), ctypes.byref(T(dq)),
+                                            ctypes.byref(T(dk)), ctypes.byref(T(dv)),
+                                            km.data_ptr() if km is not None else None,
+                                            km.shape[1] if km is not None else 0, ctypes.byref(shape), _stream(q))
         _hip._check(rc, "smt_attn_bwd")
-        return dq, dk, dv, None
+        return dq, dk, dv, None, None
 
 
-def flash_attention(q, k, v, scale=None):
-    """Causal attention ``[B, Hq, S, 128]`` x ``[B, Hkv, S, 128]`` -> ``[B, S, Hq, 128]``."""
-    return FlashAttnFn.apply(q, k, v, scale if scale is not None else q.shape[-1] ** -0.5)
+def flash_attention(q, k, v, scale=None, key_mask: "KeyMask" = None):
+    """Causal attention ``[B, Hq, S, 128]`` x ``[B, Hkv, S, 128]`` -> ``[B, S, Hq, 128]``; with
+    ``key_mask`` the keys it clears take no part (padded batches)."""
+    return FlashAttnFn.apply(q, k, v, scale if scale is not None else q.shape[-1] ** -0.5, key_mask)
 
 
 def smt_flash_attention_forward(module, query, key, value, attention_mask, dropout=0.0, scaling=None,
                                 is_causal=None, **kwargs):
-    """transformers attention-function signature (``AttentionInterface``). Causal self-attention
-    without padding only: anything else raises rather than silently changing semantics."""
-    if attention_mask is not None:
-        raise NotImplementedError("smt_flash attention: padded / custom masks are not supported "
-                                  "(the bench and the reference's packed batches use none)")
+    """transformers attention-function signature (``AttentionInterface``). Causal self-attention,
+    unpadded (``attention_mask`` None) or padded (a :class:`KeyMask` from :func:`smt_flash_mask`);
+    anything else raises rather than silently changing semantics."""
+    if attention_mask is not None and not isinstance(attention_mask, KeyMask):
+        raise NotImplementedError("smt_flash attention: only key-padding masks built by smt_flash_mask are "
+                                  f"supported (got {type(attention_mask).__name__})")
     if dropout:
         raise NotImplementedError("smt_flash attention: dropout is not supported")
     if is_causal is False or not getattr(module, "is_causal", True):
         raise NotImplementedError("smt_flash attention: causal attention only")
-    return flash_attention(query, key, value, scaling), None
+    return flash_attention(query, key, value, scaling, attention_mask), None
+
+
+def smt_flash_mask(batch_size, q_length, kv_length, q_offset=0, kv_offset=0, mask_function=None,
+                   attention_mask=None, **kwargs):
+    """transformers mask-interface builder for ``smt_flash`` (what ``create_causal_mask`` calls):
+    ``None`` for a plain causal batch (no mask, or every key valid), a :class:`KeyMask` for a padded
+    one: the causal mask AND the 2-D padding mask, exactly the mask ``sdpa_mask`` would materialise
+    as [B, 1, S, S]. Anything the kernels do not implement (a KV cache / offsets, packed sequences,
+    custom mask functions) raises."""
+    from transformers.masking_utils import causal_mask_function
+    if mask_function is not None and mask_function is not causal_mask_function:
+        raise NotImplementedError("smt_flash attention: custom / packed-sequence masks are not supported")
+    if q_offset or kv_offset or q_length != kv_length:
+        raise NotImplementedError("smt_flash attention: training-style self-attention only (no KV cache)")
+    if attention_mask is None:
+        return None
+    am = attention_mask
+    if am.dim() != 2 or am.shape[0] != batch_size or am.shape[1] < kv_length:
+        raise NotImplementedError(f"smt_flash attention: 2-D [B, S] padding mask expected, got {tuple(am.shape)}")
+    am = am[:, :kv_length].to(torch.bool)
+    if bool(am.all()):
+        return None
+    return KeyMask.from_padding_mask(am)
 
 
 ATTN_NAME = "smt_flash"
 
 
 def register_attention() -> str:
-    """Register ``smt_flash`` with transformers (attention function + the sdpa mask builder, which
-    returns no mask for plain causal batches)."""
+    """Register ``smt_flash`` with transformers (attention function + its mask builder)."""
     from transformers import AttentionInterface
-    from transformers.masking_utils import ALL_MASK_ATTENTION_FUNCTIONS, sdpa_mask
+    from transformers.masking_utils import ALL_MASK_ATTENTION_FUNCTIONS
     AttentionInterface.register(ATTN_NAME, smt_flash_attention_forward)
-    ALL_MASK_ATTENTION_FUNCTIONS.register(ATTN_NAME, sdpa_mask)
+    ALL_MASK_ATTENTION_FUNCTIONS.register(ATTN_NAME, smt_flash_mask)
     return ATTN_NAME
 
 

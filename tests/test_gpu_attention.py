@@ -12,7 +12,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from sparse_matrix_tuning_amd.fused_llama import FlashAttnFn, flash_attention
+from sparse_matrix_tuning_amd.fused_llama import FlashAttnFn, KeyMask, flash_attention, smt_flash_mask
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
@@ -81,3 +81,58 @@ def test_flash_attention_rejects_unsupported():
         flash_attention(q, q, q)
     with pytest.raises(RuntimeError):
         flash_attention(q.float(), q.float(), q.float())
+
+
+def _ref_masked(q, k, v, g, scale, keep):
+    """fp32 reference with a key mask ``keep`` [B, S] (bool) AND causal; a row with no visible key
+    has zero output and zero gradients (the kernels' safe-softmax convention)."""
+    G = q.shape[1] // k.shape[1]
+    qf, kf, vf = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    S = q.shape[2]
+    causal = torch.ones(S, S, dtype=torch.bool, device=q.device).tril()
+    allowed = causal[None, None] & keep[:, None, None, :]
+    s = (qf @ kf.repeat_interleave(G, 1).transpose(-1, -2)) * scale
+    s = s.masked_fill(~allowed, float("-inf"))
+    any_key = allowed.any(-1, keepdim=True)
+    p = torch.softmax(s.masked_fill(~any_key, 0.0), -1) * any_key
+    o = p @ vf.repeat_interleave(G, 1)
+    o.transpose(1, 2).backward(g.float())
+    lse2 = torch.logsumexp(s, dim=-1) / math.log(2.0)
+    return o.transpose(1, 2).detach(), qf.grad, kf.grad, vf.grad, lse2, any_key.squeeze(-1)
+
+
+@pytest.mark.parametrize("B,Hq,Hkv,S", [(3, 8, 2, 256), (2, 4, 4, 200), (2, 32, 8, 1024)])
+def test_flash_attention_key_mask_matches_fp32_reference(B, Hq, Hkv, S):
+    """Padded batches: right padding of mixed lengths plus pad-id holes inside a
+    sequence (LLaMA-3's pad id 0 is an ordinary token, deepspeed_helpers.py:600-602, and the collator's
+    mask is input_ids != pad, helper.py:194-204), including a row whose first key is masked (its first
+    queries see no key at all)."""
+    torch.manual_seed(S + B)
+    D = 128
+    mk = lambda H: torch.randn(B, S, H, D, device=DEV).bfloat16().transpose(1, 2).requires_grad_(True)
+    q, k, v = mk(Hq), mk(Hkv), mk(Hkv)
+    g = torch.randn(B, S, Hq, D, device=DEV).bfloat16()
+    keep = torch.ones(B, S, dtype=torch.bool, device=DEV)
+    keep[0, S - S // 3:] = False                       # right padding
+    keep[1, S // 2 + 7:] = False
+    keep[1, 5] = keep[1, 64] = keep[1, 100] = False     # holes (pad id inside the sequence)
+    if B > 2:
+        keep[2, 0:3] = False                            # queries 0-2 see no key
+    km = smt_flash_mask(B, S, S, attention_mask=keep.long())
+    assert isinstance(km, KeyMask)
+    o = flash_attention(q, k, v, key_mask=km)
+    lse = o.grad_fn.saved_tensors[4].clone()
+    o.backward(g)
+    ro, rdq, rdk, rdv, rlse, visible = _ref_masked(q, k, v, g, D ** -0.5, keep)
+    for name, mine, ref in (("o", o, ro), ("dq", q.grad, rdq), ("dk", k.grad, rdk), ("dv", v.grad, rdv)):
+        e = _rel(mine, ref)
+        assert e <= 8e-3, (name, e)
+        assert torch.isfinite(mine.float()).all(), name
+    vis = visible.expand_as(rlse)
+    assert (lse[vis] - rlse[vis]).abs().max().item() < 2e-3
+    assert torch.isinf(lse[~vis]).all() and (lse[~vis] > 0).all()
+    # masked keys get exactly zero dK / dV
+    dead = ~keep[:, None, :, None].expand(B, Hkv, S, D)
+    assert (k.grad.float()[dead] == 0).all() and (v.grad.float()[dead] == 0).all()
+    # an all-valid mask is no mask
+    assert smt_flash_mask(B, S, S, attention_mask=torch.ones(B, S, device=DEV)) is None
