@@ -92,6 +92,10 @@ def parse():
     ap.add_argument("--ref-mode-steps", type=int, default=None,
                     help="after the timed steps, also time this many steps with gradient checkpointing "
                          "(reported under 'grad_ckpt_mode'; default: as many as --steps; 0 disables)")
+    ap.add_argument("--selective-steps", type=int, default=None,
+                    help="after the timed steps, also time this many steps with the 'selective' activation "
+                         "policy (SMT linears fed by RMSNorm / SwiGLU keep no input blocks; the backward rebuilds "
+                         "them; reported under 'selective_mode'; default: as many as --steps; 0 disables)")
     ap.add_argument("--tile-spread", default="layers", choices=("layers", "none"),
                     help="layers: scale each layer's harvested gradients to a common mean |g| before the "
                          "selection, so the 872 tiles spread over all 32 layers as in a real fine-tune (random "
@@ -123,6 +127,8 @@ def parse():
     args.mlp_ratio = default_ratio if args.mlp_ratio is None else args.mlp_ratio
     if args.ref_mode_steps is None:
         args.ref_mode_steps = args.steps
+    if args.selective_steps is None:
+        args.selective_steps = args.steps
     return args
 
 
@@ -859,6 +865,35 @@ def main():
                 tg.buckets.side_stream = side
         del iso
 
+    # ---- the selective activation policy: GEMM outputs, attention O / LSE resident; the SMT linears'
+    # RMSNorm / SwiGLU input blocks rebuilt in the backward (smt.set_activation_policy) ----
+    def policy_point(n_steps, offset, label):
+        pb = batches(1 + n_steps, B, S, vocab, rank, device, offset=offset)
+        step(pb[0])
+        torch.cuda.synchronize()
+        torch.cuda.reset_peak_memory_stats(device)
+        el, per, _ = timed_steps(step, pb[1:], world, device)
+        r = torch.tensor([el, _median(per), torch.cuda.max_memory_allocated(device) / 1e9],
+                         dtype=torch.float64, device=device)
+        if world > 1:
+            dist.all_reduce(r, op=dist.ReduceOp.MAX)
+        del pb
+        return {label: True, "steps": n_steps,
+                "value": round(world * B * S * n_steps / r[0].item(), 1),
+                "ms_per_step": round(r[0].item() / n_steps * 1e3, 2),
+                "median_ms_per_step": round(r[1].item() * 1e3, 2),
+                "median_tokens_per_s": round(world * B * S / r[1].item(), 1),
+                "peak_hbm_gb": round(r[2].item(), 2)}
+
+    selective_mode = None
+    if args.selective_steps > 0 and not args.grad_ckpt and not args.fp8:
+        from sparse_matrix_tuning_amd.smt import smt as _smt
+        old_policy = _smt.set_activation_policy("selective")
+        selective_mode = policy_point(args.selective_steps, 60000, "selective")
+        selective_mode["recomputed"] = ("the column blocks SMT linears read of RMSNorm / SwiGLU outputs "
+                                        "(smt_colblock_recompute in the backward)")
+        _smt.set_activation_policy(old_policy)
+
     # ---- the reference's memory policy (per-layer recompute), same engine and tiles ----
     ckpt_mode = None
     if args.ref_mode_steps > 0 and not args.grad_ckpt:
@@ -991,6 +1026,7 @@ def main():
             "selection": {"seconds": round(sel_timer.seconds, 3), "elements": sel_timer.elements,
                           "band": sel_timer.reports},
             "grad_ckpt_mode": ckpt_mode,
+            "selective_mode": selective_mode,
             "step_mfma_frac": (round(per_gpu * F_ALG_GFLOP_PER_TOKEN * 1e9 / (PEAK_BF16_TFLOPS * 1e12), 4)
                                if args.model == "llama3-8b" else None),
             "roofline": roofline,

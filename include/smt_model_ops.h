@@ -76,6 +76,20 @@ int smt_swiglu_fwd(const void* gate, const void* up, void* out, int64_t n, hipSt
 int smt_swiglu_bwd(const void* gate, const void* up, const void* grad_out, void* grad_gate, void* grad_up, int64_t n,
                    hipStream_t stream);
 
+/* Activation policy "selective" (ABI 9): the 256-column blocks linearZ's tile weight gradient reads,
+ * rebuilt in the backward from the producer's saved operands instead of kept from the forward
+ * (deepspeed/smt/smt.py:351-358 keeps them as ctx.list1). Same block-major output as
+ * smt_colblock_gather (out[j][t][256] = value[t, col_blocks[j]*256 + k]) and bit-identical values:
+ *   SMT_RECOMPUTE_RMSNORM: value = bf16(float(w) * float(bf16(a * rstd[t])))   (smt_rmsnorm_fwd's y)
+ *   SMT_RECOMPUTE_SWIGLU:  value = bf16(float(bf16(silu(a))) * b)            (smt_swiglu_fwd's out)
+ * a / b: [T, >= cols] bf16 rows with leading dimensions ld_a / ld_b; weight: the norm's [cols] bf16;
+ * rstd: the norm's saved [T] fp32; col_blocks_dev: device int32 [n_cb]. */
+#define SMT_RECOMPUTE_RMSNORM 0
+#define SMT_RECOMPUTE_SWIGLU 1
+int smt_colblock_recompute(int32_t op, const void* a, int64_t ld_a, const void* b, int64_t ld_b, const void* weight,
+                           const float* rstd, int64_t T, const int32_t* col_blocks_dev, int32_t n_cb, void* out,
+                           hipStream_t stream);
+
 /* Causal-LM cross entropy over bf16 logits [rows, vocab] (transformers ForCausalLMLoss:
  * logits.float() -> log_softmax -> nll), without materialising fp32 logits.
  * Forward:  lse[r] = logsumexp(float(logits[r, :]));  loss[r] = lse[r] - float(logits[r, label[r]]),

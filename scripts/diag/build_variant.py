@@ -5,7 +5,6 @@ scripts/diag/_variants/ (git-ignored; built .so files travel to the GPU box with
     python scripts/diag/build_variant.py ring2 -DSMT_DKV_RING=2
 """
 import os
-import subprocess
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
@@ -16,9 +15,7 @@ def main(name, *defines):
     out_dir = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_variants")
     os.makedirs(out_dir, exist_ok=True)
     out = os.path.join(out_dir, f"libsmt_hip_{name}.so")
-    cmd = [b.hipcc(), f"--offload-arch={b.ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", "-Wall",
-           "-Wno-unused-function", "-I", os.path.join(b.REPO_DIR, "include"), *defines, "-o", out, *b.SRCS]
-    subprocess.run(cmd, check=True)
+    b.run_build(out, defines)
     print(out)
 
 

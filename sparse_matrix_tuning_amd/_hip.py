@@ -37,7 +37,7 @@ ABI_FUNCTIONS = (
     "smt_channel_score_workspace_bytes", "smt_channel_score",
     "smt_channel_mean_aten_workspace_bytes", "smt_channel_mean_aten",
     "smt_model_ops_last_error", "smt_rmsnorm_fwd", "smt_rmsnorm_bwd_waves", "smt_rmsnorm_bwd", "smt_rmsnorm_bwd_add_dw",
-    "smt_add_rmsnorm_fwd", "smt_rmsnorm_bwd_add",
+    "smt_add_rmsnorm_fwd", "smt_rmsnorm_bwd_add", "smt_colblock_recompute",
     "smt_rope_fwd", "smt_rope_bwd", "smt_swiglu_fwd", "smt_swiglu_bwd", "smt_ce_fwd", "smt_ce_bwd",
     "smt_attn_last_error", "smt_attn_fwd", "smt_attn_bwd", "smt_attn_fwd_kmask", "smt_attn_bwd_kmask",
     "smt_fp8_last_error", "smt_quant_rows_e4m3", "smt_quant_cols_t_e4m3", "smt_quant_rows_cat_e4m3",
@@ -165,6 +165,7 @@ _SIGS = {
     "smt_rope_fwd": (ctypes.c_int, [ctypes.POINTER(RopeTensor), ctypes.POINTER(RopeTensor), _P, _P, _I64, _I64, _I64, _I32, _I32, _P]),
     "smt_rope_bwd": (ctypes.c_int, [ctypes.POINTER(RopeTensor), ctypes.POINTER(RopeTensor), _P, _P, _I64, _I64, _I64, _I32, _I32, _P]),
     "smt_swiglu_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _P]),
+    "smt_colblock_recompute": (ctypes.c_int, [_I32, _P, _I64, _P, _I64, _P, _P, _I64, _P, _I32, _P, _P]),
     "smt_swiglu_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I64, _P]),
     "smt_ce_fwd": (ctypes.c_int, [_P, _I64, _P, _I64, _I64, _I64, _P, _P, _P]),
     "smt_ce_bwd": (ctypes.c_int, [_P, _I64, _P, _P, _P, _I64, _I64, _I64, _P, _I64, _P]),
@@ -215,7 +216,8 @@ def _check(rc: int, what: str) -> None:
         lib = load()
         if what.startswith(("smt_quant", "smt_swiglu_fwd_quant", "smt_swiglu_bwd_quant")):
             err = lib.smt_fp8_last_error                 # fp8_kernels.hip
-        elif what.startswith(("smt_rmsnorm", "smt_add_rmsnorm", "smt_rope", "smt_swiglu", "smt_ce_")):
+        elif what.startswith(("smt_rmsnorm", "smt_add_rmsnorm", "smt_rope", "smt_swiglu", "smt_ce_",
+                              "smt_colblock_recompute")):
             err = lib.smt_model_ops_last_error           # llama_kernels.hip (incl. smt_rmsnorm_fwd_quant_e4m3)
         elif what.startswith("smt_attn"):
             err = lib.smt_attn_last_error
@@ -415,6 +417,35 @@ def colblock_gather(x2d: torch.Tensor, col_blocks: torch.Tensor) -> torch.Tensor
     rc = load().smt_colblock_gather(_ptr(x2d), x2d.stride(0), x2d.shape[0], _ptr(col_blocks), n_cb, _ptr(out),
                                     _stream(dev))
     _check(rc, "smt_colblock_gather")
+    return out
+
+
+RECOMPUTE_RMSNORM, RECOMPUTE_SWIGLU = 0, 1
+
+
+def colblock_recompute(op: int, a2d: torch.Tensor, col_blocks: torch.Tensor, b2d: torch.Tensor = None,
+                       weight: torch.Tensor = None, rstd: torch.Tensor = None) -> torch.Tensor:
+    """:func:`colblock_gather`'s [n_cb, T, 256] blocks of a norm's (``RECOMPUTE_RMSNORM``: ``a2d`` = its
+    input, ``weight``, ``rstd``) or SwiGLU's (``RECOMPUTE_SWIGLU``: ``a2d`` = gate, ``b2d`` = up) output,
+    rebuilt from those operands (bit-identical to gathering the producer's output)."""
+    dev = _require_device(a2d, col_blocks, b2d, weight, rstd)
+    for t in (a2d, b2d):
+        if t is not None and (t.dim() != 2 or t.stride(1) != 1 or t.dtype != torch.bfloat16):
+            raise ValueError("colblock_recompute: operands must be 2-D row-major bf16")
+    if b2d is not None and b2d.shape != a2d.shape:
+        raise ValueError("colblock_recompute: gate and up shapes differ")
+    if rstd is not None and (rstd.dtype != torch.float32 or rstd.numel() != a2d.shape[0] or not rstd.is_contiguous()):
+        raise ValueError("colblock_recompute: rstd must be a contiguous fp32 [T]")
+    if weight is not None and (weight.numel() != a2d.shape[1] or not weight.is_contiguous()):
+        raise ValueError("colblock_recompute: weight must be a contiguous [cols]")
+    n_cb = col_blocks.numel()
+    out = torch.empty(n_cb, a2d.shape[0], BLOCK, dtype=a2d.dtype, device=dev)
+    rc = load().smt_colblock_recompute(op, _ptr(a2d), a2d.stride(0), _ptr(b2d) if b2d is not None else None,
+                                       b2d.stride(0) if b2d is not None else 0,
+                                       _ptr(weight) if weight is not None else None,
+                                       _ptr(rstd) if rstd is not None else None, a2d.shape[0], _ptr(col_blocks), n_cb,
+                                       _ptr(out), _stream(dev))
+    _check(rc, "smt_colblock_recompute")
     return out
 
 

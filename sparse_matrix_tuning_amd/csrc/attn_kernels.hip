@@ -21,6 +21,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <utility>
+
 #include "smt_attention.h"
 
 namespace {
@@ -413,10 +415,601 @@ __device__ __forceinline__ void fwd_block(const FwdArgs& a, uint8_t* lds, int b,
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Forward, software-pipelined (SMT_ATTN_FWD_PIPE, default). Same workgroup geometry, K/V tiles and
+// LDS ring as fwd_block; the loop is restructured after the PMC capture of round 3
+// (profiles/r03_attn_pmc.json: 8.1 VALU instructions per MFMA, MFMA busy 0.39 -- the softmax VALU
+// of a tile sat between that tile's QK^T and PV MFMAs, and the diagonal masking and O rescale were
+// branches inside the loop body). Step t of a wave runs three independent pieces of work:
+//   QK^T of tile t+1 (16 MFMA, K rows by ds_read_b128)       -> scores S(t+1)
+//   softmax of tile t  (VALU: max, exp2, sum, bf16 pack)     -> P(t)
+//   PV of tile t-1     (16 MFMA, V by ds_read_b64_tr_b16)    -> O += P(t-1) V(t-1)
+// in one branch-free basic block, so the scheduler interleaves the VALU with the 32 MFMAs. K(t+1)
+// and V(t-1) are read in step t, K(t+2) and V(t) are written: both live in LDS slot t%2 / (t+1)%2,
+// one barrier per step. The running max is deferred (cdna_hip_programming T13): a row's max moves
+// only when a tile's max exceeds it by more than kFwdThr (log2 units), so P <= 2^kFwdThr and the O
+// rescale (a branch after the step's PV) is rare; P = exp2(s*c - m) keeps bf16's relative precision.
+// The only masked tile of a wave (the causal diagonal) is its last one, handled by a step variant.
+// ------------------------------------------------------------------------------------------------
+// SMT_ATTN_FWD_IMPL: 0 fwd_block, 1 FwdPipe (one workgroup per CU), 2 FwdLean (two per CU)
+#ifndef SMT_ATTN_FWD_IMPL
+#define SMT_ATTN_FWD_IMPL 2
+#endif
+#define SMT_ATTN_FWD_PIPE (SMT_ATTN_FWD_IMPL == 1)
+constexpr float kFwdThr = 8.f;
+constexpr int kFwdSlots = 3;
+// SMT_ATTN_FWD_AHEAD: LDS fragment reads issued this many MFMAs ahead of their use
+#ifndef SMT_ATTN_FWD_AHEAD
+#define SMT_ATTN_FWD_AHEAD 2
+#endif
+constexpr int kFwdAhead = SMT_ATTN_FWD_AHEAD;
+
+
+// v_max3_f32 as one instruction: fmaxf on MFMA results makes hipcc canonicalise both inputs first
+// (an extra v_max per operand; cdna_hip_programming Appendix B, attention pitfalls)
+__device__ __forceinline__ float max3f(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 template <bool KMASK>
-__global__ __launch_bounds__(64 * kFwdWaves, 8 / kFwdWaves)
+struct FwdPipe {
+    const FwdArgs& a;
+    uint8_t* lds;
+    uint32_t lds0;
+    __amdgpu_buffer_rsrc_t rk, rv;
+    const uint64_t* km;
+    const uint8_t* qimg;        // this wave's 32 Q rows in LDS (read per MFMA: frees 32 VGPRs)
+    f32x16_t o[4];
+    f32x16_t sc[2][2];          // scores of two tiles (step parity)
+    bf16x8_t pf[2][4];          // packed P of two tiles (step parity)
+    float m_run, l_run;
+    int qw, qrow, hi, l32, wave, lane, nt, last;
+    TrLane tl;
+
+    __device__ __forceinline__ FwdPipe(const FwdArgs& a_, uint8_t* lds_) : a(a_), lds(lds_) {}
+
+    // LDS ring of 3 slots of {K tile, V tile}: tile t lives in slot t % 3 (K(t+3) and V(t+1) are
+    // fetched in step t, two steps before they are read, so an HBM fetch has a whole step to land)
+    __device__ __forceinline__ uint8_t* slot(int t) { return lds + (t % kFwdSlots) * 2 * kTileB; }
+
+    __device__ __forceinline__ void issue_k(int t) {
+        dma_rows(rk, a.k.ss, lds0 + (uint32_t)((t % kFwdSlots) * 2 * kTileB), t * kKV, t * kKV + 16 * wave, 4, lane);
+    }
+    __device__ __forceinline__ void issue_v(int t) {
+        dma_rows(rv, a.v.ss, lds0 + (uint32_t)((t % kFwdSlots) * 2 * kTileB + kTileB), t * kKV, t * kKV + 16 * wave, 4,
+                 lane);
+    }
+
+    template <int P>
+    __device__ __forceinline__ void qk(int t) {               // S(t) = K(t) Q^T  -> sc[P]
+        const uint8_t* K = slot(t);
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+            const bf16x8_t qf = row_frag(qimg, l32, 32 * ks + 16 * hi);
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                sc[P][j] = mfma(row_frag(K, 32 * j + l32, 32 * ks + 16 * hi), qf, ks == 0 ? f32x16_t{} : sc[P][j]);
+        }
+    }
+
+    template <int P>
+    __device__ __forceinline__ void pv(int t) {               // O += P(t) V(t)  (pf[P])
+        const uint8_t* V = slot(t) + kTileB;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int kst = 0; kst < 4; ++kst) o[dt] = mfma(tr_frag(V, tl, 16 * kst, 32 * dt), pf[P][kst], o[dt]);
+    }
+
+    // softmax of tile t (scores sc[P]) -> pf[P]; returns this lane's rescale factor (1: none).
+    // Used by the first / last steps of a wave (and the diagonal tile, DIAG).
+    template <int P, bool DIAG>
+    __device__ __forceinline__ float softmax(int t) {
+        const int k0 = t * kKV;
+        float x[32];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) x[16 * j + i] = sc[P][j][i];
+        if (DIAG) {
+#pragma unroll
+            for (int i = 0; i < 32; ++i) {
+                const int key = k0 + 32 * (i >> 4) + (i & 3) + 8 * ((i & 15) >> 2) + 4 * hi;
+                if (key > qrow) x[i] = kNegInf;
+            }
+        }
+        if (KMASK) {
+            const uint64_t w = km[k0 >> 6];                    // workgroup-uniform
+            if (~w != 0ull) {
+#pragma unroll
+                for (int i = 0; i < 32; ++i) {
+                    const int key = k0 + 32 * (i >> 4) + (i & 3) + 8 * ((i & 15) >> 2) + 4 * hi;
+                    if (!key_bit(w, key)) x[i] = kNegInf;
+                }
+            }
+        }
+        float mx[11];
+#pragma unroll
+        for (int i = 0; i < 10; ++i) mx[i] = max3f(x[3 * i], x[3 * i + 1], x[3 * i + 2]);
+        mx[10] = max3f(x[30], x[31], mx[0]);
+        mx[0] = max3f(mx[0], mx[1], mx[2]);
+        mx[3] = max3f(mx[3], mx[4], mx[5]);
+        mx[6] = max3f(mx[6], mx[7], mx[8]);
+        mx[9] = max3f(mx[9], mx[10], mx[0]);
+        const float m_tile = other_half_max(max3f(mx[3], mx[6], mx[9])) * a.sl2;
+        const bool move = m_tile > m_run + kFwdThr;           // -inf + thr = -inf: the first tile moves
+        const float m_new = move ? m_tile : m_run;
+        const float alpha = move ? __builtin_amdgcn_exp2f(m_run - m_new) : 1.f;
+        const float m_use = (KMASK && m_new == kNegInf) ? 0.f : m_new;
+#pragma unroll
+        for (int i = 0; i < 32; ++i) x[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(x[i], a.sl2, -m_use));
+        float sm[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sm[i] = x[i] + x[i + 16];
+#pragma unroll
+        for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+            for (int i = 0; i < w; ++i) sm[i] += sm[i + w];
+        l_run = l_run * alpha + sm[0];
+        m_run = m_new;
+        pack_b_frags(*reinterpret_cast<const float(*)[16]>(&x[0]), pf[P][0], pf[P][1]);
+        pack_b_frags(*reinterpret_cast<const float(*)[16]>(&x[16]), pf[P][2], pf[P][3]);
+        return alpha;
+    }
+
+    __device__ __forceinline__ void rescale(float alpha) {
+        if (__builtin_amdgcn_ballot_w64(alpha != 1.f) != 0) {      // rare (deferred max)
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+        }
+    }
+
+    // The steady-state step (1 <= t < last), hand-interleaved: 32 chunks, each one MFMA (16 of
+    // QK(t+1), then 16 of PV(t-1)) with the LDS reads of the MFMA two chunks ahead and a slice of the
+    // softmax of tile t (chunks 0-7 row max, 8 the deferred-max decision, 9-24 exp2, 25-27 row sum,
+    // 28-31 bf16 pack of P(t) into pf[P]), fenced by sched_barrier so that every MFMA gap carries
+    // about 24 cycles of VALU issue (MI355X_MICROARCH "vector-instruction ISSUE cost";
+    // cdna_hip_programming Appendix B). The empty asm statements pin each slice's results to its chunk
+    // (the SelectionDAG otherwise emits pure arithmetic next to its first use, e.g. the row sum at the
+    // next step's head).
+    // per-step state of the chunked softmax
+    struct Chunks {
+        const uint8_t* K;
+        const uint8_t* V;
+        float x[32], mx[1], sm[16];
+        bf16x8_t fr[kFwdAhead + 1], qr[2];
+        float m_new, alpha, m_use;
+        int k0;
+        uint64_t kw;                                             // key-mask word of tile t (KMASK)
+    };
+
+    __device__ __forceinline__ bf16x8_t frag(const Chunks& st, int c) {   // operand A of MFMA c
+        if (c < 16) return row_frag(st.K, 32 * (c & 1) + l32, 32 * (c >> 1) + 16 * hi);
+        const int cc = c - 16;                                   // PV: key step cc >> 2, d tile cc & 3
+        return tr_frag(st.V, tl, 16 * (cc >> 2), 32 * (cc & 3));
+    }
+
+    template <int P, int C>
+    __device__ __forceinline__ void chunk(Chunks& st) {
+        constexpr int A = kFwdAhead;
+        if constexpr (C + A < 32) st.fr[(C + A) % (A + 1)] = frag(st, C + A);
+        // Q fragment ks is read two chunks before its first MFMA (chunk 2 ks) and used twice
+        if constexpr (C + 2 < 16 && ((C + 2) & 1) == 0) st.qr[((C + 2) >> 1) & 1] = row_frag(qimg, l32, 32 * ((C + 2) >> 1) + 16 * hi);
+        if constexpr (C < 16) {
+            constexpr int ks = C >> 1, j = C & 1;
+            sc[P ^ 1][j] = mfma(st.fr[C % (A + 1)], st.qr[ks & 1], ks == 0 ? f32x16_t{} : sc[P ^ 1][j]);
+        } else {
+            constexpr int cc = C - 16;
+            o[cc & 3] = mfma(st.fr[C % (A + 1)], pf[P ^ 1][cc >> 2], o[cc & 3]);
+        }
+        float* x = st.x;
+        float* sm = st.sm;
+        // ---- softmax slice C of tile t ----
+        if constexpr (C < 8) {                                   // row max over x[4C .. 4C+3]
+            float v[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = sc[P][C >> 2][4 * (C & 3) + i];
+            if (KMASK) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int idx = 4 * C + i;
+                    const int key = st.k0 + 32 * (idx >> 4) + (idx & 3) + 8 * ((idx & 15) >> 2) + 4 * hi;
+                    if (!key_bit(st.kw, key)) v[i] = kNegInf;
+                }
+            }
+            const float m0 = C == 0 ? v[0] : st.mx[0];
+            st.mx[0] = max3f(max3f(m0, v[0], v[1]), v[2], v[3]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) x[4 * C + i] = v[i];
+            asm volatile("" ::"v"(st.mx[0]));
+        } else if constexpr (C == 8) {
+            const float m_tile = other_half_max(st.mx[0]) * a.sl2;
+            const bool move = m_tile > m_run + kFwdThr;          // -inf + thr = -inf: the first tile moves
+            st.m_new = move ? m_tile : m_run;
+            st.alpha = move ? __builtin_amdgcn_exp2f(m_run - st.m_new) : 1.f;
+            st.m_use = (KMASK && st.m_new == kNegInf) ? 0.f : st.m_new;
+            asm volatile("" ::"v"(st.m_use), "v"(st.alpha));
+        } else if constexpr (C < 25) {                           // 2 x exp2(s*c - m)
+            constexpr int i = 2 * (C - 9);
+            x[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(x[i], a.sl2, -st.m_use));
+            x[i + 1] = __builtin_amdgcn_exp2f(__builtin_fmaf(x[i + 1], a.sl2, -st.m_use));
+            asm volatile("" ::"v"(x[i]), "v"(x[i + 1]));
+        } else if constexpr (C == 25) {                          // row sum (tree)
+#pragma unroll
+            for (int i = 0; i < 11; ++i) sm[i] = x[i] + x[i + 16];
+            asm volatile("" ::"v"(sm[0]), "v"(sm[1]), "v"(sm[2]), "v"(sm[3]), "v"(sm[4]), "v"(sm[5]), "v"(sm[6]),
+                         "v"(sm[7]), "v"(sm[8]), "v"(sm[9]), "v"(sm[10]));
+        } else if constexpr (C == 26) {
+#pragma unroll
+            for (int i = 11; i < 16; ++i) sm[i] = x[i] + x[i + 16];
+#pragma unroll
+            for (int i = 0; i < 5; ++i) sm[i] += sm[i + 8];
+            asm volatile("" ::"v"(sm[0]), "v"(sm[1]), "v"(sm[2]), "v"(sm[3]), "v"(sm[4]), "v"(sm[5]), "v"(sm[6]),
+                         "v"(sm[7]), "v"(sm[13]), "v"(sm[14]), "v"(sm[15]));
+        } else if constexpr (C == 27) {
+#pragma unroll
+            for (int i = 5; i < 8; ++i) sm[i] += sm[i + 8];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) sm[i] += sm[i + 4];
+            sm[0] += sm[2];
+            sm[1] += sm[3];
+            l_run = l_run * st.alpha + (sm[0] + sm[1]);
+            m_run = st.m_new;
+            asm volatile("" ::"v"(l_run), "v"(m_run));
+        } else {                                                 // 28..31: bf16 pack of P(t) into pf[P]
+            constexpr int h = (C - 28) >> 1, g = (C - 28) & 1;   // P[16h + 8g .. 16h + 8g + 7]
+            uint32_t w[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) w[i] = pk_bf16(x[16 * h + 8 * g + 2 * i], x[16 * h + 8 * g + 2 * i + 1]);
+            // pack_b_frags for half h: words 4g'..4g'+3 of that half; chunk g = 0 holds words 0-3, g = 1 words 4-7
+            auto p0 = __builtin_amdgcn_permlane32_swap(w[0], w[2], false, false);
+            auto p1 = __builtin_amdgcn_permlane32_swap(w[1], w[3], false, false);
+            u32x4_t v = {p0[0], p1[0], p0[1], p1[1]};
+            pf[P][2 * h + g] = __builtin_bit_cast(bf16x8_t, v);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+
+    template <int P, int... C>
+    __device__ __forceinline__ void chunks(Chunks& st, std::integer_sequence<int, C...>) {
+        (chunk<P, C>(st), ...);
+    }
+
+    // The steady-state step (1 <= t < last), hand-interleaved: 32 chunks, each one MFMA (16 of
+    // QK(t+1), then 16 of PV(t-1)) with the LDS reads of the MFMA two chunks ahead and a slice of the
+    // softmax of tile t (chunks 0-7 row max, 8 the deferred-max decision, 9-24 exp2, 25-27 row sum,
+    // 28-31 bf16 pack of P(t) into pf[P]), fenced by sched_barrier so that every MFMA gap carries
+    // about 24 cycles of VALU issue (MI355X_MICROARCH "vector-instruction ISSUE cost";
+    // cdna_hip_programming Appendix B). The empty asm statements pin each slice's results to its chunk
+    // (the SelectionDAG otherwise emits pure arithmetic next to its first use, e.g. the row sum at the
+    // next step's head).
+    template <int P, int R>
+    __device__ __forceinline__ float steady(int t) {
+        Chunks st;
+        // P == t & 1, R == t % 3: K(t+1) in slot (R+1) % 3, V(t-1) in slot (R+2) % 3, compile-time LDS
+        // offsets, so the per-lane fragment addresses are loop-invariant and the slot an immediate
+        st.K = lds + ((R + 1) % kFwdSlots) * 2 * kTileB;
+        st.V = lds + ((R + 2) % kFwdSlots) * 2 * kTileB + kTileB;
+        st.k0 = t * kKV;
+        st.kw = KMASK ? km[st.k0 >> 6] : ~0ull;
+#pragma unroll
+        for (int i = 0; i < kFwdAhead; ++i) st.fr[i] = frag(st, i);
+        st.qr[0] = row_frag(qimg, l32, 16 * hi);
+        st.m_new = 0.f;
+        st.alpha = 1.f;
+        st.m_use = 0.f;
+        chunks<P>(st, std::make_integer_sequence<int, 32>{});
+        return st.alpha;
+    }
+
+    // Step t with P = t & 1: DMA K(t+3) and V(t+1); QK(t+1) -> sc[P^1]; softmax(t): sc[P] -> pf[P];
+    // PV(t-1) with pf[P^1]; then wait for the DMAs of the previous step (K(t+2), V(t)) and the
+    // barrier. Every wave runs steps 0..nt (one barrier each): its steady steps 1..last-1 in a loop
+    // of their own (so the O accumulators stay in one register set across the loop), the first,
+    // diagonal, drain and idle steps through gen_step.
+    __device__ __forceinline__ int issue(int t) {           // returns the DMA instructions issued
+        int n = 0;
+        if (t + 3 < nt) { issue_k(t + 3); n += 4; }
+        if (t + 1 < nt) { issue_v(t + 1); n += 4; }
+        return n;
+    }
+
+    template <int P, int R>
+    __device__ __forceinline__ void steady_step(int t) {
+        const int n = issue(t);
+        rescale(steady<P, R>(t));
+        vm_wait_upto(n);                                       // this step's DMAs may stay in flight
+        __syncthreads();
+    }
+
+    template <int P>
+    __device__ __forceinline__ void gen_step(int t) {
+        const int n = issue(t);
+        if (t <= last + 1) {
+            float alpha = 1.f;
+            if (t + 1 <= last) qk<P ^ 1>(t + 1);
+            if (t == last) alpha = softmax<P, true>(t);
+            else if (t < last) alpha = softmax<P, false>(t);
+            if (t >= 1) pv<P ^ 1>(t - 1);
+            rescale(alpha);
+        }
+        vm_wait_upto(n);
+        __syncthreads();
+    }
+
+    __device__ __forceinline__ void run(int b, int h, int hk, int qb) {
+        const int tid = threadIdx.x;
+        lane = tid & 63;
+        wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        hi = lane >> 5;
+        l32 = lane & 31;
+        const int q0 = qb * kFwdQB;
+        qw = q0 + wave * kFwdQW;
+        qrow = qw + l32;
+        const uint16_t* qp = a.q.p + b * a.q.sb + h * a.q.sh;
+        const uint16_t* kp = a.k.p + b * a.k.sb + hk * a.k.sh;
+        const uint16_t* vp = a.v.p + b * a.v.sb + hk * a.v.sh;
+        km = KMASK ? a.kmask + (int64_t)b * a.kmask_ld : nullptr;
+        const int kv_end = min(a.S, q0 + kFwdQB);
+        nt = (kv_end + kKV - 1) / kKV;
+        last = min(nt - 1, qw / kKV);                          // this wave's diagonal tile
+        rk = uniform_rsrc(kp, (int64_t)a.S * a.k.ss * 2);
+        rv = uniform_rsrc(vp, (int64_t)a.S * a.v.ss * 2);
+        lds0 = lds_addr(lds);
+        tl = tr_lane(lane);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) o[dt][i] = 0.f;
+        m_run = kNegInf;
+        l_run = 0.f;
+
+        // LDS: K/V ring (3 slots x 32 KiB), then the 4 waves' Q rows (4 x 8 KiB)
+        constexpr int kRingB = kFwdSlots * 2 * kTileB;
+        qimg = lds + kRingB + wave * (kFwdQW * kRowB);
+        dma_rows(uniform_rsrc(qp, (int64_t)a.S * a.q.ss * 2), a.q.ss, lds0 + kRingB + wave * (kFwdQW * kRowB),
+                 qw, qw, kFwdQW / 4, lane);
+        for (int i = 0; i < 3; ++i)
+            if (i < nt) issue_k(i);
+        issue_v(0);
+        vm_wait_all();
+        __syncthreads();
+        qk<0>(0);
+        __syncthreads();                                       // K(0)'s slot is rewritten in step 0
+        gen_step<0>(0);
+        int t = 1;
+        // the steady steps, six per trip (t % 2 and t % 3 compile-time; t % 6 == 1 at entry), leaving
+        // after any step
+        while (t < last) {
+            steady_step<1, 1>(t++);
+            if (t >= last) break;
+            steady_step<0, 2>(t++);
+            if (t >= last) break;
+            steady_step<1, 0>(t++);
+            if (t >= last) break;
+            steady_step<0, 1>(t++);
+            if (t >= last) break;
+            steady_step<1, 2>(t++);
+            if (t >= last) break;
+            steady_step<0, 0>(t++);
+        }
+        for (; t <= nt; ++t) {
+            if (t & 1) gen_step<1>(t);
+            else gen_step<0>(t);
+        }
+
+        const float l_tot = halves_sum(l_run);
+        if (qrow < a.S) {
+            const float inv = (KMASK && !(l_tot > 0.f)) ? 0.f : 1.f / l_tot;
+            uint16_t* op = a.o + b * a.o_sb + h * a.o_sh + (int64_t)qrow * a.o_ss;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int d = 32 * dt + 8 * g + 4 * hi;
+                    uint2 w;
+                    w.x = pk_bf16(o[dt][4 * g] * inv, o[dt][4 * g + 1] * inv);
+                    w.y = pk_bf16(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
+                    *reinterpret_cast<uint2*>(op + d) = w;
+                }
+            if (hi == 0)
+                a.lse[((int64_t)b * a.Hq + h) * a.S + qrow] =
+                    (KMASK && !(l_tot > 0.f)) ? __builtin_huge_valf() : m_run + __log2f(l_tot);
+        }
+    }
+};
+
+// ------------------------------------------------------------------------------------------------
+// Forward, lean (SMT_ATTN_FWD_IMPL 2): fwd_block's structure (two workgroups per CU, i.e. two waves
+// per SIMD whose MFMA and VALU phases overlap each other; Q in registers; a 2-slot K/V ring, one
+// barrier per 64-key tile) with the per-tile VALU cut to what the softmax needs: tiles in pairs so the
+// LDS slot is a compile-time offset (no per-read address adds), the scores' first MFMA on a zero
+// accumulator (no per-tile zeroing), the row max by v_max3 without canonicalisation, row max / sum
+// as trees, the deferred max of FwdPipe (no per-tile O rescale) and the causal mask only on the
+// wave's diagonal tile.
+// ------------------------------------------------------------------------------------------------
+template <bool KMASK>
+struct FwdLean {
+    const FwdArgs& a;
+    uint8_t* lds;
+    __amdgpu_buffer_rsrc_t rk, rv;
+    uint32_t lds0;
+    const uint64_t* km;
+    bf16x8_t qf[8];
+    f32x16_t o[4];
+    float m_run, l_run;
+    int qw, qrow, hi, l32, wave, lane, nt, last;
+    TrLane tl;
+
+    __device__ __forceinline__ FwdLean(const FwdArgs& a_, uint8_t* lds_) : a(a_), lds(lds_) {}
+
+    __device__ __forceinline__ void issue(int t) {            // K(t), V(t) into slot t & 1
+        const uint32_t slot = lds0 + (uint32_t)((t & 1) * 2 * kTileB);
+        dma_rows(rk, a.k.ss, slot, t * kKV, t * kKV + 16 * wave, 4, lane);
+        dma_rows(rv, a.v.ss, slot + kTileB, t * kKV, t * kKV + 16 * wave, 4, lane);
+    }
+
+    template <int SLOT, bool DIAG_>
+    __device__ __forceinline__ void compute(int t, bool DIAG) {
+        const uint8_t* K = lds + SLOT * 2 * kTileB;
+        const uint8_t* V = K + kTileB;
+        const int k0 = t * kKV;
+        f32x16_t sc[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) sc[j] = mfma(row_frag(K, 32 * j + l32, 16 * hi), qf[0], f32x16_t{});
+#pragma unroll
+        for (int ks = 1; ks < 8; ++ks)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) sc[j] = mfma(row_frag(K, 32 * j + l32, 32 * ks + 16 * hi), qf[ks], sc[j]);
+        float x[32];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) x[16 * j + i] = sc[j][i];
+        if (DIAG) {
+#pragma unroll
+            for (int i = 0; i < 32; ++i) {
+                const int key = k0 + 32 * (i >> 4) + (i & 3) + 8 * ((i & 15) >> 2) + 4 * hi;
+                if (key > qrow) x[i] = kNegInf;
+            }
+        }
+        if (KMASK) {
+            const uint64_t w = km[k0 >> 6];                    // workgroup-uniform
+            if (~w != 0ull) {
+#pragma unroll
+                for (int i = 0; i < 32; ++i) {
+                    const int key = k0 + 32 * (i >> 4) + (i & 3) + 8 * ((i & 15) >> 2) + 4 * hi;
+                    if (!key_bit(w, key)) x[i] = kNegInf;
+                }
+            }
+        }
+        float mx[11];
+#pragma unroll
+        for (int i = 0; i < 10; ++i) mx[i] = max3f(x[3 * i], x[3 * i + 1], x[3 * i + 2]);
+        mx[10] = max3f(x[30], x[31], mx[0]);
+        mx[0] = max3f(mx[0], mx[1], mx[2]);
+        mx[3] = max3f(mx[3], mx[4], mx[5]);
+        mx[6] = max3f(mx[6], mx[7], mx[8]);
+        mx[9] = max3f(mx[9], mx[10], mx[0]);
+        const float m_tile = other_half_max(max3f(mx[3], mx[6], mx[9])) * a.sl2;
+        const bool move = m_tile > m_run + kFwdThr;
+        const float m_new = move ? m_tile : m_run;
+        const float alpha = move ? __builtin_amdgcn_exp2f(m_run - m_new) : 1.f;
+        const float m_use = (KMASK && m_new == kNegInf) ? 0.f : m_new;
+        // packed fp32 (v_pk_fma_f32 / v_pk_add_f32: two lanes' worth per VALU issue)
+        const f32x2_t sl2v = {a.sl2, a.sl2}, mv = {-m_use, -m_use};
+        f32x2_t sm[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const f32x2_t e = __builtin_elementwise_fma(f32x2_t{x[2 * i], x[2 * i + 1]}, sl2v, mv);
+            x[2 * i] = __builtin_amdgcn_exp2f(e.x);
+            x[2 * i + 1] = __builtin_amdgcn_exp2f(e.y);
+            sm[i] = f32x2_t{x[2 * i], x[2 * i + 1]};
+        }
+#pragma unroll
+        for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+            for (int i = 0; i < w; ++i) sm[i] += sm[i + w];
+        l_run = l_run * alpha + (sm[0].x + sm[0].y);
+        m_run = m_new;
+        if (__builtin_amdgcn_ballot_w64(move) != 0) {          // rare (deferred max)
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+        }
+        bf16x8_t pf[4];
+        pack_b_frags(*reinterpret_cast<const float(*)[16]>(&x[0]), pf[0], pf[1]);
+        pack_b_frags(*reinterpret_cast<const float(*)[16]>(&x[16]), pf[2], pf[3]);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int kst = 0; kst < 4; ++kst) o[dt] = mfma(tr_frag(V, tl, 16 * kst, 32 * dt), pf[kst], o[dt]);
+    }
+
+    // tile t (t & 1 == SLOT): fetch tile t+1 into the other slot, compute, wait, barrier
+    template <int SLOT>
+    __device__ __forceinline__ void tile(int t) {
+        if (t + 1 < nt) issue(t + 1);
+        if (t <= last) compute<SLOT, true>(t, t == last);
+        vm_wait_all();
+        __syncthreads();
+    }
+
+    __device__ __forceinline__ void run(int b, int h, int hk, int qb) {
+        const int tid = threadIdx.x;
+        lane = tid & 63;
+        wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        hi = lane >> 5;
+        l32 = lane & 31;
+        const int q0 = qb * kFwdQB;
+        qw = q0 + wave * kFwdQW;
+        qrow = qw + l32;
+        const uint16_t* qp = a.q.p + b * a.q.sb + h * a.q.sh;
+        const uint16_t* kp = a.k.p + b * a.k.sb + hk * a.k.sh;
+        const uint16_t* vp = a.v.p + b * a.v.sb + hk * a.v.sh;
+        km = KMASK ? a.kmask + (int64_t)b * a.kmask_ld : nullptr;
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+            if (qrow < a.S) qf[ks] = *reinterpret_cast<const bf16x8_t*>(qp + qrow * a.q.ss + 16 * ks + 8 * hi);
+            else qf[ks] = __builtin_bit_cast(bf16x8_t, u32x4_t{0u, 0u, 0u, 0u});
+        }
+        const int kv_end = min(a.S, q0 + kFwdQB);
+        nt = (kv_end + kKV - 1) / kKV;
+        last = min(nt - 1, qw / kKV);
+        rk = uniform_rsrc(kp, (int64_t)a.S * a.k.ss * 2);
+        rv = uniform_rsrc(vp, (int64_t)a.S * a.v.ss * 2);
+        lds0 = lds_addr(lds);
+        tl = tr_lane(lane);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) o[dt][i] = 0.f;
+        m_run = kNegInf;
+        l_run = 0.f;
+        issue(0);
+        vm_wait_all();
+        vm_wait_all_known();                                   // the Q fragments too (compiler-visible)
+        __syncthreads();
+        for (int t = 0; t < nt; t += 2) {
+            tile<0>(t);
+            if (t + 1 < nt) tile<1>(t + 1);
+        }
+        const float l_tot = halves_sum(l_run);
+        if (qrow < a.S) {
+            const float inv = (KMASK && !(l_tot > 0.f)) ? 0.f : 1.f / l_tot;
+            uint16_t* op = a.o + b * a.o_sb + h * a.o_sh + (int64_t)qrow * a.o_ss;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int d = 32 * dt + 8 * g + 4 * hi;
+                    uint2 w;
+                    w.x = pk_bf16(o[dt][4 * g] * inv, o[dt][4 * g + 1] * inv);
+                    w.y = pk_bf16(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
+                    *reinterpret_cast<uint2*>(op + d) = w;
+                }
+            if (hi == 0)
+                a.lse[((int64_t)b * a.Hq + h) * a.S + qrow] =
+                    (KMASK && !(l_tot > 0.f)) ? __builtin_huge_valf() : m_run + __log2f(l_tot);
+        }
+    }
+};
+
+// SMT_ATTN_FWD_OCC: workgroups per CU of the forward (2: 256 VGPRs per wave; 1: 512)
+#ifndef SMT_ATTN_FWD_OCC
+#define SMT_ATTN_FWD_OCC 1
+#endif
+template <bool KMASK>
+__global__ __launch_bounds__(64 * kFwdWaves, (SMT_ATTN_FWD_IMPL == 1 ? SMT_ATTN_FWD_OCC * 4 : 8) / kFwdWaves)
 void attn_fwd_kernel(FwdArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kFRing * 2 * kFTileB];      // 64 KiB
+    // K/V ring: 2 x 32 KiB (fwd_block) or 3 x 32 KiB + 32 KiB of Q rows (the pipelined forward)
+    __shared__ __attribute__((aligned(16))) uint8_t lds[SMT_ATTN_FWD_PIPE ? kFwdSlots * 2 * kTileB + kFwdQB * kRowB
+                                                                          : kFRing * 2 * kFTileB];
     const int nqb = (a.S + kFwdQB - 1) / kFwdQB;
     const int G = a.Hq / a.Hkv;
     const int total = nqb * a.Hq * a.B;
@@ -427,7 +1020,15 @@ void attn_fwd_kernel(FwdArgs a) {
     const int grp = L / per_group;
     const int rem = L - grp * per_group;
     const int hk = grp % a.Hkv;
-    fwd_block<KMASK>(a, lds, grp / a.Hkv, hk * G + rem % G, hk, nqb - 1 - rem / G);
+    if (SMT_ATTN_FWD_IMPL == 1 && kFwdWaves == 4 && kFKV == kKV && kFRing == 2) {
+        FwdPipe<KMASK> fp(a, lds);
+        fp.run(grp / a.Hkv, hk * G + rem % G, hk, nqb - 1 - rem / G);
+    } else if (SMT_ATTN_FWD_IMPL == 2 && kFwdWaves == 4 && kFKV == kKV && kFRing == 2) {
+        FwdLean<KMASK> fl(a, lds);
+        fl.run(grp / a.Hkv, hk * G + rem % G, hk, nqb - 1 - rem / G);
+    } else {
+        fwd_block<KMASK>(a, lds, grp / a.Hkv, hk * G + rem % G, hk, nqb - 1 - rem / G);
+    }
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -461,6 +461,40 @@ void swiglu_fwd_kernel(const uint16_t* __restrict__ g, const uint16_t* __restric
     st8(h + i * 8, o);
 }
 
+// Column blocks of a norm's or SwiGLU's output rebuilt from the producer's own saved operands
+// (activation policy "selective": linearZ keeps no copy of these inputs between forward and
+// backward). Same block-major layout as smt_colblock_gather (out[j][t][256]) and the producers'
+// arithmetic, so the values are bit-identical to the gathered ones:
+//   OP 0 (RMSNorm): out = bf16(float(w) * float(bf16(x * rstd)))   (rmsnorm_fwd_kernel, _reg_kernel)
+//   OP 1 (SwiGLU):  out = bf16(float(bf16(g * sigmoid(g))) * u)    (swiglu_fwd_kernel)
+// 16 B per thread, a wave covers two 512-B row pieces.
+template <int OP>
+__global__ __launch_bounds__(256)
+void colblock_recompute_kernel(const uint16_t* __restrict__ a, int64_t lda, const uint16_t* __restrict__ b, int64_t ldb,
+                               const uint16_t* __restrict__ w, const float* __restrict__ rstd, int64_t T,
+                               const int32_t* __restrict__ col_blocks, int32_t n_cb, uint16_t* __restrict__ out) {
+    const int64_t per_row = (int64_t)n_cb * 32;
+    const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t t = v / per_row;
+    if (t >= T) return;
+    const int r = (int)(v - t * per_row);
+    const int j = r >> 5, ch = r & 31;
+    const int64_t c = (int64_t)col_blocks[j] * 256 + ch * 8;
+    const F8 av = ld8(a + t * lda + c);
+    F8 o;
+    if (OP == 0) {
+        const float rs = rstd[t];
+        const F8 wv = ld8(w + c);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o.v[k] = wv.v[k] * rbf(av.v[k] * rs);
+    } else {
+        const F8 bv = ld8(b + t * ldb + c);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o.v[k] = rbf(av.v[k] * smt_sigmoid(av.v[k])) * bv.v[k];
+    }
+    st8(out + ((int64_t)j * T + t) * 256 + ch * 8, o);
+}
+
 __global__ __launch_bounds__(256)
 void swiglu_bwd_kernel(const uint16_t* __restrict__ g, const uint16_t* __restrict__ u, const uint16_t* __restrict__ dh,
                        uint16_t* __restrict__ dg, uint16_t* __restrict__ du, int64_t n8) {
@@ -904,6 +938,30 @@ int smt_swiglu_bwd(const void* gate, const void* up, const void* grad_out, void*
                        (const uint16_t*)gate, (const uint16_t*)up, (const uint16_t*)grad_out, (uint16_t*)grad_gate,
                        (uint16_t*)grad_up, n8);
     return check_launch("swiglu_bwd_kernel");
+}
+
+int smt_colblock_recompute(int32_t op, const void* a, int64_t ld_a, const void* b, int64_t ld_b, const void* weight,
+                           const float* rstd, int64_t T, const int32_t* col_blocks_dev, int32_t n_cb, void* out,
+                           hipStream_t stream) {
+    if (op != SMT_RECOMPUTE_RMSNORM && op != SMT_RECOMPUTE_SWIGLU)
+        return fail(-1, "smt_colblock_recompute: unknown op %d", (int)op);
+    if (T < 0 || n_cb < 0 || ld_a < 0 || ld_b < 0) return fail(-1, "smt_colblock_recompute: negative size");
+    if (T == 0 || n_cb == 0) return 0;
+    if (!a || !out || !col_blocks_dev) return fail(-1, "smt_colblock_recompute: null pointer");
+    if (op == SMT_RECOMPUTE_RMSNORM && (!weight || !rstd)) return fail(-1, "smt_colblock_recompute: null weight/rstd");
+    if (op == SMT_RECOMPUTE_SWIGLU && !b) return fail(-1, "smt_colblock_recompute: null up operand");
+    if (!aligned16(a) || !aligned16(out) || (ld_a & 7) || (op == SMT_RECOMPUTE_SWIGLU && (!aligned16(b) || (ld_b & 7))) ||
+        (op == SMT_RECOMPUTE_RMSNORM && !aligned16(weight)))
+        return fail(-2, "smt_colblock_recompute: 16-byte aligned rows required");
+    const int64_t blocks = (T * n_cb * 32 + 255) / 256;
+    if (blocks > 0x7fffffffLL) return fail(-1, "smt_colblock_recompute: too large");
+    if (op == SMT_RECOMPUTE_RMSNORM)
+        hipLaunchKernelGGL(colblock_recompute_kernel<0>, dim3((unsigned)blocks), dim3(256), 0, stream, (const uint16_t*)a,
+                           ld_a, nullptr, (int64_t)0, (const uint16_t*)weight, rstd, T, col_blocks_dev, n_cb, (uint16_t*)out);
+    else
+        hipLaunchKernelGGL(colblock_recompute_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, stream, (const uint16_t*)a,
+                           ld_a, (const uint16_t*)b, ld_b, nullptr, nullptr, T, col_blocks_dev, n_cb, (uint16_t*)out);
+    return check_launch("colblock_recompute_kernel");
 }
 
 }  // extern "C"

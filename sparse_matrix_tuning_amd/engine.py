@@ -633,6 +633,11 @@ class SMTEngine:
             # "reference": the tile gradients rounded as smt.py:397-404 does (per-sample bf16 partials)
             from .smt import smt as _smt
             _smt.set_wgrad_rounding(cfg["wgrad_rounding"])
+        if "activation_policy" in cfg:
+            # "selective": SMT linears fed by a norm / SwiGLU keep no input blocks; the backward
+            # rebuilds them (smt.smt.set_activation_policy)
+            from .smt import smt as _smt
+            _smt.set_activation_policy(cfg["activation_policy"])
         self.micro_steps = 0
         self.global_steps = 0
         self.device = next(model.parameters()).device

@@ -39,6 +39,13 @@ def _need(t: torch.Tensor, what: str):
         raise RuntimeError(f"fused {what}: bf16 ROCm tensors only (got {t.dtype} on {t.device})")
 
 
+def _tag(out, op, a2d, b2d=None, w=None, rstd=None):
+    """Under the "selective" activation policy, let an SMT linear consuming ``out`` rebuild its column
+    blocks from these operands in the backward instead of keeping them (smt.tag_recompute)."""
+    from .smt.smt import tag_recompute
+    return tag_recompute(out, op, a2d, b2d, w, rstd)
+
+
 def _rows2d(t: torch.Tensor):
     t2 = t.reshape(-1, t.shape[-1])
     if t2.stride(-1) != 1 or t2.stride(0) % 8 or t2.data_ptr() % 16:
@@ -64,7 +71,7 @@ class FusedRMSNormFn(torch.autograd.Function):
         _hip._check(rc, "smt_rmsnorm_fwd")
         ctx.save_for_backward(x2, w, rstd)
         ctx.shape = x.shape
-        return y.view(x.shape)
+        return _tag(y.view(x.shape), _hip.RECOMPUTE_RMSNORM, x2, None, w, rstd)
 
     @staticmethod
     def backward(ctx, dy):
@@ -185,7 +192,7 @@ class FusedAddRMSNormFn(torch.autograd.Function):
         _hip._check(rc, "smt_add_rmsnorm_fwd")
         ctx.save_for_backward(h, w, rstd)
         ctx.shape = x.shape
-        return h.view(x.shape), y.view(x.shape)
+        return h.view(x.shape), _tag(y.view(x.shape), _hip.RECOMPUTE_RMSNORM, h, None, w, rstd)
 
     @staticmethod
     def backward(ctx, dh, dy):
@@ -347,7 +354,7 @@ class FusedSwiGLUFn(torch.autograd.Function):
         h = torch.empty_like(g)
         rc = _hip.load().smt_swiglu_fwd(g.data_ptr(), u.data_ptr(), h.data_ptr(), g.numel(), _stream(g))
         _hip._check(rc, "smt_swiglu_fwd")
-        return h
+        return _tag(h, _hip.RECOMPUTE_SWIGLU, _rows2d(g), _rows2d(u))
 
     @staticmethod
     def backward(ctx, dh):

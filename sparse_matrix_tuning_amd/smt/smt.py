@@ -59,6 +59,41 @@ def set_wgrad_rounding(mode: str) -> str:
 
 def wgrad_rounding() -> str:
     return _wgrad_rounding
+
+
+# What linearZ keeps of its input for the tile weight gradient (smt.py:351-358 keeps column slices
+# of it): "resident" (the input, or a packed copy of its column blocks when the tiles touch at most
+# half of them), "selective" (when the input is an RMSNorm's or SwiGLU's output produced by
+# fused_llama, nothing: the backward rebuilds the column blocks from the producer's own saved
+# operands with smt_colblock_recompute; bit-identical tile gradients)
+ACTIVATION_POLICIES = ("resident", "selective")
+_activation_policy = os.environ.get("SMT_ACTIVATION_POLICY", "resident")
+if _activation_policy not in ACTIVATION_POLICIES:
+    raise ValueError(f"SMT_ACTIVATION_POLICY={_activation_policy!r}: one of {ACTIVATION_POLICIES}")
+
+
+def set_activation_policy(mode: str) -> str:
+    """Select what every later ``linearZ`` forward keeps of its input; returns the old policy."""
+    global _activation_policy
+    if mode not in ACTIVATION_POLICIES:
+        raise ValueError(f"activation policy {mode!r}: one of {ACTIVATION_POLICIES}")
+    old, _activation_policy = _activation_policy, mode
+    return old
+
+
+def activation_policy() -> str:
+    return _activation_policy
+
+
+def tag_recompute(out: torch.Tensor, op: int, a2d: torch.Tensor, b2d: Optional[torch.Tensor] = None,
+                  weight: Optional[torch.Tensor] = None, rstd: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Mark ``out`` (a norm's / SwiGLU's output) as rebuildable from the producer's operands (which
+    the producer saves for its own backward anyway); read by linearZ under the "selective" policy."""
+    if _activation_policy == "selective":
+        out._smt_recompute = (out._version, op, a2d, b2d, weight, rstd)
+    return out
+
+
 _NO_DECAY = ["bias", "layer_norm.weight", "layernorm.weight", "norm.weight", "ln_f.weight"]
 
 
@@ -322,6 +357,24 @@ def _rows_ready(t: torch.Tensor) -> torch.Tensor:
     return t
 
 
+def _recompute_source(input: torch.Tensor):
+    """The producer operands ``tag_recompute`` attached to ``input`` (None if absent or if ``input``
+    was modified in place since), with their versions for the backward's check."""
+    src = input.__dict__.get("_smt_recompute")
+    if src is None or src[0] != input._version:
+        return None
+    ops = src[2:]
+    return src[1], ops, tuple(None if t is None else t._version for t in ops)
+
+
+def _recompute_blocks(rec, cb_dev: torch.Tensor) -> torch.Tensor:
+    op, (a2d, b2d, w, rstd), versions = rec
+    if any(t is not None and t._version != v for t, v in zip((a2d, b2d, w, rstd), versions)):
+        raise RuntimeError("linearZ (selective activation policy): an operand of the input's producer was "
+                           "modified in place after the forward; its column blocks cannot be rebuilt")
+    return _hip.colblock_recompute(op, a2d, cb_dev, b2d=b2d, weight=w, rstd=rstd)
+
+
 class linearZ(torch.autograd.Function):
     """``y = x @ W^T`` (smt.py:350-373); backward returns ``(grad_input, grad_tiles, None, None)``
     (smt.py:376-413) with every tile's gradient from one grouped MFMA launch.
@@ -368,6 +421,12 @@ class linearZ(torch.autograd.Function):
                 ctx.mx = _hip.mx_quant_cols(_rows_ready(input.reshape(-1, weight.shape[1])), cb_dev)
                 ctx.mx_pos = None
             saved = None
+        elif (_activation_policy == "selective" and ctx.needs_input_grad[1] and len(tiles)
+                and input.device.type == "cuda" and _recompute_source(input) is not None):
+            # rebuilt in the backward from the producer's saved operands: nothing kept here
+            ctx.recompute = _recompute_source(input)
+            saved = None
+            ctx.packed = True
         elif (ctx.needs_input_grad[1] and len(tiles) and input.device.type == "cuda"
                 and 2 * len(tiles.column_blocks()) <= in_blocks):
             cb_dev, _ = tiles.packed_tables(input.device)
@@ -417,7 +476,11 @@ class linearZ(torch.autograd.Function):
             out_f = weight.shape[0]
             g2 = _rows_ready(grad_output.reshape(-1, out_f))
             dev = g2.device
-            if ctx.packed:
+            if getattr(ctx, "recompute", None) is not None:
+                cb_dev, table = tiles.packed_tables(dev)
+                x2 = _recompute_blocks(ctx.recompute, cb_dev)
+                ctx.recompute = None
+            elif ctx.packed:
                 x2, table = saved, tiles.packed_tables(dev)[1]
             else:
                 x2, table = _rows_ready(saved.reshape(-1, weight.shape[1])), tiles.device_table(dev)
