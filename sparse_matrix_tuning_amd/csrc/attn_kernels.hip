@@ -127,6 +127,29 @@ __device__ __forceinline__ int xcd_logical(int bid, int total) {
     return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
 }
 
+// Explicit LDS addressing for compile-time image offsets. A swizzled row read (lds_off) of row r,
+// 16-B chunk (ks, hi) is (r*256 + (16hi ^ swz(r)<<4)) ^ (ks<<5), and a transposed read at rows
+// 16kq + krow (+4) and column block dt is 4096kq + ((r*256 + (feat_byte ^ swz<<4)) ^ (dt<<6)): one
+// lane constant per read family, one v_xor per read, the image base in the instruction's offset.
+// The lane constants are re-materialised per slice (an opaque copy), so hipcc cannot hoist the 8-16
+// derived addresses out of the loop and spill them.
+__device__ __forceinline__ uint32_t opaque(uint32_t v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+template <int IMG>
+__device__ __forceinline__ bf16x8_t rowx(const uint8_t* lds, uint32_t lo, int ks) {
+    return *reinterpret_cast<const bf16x8_t*>(lds + IMG + (lo ^ (uint32_t)(ks << 5)));
+}
+template <int IMG>
+__device__ __forceinline__ bf16x8_t trx(const uint8_t* lds, uint32_t t0, uint32_t t4, int kq, int dt) {
+    const uint32_t x = (uint32_t)(dt << 6);
+    s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(lds + IMG + 4096 * kq + (t0 ^ x)));
+    s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(lds + IMG + 4096 * kq + (t4 ^ x)));
+    const s16x8_t both = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8_t, both);
+}
+
 // LDS-DMA: lane l's 16 B from rsrc + voff land at LDS byte lds_base + 16*l (buffer_load ... lds).
 // Inline asm so that hipcc does not treat it as an LDS write aliasing every ds_read (it then drains
 // vmcnt before each read); completion is waited for explicitly (s_waitcnt vmcnt(0) + barrier).
@@ -1209,6 +1232,193 @@ __device__ __forceinline__ void dq_block(const DqArgs& a, uint8_t* lds, int b, i
     }
 }
 
+// dQ, lean (SMT_ATTN_DQ_IMPL 1, default): dq_block's algorithm with DkvLean's loop treatment: tiles
+// in pairs (compile-time ring slot), explicit LDS addresses from two lane constants, S and dP from
+// zero accumulators, p = exp2(c s - lse) and ds = p (dp - delta) in packed fp32, the causal test only
+// on the wave's diagonal tile, scheduling fences that bound the fragment reads hoisted ahead.
+#ifndef SMT_ATTN_DQ_IMPL
+#define SMT_ATTN_DQ_IMPL 1
+#endif
+template <bool KMASK>
+struct DqLean {
+    const DqArgs& a;
+    uint8_t* lds;
+    bf16x8_t qf[8], df[8];
+    f32x16_t dq[4];
+    float lse, dlt;
+    const uint64_t* km;
+    __amdgpu_buffer_rsrc_t rk, rv;
+    uint32_t lds0, lo_row, lo_t0, lo_t4;
+    int lane, wave, hi, l32, qw, qrow, nt, last;
+
+    __device__ __forceinline__ DqLean(const DqArgs& a_, uint8_t* lds_) : a(a_), lds(lds_) {}
+
+    __device__ __forceinline__ void issue(int t) {            // K(t), V(t) into slot t & 1
+        const uint32_t slot = lds0 + (uint32_t)((t & 1) * 2 * kTileB);
+        constexpr int rows_w = kKV / kDqWaves;
+        dma_rows(rk, a.k.ss, slot, t * kKV, t * kKV + rows_w * wave, rows_w / 4, lane);
+        dma_rows(rv, a.v.ss, slot + kTileB, t * kKV, t * kKV + rows_w * wave, rows_w / 4, lane);
+    }
+
+    template <int SLOT>
+    __device__ __forceinline__ void compute(int t, bool diag) {
+        constexpr int KI = SLOT * 2 * kTileB, VI = KI + kTileB;
+        const int k0 = t * kKV;
+        const uint32_t lr = opaque(lo_row);
+        constexpr int KH = KI + 32 * kRowB, VH = VI + 32 * kRowB;     // keys 32..63 of the tile
+        f32x16_t s[2], dp[2];
+        s[0] = mfma(rowx<KI>(lds, lr, 0), qf[0], f32x16_t{});
+        s[1] = mfma(rowx<KH>(lds, lr, 0), qf[0], f32x16_t{});
+        dp[0] = mfma(rowx<VI>(lds, lr, 0), df[0], f32x16_t{});
+        dp[1] = mfma(rowx<VH>(lds, lr, 0), df[0], f32x16_t{});
+#pragma unroll
+        for (int ks = 1; ks < 8; ++ks) {
+            s[0] = mfma(rowx<KI>(lds, lr, ks), qf[ks], s[0]);
+            s[1] = mfma(rowx<KH>(lds, lr, ks), qf[ks], s[1]);
+            dp[0] = mfma(rowx<VI>(lds, lr, ks), df[ks], dp[0]);
+            dp[1] = mfma(rowx<VH>(lds, lr, ks), df[ks], dp[1]);
+            if (ks & 1) __builtin_amdgcn_sched_barrier(0);
+        }
+        float pr[32];
+        const f32x2_t sl2v = {a.sl2, a.sl2}, lv = {-lse, -lse}, dv = {dlt, dlt};
+#pragma unroll
+        for (int i = 0; i < 32; i += 2) {
+            const int j = i >> 4, ii = i & 15;
+            const f32x2_t e = __builtin_elementwise_fma(f32x2_t{s[j][ii], s[j][ii + 1]}, sl2v, lv);
+            pr[i] = __builtin_amdgcn_exp2f(e.x);
+            pr[i + 1] = __builtin_amdgcn_exp2f(e.y);
+        }
+        if (diag) {
+#pragma unroll
+            for (int i = 0; i < 32; ++i) {
+                const int key = k0 + 32 * (i >> 4) + (i & 3) + 8 * ((i & 15) >> 2) + 4 * hi;
+                if (key > qrow) pr[i] = 0.f;
+            }
+        }
+        if (KMASK) {
+            const uint64_t w = km[k0 >> 6];                    // workgroup-uniform
+            if (~w != 0ull) {
+#pragma unroll
+                for (int i = 0; i < 32; ++i) {
+                    const int key = k0 + 32 * (i >> 4) + (i & 3) + 8 * ((i & 15) >> 2) + 4 * hi;
+                    if (!key_bit(w, key)) pr[i] = 0.f;
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 32; i += 2) {
+            const int j = i >> 4, ii = i & 15;
+            const f32x2_t r = (f32x2_t{dp[j][ii], dp[j][ii + 1]} - dv) * f32x2_t{pr[i], pr[i + 1]};
+            pr[i] = r.x;
+            pr[i + 1] = r.y;
+        }
+        bf16x8_t sf[4];
+        pack_b_frags(*reinterpret_cast<const float(*)[16]>(&pr[0]), sf[0], sf[1]);
+        pack_b_frags(*reinterpret_cast<const float(*)[16]>(&pr[16]), sf[2], sf[3]);
+        const uint32_t t0 = opaque(lo_t0), t4 = opaque(lo_t4);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+#pragma unroll
+            for (int kst = 0; kst < 4; ++kst) dq[dt] = mfma(trx<KI>(lds, t0, t4, kst, dt), sf[kst], dq[dt]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+
+    template <int SLOT>
+    __device__ __forceinline__ void tile(int t) {
+        if (t + 1 < nt) issue(t + 1);
+        if (t <= last) compute<SLOT>(t, t == last);
+        vm_wait_all();
+        __syncthreads();
+    }
+
+    __device__ __forceinline__ void run(int b, int h, int hk, int qb) {
+        const int tid = threadIdx.x;
+        lane = tid & 63;
+        wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        hi = lane >> 5;
+        l32 = lane & 31;
+        const int q0 = qb * kDqQB;
+        qw = q0 + wave * kFwdQW;
+        qrow = qw + l32;
+        const bool qvalid = qrow < a.S;
+        const uint16_t* qp = a.q.p + b * a.q.sb + h * a.q.sh;
+        const uint16_t* dop = a.dout.p + b * a.dout.sb + h * a.dout.sh;
+        const uint16_t* kp = a.k.p + b * a.k.sb + hk * a.k.sh;
+        const uint16_t* vp = a.v.p + b * a.v.sb + hk * a.v.sh;
+        km = KMASK ? a.kmask + (int64_t)b * a.kmask_ld : nullptr;
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+            if (qvalid) {
+                qf[ks] = *reinterpret_cast<const bf16x8_t*>(qp + qrow * a.q.ss + 16 * ks + 8 * hi);
+                df[ks] = *reinterpret_cast<const bf16x8_t*>(dop + qrow * a.dout.ss + 16 * ks + 8 * hi);
+            } else {
+                qf[ks] = __builtin_bit_cast(bf16x8_t, u32x4_t{0u, 0u, 0u, 0u});
+                df[ks] = qf[ks];
+            }
+        }
+        const int64_t srow = ((int64_t)b * a.Hq + h) * a.S + (qvalid ? qrow : 0);
+        lse = qvalid ? a.lse[srow] : 0.f;
+        if (SMT_DQ_DELTA) {
+            const uint16_t* op = a.o.p + b * a.o.sb + h * a.o.sh;
+            float part = 0.f;
+#pragma unroll
+            for (int ks = 0; ks < 8; ++ks) {
+                const u32x4_t ov = qvalid ? *reinterpret_cast<const u32x4_t*>(op + qrow * a.o.ss + 16 * ks + 8 * hi)
+                                          : u32x4_t{0u, 0u, 0u, 0u};
+                const u32x4_t dv = __builtin_bit_cast(u32x4_t, df[ks]);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    part += __uint_as_float(ov[j] << 16) * __uint_as_float(dv[j] << 16);
+                    part += __uint_as_float(ov[j] & 0xffff0000u) * __uint_as_float(dv[j] & 0xffff0000u);
+                }
+            }
+            dlt = halves_sum(part);
+            if (qvalid && hi == 0) a.delta[srow] = dlt;
+        } else {
+            dlt = qvalid ? a.delta[srow] : 0.f;
+        }
+        const int kv_end = min(a.S, q0 + kDqQB);
+        nt = (kv_end + kKV - 1) / kKV;
+        last = min(nt - 1, qw / kKV);
+        rk = uniform_rsrc(kp, (int64_t)a.S * a.k.ss * 2);
+        rv = uniform_rsrc(vp, (int64_t)a.S * a.v.ss * 2);
+        lds0 = lds_addr(lds);
+        {
+            const uint32_t r = (uint32_t)l32;
+            lo_row = r * kRowB + ((16u * hi) ^ (swz(r) << 4));
+            const TrLane tl = tr_lane(lane);
+            lo_t0 = tl.krow * kRowB + (tl.feat_byte ^ (swz(tl.krow) << 4));
+            lo_t4 = (tl.krow + 4) * kRowB + (tl.feat_byte ^ (swz(tl.krow + 4) << 4));
+        }
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) dq[dt][i] = 0.f;
+        if (nt > 0) issue(0);
+        vm_wait_all();
+        vm_wait_all_known();
+        __syncthreads();
+        for (int t = 0; t < nt; t += 2) {
+            tile<0>(t);
+            if (t + 1 < nt) tile<1>(t + 1);
+        }
+        if (qvalid) {
+            uint16_t* out = a.dq + b * a.dq_sb + h * a.dq_sh + (int64_t)qrow * a.dq_ss;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int d = 32 * dt + 8 * g + 4 * hi;
+                    uint2 w;
+                    w.x = pk_bf16(dq[dt][4 * g] * a.scale, dq[dt][4 * g + 1] * a.scale);
+                    w.y = pk_bf16(dq[dt][4 * g + 2] * a.scale, dq[dt][4 * g + 3] * a.scale);
+                    *reinterpret_cast<uint2*>(out + d) = w;
+                }
+        }
+    }
+};
+
 template <bool KMASK>
 __global__ __launch_bounds__(64 * kDqWaves, 8 / kDqWaves)
 void attn_dq_kernel(DqArgs a) {
@@ -1223,7 +1433,12 @@ void attn_dq_kernel(DqArgs a) {
     const int grp = L / per_group;
     const int rem = L - grp * per_group;
     const int hk = grp % a.Hkv;
-    dq_block<KMASK>(a, lds, grp / a.Hkv, hk * G + rem % G, hk, nqb - 1 - rem / G);
+    if (SMT_ATTN_DQ_IMPL == 1 && kDqWaves == 4) {
+        DqLean<KMASK> dl(a, lds);
+        dl.run(grp / a.Hkv, hk * G + rem % G, hk, nqb - 1 - rem / G);
+    } else {
+        dq_block<KMASK>(a, lds, grp / a.Hkv, hk * G + rem % G, hk, nqb - 1 - rem / G);
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1397,10 +1612,231 @@ __device__ __forceinline__ void dkdv_block(const DkvArgs& a, uint8_t* lds, int b
     }
 }
 
+// dK / dV, lean (SMT_ATTN_DKV_IMPL 1, default): dkdv_block's algorithm with the slice loop unrolled
+// by two so that the ring slot is a compile-time LDS offset (the ring now sits in front of the V
+// image, within the ds_read immediate range), S and dP started from zero accumulators and the row
+// constants applied afterwards in packed fp32 (p = exp2(c s - lse), ds = p (dp - delta): v_pk_fma /
+// v_pk_add / v_pk_mul), the causal test only on diagonal slices. Round 2's loop spilled ~30 VGPRs
+// (the per-lane addresses of the runtime slot), and each scratch reload inside the loop carried a
+// vmcnt wait that also drained the slice prefetch.
+#ifndef SMT_ATTN_DKV_IMPL
+#define SMT_ATTN_DKV_IMPL 1
+#endif
+// slices in the lean loop's ring (slices it+1 .. it+R-1 in flight while slice it is computed; rings
+// of 2, 3 and 4 measured 2.17, 2.21, 2.21 ms for the whole backward: profiles/r03_attn_bwd_variants.jsonl)
+#ifndef SMT_DKV_LEAN_RING
+#define SMT_DKV_LEAN_RING 2
+#endif
+constexpr int kDkvLeanRing = SMT_DKV_LEAN_RING;
+static_assert(kDkvLeanRing >= 2 && kDkvLeanRing * kSliceBuf + kVImg <= 160 * 1024, "dK/dV lean ring");
+template <bool KMASK>
+struct DkvLean {
+    const DkvArgs& a;
+    uint8_t* lds;
+    bf16x8_t kf[8];
+    f32x16_t dvt[4], dkt[4];
+    int G, lane, wave, hi, l32, k0, kw, key, n_sl, n_it, b, hk, per_slice;
+    bool kvalid;
+    uint32_t lds0;
+    uint32_t lo_row, lo_v, lo_t0, lo_t4;      // lane constants of the row / V-row / transposed reads
+
+    __device__ __forceinline__ DkvLean(const DkvArgs& a_, uint8_t* lds_) : a(a_), lds(lds_) {}
+
+    __device__ __forceinline__ void issue(int it) {
+        const int hh = it / n_sl, sl = n_sl - 1 - (it - hh * n_sl);
+        const int h = hk * G + hh;
+        const int s0 = k0 + sl * kSlice;
+        const uint32_t buf = lds0 + (uint32_t)((it % kDkvLeanRing) * kSliceBuf);
+        const bool is_q = wave < 4;
+        const Tns& src = is_q ? a.q : a.dout;
+        const uint16_t* base = src.p + b * src.sb + h * src.sh;
+        dma_rows(uniform_rsrc(base, (int64_t)a.S * src.ss * 2), src.ss, buf + (is_q ? 0u : (uint32_t)kSliceB), s0,
+                 s0 + 8 * (wave & 3), 2, lane);
+        if (wave < 2 && lane < 8) {
+            const float* row = (wave == 0 ? a.lse : a.delta) + ((int64_t)b * a.Hq + h) * a.S;
+            dma16(uniform_rsrc(row, (int64_t)a.S * 4), __builtin_amdgcn_readfirstlane(buf + 2 * kSliceB + 128 * wave),
+                  (s0 + 4 * lane) * 4);
+        }
+    }
+
+    // the slice's s0, or -1 when no q of the slice sees a key of the wave (both phases skip it)
+    __device__ __forceinline__ int slice_s0(int it) const {
+        const int sl = n_sl - 1 - it % n_sl;               // descending q (see dkdv_block)
+        const int s0 = k0 + sl * kSlice;
+        return (s0 + kSlice - 1 < kw) ? -1 : s0;
+    }
+
+    // phase 1 of a slice (ring slot SLOT): S = Q K^T and dP = dO V^T
+    template <int SLOT>
+    __device__ __forceinline__ void qk(f32x16_t& s, f32x16_t& dp) {
+        // ring slot SLOT at [SLOT * kSliceBuf, ...): Q rows, dO rows, lse[32], delta[32]; V image after the ring
+        constexpr int QI = SLOT * kSliceBuf, DI = QI + kSliceB;
+        const uint32_t lr = opaque(lo_row), lv = opaque(lo_v);
+        s = mfma(rowx<QI>(lds, lr, 0), kf[0], f32x16_t{});
+        dp = mfma(rowx<DI>(lds, lr, 0), rowx<0>(lds, lv, 0), f32x16_t{});
+#pragma unroll
+        for (int ks = 1; ks < 8; ++ks) {
+            s = mfma(rowx<QI>(lds, lr, ks), kf[ks], s);
+            dp = mfma(rowx<DI>(lds, lr, ks), rowx<0>(lds, lv, ks), dp);
+            if (ks & 1) __builtin_amdgcn_sched_barrier(0);    // bound the reads hoisted ahead (VGPRs)
+        }
+    }
+
+    // phase 2: P, dS, dV^T += dO^T P, dK^T += Q^T dS
+    template <int SLOT>
+    __device__ __forceinline__ void pv(int s0, const f32x16_t& s, const f32x16_t& dp) {
+        constexpr int QI = SLOT * kSliceBuf, DI = QI + kSliceB;
+        const float* cst = reinterpret_cast<const float*>(lds + QI + 2 * kSliceB);
+        // rows q = s0 + (i&3) + 8(i>>2) + 4hi of register i; their constants are cst[8(i>>2) + 4hi + (i&3)]
+        float pr[16], dsv[16];
+        const f32x2_t sl2v = {a.sl2, a.sl2};
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const float4 lz = *reinterpret_cast<const float4*>(cst + 8 * g + 4 * hi);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int i = 4 * g + 2 * h;
+                const f32x2_t l2 = h ? f32x2_t{lz.z, lz.w} : f32x2_t{lz.x, lz.y};
+                const f32x2_t e = __builtin_elementwise_fma(f32x2_t{s[i], s[i + 1]}, sl2v, -l2);
+                pr[i] = __builtin_amdgcn_exp2f(e.x);
+                pr[i + 1] = __builtin_amdgcn_exp2f(e.y);
+            }
+        }
+        if (s0 < kw + kKW - 1) {                           // the slice crosses this wave's diagonal
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int q = s0 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+                if (key > q) pr[i] = 0.f;
+            }
+        }
+        if (KMASK && !kvalid) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) pr[i] = 0.f;
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const float4 dz = *reinterpret_cast<const float4*>(cst + 32 + 8 * g + 4 * hi);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int i = 4 * g + 2 * h;
+                const f32x2_t d2 = h ? f32x2_t{dz.z, dz.w} : f32x2_t{dz.x, dz.y};
+                const f32x2_t r = (f32x2_t{dp[i], dp[i + 1]} - d2) * f32x2_t{pr[i], pr[i + 1]};
+                dsv[i] = r.x;
+                dsv[i + 1] = r.y;
+            }
+        }
+        bf16x8_t pf[2], sf[2];
+        pack_b_frags(pr, pf[0], pf[1]);
+        pack_b_frags(dsv, sf[0], sf[1]);
+        const uint32_t t0 = opaque(lo_t0), t4 = opaque(lo_t4);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int kq = 0; kq < 2; ++kq) {
+                dvt[dt] = mfma(trx<DI>(lds, t0, t4, kq, dt), pf[kq], dvt[dt]);
+                dkt[dt] = mfma(trx<QI>(lds, t0, t4, kq, dt), sf[kq], dkt[dt]);
+                if (kq) __builtin_amdgcn_sched_barrier(0);
+            }
+    }
+
+    // Both phases of slice it in one barrier interval. (Tried: waves 4-7 lagging half a slice behind
+    // their SIMD partners - phase 2 of slice it-1, then phase 1 of slice it - so that one wave's MFMA
+    // chain meets its partner's softmax VALU: S / dP then stay live across the barrier, and at 256
+    // VGPRs per wave hipcc spilled ~90 registers inside the loop.)
+    template <int SLOT>
+    __device__ __forceinline__ void step(int it) {
+        constexpr int R = kDkvLeanRing;
+        if (it + R - 1 < n_it) issue(it + R - 1);          // into the slot slice it-1 used
+        const int s0 = slice_s0(it);
+        if (s0 >= 0) {
+            f32x16_t s, dp;
+            qk<SLOT>(s, dp);
+            pv<SLOT>(s0, s, dp);
+        }
+        // slice it+1 landed; it+2 .. it+R-1 (those issued) may stay in flight
+        vm_wait_upto(per_slice * max(0, min(R - 2, n_it - 2 - it)));
+        __syncthreads();
+    }
+
+    template <int SLOT>
+    __device__ __forceinline__ void steps(int it0) {       // slices it0 .. it0+R-1, slot = compile-time
+        if (it0 + SLOT < n_it) {
+            step<SLOT>(it0 + SLOT);
+            if constexpr (SLOT + 1 < kDkvLeanRing) steps<SLOT + 1>(it0);
+        }
+    }
+
+    __device__ __forceinline__ void run(int b_, int hk_, int kb) {
+        b = b_;
+        hk = hk_;
+        G = a.Hq / a.Hkv;
+        const int tid = threadIdx.x;
+        lane = tid & 63;
+        wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        hi = lane >> 5;
+        l32 = lane & 31;
+        k0 = kb * kKB;
+        kw = k0 + wave * kKW;
+        key = kw + l32;
+        kvalid = !KMASK || (key < a.S && key_bit(a.kmask[(int64_t)b * a.kmask_ld + (key >> 6)], key));
+        const uint16_t* kp = a.k.p + b * a.k.sb + hk * a.k.sh;
+        const uint16_t* vp = a.v.p + b * a.v.sb + hk * a.v.sh;
+        lds0 = lds_addr(lds);
+        dma_rows(uniform_rsrc(vp, (int64_t)a.S * a.v.ss * 2), a.v.ss, lds0 + kDkvLeanRing * kSliceBuf, k0, kw, kKW / 4, lane);
+        {
+            const uint32_t r = (uint32_t)l32;
+            lo_row = r * kRowB + ((16u * hi) ^ (swz(r) << 4));
+            // V rows wave*32 + l32 (same swizzle as row l32), image after the ring (past the ds offset range)
+            lo_v = lo_row + (uint32_t)(kDkvLeanRing * kSliceBuf + wave * kKW * kRowB);
+            const TrLane tl = tr_lane(lane);
+            lo_t0 = tl.krow * kRowB + (tl.feat_byte ^ (swz(tl.krow) << 4));
+            lo_t4 = (tl.krow + 4) * kRowB + (tl.feat_byte ^ (swz(tl.krow + 4) << 4));
+        }
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+            if (key < a.S) kf[ks] = *reinterpret_cast<const bf16x8_t*>(kp + (int64_t)key * a.k.ss + 16 * ks + 8 * hi);
+            else kf[ks] = __builtin_bit_cast(bf16x8_t, u32x4_t{0u, 0u, 0u, 0u});
+        }
+        n_sl = (a.S - k0 + kSlice - 1) / kSlice;
+        n_it = G * n_sl;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) { dvt[dt][i] = 0.f; dkt[dt][i] = 0.f; }
+        per_slice = wave < 2 ? 3 : 2;                      // DMA instructions per slice (+ lse / delta)
+#pragma unroll
+        for (int i = 0; i < kDkvLeanRing - 1; ++i)
+            if (i < n_it) issue(i);
+        vm_wait_all();
+        vm_wait_all_known();                               // the K fragments too (compiler-visible)
+        __syncthreads();
+        for (int it = 0; it < n_it; it += kDkvLeanRing) steps<0>(it);
+        if (key < a.S) {
+            uint16_t* dkr = a.dk + b * a.dk_sb + hk * a.dk_sh + (int64_t)key * a.dk_ss;
+            uint16_t* dvr = a.dv + b * a.dv_sb + hk * a.dv_sh + (int64_t)key * a.dv_ss;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int d = 32 * dt + 8 * g + 4 * hi;
+                    uint2 w;
+                    w.x = pk_bf16(dkt[dt][4 * g] * a.scale, dkt[dt][4 * g + 1] * a.scale);
+                    w.y = pk_bf16(dkt[dt][4 * g + 2] * a.scale, dkt[dt][4 * g + 3] * a.scale);
+                    *reinterpret_cast<uint2*>(dkr + d) = w;
+                    w.x = pk_bf16(dvt[dt][4 * g], dvt[dt][4 * g + 1]);
+                    w.y = pk_bf16(dvt[dt][4 * g + 2], dvt[dt][4 * g + 3]);
+                    *reinterpret_cast<uint2*>(dvr + d) = w;
+                }
+        }
+    }
+};
+
 template <bool KMASK>
 __global__ __launch_bounds__(kDkvWaves * 64, 2)
 void attn_dkdv_kernel(DkvArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kVImg + kDkvRing * kSliceBuf];
+    constexpr int kLdsBytes = (SMT_ATTN_DKV_IMPL == 1 && kDkvRing == 2) ? kVImg + kDkvLeanRing * kSliceBuf
+                                                                         : kVImg + kDkvRing * kSliceBuf;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
     const int nkb = (a.S + kKB - 1) / kKB;
     const int total = ((nkb + 1) / 2) * a.Hkv * a.B;
     // key blocks kb (long causal sweep) and nkb-1-kb (short) in one workgroup: equal work per
@@ -1409,7 +1845,12 @@ void attn_dkdv_kernel(DkvArgs a) {
 #pragma nounroll
     for (int i = 0; i < t.n; ++i) {
         if (i) __syncthreads();
-        dkdv_block<KMASK>(a, lds, t.b, t.hk, t.blk[1 - i]);
+        if (SMT_ATTN_DKV_IMPL == 1 && kDkvRing == 2) {
+            DkvLean<KMASK> dl(a, lds);
+            dl.run(t.b, t.hk, t.blk[1 - i]);
+        } else {
+            dkdv_block<KMASK>(a, lds, t.b, t.hk, t.blk[1 - i]);
+        }
     }
 }
 
