@@ -198,10 +198,11 @@ def install_wgrad_timer(timer: WgradTimer):
     from sparse_matrix_tuning_amd import _hip
     orig = _hip.tile_wgrad
 
-    def timed(g2, x2, rc, out, accumulate=False, order=None):
+    def timed(g2, x2, rc, out, accumulate=False, order=None, seq_len=None):
         n_slices = len(_slice_keys(g2, x2, timer.host_rows(rc))) if timer.enabled else None
         return timer.hook(g2.shape[0], rc.shape[0], out.element_size(),
-                          lambda: orig(g2, x2, rc, out, accumulate=accumulate, order=order), slices=n_slices)
+                          lambda: orig(g2, x2, rc, out, accumulate=accumulate, order=order, seq_len=seq_len),
+                          slices=n_slices)
     _hip.tile_wgrad = timed
 
 
@@ -210,7 +211,7 @@ def install_wgrad_batch_timer(timer: WgradTimer):
     from sparse_matrix_tuning_amd import _hip
     orig = _hip.tile_wgrad_batch
 
-    def timed(items, tab, order=None):
+    def timed(items, tab, order=None, seq_len=None):
         n_slices = None
         if timer.enabled:
             keys, rows = set(), timer.host_rows(tab)
@@ -218,7 +219,7 @@ def install_wgrad_batch_timer(timer: WgradTimer):
                 keys |= _slice_keys(g2, x2, [(r, c) for mm, r, c, _k in rows if mm == m])
             n_slices = len(keys)
         return timer.hook(items[0][0].shape[0], tab.shape[0], items[0][2].element_size(),
-                          lambda: orig(items, tab, order), slices=n_slices)
+                          lambda: orig(items, tab, order, seq_len=seq_len), slices=n_slices)
     _hip.tile_wgrad_batch = timed
 
 

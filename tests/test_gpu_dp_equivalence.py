@@ -59,7 +59,11 @@ def test_dp2_equals_gradient_accumulation_bit_for_bit(tmp_path):
         assert torch.equal(dp["W"][n], acc["W"][n]), n
     # vs the concatenated batch (other GEMM shapes: bf16 noise in the gradients)
     for n in big["warm"]:
-        assert (dp["warm"][n].float() - big["warm"][n].float()).abs().max().item() <= 2.1e-3, n   # 1 AdamW step of lr
+        # one AdamW step of lr 1e-3 (first-step updates are ~lr * sign(g): a flipped sign moves a weight
+        # by 2 lr) plus one bf16 rounding step of the stored weight (at most 2^-7 relative)
+        d, w = dp["warm"][n].float(), big["warm"][n].float()
+        excess = (d - w).abs() - (2e-3 + torch.maximum(d.abs(), w.abs()) * 2.0 ** -7)
+        assert excess.max().item() <= 1e-7, (n, (d - w).abs().max().item())
     if dp["sel_mlp"] == big["sel_mlp"] and dp["sel_att"] == big["sel_att"]:
         rel = ((dp["exp_avg"] - big["exp_avg"]).norm() / big["exp_avg"].norm()).item()
         assert rel < 5e-2, rel

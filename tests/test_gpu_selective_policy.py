@@ -91,14 +91,25 @@ def _model():
 
 
 def _step(model, ids, policy):
+    """One forward + backward; returns the loss, the tile gradients and the bytes of the distinct
+    storages the autograd graph keeps for the backward (saved-tensor hooks)."""
     old = smt.set_activation_policy(policy)
+    kept = {}
+
+    def pack(t):
+        st = t.untyped_storage()
+        kept[st.data_ptr()] = st.nbytes()
+        return t
+
     try:
         model.zero_grad(set_to_none=True)
         torch.cuda.synchronize()
         base = torch.cuda.memory_allocated(DEV)
-        out = model(input_ids=ids, labels=ids, use_cache=False)
+        with torch.autograd.graph.saved_tensors_hooks(pack, lambda t: t):
+            out = model(input_ids=ids, labels=ids, use_cache=False)
         torch.cuda.synchronize()
-        held = torch.cuda.memory_allocated(DEV) - base
+        print(f"\n{policy}: allocated after forward {(torch.cuda.memory_allocated(DEV) - base) / 1e6:.1f} MB")
+        held = sum(kept.values())
         out.loss.backward()
         torch.cuda.synchronize()
     finally:
@@ -119,7 +130,7 @@ def test_selective_policy_same_tile_grads_less_memory():
         loss_r2, grads_r2, _ = _step(model, ids, "resident")
     finally:
         fl.unpatch_llama()
-    print(f"\nactivations held after forward: resident {held_r / 1e6:.1f} MB, selective {held_s / 1e6:.1f} MB")
+    print(f"\nsaved for backward: resident {held_r / 1e6:.1f} MB, selective {held_s / 1e6:.1f} MB")
     assert torch.equal(loss_r, loss_r2)               # the step itself is deterministic
     assert torch.equal(loss_r, loss_s)
     assert grads_r.keys() == grads_s.keys() and len(grads_r) == 8
