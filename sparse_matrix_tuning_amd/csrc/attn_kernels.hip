@@ -454,7 +454,8 @@ __device__ __forceinline__ void fwd_block(const FwdArgs& a, uint8_t* lds, int b,
 // rescale (a branch after the step's PV) is rare; P = exp2(s*c - m) keeps bf16's relative precision.
 // The only masked tile of a wave (the causal diagonal) is its last one, handled by a step variant.
 // ------------------------------------------------------------------------------------------------
-// SMT_ATTN_FWD_IMPL: 0 fwd_block, 1 FwdPipe (one workgroup per CU), 2 FwdLean (two per CU)
+// SMT_ATTN_FWD_IMPL: 0 fwd_block, 1 FwdPipe (one workgroup per CU), 2 FwdLean (two per CU),
+// 3 FwdDual (one wave per SIMD, 64 rows per wave; attn_fwd_dual_kernel)
 #ifndef SMT_ATTN_FWD_IMPL
 #define SMT_ATTN_FWD_IMPL 2
 #endif
@@ -1022,6 +1023,254 @@ struct FwdLean {
         }
     }
 };
+
+// ------------------------------------------------------------------------------------------------
+// Forward, one wave per SIMD (SMT_ATTN_FWD_IMPL 3): a workgroup = 4 waves x 64 query rows (two 32-row
+// blocks A, B per wave) = 256 rows of one (b, q head); 64-key K/V tiles in a kDualRing-deep LDS-DMA
+// ring shared by the 4 waves. Each wave reads a tile's K and V fragments from LDS ONCE for both of
+// its row blocks (half the LDS bytes per MFMA of the 32-row kernels, whose LDS traffic was ~3/4 of
+// their MFMA time) and, with the whole 512-register file, holds both blocks' O (AGPRs), Q and scores.
+// Per tile the two blocks are offset by one phase so that one block's softmax VALU overlaps the
+// other block's MFMA chain inside the wave: QK(A); QK(B) || softmax(A); PV(A) || softmax(B); PV(B).
+// ------------------------------------------------------------------------------------------------
+#ifndef SMT_ATTN_DUAL_RING
+#define SMT_ATTN_DUAL_RING 3
+#endif
+constexpr int kDualRing = SMT_ATTN_DUAL_RING, kDualQB = 256;
+
+template <bool KMASK>
+struct FwdDual {
+    const FwdArgs& a;
+    uint8_t* lds;
+    bf16x8_t qa[8], qb[8];
+    f32x16_t oa[4], ob[4];
+    float ma, mb, la, lb;
+    const uint64_t* km;
+    __amdgpu_buffer_rsrc_t rk, rv;
+    uint32_t lds0, lo_row, lo_t0, lo_t4;
+    int lane, wave, hi, l32, qw, nt, last;
+
+    __device__ __forceinline__ FwdDual(const FwdArgs& a_, uint8_t* lds_) : a(a_), lds(lds_) {}
+
+    __device__ __forceinline__ void issue(int t) {            // K(t), V(t): 16 rows of each per wave
+        const uint32_t slot = lds0 + (uint32_t)((t % kDualRing) * 2 * kTileB);
+        dma_rows(rk, a.k.ss, slot, t * kKV, t * kKV + 16 * wave, 4, lane);
+        dma_rows(rv, a.v.ss, slot + kTileB, t * kKV, t * kKV + 16 * wave, 4, lane);
+    }
+
+    __device__ __forceinline__ static void rescale(f32x16_t (&o)[4], float alpha) {
+        if (__builtin_amdgcn_ballot_w64(alpha != 1.f) != 0) {     // rare (deferred max)
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+        }
+    }
+
+    // scores of one 32-row block against the tile's 64 keys (two 32-key halves) -> probabilities packed
+    // as the PV B operand; the block's running max / sum and O updated (deferred max, T13)
+    __device__ __forceinline__ void softmax(const f32x16_t (&sc)[2], int qrow, int k0, bool DIAG, float& m_run,
+                                            float& l_run, f32x16_t (&o)[4], bf16x8_t (&pf)[4]) {
+        float x[32];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) x[16 * j + i] = sc[j][i];
+        if (DIAG) {
+#pragma unroll
+            for (int i = 0; i < 32; ++i) {
+                const int key = k0 + 32 * (i >> 4) + (i & 3) + 8 * ((i & 15) >> 2) + 4 * hi;
+                if (key > qrow) x[i] = kNegInf;
+            }
+        }
+        if (KMASK) {
+            const uint64_t w = km[k0 >> 6];
+#pragma unroll
+            for (int i = 0; i < 32; ++i) {
+                const int key = k0 + 32 * (i >> 4) + (i & 3) + 8 * ((i & 15) >> 2) + 4 * hi;
+                if (!key_bit(w, key)) x[i] = kNegInf;
+            }
+        }
+        float mx[11];
+#pragma unroll
+        for (int i = 0; i < 10; ++i) mx[i] = max3f(x[3 * i], x[3 * i + 1], x[3 * i + 2]);
+        mx[10] = max3f(x[30], x[31], mx[0]);
+        mx[0] = max3f(mx[0], mx[1], mx[2]);
+        mx[3] = max3f(mx[3], mx[4], mx[5]);
+        mx[6] = max3f(mx[6], mx[7], mx[8]);
+        mx[9] = max3f(mx[9], mx[10], mx[0]);
+        const float m_tile = other_half_max(max3f(mx[3], mx[6], mx[9])) * a.sl2;
+        const bool move = m_tile > m_run + kFwdThr;
+        const float m_new = move ? m_tile : m_run;
+        const float alpha = move ? __builtin_amdgcn_exp2f(m_run - m_new) : 1.f;
+        const float m_use = (KMASK && m_new == kNegInf) ? 0.f : m_new;
+        const f32x2_t sl2v = {a.sl2, a.sl2}, mv = {-m_use, -m_use};
+        f32x2_t sm[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const f32x2_t e = __builtin_elementwise_fma(f32x2_t{x[2 * i], x[2 * i + 1]}, sl2v, mv);
+            x[2 * i] = __builtin_amdgcn_exp2f(e.x);
+            x[2 * i + 1] = __builtin_amdgcn_exp2f(e.y);
+            sm[i] = f32x2_t{x[2 * i], x[2 * i + 1]};
+        }
+#pragma unroll
+        for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+            for (int i = 0; i < w; ++i) sm[i] += sm[i + w];
+        l_run = l_run * alpha + (sm[0].x + sm[0].y);
+        m_run = m_new;
+        rescale(o, alpha);
+        pack_b_frags(*reinterpret_cast<const float(*)[16]>(&x[0]), pf[0], pf[1]);
+        pack_b_frags(*reinterpret_cast<const float(*)[16]>(&x[16]), pf[2], pf[3]);
+    }
+
+    template <int SLOT>
+    __device__ __forceinline__ void compute(int t, bool diag) {
+        constexpr int KI = SLOT * 2 * kTileB, KH = KI + 32 * kRowB, VI = KI + kTileB;
+        const int k0 = t * kKV;
+        const uint32_t lr = opaque(lo_row);
+        bf16x8_t kr[16];                                       // the tile's K fragments, read once
+        f32x16_t sa[2], sb[2];
+        kr[0] = rowx<KI>(lds, lr, 0);
+        kr[1] = rowx<KH>(lds, lr, 0);
+        sa[0] = mfma(kr[0], qa[0], f32x16_t{});
+        sa[1] = mfma(kr[1], qa[0], f32x16_t{});
+#pragma unroll
+        for (int ks = 1; ks < 8; ++ks) {
+            kr[2 * ks] = rowx<KI>(lds, lr, ks);
+            kr[2 * ks + 1] = rowx<KH>(lds, lr, ks);
+            sa[0] = mfma(kr[2 * ks], qa[ks], sa[0]);
+            sa[1] = mfma(kr[2 * ks + 1], qa[ks], sa[1]);
+        }
+        // QK(B) || softmax(A)
+        sb[0] = mfma(kr[0], qb[0], f32x16_t{});
+        sb[1] = mfma(kr[1], qb[0], f32x16_t{});
+#pragma unroll
+        for (int ks = 1; ks < 8; ++ks) {
+            sb[0] = mfma(kr[2 * ks], qb[ks], sb[0]);
+            sb[1] = mfma(kr[2 * ks + 1], qb[ks], sb[1]);
+        }
+        bf16x8_t pa[4], pb[4];
+        softmax(sa, qw + l32, k0, diag, ma, la, oa, pa);
+        // PV(A) || softmax(B)
+        const uint32_t t0 = opaque(lo_t0), t4 = opaque(lo_t4);
+        bf16x8_t vr[16];
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int kst = 0; kst < 4; ++kst) {
+                vr[4 * dt + kst] = trx<VI>(lds, t0, t4, kst, dt);
+                oa[dt] = mfma(vr[4 * dt + kst], pa[kst], oa[dt]);
+            }
+        softmax(sb, qw + 32 + l32, k0, diag, mb, lb, ob, pb);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int kst = 0; kst < 4; ++kst) ob[dt] = mfma(vr[4 * dt + kst], pb[kst], ob[dt]);
+    }
+
+    template <int SLOT>
+    __device__ __forceinline__ void tile(int t) {
+        if (t + kDualRing - 1 < nt) issue(t + kDualRing - 1);  // into the slot tile t-1 used
+        if (t <= last) compute<SLOT>(t, t == last);
+        vm_wait_upto(8 * max(0, min(kDualRing - 2, nt - 2 - t)));   // tile t+1 landed
+        __syncthreads();
+    }
+
+    template <int SLOT>
+    __device__ __forceinline__ void tiles(int t0) {            // tiles t0 .. t0+R-1, slot = compile-time
+        if (t0 + SLOT < nt) {
+            tile<SLOT>(t0 + SLOT);
+            if constexpr (SLOT + 1 < kDualRing) tiles<SLOT + 1>(t0);
+        }
+    }
+
+    __device__ __forceinline__ void store(const f32x16_t (&o)[4], float m_run, float l_run, int qrow, int b, int h) {
+        const float l_tot = halves_sum(l_run);
+        if (qrow >= a.S) return;
+        const float inv = (KMASK && !(l_tot > 0.f)) ? 0.f : 1.f / l_tot;
+        uint16_t* op = a.o + b * a.o_sb + h * a.o_sh + (int64_t)qrow * a.o_ss;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int d = 32 * dt + 8 * g + 4 * hi;
+                uint2 w;
+                w.x = pk_bf16(o[dt][4 * g] * inv, o[dt][4 * g + 1] * inv);
+                w.y = pk_bf16(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
+                *reinterpret_cast<uint2*>(op + d) = w;
+            }
+        if (hi == 0)
+            a.lse[((int64_t)b * a.Hq + h) * a.S + qrow] =
+                (KMASK && !(l_tot > 0.f)) ? __builtin_huge_valf() : m_run + __log2f(l_tot);
+    }
+
+    __device__ __forceinline__ void run(int b, int h, int hk, int qblk) {
+        const int tid = threadIdx.x;
+        lane = tid & 63;
+        wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        hi = lane >> 5;
+        l32 = lane & 31;
+        const int q0 = qblk * kDualQB;
+        qw = q0 + wave * 64;
+        const uint16_t* qp = a.q.p + b * a.q.sb + h * a.q.sh;
+        const uint16_t* kp = a.k.p + b * a.k.sb + hk * a.k.sh;
+        const uint16_t* vp = a.v.p + b * a.v.sb + hk * a.v.sh;
+        km = KMASK ? a.kmask + (int64_t)b * a.kmask_ld : nullptr;
+        const int ra = qw + l32, rb = qw + 32 + l32;
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+            qa[ks] = ra < a.S ? *reinterpret_cast<const bf16x8_t*>(qp + ra * a.q.ss + 16 * ks + 8 * hi)
+                              : __builtin_bit_cast(bf16x8_t, u32x4_t{0u, 0u, 0u, 0u});
+            qb[ks] = rb < a.S ? *reinterpret_cast<const bf16x8_t*>(qp + rb * a.q.ss + 16 * ks + 8 * hi)
+                              : __builtin_bit_cast(bf16x8_t, u32x4_t{0u, 0u, 0u, 0u});
+        }
+        const int kv_end = min(a.S, q0 + kDualQB);
+        nt = (kv_end + kKV - 1) / kKV;
+        last = min(nt - 1, qw / kKV);                          // both blocks' diagonal tile (qw % 64 == 0)
+        rk = uniform_rsrc(kp, (int64_t)a.S * a.k.ss * 2);
+        rv = uniform_rsrc(vp, (int64_t)a.S * a.v.ss * 2);
+        lds0 = lds_addr(lds);
+        {
+            const uint32_t r = (uint32_t)l32;
+            lo_row = r * kRowB + ((16u * hi) ^ (swz(r) << 4));
+            const TrLane tl = tr_lane(lane);
+            lo_t0 = tl.krow * kRowB + (tl.feat_byte ^ (swz(tl.krow) << 4));
+            lo_t4 = (tl.krow + 4) * kRowB + (tl.feat_byte ^ (swz(tl.krow + 4) << 4));
+        }
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) { oa[dt][i] = 0.f; ob[dt][i] = 0.f; }
+        ma = mb = kNegInf;
+        la = lb = 0.f;
+#pragma unroll
+        for (int i = 0; i < kDualRing - 1; ++i)
+            if (i < nt) issue(i);
+        vm_wait_all();
+        vm_wait_all_known();                                   // the Q fragments too (compiler-visible)
+        __syncthreads();
+        for (int t = 0; t < nt; t += kDualRing) tiles<0>(t);
+        store(oa, ma, la, ra, b, h);
+        store(ob, mb, lb, rb, b, h);
+    }
+};
+
+template <bool KMASK>
+__global__ __launch_bounds__(256, 1)
+void attn_fwd_dual_kernel(FwdArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kDualRing * 2 * kTileB];
+    const int nqb = (a.S + kDualQB - 1) / kDualQB;
+    const int G = a.Hq / a.Hkv;
+    const int total = nqb * a.Hq * a.B;
+    const int L = xcd_logical(blockIdx.x, total);              // as attn_fwd_kernel: heaviest q blocks first
+    const int per_group = G * nqb;
+    const int grp = L / per_group;
+    const int rem = L - grp * per_group;
+    const int hk = grp % a.Hkv;
+    FwdDual<KMASK> fd(a, lds);
+    fd.run(grp / a.Hkv, hk * G + rem % G, hk, nqb - 1 - rem / G);
+}
 
 // SMT_ATTN_FWD_OCC: workgroups per CU of the forward (2: 256 VGPRs per wave; 1: 512)
 #ifndef SMT_ATTN_FWD_OCC
@@ -1897,6 +2146,14 @@ int smt_attn_fwd_kmask(const smt_attn_tensor* q, const smt_attn_tensor* k, const
     a.kmask = key_mask; a.kmask_ld = key_mask_ld;
     a.B = shape->B; a.Hq = shape->Hq; a.Hkv = shape->Hkv; a.S = shape->S;
     a.sl2 = shape->scale * 1.4426950408889634f;
+    if (SMT_ATTN_FWD_IMPL == 3) {
+        const int64_t nqb = (shape->S + kDualQB - 1) / kDualQB;
+        const int64_t blocks = nqb * shape->Hq * shape->B;
+        if (blocks > 0x7fffffffLL) return fail(-1, "%s: too many blocks", fn);
+        if (key_mask) hipLaunchKernelGGL(attn_fwd_dual_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, stream, a);
+        else hipLaunchKernelGGL(attn_fwd_dual_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, stream, a);
+        return check_launch("attn_fwd_dual_kernel");
+    }
     const int64_t nqb = (shape->S + kFwdQB - 1) / kFwdQB;
     const int64_t blocks = nqb * shape->Hq * shape->B;
     if (blocks > 0x7fffffffLL) return fail(-1, "%s: too many blocks", fn);
