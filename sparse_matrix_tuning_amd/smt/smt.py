@@ -357,6 +357,26 @@ def _rows_ready(t: torch.Tensor) -> torch.Tensor:
     return t
 
 
+def _off_stream(sink, make, *reads: torch.Tensor):
+    """Run ``make()`` (the copy / quantisation of the input blocks linearZ keeps for its tile
+    gradient) on the engine's wgrad stream when there is one: its only consumer is the tile-gradient
+    launch on that stream, so the forward's critical path does not wait for it. The stream first waits
+    for the current one (the input is written there); ``reads`` are held for the caching allocator
+    until the wgrad stream has passed them."""
+    side = None
+    if sink is not None and sink.engine is not None:
+        side = sink.engine.wgrad_stream
+    if side is None:
+        return make()
+    cur = torch.cuda.current_stream(side.device)
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        out = make()
+    for t in reads:
+        t.record_stream(side)
+    return out
+
+
 def _recompute_source(input: torch.Tensor):
     """The producer operands ``tag_recompute`` attached to ``input`` (None if absent or if ``input``
     was modified in place since), with their versions for the backward's check."""
@@ -411,14 +431,15 @@ class linearZ(torch.autograd.Function):
             # fp8 path: the tile weight gradient runs on MX-fp8 operands; keep only the input's
             # column blocks, quantised (half the bytes of the bf16 blocks)
             grp = fw.group
+            x2d = _rows_ready(input.reshape(-1, weight.shape[1]))
             if grp is not None and grp.mx_union is not None:
                 # q/k/v (gate/up) read one input: its MX blocks are quantised once for the group's
                 # union of column blocks and shared
-                ctx.mx = grp.mx_input_blocks(input, _rows_ready(input.reshape(-1, weight.shape[1])))
+                ctx.mx = _off_stream(ctx.sink, lambda: grp.mx_input_blocks(input, x2d), x2d)
                 ctx.mx_pos = grp.mx_union[1]
             else:
                 _rb, cb_dev, _table = tiles.mx_tables(input.device)
-                ctx.mx = _hip.mx_quant_cols(_rows_ready(input.reshape(-1, weight.shape[1])), cb_dev)
+                ctx.mx = _off_stream(ctx.sink, lambda: _hip.mx_quant_cols(x2d, cb_dev), x2d)
                 ctx.mx_pos = None
             saved = None
         elif (_activation_policy == "selective" and ctx.needs_input_grad[1] and len(tiles)
@@ -430,7 +451,8 @@ class linearZ(torch.autograd.Function):
         elif (ctx.needs_input_grad[1] and len(tiles) and input.device.type == "cuda"
                 and 2 * len(tiles.column_blocks()) <= in_blocks):
             cb_dev, _ = tiles.packed_tables(input.device)
-            saved = _hip.colblock_gather(_rows_ready(input.reshape(-1, weight.shape[1])), cb_dev)
+            x2d = _rows_ready(input.reshape(-1, weight.shape[1]))
+            saved = _off_stream(ctx.sink, lambda: _hip.colblock_gather(x2d, cb_dev), x2d)
             ctx.packed = True
         ctx.save_for_backward(saved, weight)
         # q/k/v (gate/up) share their input: their data gradients accumulate in one buffer (bf16)
