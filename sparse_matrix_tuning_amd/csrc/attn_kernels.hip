@@ -1037,6 +1037,13 @@ struct FwdLean {
 #define SMT_ATTN_DUAL_RING 3
 #endif
 constexpr int kDualRing = SMT_ATTN_DUAL_RING, kDualQB = 256;
+// SMT_ATTN_DUAL_OVERLAP=1: interior tiles run the two blocks offset by one phase (softmax chunks pinned
+// beside the other block's MFMAs by scheduling fences). hipcc's register allocation of that body
+// (O in AGPRs, Q / scores / probabilities / fragments in VGPRs) produced ~300 spill slots and ~2400
+// AGPR<->VGPR moves, so it is off; the guide's one-wave-per-SIMD kernel owns its registers in asm.
+#ifndef SMT_ATTN_DUAL_OVERLAP
+#define SMT_ATTN_DUAL_OVERLAP 0
+#endif
 
 template <bool KMASK>
 struct FwdDual {
@@ -1169,10 +1176,120 @@ struct FwdDual {
             for (int kst = 0; kst < 4; ++kst) ob[dt] = mfma(vr[4 * dt + kst], pb[kst], ob[dt]);
     }
 
+    // ---- the overlapped tile (interior tiles, no key mask): one block's softmax in 8 chunks, each
+    // pinned beside two MFMAs of the other block's chain by scheduling fences ----
+    struct Sm {
+        float x[32];
+        float mx;
+        f32x2_t acc[4];
+        float m_new, alpha, m_use;
+    };
+
+    template <int C>
+    __device__ __forceinline__ void sm_chunk(Sm& st, const f32x16_t (&sc)[2], float& m_run, float& l_run,
+                                             bf16x8_t (&pf)[4]) {
+        float* x = st.x;
+        if constexpr (C == 0 || C == 1) {                      // copy + row max over 16 scores
+#pragma unroll
+            for (int i = 0; i < 16; ++i) x[16 * C + i] = sc[C][i];
+            const float* v = x + 16 * C;
+            float m = max3f(v[0], v[1], v[2]);
+            m = max3f(m, v[3], v[4]);
+            m = max3f(m, v[5], v[6]);
+            m = max3f(m, v[7], v[8]);
+            m = max3f(m, v[9], v[10]);
+            m = max3f(m, v[11], v[12]);
+            m = max3f(m, v[13], v[14]);
+            if constexpr (C == 0) {
+                st.mx = fmaxf(m, v[15]);
+            } else {
+                m = max3f(m, v[15], st.mx);
+                const float m_tile = other_half_max(m) * a.sl2;
+                const bool move = m_tile > m_run + kFwdThr;
+                st.m_new = move ? m_tile : m_run;
+                st.alpha = move ? __builtin_amdgcn_exp2f(m_run - st.m_new) : 1.f;
+                st.m_use = st.m_new;
+            }
+        } else if constexpr (C >= 2 && C <= 5) {               // 8 exponentials, packed scale-subtract
+            constexpr int e0 = 8 * (C - 2);
+            const f32x2_t sl2v = {a.sl2, a.sl2}, mv = {-st.m_use, -st.m_use};
+            f32x2_t part = {0.f, 0.f};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const f32x2_t e = __builtin_elementwise_fma(f32x2_t{x[e0 + 2 * i], x[e0 + 2 * i + 1]}, sl2v, mv);
+                x[e0 + 2 * i] = __builtin_amdgcn_exp2f(e.x);
+                x[e0 + 2 * i + 1] = __builtin_amdgcn_exp2f(e.y);
+                part = i ? part + f32x2_t{x[e0 + 2 * i], x[e0 + 2 * i + 1]} : f32x2_t{x[e0], x[e0 + 1]};
+            }
+            st.acc[C - 2] = part;
+        } else if constexpr (C == 6) {                         // row sum, running max / sum
+            const f32x2_t s2 = (st.acc[0] + st.acc[1]) + (st.acc[2] + st.acc[3]);
+            l_run = l_run * st.alpha + (s2.x + s2.y);
+            m_run = st.m_new;
+            pack_b_frags(*reinterpret_cast<const float(*)[16]>(&x[0]), pf[0], pf[1]);
+        } else {
+            pack_b_frags(*reinterpret_cast<const float(*)[16]>(&x[16]), pf[2], pf[3]);
+        }
+    }
+
+    // QK(B) re-reads the K fragments (16 KiB more LDS per tile) rather than keep 64 VGPRs of them
+    template <int KI, int KH, int C>
+    __device__ __forceinline__ void qk_b_step(uint32_t lr, f32x16_t (&sb)[2], Sm& st, const f32x16_t (&sa)[2],
+                                              bf16x8_t (&pa)[4]) {
+        sb[0] = mfma(rowx<KI>(lds, lr, C), qb[C], C == 0 ? f32x16_t{} : sb[0]);
+        sb[1] = mfma(rowx<KH>(lds, lr, C), qb[C], C == 0 ? f32x16_t{} : sb[1]);
+        sm_chunk<C>(st, sa, ma, la, pa);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (C + 1 < 8) qk_b_step<KI, KH, C + 1>(lr, sb, st, sa, pa);
+    }
+
+    template <int VI, int C>
+    __device__ __forceinline__ void pv_a_step(uint32_t t0, uint32_t t4, bf16x8_t (&vr)[16], const bf16x8_t (&pa)[4],
+                                              Sm& st, const f32x16_t (&sb)[2], bf16x8_t (&pb)[4]) {
+        constexpr int dt = C >> 1, k0 = 2 * (C & 1);
+        vr[4 * dt + k0] = trx<VI>(lds, t0, t4, k0, dt);
+        vr[4 * dt + k0 + 1] = trx<VI>(lds, t0, t4, k0 + 1, dt);
+        oa[dt] = mfma(vr[4 * dt + k0], pa[k0], oa[dt]);
+        oa[dt] = mfma(vr[4 * dt + k0 + 1], pa[k0 + 1], oa[dt]);
+        sm_chunk<C>(st, sb, mb, lb, pb);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (C + 1 < 8) pv_a_step<VI, C + 1>(t0, t4, vr, pa, st, sb, pb);
+    }
+
+    template <int SLOT>
+    __device__ __forceinline__ void compute_overlap(int t) {
+        constexpr int KI = SLOT * 2 * kTileB, KH = KI + 32 * kRowB, VI = KI + kTileB;
+        const uint32_t lr = opaque(lo_row);
+        f32x16_t sa[2], sb[2];
+        sa[0] = mfma(rowx<KI>(lds, lr, 0), qa[0], f32x16_t{});
+        sa[1] = mfma(rowx<KH>(lds, lr, 0), qa[0], f32x16_t{});
+#pragma unroll
+        for (int ks = 1; ks < 8; ++ks) {
+            sa[0] = mfma(rowx<KI>(lds, lr, ks), qa[ks], sa[0]);
+            sa[1] = mfma(rowx<KH>(lds, lr, ks), qa[ks], sa[1]);
+            if (ks & 1) __builtin_amdgcn_sched_barrier(0);
+        }
+        Sm st;
+        bf16x8_t pa[4], pb[4];
+        const uint32_t lr2 = opaque(lo_row);
+        qk_b_step<KI, KH, 0>(lr2, sb, st, sa, pa);             // QK(B) || softmax(A)
+        rescale(oa, st.alpha);
+        const uint32_t t0 = opaque(lo_t0), t4 = opaque(lo_t4);
+        bf16x8_t vr[16];
+        Sm st2;
+        pv_a_step<VI, 0>(t0, t4, vr, pa, st2, sb, pb);         // PV(A) || softmax(B)
+        rescale(ob, st2.alpha);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int kst = 0; kst < 4; ++kst) ob[dt] = mfma(vr[4 * dt + kst], pb[kst], ob[dt]);
+    }
+
     template <int SLOT>
     __device__ __forceinline__ void tile(int t) {
         if (t + kDualRing - 1 < nt) issue(t + kDualRing - 1);  // into the slot tile t-1 used
-        if (t <= last) compute<SLOT>(t, t == last);
+        if (!KMASK && SMT_ATTN_DUAL_OVERLAP && t < last) compute_overlap<SLOT>(t);
+        else if (t <= last) compute<SLOT>(t, t == last);
         vm_wait_upto(8 * max(0, min(kDualRing - 2, nt - 2 - t)));   // tile t+1 landed
         __syncthreads();
     }
