@@ -640,21 +640,25 @@ def cpu_baseline(seconds: float, tiles_one_layer: dict, model_name: str, gpu: di
     cfg = MODELS[model_name]
     units = []
     gpu_layer = gpu_unit_layer(tiles_one_layer, cfg, device)
+    log("cpu baseline: unit 1 (decoder layer)")
     cpu_layer, s1 = cpu_unit_layer(seconds, tiles_one_layer, cfg)
     units.append({"unit": 1, "what": "one decoder layer's 7 SMT linears, fwd + bwd, B=1 S=2048 "
                   f"({sum(len(v) for v in tiles_one_layer.values())} tiles)", "metric": "tokens/s",
                   "cpu": round(cpu_layer, 2), "gpu": round(gpu_layer, 1), "cpu_sample": s1})
     if gpu.get("selection"):
+        log("cpu baseline: unit 2 (selection)")
         cpu_sel, s2 = cpu_unit_selection(model_name)
         units.append({"unit": 2, "what": "block scan + top-n selection (attention mean_abs, MLP abs_mean, n=436 each)",
                       "metric": "elements/s", "cpu": round(cpu_sel), "gpu": round(gpu["selection"]["elements_per_s"]),
                       "cpu_sample": s2, "gpu_sample": gpu["selection"]["sample"]})
     if gpu.get("adam"):
+        log("cpu baseline: unit 3 (sparse AdamW)")
         cpu_adam, s3 = cpu_unit_adam(gpu["adam"]["params"])
         units.append({"unit": 3, "what": "sparse AdamW (clip + update) over the trainable tiles", "metric": "params/s",
                       "cpu": round(cpu_adam), "gpu": round(gpu["adam"]["params_per_s"]), "cpu_sample": s3,
                       "gpu_sample": gpu["adam"]["sample"]})
     try:
+        log("cpu baseline: unit 4 (OPT-125m step)")
         gpu_opt, sel = gpu_unit_opt(device)
         cpu_opt, s4 = cpu_unit_opt(sel)
         units.append({"unit": 4, "what": "config 1: OPT-125m SMT(1%) training step (19 attention tiles), B=4 S=128",
@@ -827,6 +831,8 @@ def main():
 
     for i in range(args.warmup):
         step(smt_batches[i])
+    torch.cuda.synchronize()
+    log(f"{args.warmup} untimed SMT steps done; timing {args.steps}")
     timer.enabled = mx_timer.enabled = atimer.enabled = adam_timer.enabled = True
     elapsed, per_step, loss = timed_steps(step, smt_batches[args.warmup:], world, device)
     timer.enabled = mx_timer.enabled = atimer.enabled = adam_timer.enabled = False
@@ -843,6 +849,7 @@ def main():
     a_sum = atimer.summary()
     adam = adam_timer.summary()
     del smt_batches
+    log(f"timed: {value:.1f} tokens/s ({elapsed / args.steps * 1e3:.1f} ms/step), peak {peak[0].item():.1f} GB")
 
     # ---- the tile wgrad alone (its roofline): the same steps with the wgrad stream joined ----
     overlapped = {"bf16": w, "mx": w_mx}
@@ -860,6 +867,7 @@ def main():
         torch.cuda.synchronize()
         timer.enabled = mx_timer.enabled = False
         w, w_mx = timer.summary(), mx_timer.summary()
+        log(f"roofline steps done ({args.roofline_steps}, wgrad stream joined)")
         engine.wgrad_stream = side
         for tg in engine.tile_groups:
             if tg.buckets is not None:
@@ -894,6 +902,7 @@ def main():
         selective_mode["recomputed"] = ("the column blocks SMT linears read of RMSNorm / SwiGLU outputs "
                                         "(smt_colblock_recompute in the backward)")
         _smt.set_activation_policy(old_policy)
+        log(f"selective policy: {selective_mode['value']} tokens/s at {selective_mode['peak_hbm_gb']} GB")
 
     # ---- the reference's memory policy (per-layer recompute), same engine and tiles ----
     ckpt_mode = None
@@ -916,6 +925,7 @@ def main():
                      "peak_hbm_gb": round(r[2].item(), 2)}
         engine.module.gradient_checkpointing_disable()
         del ref_batches
+        log(f"recompute policy: {ckpt_mode['value']} tokens/s at {ckpt_mode['peak_hbm_gb']} GB")
 
     if rank == 0:
         per_gpu = value / world
