@@ -336,10 +336,9 @@ constexpr int kDmaSlotBytes = 2 * kDmaImg;                 // A + B
 // 1-10 % SLOWER at 4-436 tiles, T = 32768 (profiles/r02_wgrad_ring_depth.jsonl): the kernel is not
 // bound by the bytes in flight per CU.
 constexpr int kDmaSlotsDefault = 4;
-// SMT_WGRAD_STAGGER=1: waves 4-7 one k-step behind their SIMD partners (wgrad_dma_kernel)
-#ifndef SMT_WGRAD_STAGGER
-#define SMT_WGRAD_STAGGER 0
-#endif
+// Measured, not kept (profiles/r03_wgrad_stagger_ab.jsonl, scripts/ab_wgrad_batch.sh on bench-shaped
+// batches): waves 4-7 one k-step behind their SIMD partners (MI355X_MICROARCH "Two waves per SIMD",
+// item 9), with and without s_setprio 1 on the lagging half: 1-3 % slower, bit-identical tiles.
 
 // s_waitcnt vmcnt(n) for a run-time n in {0, 4, 8, 12} (the immediate must be a constant)
 __device__ __forceinline__ void wait_vm_stages(int stages_in_flight) {
@@ -480,30 +479,6 @@ void wgrad_dma_kernel(const WgradModules mods, int64_t T, int64_t chunk, int S, 
 #pragma unroll
     for (int i = 0; i < AHEAD; ++i)
         if (i < nst) issue(i);
-#if SMT_WGRAD_STAGGER
-    // Staggered SIMD partners (MI355X_MICROARCH "Two waves per SIMD", item 9): waves 4-7 run one
-    // k-step behind waves 0-3, so in every barrier interval a SIMD's two waves are at different
-    // points of their MFMA / fragment-read sequence instead of in lockstep. Interval st: waves 0-3
-    // compute k-steps 0, 1 of stage st; waves 4-7 k-step 1 of stage st-1, then k-step 0 of stage st
-    // (every accumulator still sees the k-steps in the same order: bit-identical results). Stage
-    // st-1's slot stays live through interval st, so the refill of slot (st+AHEAD) % SLOTS is issued
-    // after barrier st, when every wave has left interval st-1.
-    const bool late = wave >= 4;
-    for (int st = 0; st < nst; ++st) {
-        wait_vm_stages(min(AHEAD - 1, nst - 1 - st));             // stage st landed (this wave's part)
-        __builtin_amdgcn_s_barrier();                              // ... every wave's part
-        __builtin_amdgcn_sched_barrier(0);
-        if (st + AHEAD < nst) issue(st + AHEAD);
-        if (late) {
-            if (st > 0) kstep(st - 1, 1);
-            kstep(st, 0);
-        } else {
-            kstep(st, 0);
-            kstep(st, 1);
-        }
-    }
-    if (late && nst > 0) kstep(nst - 1, 1);
-#else
     for (int st = 0; st < nst; ++st) {
         // 4 DMA instructions per wave per stage: stage st has landed once at most 4 * (stages issued
         // after it) are outstanding
@@ -518,7 +493,6 @@ void wgrad_dma_kernel(const WgradModules mods, int64_t T, int64_t chunk, int S, 
 #pragma unroll
         for (int ks = 0; ks < kDmaBK / 16; ++ks) kstep(st, ks);
     }
-#endif
     wgrad_store<OUT>(acc, OUT == kOutSlab ? wgrad_dst<kOutSlab>(slab, tile, s, S) : tt.out, wm, wn, lane, tt.accumulate);
 }
 
