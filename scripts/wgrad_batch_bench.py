@@ -22,15 +22,23 @@ LAYER = [("down", 4096, 14336), ("up", 14336, 4096), ("gate", 14336, 4096), ("o"
          ("v", 1024, 4096), ("k", 1024, 4096), ("q", 4096, 4096)]
 
 
-def make_batches(T, tiles_per_module, batch_tiles, n_layers, dev, gen):
-    """Lists of modules (g, x_packed, out, tiles in packed coordinates, distinct-slice keys)."""
+def make_batches(T, tiles_per_module, batch_tiles, n_layers, dev, gen, pattern="spread", g_width=None):
+    """Lists of modules (g, x_packed, out, tiles in packed coordinates, distinct-slice keys).
+    pattern "rowblock": every tile of a module in ONE row block (one shared g slice, distinct x
+    slices), the g row width ``g_width`` (256: contiguous 512-B rows, else a strided column slice)."""
     batches, cur, cur_n = [], [], 0
     for layer in range(n_layers):
         for name, out_f, in_f in LAYER:
+            if g_width:
+                out_f = g_width
             rb, cb = out_f // 256, in_f // 256
             n = tiles_per_module
-            perm = torch.randperm(rb * cb, generator=gen)[:n].tolist()
-            rc = [(p // cb, p % cb) for p in perm]
+            if pattern == "rowblock":
+                r0 = int(torch.randint(rb, (1,), generator=gen))
+                rc = [(r0, c) for c in torch.randperm(cb, generator=gen)[:n].tolist()]
+            else:
+                perm = torch.randperm(rb * cb, generator=gen)[:n].tolist()
+                rc = [(p // cb, p % cb) for p in perm]
             cols = sorted({c for _r, c in rc})
             pos = {c: i for i, c in enumerate(cols)}
             g = torch.randn(T, out_f, device=dev, dtype=torch.bfloat16)      # this module's output gradient
@@ -55,12 +63,15 @@ def main():
     ap.add_argument("--batch-tiles", type=int, default=48)
     ap.add_argument("--layers", type=int, default=2)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--pattern", default="spread", choices=("spread", "rowblock"))
+    ap.add_argument("--g-width", type=int, default=None, help="override every module's out features")
     ap.add_argument("--tag", default=os.environ.get("SMT_HIP_LIB", "default"))
     args = ap.parse_args()
     dev = torch.device("cuda")
     gen = torch.Generator().manual_seed(1234)
     torch.manual_seed(0)
-    batches = make_batches(args.T, args.tiles_per_module, args.batch_tiles, args.layers, dev, gen)
+    batches = make_batches(args.T, args.tiles_per_module, args.batch_tiles, args.layers, dev, gen, args.pattern,
+                           args.g_width)
     prepared = []
     for mods in batches:
         tab, order = _hip.wgrad_batch_table([m[3] for m in mods], dev)

@@ -427,7 +427,11 @@ void wgrad_dma_kernel(const WgradModules mods, int64_t T, int64_t chunk, int S, 
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
         const int k = 4 * wave + 2 * j + (lane >> 5);
+#ifdef SMT_WGRAD_DIAG_NOSWZ
+        const int lb = 16 * (lane & 31);                         // diagnostic build only (wrong tiles)
+#else
         const int lb = (16 * (lane & 31)) ^ ((k & 3) << 6);
+#endif
         voff_g[j] = (int)(k * ldg * 2) + lb;
         voff_x[j] = (int)(k * ldx * 2) + lb;
     }
@@ -490,8 +494,10 @@ void wgrad_dma_kernel(const WgradModules mods, int64_t T, int64_t chunk, int S, 
         }
         __builtin_amdgcn_s_barrier();                              // every wave's DMA for stage st landed
         __builtin_amdgcn_sched_barrier(0);
+#ifndef SMT_WGRAD_DIAG_NOMFMA
 #pragma unroll
         for (int ks = 0; ks < kDmaBK / 16; ++ks) kstep(st, ks);
+#endif
     }
     wgrad_store<OUT>(acc, OUT == kOutSlab ? wgrad_dst<kOutSlab>(slab, tile, s, S) : tt.out, wm, wn, lane, tt.accumulate);
 }
