@@ -87,7 +87,9 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not is_stale():
         return LIB_PATH
     os.makedirs(LIB_DIR, exist_ok=True)
-    tmp = LIB_PATH + ".tmp"
+    # per-process scratch names: ranks of one node that find the library stale may build at once;
+    # each renames its own complete result into place (atomic)
+    tmp = f"{LIB_PATH}.tmp{os.getpid()}"
     run_build(tmp, verbose=verbose)
     os.replace(tmp, LIB_PATH)
     return LIB_PATH

@@ -1820,7 +1820,13 @@ void attn_dq_kernel(DqArgs a) {
 // 256 VGPRs the kernel already spills ~30 registers, and every extra live value adds scratch reloads
 // (each one a vmcnt wait) to the loop.
 // ------------------------------------------------------------------------------------------------
-constexpr int kKB = 256, kKW = 32, kDkvWaves = kKB / kKW, kSlice = 32;
+// SMT_DKV_KB: keys per dK/dV workgroup (256: 8 waves, one workgroup per CU; 128: 4 waves, two
+// workgroups per CU, whose barriers are independent)
+#ifndef SMT_DKV_KB
+#define SMT_DKV_KB 256
+#endif
+constexpr int kKB = SMT_DKV_KB, kKW = 32, kDkvWaves = kKB / kKW, kSlice = 32;
+static_assert(kKB == 128 || kKB == 256, "dK/dV key block");
 constexpr int kSliceB = kSlice * kRowB;            // 8 KiB per operand slice
 constexpr int kSliceBuf = 2 * kSliceB + 256;       // Q, dO, 32 lse + 32 delta
 constexpr int kVImg = kKB * kRowB;                 // 64 KiB
@@ -2013,11 +2019,19 @@ struct DkvLean {
         const int h = hk * G + hh;
         const int s0 = k0 + sl * kSlice;
         const uint32_t buf = lds0 + (uint32_t)((it % kDkvLeanRing) * kSliceBuf);
-        const bool is_q = wave < 4;
-        const Tns& src = is_q ? a.q : a.dout;
-        const uint16_t* base = src.p + b * src.sb + h * src.sh;
-        dma_rows(uniform_rsrc(base, (int64_t)a.S * src.ss * 2), src.ss, buf + (is_q ? 0u : (uint32_t)kSliceB), s0,
-                 s0 + 8 * (wave & 3), 2, lane);
+        if (kDkvWaves == 8) {                              // waves 0-3: Q rows 8w.., waves 4-7: dO rows
+            const bool is_q = wave < 4;
+            const Tns& src = is_q ? a.q : a.dout;
+            const uint16_t* base = src.p + b * src.sb + h * src.sh;
+            dma_rows(uniform_rsrc(base, (int64_t)a.S * src.ss * 2), src.ss, buf + (is_q ? 0u : (uint32_t)kSliceB), s0,
+                     s0 + 8 * (wave & 3), 2, lane);
+        } else {                                           // 4 waves: Q and dO rows 8w .. 8w+7 each
+            const uint16_t* qb = a.q.p + b * a.q.sb + h * a.q.sh;
+            const uint16_t* db = a.dout.p + b * a.dout.sb + h * a.dout.sh;
+            dma_rows(uniform_rsrc(qb, (int64_t)a.S * a.q.ss * 2), a.q.ss, buf, s0, s0 + 8 * wave, 2, lane);
+            dma_rows(uniform_rsrc(db, (int64_t)a.S * a.dout.ss * 2), a.dout.ss, buf + (uint32_t)kSliceB, s0,
+                     s0 + 8 * wave, 2, lane);
+        }
         if (wave < 2 && lane < 8) {
             const float* row = (wave == 0 ? a.lse : a.delta) + ((int64_t)b * a.Hq + h) * a.S;
             dma16(uniform_rsrc(row, (int64_t)a.S * 4), __builtin_amdgcn_readfirstlane(buf + 2 * kSliceB + 128 * wave),
@@ -2169,7 +2183,7 @@ struct DkvLean {
         for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
             for (int i = 0; i < 16; ++i) { dvt[dt][i] = 0.f; dkt[dt][i] = 0.f; }
-        per_slice = wave < 2 ? 3 : 2;                      // DMA instructions per slice (+ lse / delta)
+        per_slice = (kDkvWaves == 8 ? 2 : 4) + (wave < 2 ? 1 : 0);   // DMA instructions per slice (+ lse / delta)
 #pragma unroll
         for (int i = 0; i < kDkvLeanRing - 1; ++i)
             if (i < n_it) issue(i);
@@ -2200,6 +2214,7 @@ struct DkvLean {
 template <bool KMASK>
 __global__ __launch_bounds__(kDkvWaves * 64, 2)
 void attn_dkdv_kernel(DkvArgs a) {
+    static_assert(kDkvWaves == 8 || (SMT_ATTN_DKV_IMPL == 1 && kDkvRing == 2), "4-wave dK/dV: lean loop only");
     constexpr int kLdsBytes = (SMT_ATTN_DKV_IMPL == 1 && kDkvRing == 2) ? kVImg + kDkvLeanRing * kSliceBuf
                                                                          : kVImg + kDkvRing * kSliceBuf;
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
