@@ -117,6 +117,13 @@ class Fp8Group:
         self.weights = list(weights)
         self.outs = [w.shape[0] for w in self.weights]
         self.offsets = [sum(self.outs[:i]) for i in range(len(self.outs))]
+        # the members' W become row slices of ONE joint [sum(out), in] buffer (same values, same
+        # Parameter objects; built before any tile descriptor records a W address), so the per-step
+        # re-quantisation of the joint transposed copy reads it in place instead of concatenating
+        # the members (was 2 torch.cat copies of 50 + 235 MB per layer and step at the 8B point)
+        self.joint = torch.cat([w.detach() for w in self.weights], 0)
+        for w, off, n in zip(self.weights, self.offsets, self.outs):
+            w.data = self.joint[off:off + n]
         self.wt8, self.swt = quant_cols_t(self._cat())           # [in, sum(out)]
         self.swt_row = self.swt.view(1, -1)
         # the MX column blocks of the members' shared input, quantised once per forward for the union
@@ -144,6 +151,13 @@ class Fp8Group:
         self._mx_cache = None
 
     def _cat(self) -> torch.Tensor:
+        """The members' current W stacked: the joint buffer itself while every member still aliases
+        its slice of it (a member whose ``.data`` was replaced since is concatenated afresh)."""
+        j = self.joint
+        row = j.stride(0) * j.element_size()
+        if all(w.data_ptr() == j.data_ptr() + off * row and w.shape[0] == n
+               for w, off, n in zip(self.weights, self.offsets, self.outs)):
+            return j
         return torch.cat([w.detach() for w in self.weights], 0)
 
     def refresh(self, col_blocks: torch.Tensor) -> None:

@@ -202,6 +202,25 @@ def test_fp8_group_joint_input_grad():
     assert _rel(x2.grad, ref2) < 8e-2
 
 
+def test_fp8_group_members_alias_one_joint_buffer():
+    """The members' W are row slices of the group's joint buffer: the per-step re-quantisation reads
+    it in place (no concatenation), sees in-place tile updates, and a replaced member falls back."""
+    torch.manual_seed(8)
+    ws = [torch.nn.Parameter((torch.randn(o, 512, device=DEV) * 0.02).bfloat16(), requires_grad=False)
+          for o in (512, 256, 256)]
+    vals = [w.detach().clone() for w in ws]
+    g = f8.Fp8Group(ws)
+    assert all(torch.equal(w, v) for w, v in zip(ws, vals))
+    assert g._cat() is g.joint and g.joint.shape == (1024, 512)
+    ws[1].data[0:256, 256:512] += 0.5                  # an AdamW scatter into member 1's tile
+    cb = torch.tensor([1], dtype=torch.int32, device=DEV)
+    g.refresh(cb)
+    ref_q, ref_s = f8.quant_cols_t(torch.cat([w.detach() for w in ws], 0))
+    assert torch.equal(g.wt8.view(torch.uint8), ref_q.view(torch.uint8)) and torch.equal(g.swt, ref_s)
+    ws[2].data = ws[2].detach().clone()                # no longer a view: concatenated afresh
+    assert g._cat() is not g.joint and torch.equal(g._cat(), torch.cat([w.detach() for w in ws], 0))
+
+
 def test_fp8_rejects_cpu_and_fp32():
     with pytest.raises(RuntimeError):
         f8.quant_rows(torch.randn(4, 16).bfloat16())
