@@ -703,6 +703,10 @@ def timed_steps(step, batch_list, world, device):
 
 def main():
     args = parse()
+    if os.environ.get("SMT_BENCH_STACKS"):
+        # diagnostics: every thread's Python stack to stderr every N seconds (a stalled multi-rank run)
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["SMT_BENCH_STACKS"]), repeat=True)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
