@@ -417,7 +417,7 @@ def pmc_traffic(args):
     configuration (scripts/pmc_traffic.py; FETCH_SIZE x2 + WRITE_SIZE), or None."""
     path = None
     # the counters of the launch pattern this run uses: batched (engine default) or one per module
-    cands = (("r02_final_wgrad_pmc.json", "r02_wgrad_batch_pmc.json") if args.wgrad_batch_tiles > 0 else ("r02_wgrad_pmc.json", "r01_wgrad_pmc.json"))
+    cands = (("r03_final_wgrad_pmc.json", "r02_final_wgrad_pmc.json", "r02_wgrad_batch_pmc.json") if args.wgrad_batch_tiles > 0 else ("r02_wgrad_pmc.json", "r01_wgrad_pmc.json"))
     for cand in cands:
         if os.path.exists(os.path.join(ROOT, "profiles", cand)):
             path = os.path.join(ROOT, "profiles", cand)
