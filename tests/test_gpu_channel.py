@@ -63,6 +63,20 @@ def test_column_gather_bit_exact_and_zero_pad(T, k, in_f):
     assert not out[:, k:].any()
 
 
+@pytest.mark.parametrize("T,k,in_f", [(37, 100, 517), (6, 2000, 5123)])   # rows end in a partial 16-B chunk
+def test_column_gather_ragged_row_width(T, k, in_f):
+    torch.manual_seed(3)
+    wide = torch.randn(T, in_f + 13).bfloat16().to(DEV)
+    ld = (in_f + 13 + 7) // 8 * 8
+    buf = torch.zeros(T, ld, dtype=torch.bfloat16, device=DEV)
+    buf[:, :in_f + 13] = wide
+    x = buf[:, :in_f]                                   # row stride ld, n_in not a multiple of 8
+    idx = torch.randperm(in_f)[:k].tolist()
+    out = _hip.column_gather(x, _hip.index_table(idx, DEV), k, -(-k // 256) * 256)
+    assert torch.equal(out[:, :k].cpu(), x.cpu()[:, idx])
+    assert not out[:, k:].any()
+
+
 @pytest.mark.parametrize("strategy", ["mean_abs", "abs_mean", "L1", "L2"])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_act_accumulate_and_channel_scores_bit_exact(strategy, dtype):
