@@ -1551,31 +1551,16 @@ void column_gather_kernel(const uint16_t* __restrict__ x, int64_t ld_x, int64_t 
     const int64_t n_in8 = (n_in + 7) & ~(int64_t)7;
     const int64_t t0 = (int64_t)blockIdx.x * rows;
     const int tid = threadIdx.x;
-    const int chunks = (int)(n_in8 >> 3);                  // 16-B chunks per staged row
-    const int full = (int)(n_in >> 3);                      // chunks wholly inside the row
-    const int rows_here = (int)(T - t0 < rows ? T - t0 : rows);
-    // issue up to 8 of this thread's 16-B loads before any LDS write (a load-wait-store loop kept one
-    // load in flight per thread: 0.25 of HBM), then write them
-    const int total = rows_here * chunks;
-    for (int base = 0; base < total; base += 8 * 256) {
-        uint4 v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int i = base + u * 256 + tid;
-            const int r = i / chunks, k = i - r * chunks;
-            if (i < total && k < full)
-                v[u] = *reinterpret_cast<const uint4*>(x + (t0 + r) * ld_x + 8 * k);
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int i = base + u * 256 + tid;
-            const int r = i / chunks, k = i - r * chunks;
-            if (i >= total) continue;
-            if (k < full) {
-                *reinterpret_cast<uint4*>(rowbuf + r * n_in8 + 8 * k) = v[u];
-            } else {                                        // the row's ragged last chunk
-                const uint16_t* xr = x + (t0 + r) * ld_x;
-                for (int64_t e = 8 * (int64_t)k; e < n_in8; ++e) rowbuf[r * n_in8 + e] = e < n_in ? xr[e] : 0;
+    const int64_t chunks = n_in8 >> 3;
+    for (int r = 0; r < rows; ++r) {
+        const int64_t t = t0 + r;
+        if (t >= T) break;
+        const uint16_t* xr = x + t * ld_x;
+        for (int64_t k = tid; k < chunks; k += 256) {
+            if (8 * k + 8 <= n_in) {
+                *reinterpret_cast<uint4*>(rowbuf + r * n_in8 + 8 * k) = *reinterpret_cast<const uint4*>(xr + 8 * k);
+            } else {
+                for (int64_t e = 8 * k; e < n_in8; ++e) rowbuf[r * n_in8 + e] = e < n_in ? xr[e] : 0;
             }
         }
     }
