@@ -41,9 +41,30 @@ def main():
                 torch.mm(g[:, bounds[0]:bounds[1]], WT[:, bounds[0]:bounds[1]].t(), out=dx)
                 for i in range(1, n):
                     dx.addmm_(g[:, bounds[i]:bounds[i + 1]], WT[:, bounds[i]:bounds[i + 1]].t())
-            tf, td = timed(fwd), timed(dgrad)
+            full = torch.empty(T, V, device=dev, dtype=torch.bfloat16)
+
+            def fwd_slices():                     # chunk GEMMs writing column slices of one [T, V] buffer
+                for i in range(n):
+                    torch.mm(x, W[bounds[i]:bounds[i + 1]].t(), out=full[:, bounds[i]:bounds[i + 1]])
+            dx32 = torch.empty(T, H, device=dev, dtype=torch.float32)
+
+            def dgrad32():                        # chunks accumulated in fp32 (one bf16 rounding at the end)
+                torch.mm(g[:, bounds[0]:bounds[1]], WT[:, bounds[0]:bounds[1]].t(), out_dtype=torch.float32, out=dx32)
+                for i in range(1, n):
+                    torch.addmm(dx32, g[:, bounds[i]:bounds[i + 1]], WT[:, bounds[i]:bounds[i + 1]].t(),
+                                out_dtype=torch.float32, out=dx32)
+                return dx32.to(torch.bfloat16)
+            tf, td, ts, t32 = timed(fwd), timed(dgrad), timed(fwd_slices), timed(dgrad32)
+            if n > 1:
+                ref = x @ W.t()
+                fwd_slices()
+                same = bool(torch.equal(full, ref))
+            else:
+                same = None
             print(json.dumps({"round": rnd, "chunks": n, "fwd_ms": round(tf, 3), "fwd_tflops": round(fl / tf / 1e9, 1),
-                              "dgrad_ms": round(td, 3), "dgrad_tflops": round(fl / td / 1e9, 1)}), flush=True)
+                              "fwd_slices_ms": round(ts, 3), "fwd_slices_bit_equal_unchunked": same,
+                              "dgrad_ms": round(td, 3), "dgrad_tflops": round(fl / td / 1e9, 1),
+                              "dgrad_fp32acc_ms": round(t32, 3)}), flush=True)
 
 
 if __name__ == "__main__":
