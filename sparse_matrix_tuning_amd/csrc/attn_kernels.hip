@@ -856,10 +856,22 @@ struct FwdPipe {
 // as trees, the deferred max of FwdPipe (no per-tile O rescale) and the causal mask only on the
 // wave's diagonal tile.
 // ------------------------------------------------------------------------------------------------
+// SMT_ATTN_STAMPS (diagnostic builds only): every 64th forward workgroup's waves record, per K/V
+// tile, the shader clock (s_memtime) at the tile start, after its compute, after the DMA wait and
+// after the barrier; read back with smt_attn_debug_fwd_stamps (scripts/diag/attn_stamps.py)
+#ifndef SMT_ATTN_STAMPS
+#define SMT_ATTN_STAMPS 0
+#endif
+constexpr int kStampEvery = 64, kStampBlocks = 256, kStampTiles = 32;
+#if SMT_ATTN_STAMPS
+__device__ uint64_t g_fwd_stamps[kStampBlocks][4][kStampTiles][4];
+#endif
+
 template <bool KMASK>
 struct FwdLean {
     const FwdArgs& a;
     uint8_t* lds;
+    uint64_t* stamps = nullptr;   // SMT_ATTN_STAMPS: this wave's [kStampTiles][4] record, or null
     __amdgpu_buffer_rsrc_t rk, rv;
     uint32_t lds0;
     const uint64_t* km;
@@ -958,10 +970,25 @@ struct FwdLean {
     // tile t (t & 1 == SLOT): fetch tile t+1 into the other slot, compute, wait, barrier
     template <int SLOT>
     __device__ __forceinline__ void tile(int t) {
+#if SMT_ATTN_STAMPS
+        const uint64_t s0 = __builtin_amdgcn_s_memtime();
+#endif
         if (t + 1 < nt) issue(t + 1);
         if (t <= last) compute<SLOT, true>(t, t == last);
+#if SMT_ATTN_STAMPS
+        const uint64_t s1 = __builtin_amdgcn_s_memtime();
+#endif
         vm_wait_all();
+#if SMT_ATTN_STAMPS
+        const uint64_t s2 = __builtin_amdgcn_s_memtime();
+#endif
         __syncthreads();
+#if SMT_ATTN_STAMPS
+        const uint64_t s3 = __builtin_amdgcn_s_memtime();
+        if (stamps != nullptr && lane == 0 && t < kStampTiles) {
+            stamps[4 * t] = s0; stamps[4 * t + 1] = s1; stamps[4 * t + 2] = s2; stamps[4 * t + 3] = s3;
+        }
+#endif
     }
 
     __device__ __forceinline__ void run(int b, int h, int hk, int qb) {
@@ -1414,6 +1441,10 @@ void attn_fwd_kernel(FwdArgs a) {
         fp.run(grp / a.Hkv, hk * G + rem % G, hk, nqb - 1 - rem / G);
     } else if (SMT_ATTN_FWD_IMPL == 2 && kFwdWaves == 4 && kFKV == kKV && kFRing == 2) {
         FwdLean<KMASK> fl(a, lds);
+#if SMT_ATTN_STAMPS
+        if (L % kStampEvery == 0 && L / kStampEvery < kStampBlocks)
+            fl.stamps = &g_fwd_stamps[L / kStampEvery][__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)][0][0];
+#endif
         fl.run(grp / a.Hkv, hk * G + rem % G, hk, nqb - 1 - rem / G);
     } else {
         fwd_block<KMASK>(a, lds, grp / a.Hkv, hk * G + rem % G, hk, nqb - 1 - rem / G);
@@ -2259,6 +2290,15 @@ Tns tns(const smt_attn_tensor* t) { return Tns{static_cast<const uint16_t*>(t->p
 extern "C" {
 
 const char* smt_attn_last_error(void) { return g_err; }
+
+#if SMT_ATTN_STAMPS
+// diagnostic builds only: copy the forward's tile stamps (uint64 [256][4][32][4]) to host memory
+int smt_attn_debug_fwd_stamps(void* host, size_t bytes) {
+    if (bytes < sizeof(g_fwd_stamps)) return fail(-1, "smt_attn_debug_fwd_stamps: %zu < %zu bytes", bytes, sizeof(g_fwd_stamps));
+    hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fwd_stamps), sizeof(g_fwd_stamps), 0, hipMemcpyDeviceToHost);
+    return e == hipSuccess ? 0 : fail(-4, "smt_attn_debug_fwd_stamps: %s", hipGetErrorString(e));
+}
+#endif
 
 int smt_attn_fwd_kmask(const smt_attn_tensor* q, const smt_attn_tensor* k, const smt_attn_tensor* v,
                        const smt_attn_tensor* o, float* lse, const uint64_t* key_mask, int64_t key_mask_ld,
