@@ -1,4 +1,4 @@
-"""Per-tile phase timeline of the forward attention loop (FwdLean) from the shader-clock stamps of a
+"""Per-tile phase timeline of the forward attention loop (FwdLean) and per-slice timeline of the dK/dV loop (DkvLean) from the shader-clock stamps of a
 diagnostic build (SMT_ATTN_STAMPS=1, scripts/diag/build_variant.py; load it with SMT_HIP_LIB): every
 64th workgroup's waves record s_memtime at each K/V tile's start, after its compute (QK^T, softmax,
 PV issued), after the DMA wait for the next tile, and after the barrier. Prints one JSON summary.
@@ -64,6 +64,36 @@ def main():
            "mfma_cycles_per_tile_per_wave": 32 * 32,
            "block_span_cycles_median": float(np.median(spans)) if spans else None}
     print(json.dumps(out), flush=True)
+
+    # dK/dV kernel: per 32-row query slice of a wave (SMT_ATTN_STAMPS also stamps DkvLean)
+    qg, kg, vg = (t.detach().clone().requires_grad_(True) for t in (q, k, v))
+    g = torch.randn(B, S, Hq, D, device="cuda", dtype=torch.bfloat16)
+    for _ in range(2):
+        flash_attention(qg, kg, vg).backward(g)
+    torch.cuda.synchronize()
+    fn2 = lib.smt_attn_debug_dkv_stamps
+    fn2.restype, fn2.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t]
+    dbuf = np.zeros((256, 8, 64, 5), dtype=np.uint64)
+    if fn2(dbuf.ctypes.data, dbuf.nbytes):
+        raise RuntimeError(lib.smt_attn_last_error().decode())
+    rows = []
+    for blk in range(dbuf.shape[0]):
+        for w in range(8):
+            st = dbuf[blk, w].astype(np.int64)
+            n = int((st[:, 0] > 0).sum())
+            for i in range(n - 1):
+                if st[i, 1] == st[i, 0]:                 # a slice this wave skips (above its diagonal)
+                    continue
+                rows.append((st[i, 1] - st[i, 0], st[i, 2] - st[i, 1], st[i, 3] - st[i, 2], st[i, 4] - st[i, 3],
+                             st[i + 1, 0] - st[i, 0]))
+    a = np.array(rows, dtype=np.float64)
+    mean = a.mean(axis=0)
+    print(json.dumps({"kernel": "attn_dkdv_kernel (DkvLean)", "slices": len(rows),
+                      "median_cycles": dict(zip(("s_dp", "dv_dk", "dma_wait", "barrier", "slice"),
+                                                np.median(a, axis=0).tolist())),
+                      "share_of_slice": dict(zip(("s_dp", "dv_dk", "dma_wait", "barrier"),
+                                                 [round(x / mean[4], 3) for x in mean[:4]])),
+                      "mfma_cycles_per_slice_per_wave": 32 * 32}), flush=True)
 
 
 if __name__ == "__main__":

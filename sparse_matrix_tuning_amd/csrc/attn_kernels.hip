@@ -865,6 +865,10 @@ struct FwdPipe {
 constexpr int kStampEvery = 64, kStampBlocks = 256, kStampTiles = 32;
 #if SMT_ATTN_STAMPS
 __device__ uint64_t g_fwd_stamps[kStampBlocks][4][kStampTiles][4];
+// dK/dV: every 64th workgroup's 8 waves, the first 64 query slices: start, after S / dP, after the
+// dV / dK products, after the DMA wait, after the barrier
+constexpr int kDkvStampSlices = 64;
+__device__ uint64_t g_dkv_stamps[kStampBlocks][8][kDkvStampSlices][5];
 #endif
 
 template <bool KMASK>
@@ -2036,6 +2040,7 @@ template <bool KMASK>
 struct DkvLean {
     const DkvArgs& a;
     uint8_t* lds;
+    uint64_t* stamps = nullptr;   // SMT_ATTN_STAMPS: this wave's [kDkvStampSlices][5] record, or null
     bf16x8_t kf[8];
     f32x16_t dvt[4], dkt[4];
     int G, lane, wave, hi, l32, k0, kw, key, n_sl, n_it, b, hk, per_slice;
@@ -2157,16 +2162,35 @@ struct DkvLean {
     template <int SLOT>
     __device__ __forceinline__ void step(int it) {
         constexpr int R = kDkvLeanRing;
+#if SMT_ATTN_STAMPS
+        uint64_t st[5];
+        st[0] = __builtin_amdgcn_s_memtime();
+        st[1] = st[0];
+#endif
         if (it + R - 1 < n_it) issue(it + R - 1);          // into the slot slice it-1 used
         const int s0 = slice_s0(it);
         if (s0 >= 0) {
             f32x16_t s, dp;
             qk<SLOT>(s, dp);
+#if SMT_ATTN_STAMPS
+            st[1] = __builtin_amdgcn_s_memtime();
+#endif
             pv<SLOT>(s0, s, dp);
         }
+#if SMT_ATTN_STAMPS
+        st[2] = __builtin_amdgcn_s_memtime();
+#endif
         // slice it+1 landed; it+2 .. it+R-1 (those issued) may stay in flight
         vm_wait_upto(per_slice * max(0, min(R - 2, n_it - 2 - it)));
+#if SMT_ATTN_STAMPS
+        st[3] = __builtin_amdgcn_s_memtime();
+#endif
         __syncthreads();
+#if SMT_ATTN_STAMPS
+        st[4] = __builtin_amdgcn_s_memtime();
+        if (stamps != nullptr && lane == 0 && it < kDkvStampSlices)
+            for (int j = 0; j < 5; ++j) stamps[5 * it + j] = st[j];
+#endif
     }
 
     template <int SLOT>
@@ -2259,6 +2283,11 @@ void attn_dkdv_kernel(DkvArgs a) {
         if (i) __syncthreads();
         if (SMT_ATTN_DKV_IMPL == 1 && kDkvRing == 2) {
             DkvLean<KMASK> dl(a, lds);
+#if SMT_ATTN_STAMPS
+            const int L = xcd_logical(blockIdx.x, total);
+            if (i == 0 && L % kStampEvery == 0 && L / kStampEvery < kStampBlocks)
+                dl.stamps = &g_dkv_stamps[L / kStampEvery][__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) & 7][0][0];
+#endif
             dl.run(t.b, t.hk, t.blk[1 - i]);
         } else {
             dkdv_block<KMASK>(a, lds, t.b, t.hk, t.blk[1 - i]);
@@ -2297,6 +2326,12 @@ int smt_attn_debug_fwd_stamps(void* host, size_t bytes) {
     if (bytes < sizeof(g_fwd_stamps)) return fail(-1, "smt_attn_debug_fwd_stamps: %zu < %zu bytes", bytes, sizeof(g_fwd_stamps));
     hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fwd_stamps), sizeof(g_fwd_stamps), 0, hipMemcpyDeviceToHost);
     return e == hipSuccess ? 0 : fail(-4, "smt_attn_debug_fwd_stamps: %s", hipGetErrorString(e));
+}
+// the dK/dV kernel's slice stamps (uint64 [256][8][64][5])
+int smt_attn_debug_dkv_stamps(void* host, size_t bytes) {
+    if (bytes < sizeof(g_dkv_stamps)) return fail(-1, "smt_attn_debug_dkv_stamps: %zu < %zu bytes", bytes, sizeof(g_dkv_stamps));
+    hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(g_dkv_stamps), sizeof(g_dkv_stamps), 0, hipMemcpyDeviceToHost);
+    return e == hipSuccess ? 0 : fail(-4, "smt_attn_debug_dkv_stamps: %s", hipGetErrorString(e));
 }
 #endif
 
