@@ -96,6 +96,10 @@ def parse():
                     help="after the timed steps, also time this many steps with the 'selective' activation "
                          "policy (SMT linears fed by RMSNorm / SwiGLU keep no input blocks; the backward rebuilds "
                          "them; reported under 'selective_mode'; default: as many as --steps; 0 disables)")
+    ap.add_argument("--half-resident-steps", type=int, default=None,
+                    help="after the recompute point, also time this many steps with the same per-layer recompute "
+                         "but the last half of the decoder layers resident (reported under "
+                         "'grad_ckpt_half_resident_mode'; default: min(--steps, 20); 0 disables)")
     ap.add_argument("--tile-spread", default="layers", choices=("layers", "none"),
                     help="layers: scale each layer's harvested gradients to a common mean |g| before the "
                          "selection, so the 872 tiles spread over all 32 layers as in a real fine-tune (random "
@@ -129,6 +133,8 @@ def parse():
         args.ref_mode_steps = args.steps
     if args.selective_steps is None:
         args.selective_steps = args.steps
+    if args.half_resident_steps is None:
+        args.half_resident_steps = min(args.steps, 20)
     return args
 
 
@@ -909,7 +915,7 @@ def main():
         log(f"selective policy: {selective_mode['value']} tokens/s at {selective_mode['peak_hbm_gb']} GB")
 
     # ---- the reference's memory policy (per-layer recompute), same engine and tiles ----
-    ckpt_mode = None
+    ckpt_mode = half_mode = None
     if args.ref_mode_steps > 0 and not args.grad_ckpt:
         engine.module.gradient_checkpointing_enable()
         ref_batches = batches(1 + args.ref_mode_steps, B, S, vocab, rank, device, offset=50000)
@@ -927,9 +933,18 @@ def main():
                      "median_ms_per_step": round(r[1].item() * 1e3, 2),
                      "median_tokens_per_s": round(world * B * S / r[1].item(), 1),
                      "peak_hbm_gb": round(r[2].item(), 2)}
-        engine.module.gradient_checkpointing_disable()
         del ref_batches
         log(f"recompute policy: {ckpt_mode['value']} tokens/s at {ckpt_mode['peak_hbm_gb']} GB")
+        # a point between the two: the same per-layer recompute, with the last half of the decoder
+        # layers resident (trainer.set_resident_layers: the MI355X memory-budget policy)
+        if args.half_resident_steps > 0:
+            n_half = trainer.set_resident_layers(engine.module, len(trainer.checkpointed_layers(engine.module)) // 2)
+            half_mode = policy_point(args.half_resident_steps, 40000, "grad_ckpt")
+            half_mode["resident_layers"] = n_half
+            trainer.set_resident_layers(engine.module, 0)
+            log(f"recompute policy, {n_half} layers resident: {half_mode['value']} tokens/s at "
+                f"{half_mode['peak_hbm_gb']} GB")
+        engine.module.gradient_checkpointing_disable()
 
     if rank == 0:
         per_gpu = value / world
@@ -1040,7 +1055,7 @@ def main():
                                   f"{resident} layers' activations resident (HBM above the first step's peak)")},
             "selection": {"seconds": round(sel_timer.seconds, 3), "elements": sel_timer.elements,
                           "band": sel_timer.reports},
-            "grad_ckpt_mode": ckpt_mode,
+            "grad_ckpt_mode": ckpt_mode, "grad_ckpt_half_resident_mode": half_mode,
             "selective_mode": selective_mode,
             "step_mfma_frac": (round(per_gpu * F_ALG_GFLOP_PER_TOKEN * 1e9 / (PEAK_BF16_TFLOPS * 1e12), 4)
                                if args.model == "llama3-8b" else None),
