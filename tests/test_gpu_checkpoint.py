@@ -153,3 +153,87 @@ def test_resume_after_full_ft_warmup(tmp_path):
         assert torch.equal(ta.master, tc.master) and torch.equal(ta.exp_avg_sq, tc.exp_avg_sq)
     for (na, pa), (nc, pc) in zip(a.module.named_parameters(), c.module.named_parameters()):
         assert na == nc and torch.equal(pa, pc), na
+
+
+class GroupBlock(nn.Module):
+    """q/k/v and gate/up read one input each: the fp8 path turns them into groups whose members'
+    W are row slices of one joint buffer (fp8.Fp8Group)."""
+
+    def __init__(self):
+        super().__init__()
+        self.self_attn = nn.Module()
+        self.self_attn.q_proj = nn.Linear(512, 512, bias=False)
+        self.self_attn.k_proj = nn.Linear(512, 256, bias=False)
+        self.self_attn.v_proj = nn.Linear(512, 256, bias=False)
+        self.mlp = nn.Module()
+        self.mlp.gate_proj = nn.Linear(512, 768, bias=False)
+        self.mlp.up_proj = nn.Linear(512, 768, bias=False)
+        self.mlp.down_proj = nn.Linear(768, 512, bias=False)
+
+    def forward(self, x):
+        a = self.self_attn
+        h = a.q_proj(x) + torch.cat([a.k_proj(x), a.v_proj(x)], -1)
+        return self.mlp.down_proj(torch.relu(self.mlp.gate_proj(h)) * self.mlp.up_proj(h))
+
+
+class GroupNet(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.model = nn.Module()
+        self.model.layers = nn.ModuleList([GroupBlock()])
+
+    def forward(self, x):
+        return self.model.layers[0](x)
+
+
+G_MLP = {("gate_proj", 0): [(1, 0)], ("down_proj", 0): [(0, 2)]}
+G_ATT = {("q_proj", 0): [(0, 1)], ("v_proj", 0): [(0, 0)]}
+
+
+def _gbase():
+    torch.manual_seed(1)
+    net = GroupNet().to(torch.bfloat16)
+    with torch.no_grad():
+        for p in net.parameters():
+            p.mul_(4.0)
+    return net.to(DEV)
+
+
+def _gengine(net, convert=True):
+    if convert:
+        smt.freeze_unselected_matrix_layer(net, G_MLP, G_ATT)
+        smt.convert_linear_layer_to_matrix_sparsity(net, G_MLP, G_ATT)
+    groups = smt.get_optimizer_sparse_grouped_parameters(net, 0.01, 2e-3)
+    opt = SMTFusedAdam(groups, lr=2e-3, betas=(0.9, 0.95))
+    eng, _, _, _ = initialize(model=net, optimizer=opt, config={"gradient_clipping": 1.0, "fp8_linears": True})
+    return eng
+
+
+def test_fp8_group_resume_is_bit_identical(tmp_path):
+    """The fp8 path's grouped weights (joint buffers, re-quantised after every step) survive a save /
+    restore: the resumed run equals the uninterrupted one bit for bit."""
+    from sparse_matrix_tuning_amd.fp8 import Fp8Group
+    base_sd = {k: v.clone() for k, v in _gbase().state_dict().items()}
+    a = _gengine(_gbase())
+    attn = a.module.model.layers[0].self_attn
+    grp = attn.q_proj.weight._smt_fp8.group
+    assert isinstance(grp, Fp8Group) and grp._cat() is grp.joint      # members alias the joint buffer
+    for i in range(4):
+        _step(a, i)
+    b = _gengine(_gbase())
+    for i in range(2):
+        _step(b, i)
+    b.save_checkpoint(str(tmp_path), tag="s2")
+    del b
+    net = _gbase()
+    net.load_state_dict(base_sd)
+    checkpoint.restore_model(net, str(tmp_path / "s2"))
+    c = _gengine(net, convert=False)
+    c.load_checkpoint(str(tmp_path), tag="s2")
+    for i in range(2, 4):
+        _step(c, i)
+    torch.cuda.synchronize()
+    for ta, tc in zip(a.tile_groups, c.tile_groups):
+        assert torch.equal(ta.master, tc.master) and torch.equal(ta.exp_avg_sq, tc.exp_avg_sq)
+    for (na, pa), (nc, pc) in zip(a.module.named_parameters(), c.module.named_parameters()):
+        assert na == nc and torch.equal(pa, pc), na
