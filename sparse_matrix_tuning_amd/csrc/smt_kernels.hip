@@ -462,24 +462,6 @@ void wgrad_dma_kernel(const WgradModules mods, int64_t T, int64_t chunk, int S, 
     const uint32_t feat_byte = 2u * (16u * (gi & 1) + 4u * p);
     const uint32_t krow = 8u * (gi >> 1) + q;
 
-    // one 16-row k-step of stage st (its ring slot): 6 fragment reads, 8 MFMAs
-    auto kstep = [&](int st, int ks) {
-        const uint8_t* A = lds + (st % SLOTS) * kDmaSlotBytes;
-        const uint8_t* B = A + kDmaImg;
-        bf16x8_t af[4], bfr[2];
-#pragma unroll
-        for (int mb = 0; mb < 4; ++mb)
-            af[mb] = tr_frag(A, ks * 16 + krow, 2u * (wm * 128 + mb * 32) + feat_byte);
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb)
-            bfr[nb] = tr_frag(B, ks * 16 + krow, 2u * (wn * 64 + nb * 32) + feat_byte);
-#pragma unroll
-        for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb)
-                acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mb], bfr[nb], acc[mb][nb], 0, 0, 0);
-    };
-
 #pragma unroll
     for (int i = 0; i < AHEAD; ++i)
         if (i < nst) issue(i);
@@ -495,8 +477,23 @@ void wgrad_dma_kernel(const WgradModules mods, int64_t T, int64_t chunk, int S, 
         __builtin_amdgcn_s_barrier();                              // every wave's DMA for stage st landed
         __builtin_amdgcn_sched_barrier(0);
 #ifndef SMT_WGRAD_DIAG_NOMFMA
+        const uint8_t* A = lds + (st % SLOTS) * kDmaSlotBytes;
+        const uint8_t* B = A + kDmaImg;
 #pragma unroll
-        for (int ks = 0; ks < kDmaBK / 16; ++ks) kstep(st, ks);
+        for (int ks = 0; ks < kDmaBK / 16; ++ks) {
+            bf16x8_t af[4], bfr[2];
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb)
+                af[mb] = tr_frag(A, ks * 16 + krow, 2u * (wm * 128 + mb * 32) + feat_byte);
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb)
+                bfr[nb] = tr_frag(B, ks * 16 + krow, 2u * (wn * 64 + nb * 32) + feat_byte);
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb)
+                    acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mb], bfr[nb], acc[mb][nb], 0, 0, 0);
+        }
 #endif
     }
     wgrad_store<OUT>(acc, OUT == kOutSlab ? wgrad_dst<kOutSlab>(slab, tile, s, S) : tt.out, wm, wn, lane, tt.accumulate);
