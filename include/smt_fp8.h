@@ -94,6 +94,18 @@ int smt_swiglu_bwd_quant_e4m3(const void* gate, const void* up, const void* grad
                               void* out, int64_t ld_out, float* scales, void* grad_gate, void* grad_up,
                               hipStream_t stream);
 
+/* smt_swiglu_bwd_quant_e4m3 writing only some 256-column blocks of grad_gate / grad_up (fp8 path, an
+ * SMT gate/up module with MX tile gradients: the blocks its tiles read, in its row-block order, so
+ * the full bf16 gradient the data-gradient GEMM never reads is not written). gate_pos / up_pos:
+ * device int32 [cols / 256], the block's position in the packed gradient or -1 (NULL: every block, at
+ * its own column); grad_x is [rows, ld_x] bf16 and block b lands at column 256 * pos[b] (positions
+ * past ld_x / 256 are not written). cols % 256 == 0 with a map. Replaces the reference's bf16
+ * grad_output of gate/up, which linearZ.backward slices per tile (smt.py:382-404). */
+int smt_swiglu_bwd_quant_e4m3_packed(const void* gate, const void* up, const void* grad_out, int64_t rows,
+                                     int32_t cols, void* out, int64_t ld_out, float* scales, void* grad_gate,
+                                     const int32_t* gate_pos, int64_t ld_gate, void* grad_up, const int32_t* up_pos,
+                                     int64_t ld_up, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

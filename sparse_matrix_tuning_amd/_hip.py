@@ -41,7 +41,8 @@ ABI_FUNCTIONS = (
     "smt_rope_fwd", "smt_rope_bwd", "smt_swiglu_fwd", "smt_swiglu_bwd", "smt_ce_fwd", "smt_ce_bwd",
     "smt_attn_last_error", "smt_attn_fwd", "smt_attn_bwd", "smt_attn_fwd_kmask", "smt_attn_bwd_kmask",
     "smt_fp8_last_error", "smt_quant_rows_e4m3", "smt_quant_cols_t_e4m3", "smt_quant_rows_cat_e4m3",
-    "smt_swiglu_fwd_quant_e4m3", "smt_swiglu_bwd_quant_e4m3", "smt_rmsnorm_fwd_quant_e4m3",
+    "smt_swiglu_fwd_quant_e4m3", "smt_swiglu_bwd_quant_e4m3", "smt_swiglu_bwd_quant_e4m3_packed",
+    "smt_rmsnorm_fwd_quant_e4m3",
     "smt_rmsnorm_bwd_add_quant_e4m3",
 )
 
@@ -179,6 +180,8 @@ _SIGS = {
                                                        _I64, _I32, _P]),
     "smt_swiglu_fwd_quant_e4m3": (ctypes.c_int, [_P, _P, _I64, _I32, _P, _I64, _P, _P, _P]),
     "smt_swiglu_bwd_quant_e4m3": (ctypes.c_int, [_P, _P, _P, _I64, _I32, _P, _I64, _P, _P, _P, _P]),
+    "smt_swiglu_bwd_quant_e4m3_packed": (ctypes.c_int, [_P, _P, _P, _I64, _I32, _P, _I64, _P, _P, _P, _I64, _P, _P,
+                                                         _I64, _P]),
 }
 
 

@@ -267,7 +267,10 @@ void quant_rows_cat_kernel(CatSrcs src, int64_t rows, uint8_t* __restrict__ out,
 // is taken over the bf16 values of BOTH, and they are written as one e4m3 row [dgate | dup] with one
 // scale -- bit-identical to smt_swiglu_bwd followed by smt_quant_rows_cat_e4m3, without writing
 // and re-reading the bf16 gradients (written too only when grad_gate / grad_up are non-null: an SMT
-// gate/up module needs them for its tile weight gradient). One 512-thread workgroup per row.
+// gate/up module needs them for its tile weight gradient). With a position map (gpos / upos: int32
+// per 256-column block, -1 = not written) only the mapped blocks are written, block b at column
+// 256 * gpos[b] of a packed [rows, ldg] gradient: the blocks an MX tile gradient reads, and none of
+// the rest. One 512-thread workgroup per row.
 __device__ __forceinline__ uint32_t tobf16(float f) { return (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)f); }
 __device__ __forceinline__ float rbf16(float f) { return bf(tobf16(f)); }
 
@@ -276,7 +279,8 @@ __global__ __launch_bounds__(512)
 void swiglu_bwd_quant_kernel(const uint16_t* __restrict__ g, const uint16_t* __restrict__ u,
                              const uint16_t* __restrict__ dh, int64_t ld, int cols, uint8_t* __restrict__ out,
                              int64_t ldo, float* __restrict__ scales, uint16_t* __restrict__ dg_out,
-                             uint16_t* __restrict__ du_out) {
+                             const int32_t* __restrict__ gpos, int64_t ldg, uint16_t* __restrict__ du_out,
+                             const int32_t* __restrict__ upos, int64_t ldu) {
     __shared__ float wmax[8];
     const int tid = threadIdx.x;
     const int64_t row = blockIdx.x;
@@ -339,8 +343,14 @@ void swiglu_bwd_quant_kernel(const uint16_t* __restrict__ g, const uint16_t* __r
                             qv(bf(w[3] & 0xffffu), scale), qv(bf(w[3] >> 16), scale));
                 *reinterpret_cast<uint2*>(orow + (int64_t)half * cols + c * 8) = o;
             }
-            if (dg_out) *reinterpret_cast<uint4*>(dg_out + row * ld + (int64_t)c * 8) = dgv[i];
-            if (du_out) *reinterpret_cast<uint4*>(du_out + row * ld + (int64_t)c * 8) = duv[i];
+            if (dg_out) {
+                const int64_t col = gpos ? 256LL * gpos[c >> 5] + 8 * (c & 31) : 8LL * c;
+                if (col >= 0 && col + 8 <= ldg) *reinterpret_cast<uint4*>(dg_out + row * ldg + col) = dgv[i];
+            }
+            if (du_out) {
+                const int64_t col = upos ? 256LL * upos[c >> 5] + 8 * (c & 31) : 8LL * c;
+                if (col >= 0 && col + 8 <= ldu) *reinterpret_cast<uint4*>(du_out + row * ldu + col) = duv[i];
+            }
         }
     }
 }
@@ -602,19 +612,28 @@ int smt_swiglu_fwd_quant_e4m3(const void* gate, const void* up, int64_t rows, in
     return check_launch("swiglu_fwd_quant_kernel");
 }
 
-int smt_swiglu_bwd_quant_e4m3(const void* gate, const void* up, const void* grad_out, int64_t rows, int32_t cols,
-                              void* out, int64_t ld_out, float* scales, void* grad_gate, void* grad_up,
-                              hipStream_t stream) {
+}  // extern "C"
+
+namespace {
+
+int swiglu_bwd_quant_launch(const char* fn, const void* gate, const void* up, const void* grad_out, int64_t rows,
+                            int32_t cols, void* out, int64_t ld_out, float* scales, void* grad_gate,
+                            const int32_t* gate_pos, int64_t ld_gate, void* grad_up, const int32_t* up_pos,
+                            int64_t ld_up, hipStream_t stream) {
     if (rows < 0 || cols <= 0 || (cols & 7) || cols > 512 * 4 * 8)
-        return fail(-1, "smt_swiglu_bwd_quant_e4m3: bad sizes rows=%lld cols=%d (cols %% 8 == 0, <= 16384)",
-                    (long long)rows, cols);
+        return fail(-1, "%s: bad sizes rows=%lld cols=%d (cols %% 8 == 0, <= 16384)", fn, (long long)rows, cols);
+    if ((gate_pos || up_pos) && (cols % 256))
+        return fail(-1, "%s: a block position map needs cols %% 256 == 0 (cols=%d)", fn, cols);
+    if ((grad_gate && (ld_gate < (gate_pos ? 256 : cols) || (ld_gate & 7))) ||
+        (grad_up && (ld_up < (up_pos ? 256 : cols) || (ld_up & 7))))
+        return fail(-1, "%s: bad gradient row strides %lld / %lld", fn, (long long)ld_gate, (long long)ld_up);
     if (rows == 0) return 0;
-    if (!gate || !up || !grad_out || !out || !scales) return fail(-1, "smt_swiglu_bwd_quant_e4m3: null pointer");
+    if (!gate || !up || !grad_out || !out || !scales) return fail(-1, "%s: null pointer", fn);
     if (!aligned16(gate) || !aligned16(up) || !aligned16(grad_out) || (grad_gate && !aligned16(grad_gate)) ||
         (grad_up && !aligned16(grad_up)) || (reinterpret_cast<uintptr_t>(out) & 7) || (ld_out & 7) ||
         ld_out < 2LL * cols)
-        return fail(-2, "smt_swiglu_bwd_quant_e4m3: 16-byte aligned bf16 rows, 8-byte aligned fp8 rows of >= 2*cols");
-    if (rows > 0x7fffffffLL) return fail(-1, "smt_swiglu_bwd_quant_e4m3: too many rows");
+        return fail(-2, "%s: 16-byte aligned bf16 rows, 8-byte aligned fp8 rows of >= 2*cols", fn);
+    if (rows > 0x7fffffffLL) return fail(-1, "%s: too many rows", fn);
     const uint16_t *pg = static_cast<const uint16_t*>(gate), *pu = static_cast<const uint16_t*>(up),
                    *ph = static_cast<const uint16_t*>(grad_out);
     uint8_t* po = static_cast<uint8_t*>(out);
@@ -622,11 +641,30 @@ int smt_swiglu_bwd_quant_e4m3(const void* gate, const void* up, const void* grad
     const int nch = cols >> 3;
     if (nch <= 512 * 2)
         hipLaunchKernelGGL(swiglu_bwd_quant_kernel<2>, dim3((unsigned)rows), dim3(512), 0, stream, pg, pu, ph,
-                           (int64_t)cols, cols, po, ld_out, scales, dg, du);
+                           (int64_t)cols, cols, po, ld_out, scales, dg, gate_pos, ld_gate, du, up_pos, ld_up);
     else
         hipLaunchKernelGGL(swiglu_bwd_quant_kernel<4>, dim3((unsigned)rows), dim3(512), 0, stream, pg, pu, ph,
-                           (int64_t)cols, cols, po, ld_out, scales, dg, du);
+                           (int64_t)cols, cols, po, ld_out, scales, dg, gate_pos, ld_gate, du, up_pos, ld_up);
     return check_launch("swiglu_bwd_quant_kernel");
+}
+
+}  // namespace
+
+extern "C" {
+
+int smt_swiglu_bwd_quant_e4m3(const void* gate, const void* up, const void* grad_out, int64_t rows, int32_t cols,
+                              void* out, int64_t ld_out, float* scales, void* grad_gate, void* grad_up,
+                              hipStream_t stream) {
+    return swiglu_bwd_quant_launch("smt_swiglu_bwd_quant_e4m3", gate, up, grad_out, rows, cols, out, ld_out, scales,
+                                   grad_gate, nullptr, cols, grad_up, nullptr, cols, stream);
+}
+
+int smt_swiglu_bwd_quant_e4m3_packed(const void* gate, const void* up, const void* grad_out, int64_t rows,
+                                     int32_t cols, void* out, int64_t ld_out, float* scales, void* grad_gate,
+                                     const int32_t* gate_pos, int64_t ld_gate, void* grad_up, const int32_t* up_pos,
+                                     int64_t ld_up, hipStream_t stream) {
+    return swiglu_bwd_quant_launch("smt_swiglu_bwd_quant_e4m3_packed", gate, up, grad_out, rows, cols, out, ld_out,
+                                   scales, grad_gate, gate_pos, ld_gate, grad_up, up_pos, ld_up, stream);
 }
 
 int smt_quant_cols_t_e4m3(const void* w, int64_t ld_w, int32_t rows, int32_t cols, const int32_t* col_blocks_dev,

@@ -262,12 +262,17 @@ class GroupGrad:
 FUSED_SWIGLU_QUANT = os.environ.get("SMT_FP8_FUSED_SWIGLU", "1") != "0"
 # SMT_FP8_FUSED_SWIGLU_FWD=0: only the forward half (down_proj input quantised by the SwiGLU) off
 FUSED_SWIGLU_FWD_QUANT = os.environ.get("SMT_FP8_FUSED_SWIGLU_FWD", "1") != "0"
+# SMT_FP8_PACK_SWIGLU_GRAD=0: the SwiGLU backward writes an SMT gate/up module's whole bf16 output
+# gradient instead of only the row blocks its MX tile gradient reads (A/B, parity tests)
+PACK_SWIGLU_GRAD = os.environ.get("SMT_FP8_PACK_SWIGLU_GRAD", "1") != "0"
 
 
-def tag_group_output(y: torch.Tensor, reg, fw: "Fp8Weight", needs_bf16_grad: bool) -> torch.Tensor:
+def tag_group_output(y: torch.Tensor, reg, fw: "Fp8Weight", needs_bf16_grad) -> torch.Tensor:
     """Mark a group member's output so that its consumer can hand the member's gradient over
     pre-quantised (``needs_bf16_grad``: the member also needs the bf16 gradient itself, e.g. an SMT
-    module's tile weight gradient). ``reg``: what :func:`register_group` returned."""
+    module's tile weight gradient: True, or ``("mx_rows", tiles)`` when only the row blocks of its MX
+    tiles are read, which a producer may hand over packed). ``reg``: what :func:`register_group`
+    returned."""
     if reg is not None:
         y._smt_gout = (reg[0], fw.group_index, needs_bf16_grad)
     return y
@@ -346,20 +351,41 @@ def swiglu_fwd_quant(g: torch.Tensor, u: torch.Tensor, need_h: bool):
     return q.view(F8), sq, h
 
 
-def swiglu_bwd_quant(g: torch.Tensor, u: torch.Tensor, dh: torch.Tensor, need_dg: bool, need_du: bool):
+def _grad_out_spec(need, like: torch.Tensor, rows: int, n: int):
+    """``(tensor or None, position map or None, ld)`` for one bf16 output gradient: none, the whole
+    ``[.., n]`` gradient, or (``("mx_rows", tiles)``) the tiles' row blocks packed ``[rows, n_rb*256]``."""
+    if not need:
+        return None, None, n
+    if need is True:
+        return torch.empty_like(like), None, n
+    if n % 256:
+        raise ValueError(f"swiglu_bwd_quant: packed row blocks need a multiple of 256 features, got {n}")
+    n_rb, pos, _ident = need[1].mx_row_pack(n, like.device)
+    return torch.empty(rows, n_rb * 256, dtype=like.dtype, device=like.device), pos, n_rb * 256
+
+
+def swiglu_bwd_quant(g: torch.Tensor, u: torch.Tensor, dh: torch.Tensor, need_dg, need_du):
     """SwiGLU backward fused with the per-row e4m3 quantisation of ``[dgate | dup]``
-    (``smt_swiglu_bwd_quant_e4m3``): returns ``(q [T, 2n], scales [T], dgate or None, dup or None)``."""
+    (``smt_swiglu_bwd_quant_e4m3``): returns ``(q [T, 2n], scales [T], dgate or None, dup or None)``.
+    ``need_dg`` / ``need_du``: False, True (the whole bf16 gradient) or ``("mx_rows", tiles)`` (only
+    the tiles' row blocks, packed ``[T, n_rb*256]``: ``smt_swiglu_bwd_quant_e4m3_packed``)."""
     dev = _hip._require_device(g, u, dh)
     n = g.shape[-1]
     rows = g.numel() // n
     q = torch.empty(rows, 2 * n, dtype=torch.uint8, device=dev)
     sq = torch.empty(rows, dtype=torch.float32, device=dev)
-    dg = torch.empty_like(g) if need_dg else None
-    du = torch.empty_like(u) if need_du else None
-    rc = _hip.load().smt_swiglu_bwd_quant_e4m3(g.data_ptr(), u.data_ptr(), dh.data_ptr(), rows, n, q.data_ptr(),
-                                               q.stride(0), sq.data_ptr(), dg.data_ptr() if need_dg else None,
-                                               du.data_ptr() if need_du else None, _stream(dev))
-    _hip._check(rc, "smt_swiglu_bwd_quant_e4m3")
+    dg, gpos, ldg = _grad_out_spec(need_dg, g, rows, n)
+    du, upos, ldu = _grad_out_spec(need_du, u, rows, n)
+    ptr = lambda t: None if t is None else t.data_ptr()
+    if gpos is None and upos is None:
+        rc = _hip.load().smt_swiglu_bwd_quant_e4m3(g.data_ptr(), u.data_ptr(), dh.data_ptr(), rows, n, q.data_ptr(),
+                                                   q.stride(0), sq.data_ptr(), ptr(dg), ptr(du), _stream(dev))
+        _hip._check(rc, "smt_swiglu_bwd_quant_e4m3")
+    else:
+        rc = _hip.load().smt_swiglu_bwd_quant_e4m3_packed(
+            g.data_ptr(), u.data_ptr(), dh.data_ptr(), rows, n, q.data_ptr(), q.stride(0), sq.data_ptr(),
+            ptr(dg), ptr(gpos), ldg, ptr(du), ptr(upos), ldu, _stream(dev))
+        _hip._check(rc, "smt_swiglu_bwd_quant_e4m3_packed")
     return q.view(F8), sq, dg, du
 
 
@@ -395,6 +421,9 @@ def group_input_grad(reg, fw: Fp8Weight, grad_output: torch.Tensor):
     g = acc.group
     lead = grad_output.shape[:-1]
     pre, acc.prequant = acc.prequant, None
+    if pre is None and any("_smt_gpack" in t.__dict__ for t in parts.values()):
+        raise RuntimeError("fp8 group data gradient: a member's output gradient was handed over packed "
+                           "(row blocks only) without its producer's e4m3 rows")
     if sorted(parts) == list(range(len(g.outs))):
         if pre is not None:                 # quantised by the producer of the parts
             q, sq = pre

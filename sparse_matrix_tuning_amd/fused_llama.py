@@ -365,14 +365,26 @@ class FusedSwiGLUFn(torch.autograd.Function):
             acc, need_dg, need_du = ctx.fp8
             q, sq, dg, du = swiglu_bwd_quant(g, u, dh, need_dg, need_du)
             acc.prequant = (q, sq)
-            zero = g.new_zeros(()).expand_as(g)
-            return (dg if need_dg else zero), (du if need_du else zero), None, None
+            return _grad_or_placeholder(g, dg, need_dg), _grad_or_placeholder(u, du, need_du), None, None
         dg = torch.empty_like(g)
         du = torch.empty_like(u)
         rc = _hip.load().smt_swiglu_bwd(g.data_ptr(), u.data_ptr(), dh.data_ptr(), dg.data_ptr(), du.data_ptr(),
                                         g.numel(), _stream(g))
         _hip._check(rc, "smt_swiglu_bwd")
         return dg, du, None, None
+
+
+def _grad_or_placeholder(like: torch.Tensor, grad, need) -> torch.Tensor:
+    """The SwiGLU backward's gradient of gate (up) for autograd: the bf16 gradient itself, or a
+    zero-stride placeholder of its shape that nothing reads -- carrying, when the producer wrote only the
+    SMT module's row blocks (``need == ("mx_rows", tiles)``), that packed gradient as ``_smt_gpack``
+    for linearZ.backward."""
+    if grad is not None and need is True:
+        return grad
+    ph = like.new_zeros(()).expand_as(like)
+    if grad is not None:
+        ph._smt_gpack = grad
+    return ph
 
 
 def fused_mlp_forward(self, x):

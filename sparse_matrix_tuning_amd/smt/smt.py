@@ -244,6 +244,23 @@ class TileIndex:
             self._dev[key] = t
         return t
 
+    def mx_row_pack(self, out_features: int, device: torch.device):
+        """``(n_rb, int32 [out_features / 256] map)`` for an output gradient written packed by its
+        producer (``smt_swiglu_bwd_quant_e4m3_packed``): row block ``rb`` of :meth:`mx_tables` (position
+        i) goes to columns ``256 i ..``, every other block is not written (-1)."""
+        key = ("mx_pack", out_features, device.type, device.index)
+        t = self._dev.get(key)
+        if t is None:
+            pos = [-1] * (out_features // Block_dimension)
+            n = 0
+            for r, _c in self.index_list:
+                if pos[r] < 0:
+                    pos[r] = n
+                    n += 1
+            t = self._dev[key] = (n, torch.tensor(pos, dtype=torch.int32).to(device),
+                                  torch.arange(n, dtype=torch.int32).to(device))
+        return t
+
     def transposed_descs(self, weight_t: torch.Tensor) -> torch.Tensor:
         """Device smt_tile_desc[] for the transposed write-back of ``selected_weight`` into W^T."""
         key = ("wt", weight_t.data_ptr(), weight_t.device.index)
@@ -460,10 +477,12 @@ class linearZ(torch.autograd.Function):
         if fw is None:
             ctx.acc = dgrad.register(input, ctx)
         else:
-            from ..fp8 import register_group, tag_group_output
-            ctx.acc = register_group(input, fw, ctx)
-            # the tile weight gradient reads the bf16 output gradient: ask the consumer for it
-            return tag_group_output(_dense_forward(input, weight), ctx.acc, fw, True)
+            from .. import fp8
+            ctx.acc = fp8.register_group(input, fw, ctx)
+            # the tile weight gradient reads the bf16 output gradient: ask the consumer for it (only
+            # the row blocks the MX tiles read, packed, from a producer that can write them so)
+            need = ("mx_rows", tiles) if ctx.mx is not None and fp8.PACK_SWIGLU_GRAD else True
+            return fp8.tag_group_output(_dense_forward(input, weight), ctx.acc, fw, need)
         return _dense_forward(input, weight)
 
     @staticmethod
@@ -473,8 +492,15 @@ class linearZ(torch.autograd.Function):
         n = len(tiles)
         grad_input = grad_weight = None
         if ctx.needs_input_grad[1] and ctx.mx is not None:
-            g2 = _rows_ready(grad_output.reshape(-1, weight.shape[0]))
-            rb_dev, _cb, table = tiles.mx_tables(g2.device)
+            packed = grad_output.__dict__.get("_smt_gpack")
+            if packed is not None:
+                # only this module's row blocks, packed in mx_tables order (fp8.swiglu_bwd_quant)
+                g2 = packed
+                table = tiles.mx_tables(g2.device)[2]
+                rb_dev = tiles.mx_row_pack(weight.shape[0], g2.device)[2]
+            else:
+                g2 = _rows_ready(grad_output.reshape(-1, weight.shape[0]))
+                rb_dev, _cb, table = tiles.mx_tables(g2.device)
             if ctx.mx_pos is not None:
                 table = tiles.mx_group_table(ctx.mx_pos, g2.device)
             sink = ctx.sink

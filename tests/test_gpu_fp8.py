@@ -247,6 +247,78 @@ def test_swiglu_bwd_quant_matches_swiglu_bwd_then_cat_quant(rows, cols):
     assert n1 is None and n2 is None and torch.equal(q2.view(torch.uint8), q_ref.view(torch.uint8))
 
 
+@pytest.mark.parametrize("rows,cols", [(300, 14336), (7, 1024)])
+def test_swiglu_bwd_quant_packed_row_blocks(rows, cols):
+    """smt_swiglu_bwd_quant_e4m3_packed: the bf16 gradients hold only the mapped 256-column blocks,
+    in map order (bit-identical to those blocks of the full gradients); the e4m3 rows are unchanged."""
+    torch.manual_seed(rows)
+    g = (torch.randn(rows, cols, device=DEV) * 3).bfloat16()
+    u = torch.randn(rows, cols, device=DEV).bfloat16()
+    dh = (torch.randn(rows, cols, device=DEV) * 1e-3).bfloat16()
+    q_ref, s_ref, dg_ref, du_ref = f8.swiglu_bwd_quant(g, u, dh, True, True)
+    nb = cols // 256
+    g_tiles = smt.TileIndex([(nb - 1, 0), (1, 2), (nb - 1, 1)])          # row blocks in first-use order
+    u_tiles = smt.TileIndex([(0, 0)])
+    q, s, dg, du = f8.swiglu_bwd_quant(g, u, dh, ("mx_rows", g_tiles), ("mx_rows", u_tiles))
+    assert dg.shape == (rows, 512) and du.shape == (rows, 256)
+    assert torch.equal(dg[:, :256], dg_ref[:, (nb - 1) * 256:]) and torch.equal(dg[:, 256:], dg_ref[:, 256:512])
+    assert torch.equal(du, du_ref[:, :256])
+    assert torch.equal(s, s_ref) and torch.equal(q.view(torch.uint8), q_ref.view(torch.uint8))
+    # one packed, the other not written
+    _q, _s, dg2, du2 = f8.swiglu_bwd_quant(g, u, dh, ("mx_rows", u_tiles), False)
+    assert du2 is None and torch.equal(dg2, dg_ref[:, :256])
+    with pytest.raises(RuntimeError, match="cols % 256"):
+        _hip._check(_hip.load().smt_swiglu_bwd_quant_e4m3_packed(
+            g.data_ptr(), u.data_ptr(), dh.data_ptr(), rows, 1000, q.data_ptr(), q.stride(0), s.data_ptr(),
+            dg.data_ptr(), g_tiles.mx_row_pack(cols, DEV)[1].data_ptr(), 512, None, None, 1000,
+            torch.cuda.current_stream().cuda_stream), "smt_swiglu_bwd_quant_e4m3_packed")
+
+
+def test_fp8_swiglu_packed_grad_tile_grads_bit_identical():
+    """fp8 path, SMT gate/up with MX tile gradients: the SwiGLU backward hands each module only its
+    tiles' row blocks of the bf16 output gradient, packed (the rest of the [T, 14336]-shaped gradient is
+    never read: the group's data gradient uses the joint e4m3 rows). Tile gradients and loss are
+    bit-identical to writing the whole gradient, and the MX quantisation reads the packed width."""
+    import bench
+    from collections import defaultdict
+    from sparse_matrix_tuning_amd import engine as eng
+    from sparse_matrix_tuning_amd.fused_llama import patch_llama
+
+    def run(pack):
+        cfg = dict(bench.MODELS["mini"], num_hidden_layers=1)
+        bench.MODELS["_p"] = cfg
+        try:
+            model = bench.build_model("_p", DEV)
+        finally:
+            del bench.MODELS["_p"]
+        patch_llama(model)
+        sel_att = defaultdict(list, {("q_proj", 0): [(1, 1)]})
+        sel_mlp = defaultdict(list, {("gate_proj", 0): [(3, 1), (0, 0), (3, 0)], ("up_proj", 0): [(1, 0), (2, 1)]})
+        smt.freeze_unselected_matrix_layer(model, sel_mlp, sel_att)
+        smt.convert_linear_layer_to_matrix_sparsity(model, sel_mlp, sel_att)
+        opt = eng.SMTFusedAdam(smt.get_optimizer_sparse_grouped_parameters(model, 0.0, 1e-3), lr=1e-3)
+        engine, *_ = eng.initialize(model=model, optimizer=opt, config={"fp8_linears": True})
+        widths, orig, old = [], smt._hip.mx_quant_cols, f8.PACK_SWIGLU_GRAD
+        smt._hip.mx_quant_cols = lambda x, b: (widths.append(x.shape[1]), orig(x, b))[1]
+        f8.PACK_SWIGLU_GRAD = pack
+        try:
+            ids = torch.randint(0, 4096, (2, 256), generator=torch.Generator().manual_seed(0)).to(DEV)
+            loss = engine(input_ids=ids, labels=ids, use_cache=False).loss
+            engine.backward(loss)
+        finally:
+            smt._hip.mx_quant_cols, f8.PACK_SWIGLU_GRAD = orig, old
+        inter = cfg["intermediate_size"]
+        return loss.detach(), [tg.grad.clone() for tg in engine.tile_groups], widths, inter
+
+    l_pack, g_pack, w_pack, inter = run(True)
+    l_full, g_full, w_full, _ = run(False)
+    assert torch.equal(l_pack, l_full)
+    for a, b in zip(g_pack, g_full):
+        assert torch.equal(a, b)
+    assert w_full.count(inter) == 2 and inter not in w_pack          # gate / up: whole vs packed gradient
+    assert len(w_pack) == len(w_full)                                # (2 row blocks each: 512 wide)
+
+
 def test_fused_swiglu_group_grad_bit_identical_to_unfused():
     from sparse_matrix_tuning_amd.fused_llama import FusedSwiGLUFn
     torch.manual_seed(7)
