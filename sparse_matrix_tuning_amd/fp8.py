@@ -267,6 +267,16 @@ FUSED_SWIGLU_FWD_QUANT = os.environ.get("SMT_FP8_FUSED_SWIGLU_FWD", "1") != "0"
 PACK_SWIGLU_GRAD = os.environ.get("SMT_FP8_PACK_SWIGLU_GRAD", "1") != "0"
 
 
+class MxRowsNeed(tuple):
+    """``("mx_rows", tiles)``: an SMT module's request for only its MX tiles' row blocks of its bf16
+    output gradient. A producer that hands them over packed sets ``delivered``, so linearZ.backward
+    can tell a packed hand-over that autograd summed away (the output had another consumer) from a
+    producer that wrote the whole gradient."""
+
+    def __new__(cls, tiles):
+        return super().__new__(cls, ("mx_rows", tiles))
+
+
 def tag_group_output(y: torch.Tensor, reg, fw: "Fp8Weight", needs_bf16_grad) -> torch.Tensor:
     """Mark a group member's output so that its consumer can hand the member's gradient over
     pre-quantised (``needs_bf16_grad``: the member also needs the bf16 gradient itself, e.g. an SMT

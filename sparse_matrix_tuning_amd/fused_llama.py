@@ -384,6 +384,9 @@ def _grad_or_placeholder(like: torch.Tensor, grad, need) -> torch.Tensor:
     ph = like.new_zeros(()).expand_as(like)
     if grad is not None:
         ph._smt_gpack = grad
+        from .fp8 import MxRowsNeed
+        if isinstance(need, MxRowsNeed):
+            need.delivered = True
     return ph
 
 

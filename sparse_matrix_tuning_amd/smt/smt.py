@@ -481,7 +481,8 @@ class linearZ(torch.autograd.Function):
             ctx.acc = fp8.register_group(input, fw, ctx)
             # the tile weight gradient reads the bf16 output gradient: ask the consumer for it (only
             # the row blocks the MX tiles read, packed, from a producer that can write them so)
-            need = ("mx_rows", tiles) if ctx.mx is not None and fp8.PACK_SWIGLU_GRAD else True
+            need = fp8.MxRowsNeed(tiles) if ctx.mx is not None and fp8.PACK_SWIGLU_GRAD else True
+            ctx.mx_need = need if need is not True else None
             return fp8.tag_group_output(_dense_forward(input, weight), ctx.acc, fw, need)
         return _dense_forward(input, weight)
 
@@ -493,6 +494,14 @@ class linearZ(torch.autograd.Function):
         grad_input = grad_weight = None
         if ctx.needs_input_grad[1] and ctx.mx is not None:
             packed = grad_output.__dict__.get("_smt_gpack")
+            need = getattr(ctx, "mx_need", None)
+            if need is not None and need.__dict__.pop("delivered", False) and packed is None:
+                # the producer wrote only the packed row blocks and left a zero placeholder, but
+                # autograd summed that placeholder with another consumer's gradient: the packed
+                # blocks never arrived here, and the tile gradient would silently miss them
+                raise RuntimeError("linearZ (fp8, MX tile gradient): the packed output gradient was summed "
+                                   "with another consumer's gradient; set SMT_FP8_PACK_SWIGLU_GRAD=0 when a "
+                                   "gate/up output has more than one consumer")
             if packed is not None:
                 # only this module's row blocks, packed in mx_tables order (fp8.swiglu_bwd_quant)
                 g2 = packed

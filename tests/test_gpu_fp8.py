@@ -319,6 +319,47 @@ def test_fp8_swiglu_packed_grad_tile_grads_bit_identical():
     assert len(w_pack) == len(w_full)                                # (2 row blocks each: 512 wide)
 
 
+def test_fp8_packed_grad_summed_away_raises():
+    """A gate output with a second consumer: autograd sums the SwiGLU backward's zero placeholder with
+    that consumer's gradient, so the packed row blocks never reach gate_proj's linearZ. That must raise,
+    not give a tile gradient without the SwiGLU's contribution."""
+    import bench
+    from collections import defaultdict
+    from sparse_matrix_tuning_amd import engine as eng
+    from sparse_matrix_tuning_amd import fused_llama
+    from sparse_matrix_tuning_amd.fused_llama import patch_llama
+
+    cfg = dict(bench.MODELS["mini"], num_hidden_layers=1)
+    bench.MODELS["_p"] = cfg
+    try:
+        model = bench.build_model("_p", DEV)
+    finally:
+        del bench.MODELS["_p"]
+    patch_llama(model)
+    sel_mlp = defaultdict(list, {("gate_proj", 0): [(3, 1), (0, 0)], ("up_proj", 0): [(1, 0)]})
+    smt.freeze_unselected_matrix_layer(model, sel_mlp, defaultdict(list))
+    smt.convert_linear_layer_to_matrix_sparsity(model, sel_mlp, defaultdict(list))
+    opt = eng.SMTFusedAdam(smt.get_optimizer_sparse_grouped_parameters(model, 0.0, 1e-3), lr=1e-3)
+    engine, *_ = eng.initialize(model=model, optimizer=opt, config={"fp8_linears": True})
+    orig = fused_llama.FusedSwiGLUFn
+
+    class TwoConsumers:
+        @staticmethod
+        def apply(g, u, *rest):
+            return orig.apply(g, u, *rest) + 0 * g          # a second consumer of the gate output
+
+    old = f8.PACK_SWIGLU_GRAD
+    fused_llama.FusedSwiGLUFn, f8.PACK_SWIGLU_GRAD = TwoConsumers, True
+    try:
+        ids = torch.randint(0, 4096, (2, 256), generator=torch.Generator().manual_seed(0)).to(DEV)
+        loss = engine(input_ids=ids, labels=ids, use_cache=False).loss
+        with pytest.raises(RuntimeError, match="summed with another consumer"):
+            engine.backward(loss)
+    finally:
+        fused_llama.FusedSwiGLUFn, f8.PACK_SWIGLU_GRAD = orig, old
+    torch.cuda.synchronize()
+
+
 def test_fused_swiglu_group_grad_bit_identical_to_unfused():
     from sparse_matrix_tuning_amd.fused_llama import FusedSwiGLUFn
     torch.manual_seed(7)
