@@ -336,9 +336,11 @@ def test_fp8_packed_grad_summed_away_raises():
     finally:
         del bench.MODELS["_p"]
     patch_llama(model)
+    # q_proj trainable too: the MLP input then needs a gradient, so gate/up form their fp8 group
+    sel_att = defaultdict(list, {("q_proj", 0): [(1, 1)]})
     sel_mlp = defaultdict(list, {("gate_proj", 0): [(3, 1), (0, 0)], ("up_proj", 0): [(1, 0)]})
-    smt.freeze_unselected_matrix_layer(model, sel_mlp, defaultdict(list))
-    smt.convert_linear_layer_to_matrix_sparsity(model, sel_mlp, defaultdict(list))
+    smt.freeze_unselected_matrix_layer(model, sel_mlp, sel_att)
+    smt.convert_linear_layer_to_matrix_sparsity(model, sel_mlp, sel_att)
     opt = eng.SMTFusedAdam(smt.get_optimizer_sparse_grouped_parameters(model, 0.0, 1e-3), lr=1e-3)
     engine, *_ = eng.initialize(model=model, optimizer=opt, config={"fp8_linears": True})
     orig = fused_llama.FusedSwiGLUFn
