@@ -434,9 +434,16 @@ def group_input_grad(reg, fw: Fp8Weight, grad_output: torch.Tensor):
     if pre is None and any("_smt_gpack" in t.__dict__ for t in parts.values()):
         raise RuntimeError("fp8 group data gradient: a member's output gradient was handed over packed "
                            "(row blocks only) without its producer's e4m3 rows")
+    if pre is not None and (sorted(parts) != list(range(len(g.outs)))
+                            or any(parts[i] is not t for i, t in enumerate(pre[2]))):
+        # the producer's rows hold only its own share of each member's output gradient: a part that
+        # autograd summed with another consumer's gradient (or a member that did not run) is not in them
+        raise RuntimeError("fp8 group data gradient: a member's output gradient is not the tensor its "
+                           "producer quantised (summed with another consumer's gradient); the producer's "
+                           "e4m3 rows would miss that share")
     if sorted(parts) == list(range(len(g.outs))):
         if pre is not None:                 # quantised by the producer of the parts
-            q, sq = pre
+            q, sq, _handed = pre
         else:
             q, sq = quant_rows_cat([parts[i].reshape(-1, g.outs[i]) for i in range(len(g.outs))])
         gi = torch._scaled_mm(q, g.wt8.t(), scale_a=sq.view(-1, 1), scale_b=g.swt_row, out_dtype=torch.bfloat16)

@@ -364,8 +364,11 @@ class FusedSwiGLUFn(torch.autograd.Function):
             from .fp8 import swiglu_bwd_quant
             acc, need_dg, need_du = ctx.fp8
             q, sq, dg, du = swiglu_bwd_quant(g, u, dh, need_dg, need_du)
-            acc.prequant = (q, sq)
-            return _grad_or_placeholder(g, dg, need_dg), _grad_or_placeholder(u, du, need_du), None, None
+            out_g, out_u = _grad_or_placeholder(g, dg, need_dg), _grad_or_placeholder(u, du, need_du)
+            # the e4m3 rows stand for exactly these two tensors: the group checks that they reach
+            # gate and up unchanged (not summed with another consumer's gradient)
+            acc.prequant = (q, sq, (out_g, out_u))
+            return out_g, out_u, None, None
         dg = torch.empty_like(g)
         du = torch.empty_like(u)
         rc = _hip.load().smt_swiglu_bwd(g.data_ptr(), u.data_ptr(), dh.data_ptr(), dg.data_ptr(), du.data_ptr(),

@@ -319,10 +319,13 @@ def test_fp8_swiglu_packed_grad_tile_grads_bit_identical():
     assert len(w_pack) == len(w_full)                                # (2 row blocks each: 512 wide)
 
 
-def test_fp8_packed_grad_summed_away_raises():
-    """A gate output with a second consumer: autograd sums the SwiGLU backward's zero placeholder with
-    that consumer's gradient, so the packed row blocks never reach gate_proj's linearZ. That must raise,
-    not give a tile gradient without the SwiGLU's contribution."""
+@pytest.mark.parametrize("pack,match", [(True, "summed with another consumer"),
+                                        (False, "not the tensor its producer quantised")])
+def test_fp8_packed_grad_summed_away_raises(pack, match):
+    """A gate output with a second consumer: autograd sums what the SwiGLU backward hands over with
+    that consumer's gradient. Packed (a zero placeholder): the row blocks never reach gate_proj's
+    linearZ, so the tile gradient would miss the SwiGLU's share. Either way the group's data gradient
+    would use the SwiGLU's e4m3 rows, which miss the other consumer's share. Both must raise."""
     import bench
     from collections import defaultdict
     from sparse_matrix_tuning_amd import engine as eng
@@ -351,11 +354,11 @@ def test_fp8_packed_grad_summed_away_raises():
             return orig.apply(g, u, *rest) + 0 * g          # a second consumer of the gate output
 
     old = f8.PACK_SWIGLU_GRAD
-    fused_llama.FusedSwiGLUFn, f8.PACK_SWIGLU_GRAD = TwoConsumers, True
+    fused_llama.FusedSwiGLUFn, f8.PACK_SWIGLU_GRAD = TwoConsumers, pack
     try:
         ids = torch.randint(0, 4096, (2, 256), generator=torch.Generator().manual_seed(0)).to(DEV)
         loss = engine(input_ids=ids, labels=ids, use_cache=False).loss
-        with pytest.raises(RuntimeError, match="summed with another consumer"):
+        with pytest.raises(RuntimeError, match=match):
             engine.backward(loss)
     finally:
         fused_llama.FusedSwiGLUFn, f8.PACK_SWIGLU_GRAD = orig, old
