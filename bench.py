@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """SMT-phase training throughput of LLaMA-3-8B SMT(0.71%) on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W]      # N > 1: starts N ranks itself
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
@@ -53,6 +53,10 @@ PEAK_HBM_GBS = 8000.0              # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # 6.0-6.1 TB/s, the LDS-DMA weight stream 6.4-6.8 TB/s): reported beside the spec peak, not used as it
 PRACTICAL_HBM_GBS = 6300.0
 PEAK_MXFP8_TFLOPS = 5000.0         # block-scaled e4m3 MFMA, 2x bf16 per clock (MI355X_MICROARCH.md)
+WGRAD_ROUNDING_NOTE = {
+    "reference": "reference: per-sample bf16 partials summed in sample order, rounded to bf16 (smt.py:397-404; "
+                 "smt_tile_wgrad_batch_seq)",
+    "single": "single: fp32 over the whole batch, rounded once (smt_tile_wgrad_batch)"}
 F_ALG_GFLOP_PER_TOKEN = 31.744     # fwd 15.009 + dgrad 15.009 + wgrad 0.114 + attn 1.611
 
 MODELS = {
@@ -68,7 +72,11 @@ MODELS = {
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one GPU each). Without an external launcher (WORLD_SIZE unset) and N > 1, "
+                         "bench.py starts N ranks itself through torch.distributed.run before touching the GPU; "
+                         "under a launcher N must equal WORLD_SIZE (default: WORLD_SIZE, else 1)")
+    ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)  # CPU test of the launch path
     # defaults: BASELINE.md's definition, steps 10-60 after the conversion (10 untimed, 50 timed)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
@@ -100,6 +108,15 @@ def parse():
                     help="after the recompute point, also time this many steps with the same per-layer recompute "
                          "but the last half of the decoder layers resident (reported under "
                          "'grad_ckpt_half_resident_mode'; default: min(--steps, 20); 0 disables)")
+    ap.add_argument("--ref-rounding-steps", type=int, default=None,
+                    help="after the selective point, also time this many steps with the other tile-gradient rounding "
+                         "than the engine's (default engine: the reference's per-sample bf16 partials, smt.py:397-404; "
+                         "the point: single fp32 rounding; reported under 'wgrad_rounding_alt_mode'; default: "
+                         "min(--steps, 20); 0 disables)")
+    ap.add_argument("--raw-harvest-steps", type=int, default=None,
+                    help="with --tile-spread layers: at the end, swap the model over to the selection the raw "
+                         "(unscaled) harvest gives and time this many steps (reported under 'raw_harvest_mode'; "
+                         "default: min(--steps, 20); 0 disables)")
     ap.add_argument("--tile-spread", default="layers", choices=("layers", "none"),
                     help="layers: scale each layer's harvested gradients to a common mean |g| before the "
                          "selection, so the 872 tiles spread over all 32 layers as in a real fine-tune (random "
@@ -135,6 +152,10 @@ def parse():
         args.selective_steps = args.steps
     if args.half_resident_steps is None:
         args.half_resident_steps = min(args.steps, 20)
+    if args.ref_rounding_steps is None:
+        args.ref_rounding_steps = min(args.steps, 20)
+    if args.raw_harvest_steps is None:
+        args.raw_harvest_steps = min(args.steps, 20)
     return args
 
 
@@ -147,6 +168,70 @@ RESIDENT_BREAK_EVEN_STEPS = 16
 def log(*a):
     if int(os.environ.get("RANK", "0")) == 0:
         print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def launch_plan(gpus, environ) -> tuple:
+    """How this process runs ``--gpus N`` (no GPU call is made here).
+
+    * ``("run", world)``: run as one rank of ``world`` in this process (under an external launcher:
+      torch.distributed.run as the driver uses it, or the reference's ``deepspeed --include=...``
+      launcher, deepspeed/README.md:36 + fine_tune.py:968-971, which exports the same variables);
+    * ``("spawn", n)``: WORLD_SIZE is unset and N > 1: start N ranks through torch.distributed.run
+      as a child process and exit with its status;
+    * ``("error", message)``: ``--gpus`` disagrees with the launcher's WORLD_SIZE."""
+    env_world = environ.get("WORLD_SIZE")
+    if env_world is None:
+        n = 1 if gpus is None else int(gpus)
+        if n < 1:
+            return ("error", f"--gpus {n}: need at least one rank")
+        return ("spawn", n) if n > 1 else ("run", 1)
+    world = int(env_world)
+    if gpus is not None and int(gpus) != world:
+        return ("error", f"--gpus {gpus} but the launcher started WORLD_SIZE={world} ranks")
+    return ("run", world)
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """Start ``n`` ranks of this script (``torch.distributed.run``, one node, 127.0.0.1) as a child
+    process; SIGINT / SIGTERM are passed on to it. Returns its exit status (the launcher's: non-zero
+    when any rank failed)."""
+    import signal
+    import subprocess
+    cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    log("launching", n, "ranks:", " ".join(cmd))
+    proc = subprocess.Popen(cmd)
+
+    def forward(sig, _frame):
+        if proc.poll() is None:
+            proc.send_signal(sig)
+    old = {s: signal.signal(s, forward) for s in (signal.SIGINT, signal.SIGTERM)}
+    try:
+        rc = proc.wait()
+    finally:
+        for s, h in old.items():
+            signal.signal(s, h)
+    return rc if rc >= 0 else 128 - rc
+
+
+def launch_check(args, world, rank):
+    """--launch-check (CPU tests of the launch path): every rank joins the process group (gloo), sums
+    its rank, and rank 0 prints the line fields that identify the ranks -- no GPU is touched."""
+    dist.init_process_group("gloo")
+    t = torch.tensor([float(rank)])
+    dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "world_size": dist.get_world_size(), "backend": dist.get_backend(),
+                          "parallelism": f"dp{world}", "rank_sum": t.item()}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
 
 
 class WgradTimer:
@@ -393,6 +478,28 @@ def spread_over_layers(harvester):
                 g.div_(m)
 
 
+def raw_selection(harvester, dims, n_att, n_mlp, calculate_strategy):
+    """The reference's selection (fine_tune.py:304-327) on the harvest as it is, without the bench's
+    per-layer scaling: ``(selected_mlp, selected_att)``, rank 0's on every rank."""
+    from sparse_matrix_tuning_amd import trainer
+    from sparse_matrix_tuning_amd.smt.smt_helper import select_submatrix_based_on_grads
+    att = select_submatrix_based_on_grads(harvester.attention_warmup_grads, dims, n_att) if n_att > 0 else {}
+    mlp = (select_submatrix_based_on_grads(harvester.warmup_grads, dims, n_mlp, calculate_strategy=calculate_strategy)
+           if n_mlp > 0 else {})
+    return trainer._broadcast(mlp, True), trainer._broadcast(att, True)
+
+
+def tile_distribution(sel_mlp, sel_att):
+    layers = sorted({l for (_m, l) in list(sel_mlp) + list(sel_att) if l is not None})
+    per_layer = {}
+    for (_m, l), v in list(sel_mlp.items()) + list(sel_att.items()):
+        per_layer[l] = per_layer.get(l, 0) + len(v)
+    return {"tiles": sum(len(v) for v in sel_mlp.values()) + sum(len(v) for v in sel_att.values()),
+            "tile_modules": len(sel_mlp) + len(sel_att), "tile_layers": len(layers),
+            "tiles_per_layer": {str(l): per_layer[l] for l in sorted(per_layer, key=lambda x: (x is None, x))},
+            "max_tiles_per_module": max([len(v) for v in list(sel_mlp.values()) + list(sel_att.values())] or [0])}
+
+
 def build_model(name, device):
     from transformers import LlamaConfig, LlamaForCausalLM
     cfg = LlamaConfig(**MODELS[name])
@@ -418,12 +525,17 @@ def batches(n, B, S, vocab, rank, device, offset=0):
     return out
 
 
-def pmc_traffic(args):
+def pmc_traffic(args, rounding):
     """HBM bytes per wgrad launch from the committed rocprofv3 --pmc passes of this same bench
     configuration (scripts/pmc_traffic.py; FETCH_SIZE x2 + WRITE_SIZE), or None."""
     path = None
     # the counters of the launch pattern this run uses: batched (engine default) or one per module
-    cands = (("r03_final_wgrad_pmc.json", "r02_final_wgrad_pmc.json", "r02_wgrad_batch_pmc.json") if args.wgrad_batch_tiles > 0 else ("r02_wgrad_pmc.json", "r01_wgrad_pmc.json"))
+    if args.wgrad_batch_tiles <= 0:
+        cands = ("r02_wgrad_pmc.json", "r01_wgrad_pmc.json")
+    elif rounding == "reference":             # the per-sample slabs of smt_tile_wgrad_batch_seq
+        cands = ("r04_final_wgrad_pmc.json",)
+    else:
+        cands = ("r03_final_wgrad_pmc.json", "r02_final_wgrad_pmc.json", "r02_wgrad_batch_pmc.json")
     for cand in cands:
         if os.path.exists(os.path.join(ROOT, "profiles", cand)):
             path = os.path.join(ROOT, "profiles", cand)
@@ -713,12 +825,27 @@ def main():
         # diagnostics: every thread's Python stack to stderr every N seconds (a stalled multi-rank run)
         import faulthandler
         faulthandler.dump_traceback_later(float(os.environ["SMT_BENCH_STACKS"]), repeat=True)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    # decided before any GPU call: a parent that starts ranks must not initialise the device
+    mode, what = launch_plan(args.gpus, os.environ)
+    if mode == "error":
+        print(f"bench.py: {what}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if mode == "spawn":
+        sys.exit(spawn_ranks(what, sys.argv[1:]))
+    world = what
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.launch_check:
+        launch_check(args, world, rank)
+        return
+    n_dev = torch.cuda.device_count()
+    if args.dist_backend == "nccl" and world > n_dev:
+        # RCCL needs one GPU per rank: never report N ranks that shared fewer devices as N GPUs
+        raise SystemExit(f"bench.py: {world} ranks with the nccl (RCCL) backend need {world} GPUs; "
+                         f"this node has {n_dev}")
     # one process per GPU; more ranks than GPUs (functional multi-rank runs on a 1-GPU box with gloo)
     # share devices round-robin
-    dev_index = local % max(1, torch.cuda.device_count())
+    dev_index = local % max(1, n_dev)
     torch.cuda.set_device(dev_index)
     device = torch.device("cuda", dev_index)
     if world > 1:
@@ -726,6 +853,8 @@ def main():
             dist.init_process_group("nccl", device_id=device)
         else:
             dist.init_process_group(args.dist_backend)
+    backend = dist.get_backend() if world > 1 else None
+    devices_used = n_dev if world > n_dev else world
 
     from sparse_matrix_tuning_amd import _hip
     _hip.load(build_if_missing=True)
@@ -802,6 +931,11 @@ def main():
     log(f"warm-up {args.full_ft_steps} full-FT steps in {warm_s:.1f}s ({', '.join(f'{t:.2f}' for t in warm_times)} s; "
         f"{resident} layers resident after the first), peak {warm_peak:.1f} GB, loss {loss.item():.4f}")
     del warm_batches, loss
+    raw_sel = None
+    if args.tile_spread == "layers" and args.raw_harvest_steps > 0 and not args.fp8:
+        # the selection the raw harvest gives (smt_helper.py:102-139 on the unscaled gradients), kept
+        # for the raw_harvest_mode point at the end
+        raw_sel = raw_selection(harvester, dims, n_att, n_mlp, args.calculate_strategy)
     if args.tile_spread == "layers":
         spread_over_layers(harvester)
 
@@ -914,6 +1048,20 @@ def main():
         _smt.set_activation_policy(old_policy)
         log(f"selective policy: {selective_mode['value']} tokens/s at {selective_mode['peak_hbm_gb']} GB")
 
+    # ---- the other tile-gradient rounding, same engine and tiles: the headline
+    # runs the engine's default, the reference's per-sample bf16 partials (smt.py:397-404); this point
+    # runs fp32 over the whole batch, rounded once ----
+    alt_round_mode = None
+    headline_rounding = engine.wgrad_rounding
+    if args.ref_rounding_steps > 0 and not args.fp8 and engine.tile_groups:
+        alt = "single" if headline_rounding == "reference" else "reference"
+        engine.wgrad_rounding = alt
+        alt_round_mode = policy_point(args.ref_rounding_steps, 30000, "wgrad_rounding_" + alt)
+        engine.wgrad_rounding = headline_rounding
+        alt_round_mode["wgrad_rounding"] = WGRAD_ROUNDING_NOTE[alt]
+        alt_round_mode["median_step_vs_headline"] = round(alt_round_mode["median_ms_per_step"] / (med * 1e3), 4)
+        log(f"{alt} rounding: {alt_round_mode['value']} tokens/s (median step x{alt_round_mode['median_step_vs_headline']})")
+
     # ---- the reference's memory policy (per-layer recompute), same engine and tiles ----
     ckpt_mode = half_mode = None
     if args.ref_mode_steps > 0 and not args.grad_ckpt:
@@ -946,6 +1094,23 @@ def main():
                 f"{half_mode['peak_hbm_gb']} GB")
         engine.module.gradient_checkpointing_disable()
 
+    # ---- the raw harvest's selection (no per-layer scaling), swapped in at the end ----
+    raw_mode = None
+    if raw_sel is not None:
+        t_r = time.time()
+        engine, _o, _s = trainer.reselect(engine, raw_sel[0], raw_sel[1], smt_lr=args.smt_lr,
+                                          num_training_steps=total_steps, ds_config=smt_config)
+        del _o, _s
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        reconvert_s = time.time() - t_r
+        raw_mode = policy_point(args.raw_harvest_steps, 20000, "raw_harvest")
+        raw_mode.update(tile_distribution(*raw_sel))
+        raw_mode["reconversion_s"] = round(reconvert_s, 2)
+        raw_mode["median_step_vs_headline"] = round(raw_mode["median_ms_per_step"] / (med * 1e3), 4)
+        log(f"raw-harvest selection: {raw_mode['value']} tokens/s, {raw_mode['tiles']} tiles in "
+            f"{raw_mode['tile_modules']} modules of {raw_mode['tile_layers']} layers")
+
     if rank == 0:
         per_gpu = value / world
         roofline = None
@@ -960,7 +1125,7 @@ def main():
             uniq_bytes = w["unique_bytes"] / w["launches"]
             alg_gbs = alg_bytes / avg / 1e9
             uniq_gbs = uniq_bytes / avg / 1e9
-            traffic, tsrc = (None, None) if mx else pmc_traffic(args)
+            traffic, tsrc = (None, None) if mx else pmc_traffic(args, headline_rounding)
             peak_mfma = PEAK_MXFP8_TFLOPS if mx else PEAK_BF16_TFLOPS
             # The roof: the launch's intensity on its DISTINCT operand slices (each g row-block / x
             # column-block slice once, however many tiles read it) against the ridge peak_mfma / HBM.
@@ -1027,6 +1192,7 @@ def main():
                if world == 1 else None)
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "tokens/s", "n_gpus": world,
+            "world_size": dist.get_world_size() if dist.is_initialized() else 1, "backend": backend, "devices_used": devices_used,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2),
             "median_ms_per_step": round(med * 1e3, 2), "median_tokens_per_s": round(world * B * S / med, 1),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
@@ -1044,6 +1210,7 @@ def main():
                        "activations": "recomputed per layer (fine_tune.py:192)" if args.grad_ckpt else
                                       "resident in HBM (MI355X default; the reference's recompute policy: grad_ckpt_mode)",
                        "grad_ckpt": bool(args.grad_ckpt), "full_ft_steps": args.full_ft_steps,
+                       "wgrad_rounding": WGRAD_ROUNDING_NOTE.get(headline_rounding, headline_rounding),
                        "fused_llama_ops": not args.eager_ops,
                        "attention": "sdpa" if (args.eager_ops or args.sdpa_attention) else "smt_flash",
                        "loss": "transformers" if args.eager_ops else "smt_ce"},
@@ -1057,6 +1224,9 @@ def main():
                           "band": sel_timer.reports},
             "grad_ckpt_mode": ckpt_mode, "grad_ckpt_half_resident_mode": half_mode,
             "selective_mode": selective_mode,
+            "wgrad_rounding_alt_mode": alt_round_mode,
+            "raw_harvest_mode": raw_mode,
+            "tile_distribution": tile_distribution(sel_mlp, sel_att),
             "step_mfma_frac": (round(per_gpu * F_ALG_GFLOP_PER_TOKEN * 1e9 / (PEAK_BF16_TFLOPS * 1e12), 4)
                                if args.model == "llama3-8b" else None),
             "roofline": roofline,
@@ -1067,6 +1237,7 @@ def main():
                 "launches": a_sum["launches"], "avg_launch_us": round(a_sum["seconds"] / a_sum["launches"] * 1e6, 1),
                 "flops_note": "algorithmic causal FLOPs: fwd 2, bwd 5 QK^T-sized GEMMs per launch"},
             "cpu_baseline": cpu,
+            "step_ms": [round(t * 1e3, 2) for t in per_step],
             "final_loss": round(loss.item(), 5),
         }
         line = json.dumps(out)

@@ -211,6 +211,23 @@ def channel_hook_accumulate(feat: dict, key, x: torch.Tensor) -> None:
         feat[key] += a
 
 
+def channel_hook_accumulate_ranks(feat: dict, key, xs: Sequence[torch.Tensor]) -> None:
+    """fine_tune.py:651-665 cache_input_hook at world size len(xs): every rank's ``|x|`` in bf16,
+    ``all_reduce`` (sum) in bf16 -- restated for two ranks, where the collective's one addition is
+    ``bf16(fp32(a) + fp32(b))`` whatever its order -- then fp32 on the CPU, first step assigns, later
+    steps ``+=``. Rank counts above 2 depend on the collective's summation order (external)."""
+    if len(xs) == 1:
+        return channel_hook_accumulate(feat, key, xs[0])
+    if len(xs) != 2:
+        raise NotImplementedError("the bf16 rank sum is restated for two ranks")
+    a, b = (x.detach().cpu().abs() for x in xs)
+    s = (a.to(torch.float32) + b.to(torch.float32)).to(torch.bfloat16).to(torch.float32)
+    if key not in feat:
+        feat[key] = s
+    else:
+        feat[key] += s
+
+
 def channel_raw_fp64(act: torch.Tensor, strategy: str) -> torch.Tensor:
     """What ``smt_channel_score`` computes, restated with its operation order: per channel
     ``sum_s A_s`` (``sum_s A_s^2`` for L2) in fp64, ``A_s = sum_b |act[b, s, c]|`` with b ascending

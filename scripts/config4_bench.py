@@ -12,7 +12,7 @@ config LLaMA-2-13B (vocab 32008 after the reference's resize, deepspeed_helpers.
 budget 0.86 % of the parameters in 5120-wide rows. Prints one JSON line (tokens/s over the timed
 steps, peak HBM, selection time, the channel kernels' times). Per-rank data parallel as the bench.
 
-    python scripts/config4_bench.py [--steps 10 --warmup 3 --act-steps 2 --out gpurun_out/c4.json]
+    python scripts/config4_bench.py [--steps 10 --warmup 3 --act-steps 2 --out gpurun_out/c4.json] [--gpus N]
 """
 from __future__ import annotations
 
@@ -46,10 +46,36 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--grad-ckpt", action="store_true", help="per-layer recompute (fine_tune.py:192)")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks, one GPU each (WORLD_SIZE unset and N > 1: starts them itself, as bench.py)")
+    ap.add_argument("--dist-backend", default="nccl")
+    ap.add_argument("--rank-reduction", default="reference", choices=("reference", "fp32_once"),
+                    help="how the activation harvest sums ranks (trainer.ActivationHarvester)")
     args = ap.parse_args()
 
-    device = torch.device("cuda", 0)
+    mode, what = bench.launch_plan(args.gpus, os.environ)
+    if mode == "error":
+        print(f"config4_bench.py: {what}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if mode == "spawn":
+        import subprocess
+        cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={what}",
+               "--master-addr", "127.0.0.1", "--master-port", str(bench._free_port()), os.path.abspath(__file__)]
+        sys.exit(subprocess.call(cmd + sys.argv[1:]))
+    world = what
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    n_dev = torch.cuda.device_count()
+    if args.dist_backend == "nccl" and world > n_dev:
+        raise SystemExit(f"config4_bench.py: {world} RCCL ranks need {world} GPUs; this node has {n_dev}")
+    device = torch.device("cuda", local % max(1, n_dev))
     torch.cuda.set_device(device)
+    if world > 1:
+        import torch.distributed as dist
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(args.dist_backend)
     from sparse_matrix_tuning_amd import _hip, trainer
     from sparse_matrix_tuning_amd.fused_llama import patch_llama
     _hip.load()
@@ -93,10 +119,10 @@ def main():
     bench.log(f"{args.model}: {total / 1e9:.3f} B params built in {time.time() - t0:.1f}s; attention channel budget {n_att}")
 
     # ---- activation collection + selection + conversion ----
-    harvester = trainer.ActivationHarvester(model, 0, n_att)
+    harvester = trainer.ActivationHarvester(model, 0, n_att, rank_reduction=args.rank_reduction)
     torch.cuda.reset_peak_memory_stats(device)
     t_h = time.time()
-    for b in bench.batches(args.act_steps, B, S, vocab, 0, device, offset=100000):
+    for b in bench.batches(args.act_steps, B, S, vocab, rank, device, offset=100000):
         harvester.collect(b)
     torch.cuda.synchronize()
     harvest_s = time.time() - t_h
@@ -104,7 +130,7 @@ def main():
     t_s = time.time()
     engine, _opt, _sched, sel_mlp, sel_att = trainer.select_and_convert_channels(
         model, harvester, n_att, 0, num_training_steps=args.warmup + args.steps + 10,
-        ds_config={"gradient_clipping": 1.0, "train_micro_batch_size_per_gpu": B, "train_batch_size": B})
+        ds_config={"gradient_clipping": 1.0, "train_micro_batch_size_per_gpu": B, "train_batch_size": B * world})
     torch.cuda.synchronize()
     select_s = time.time() - t_s
     n_sel = sum(len(v) for v in sel_att.values())
@@ -115,7 +141,7 @@ def main():
               f"{trainable} ({100.0 * trainable / total:.3f}%)")
 
     # ---- training steps ----
-    data = bench.batches(args.warmup + args.steps, B, S, vocab, 0, device)
+    data = bench.batches(args.warmup + args.steps, B, S, vocab, rank, device)
     torch.cuda.reset_peak_memory_stats(device)
 
     def step(b):
@@ -128,24 +154,31 @@ def main():
         step(data[i])
     for t in timers.values():
         t.records, t.enabled = [], True
-    elapsed, per_step, loss = bench.timed_steps(step, data[args.warmup:], 1, device)
+    elapsed, per_step, loss = bench.timed_steps(step, data[args.warmup:], world, device)
     for t in timers.values():
         t.enabled = False
     peak = torch.cuda.max_memory_allocated(device) / 1e9
+    med = bench._median(per_step)
+    if world > 1:
+        import torch.distributed as dist
+        r = torch.tensor([elapsed, med, peak], dtype=torch.float64, device=device)
+        dist.all_reduce(r, op=dist.ReduceOp.MAX)
+        elapsed, med, peak = r.tolist()
     kernels = {}
     for name, t in timers.items():
         s = t.summary()
         if s:
             kernels[name] = {"launches_per_step": s["launches"] / args.steps, "ms_per_step": round(s["seconds"] * 1e3 / args.steps, 3)}
-    med = bench._median(per_step)
     out = {"metric": "config 4: train tokens/s + peak GB HBM, LLaMA-2-13B SMT channel path (activation selection)",
-           "value": round(B * S * args.steps / elapsed, 1), "unit": "tokens/s", "n_gpus": 1, "steps": args.steps,
+           "value": round(world * B * S * args.steps / elapsed, 1), "unit": "tokens/s", "n_gpus": world,
+           "world_size": world, "backend": args.dist_backend if world > 1 else None, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2),
            "median_ms_per_step": round(med * 1e3, 2), "peak_hbm_gb": round(peak, 2),
            "collection_peak_hbm_gb": round(harvest_peak, 2), "dtype": "bf16",
            "data": "synthetic (uniform token ids, labels=inputs; random-init weights)",
            "config": {"workload": "LLaMA-2-13B channel-sparse fine-tuning step (fwd+bwd+AdamW over selected rows)",
-                      "global_batch": B, "seq_len": S, "parallelism": "dp1", "channels": n_sel,
+                      "global_batch": B * world, "seq_len": S, "parallelism": f"dp{world}", "channels": n_sel,
+                      "rank_reduction": args.rank_reduction,
                       "channel_modules": len(sel_att), "channel_layers": len(layers), "trainable_params": trainable,
                       "trainable_pct": round(100.0 * trainable / total, 3), "grad_ckpt": bool(args.grad_ckpt),
                       "activation_steps": args.act_steps},
@@ -153,11 +186,16 @@ def main():
            "selection_and_conversion_s": round(select_s, 3), "selection_s": round(sel["seconds"], 3),
            "selection_band": sel["reports"], "channel_kernels": kernels,
            "final_loss": round(loss.item(), 5)}
-    line = json.dumps(out)
-    print(line, flush=True)
-    if args.out:
-        with open(args.out, "w") as f:
-            f.write(line + "\n")
+    if rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.out:
+            with open(args.out, "w") as f:
+                f.write(line + "\n")
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

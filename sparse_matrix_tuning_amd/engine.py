@@ -46,6 +46,10 @@ from . import _hip, dgrad
 from .smt.smt import LinearLayer_ChannelSparsity, LinearLayer_MatrixSparsity
 
 TILE_ELEMS = _hip.TILE_ELEMS
+# the engine's tile-gradient rounding unless its config names one (smt.WGRAD_ROUNDINGS): the
+# reference's per-sample bf16 partials (smt.py:397-404), so the trained tiles follow the reference's
+# arithmetic; "single" keeps fp32 over the whole batch (closer to exact, 1e-5 of fp64 in the sink)
+ENGINE_WGRAD_ROUNDING = os.environ.get("SMT_ENGINE_WGRAD_ROUNDING", "reference")
 
 
 class SMTFusedAdam(torch.optim.Optimizer):
@@ -347,6 +351,42 @@ class WgradBatcher:
             p[0].mark_ready()
 
 
+class DPTrace:
+    """Diagnostics of the DP exchange (``SMT_DP_TRACE=<path prefix>``): every rank appends JSON lines
+    ``{"ev", "t", "cpu", "thread", ...}`` to ``<prefix>.rank<r>.jsonl`` -- bucket hooks, issues, the
+    start / end of each wait in ``finish`` -- with wall time, this process's CPU time and the issuing
+    thread. ``drain`` additionally synchronises the device when ``finish`` starts, so a trace tells
+    how long the GPU backlog took apart from the collectives. Off (no cost) unless the variable is set."""
+
+    def __init__(self):
+        prefix = os.environ.get("SMT_DP_TRACE")
+        self.f = None
+        if prefix:
+            import threading
+            import time
+            rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+            self.f = open(f"{prefix}.rank{rank}.jsonl", "a", buffering=1)
+            self._time, self._thread = time, threading
+
+    def __call__(self, ev: str, **kw) -> None:
+        if self.f is None:
+            return
+        import json
+        kw.update(ev=ev, t=round(self._time.time(), 6), cpu=round(self._time.process_time(), 4),
+                  thread=self._thread.current_thread().name)
+        self.f.write(json.dumps(kw) + "\n")
+
+
+_TRACE = None
+
+
+def dp_trace() -> DPTrace:
+    global _TRACE
+    if _TRACE is None:
+        _TRACE = DPTrace()
+    return _TRACE
+
+
 class TileGradBuckets:
     """Bucketed, backward-overlapped all-reduce of one packed fp32 tile-gradient buffer.
 
@@ -455,15 +495,19 @@ class DenseGradBuckets:
     def __init__(self, params: List[torch.Tensor], bucket_elems: int, world: int):
         self.world = world
         self.buckets: List[List[torch.Tensor]] = []
-        cur, n = [], 0
+        # one flat buffer holds one dtype: parameters of different dtypes (fp32 norms beside bf16
+        # weights in a mixed-precision model) fill buckets of their own, each closed in the same
+        # construction order on every rank
+        open_: dict = {}                         # dtype -> [params, elements]
         for p in reversed(params):
-            cur.append(p)
-            n += p.numel()
-            if bucket_elems > 0 and n >= bucket_elems:
-                self.buckets.append(cur)
-                cur, n = [], 0
-        if cur:
-            self.buckets.append(cur)
+            cur = open_.setdefault(p.dtype, [[], 0])
+            cur[0].append(p)
+            cur[1] += p.numel()
+            if bucket_elems > 0 and cur[1] >= bucket_elems:
+                self.buckets.append(cur[0])
+                del open_[p.dtype]
+        for cur in open_.values():
+            self.buckets.append(cur[0])
         self.bucket_of = {id(p): i for i, b in enumerate(self.buckets) for p in b}
         self.offset_of = {}
         for b in self.buckets:
@@ -487,7 +531,8 @@ class DenseGradBuckets:
     def _flat(self, b: int, like: torch.Tensor) -> torch.Tensor:
         if self.flats[b] is None:
             n = sum(p.numel() for p in self.buckets[b])
-            self.flats[b] = torch.empty(n, dtype=like.dtype, device=like.device)
+            # the bucket's parameter dtype (= autograd's gradient dtype for it)
+            self.flats[b] = torch.empty(n, dtype=self.buckets[b][0].dtype, device=like.device)
         return self.flats[b]
 
     def _pack(self, p: torch.Tensor) -> None:
@@ -499,15 +544,16 @@ class DenseGradBuckets:
         if p.grad is None:
             view.zero_()
         elif p.grad.data_ptr() != view.data_ptr():
-            if p.grad.dtype != flat.dtype:
-                raise RuntimeError("DenseGradBuckets: gradients of one bucket must share a dtype")
-            view.copy_(p.grad)
+            view.copy_(p.grad)                  # same dtype (buckets are per dtype); copy_ casts otherwise
         p.grad = view
 
     def _hook(self, p: torch.Tensor) -> None:
         if not self.armed:
             return
         b = self.bucket_of[id(p)]
+        tr = dp_trace()
+        if tr.f is not None:
+            tr("dense_hook", bucket=b, numel=p.numel())
         if id(p) in self.seen:
             if self.works[b] is not None:
                 raise RuntimeError("a dense gradient was accumulated again after its bucket was all-reduced "
@@ -527,15 +573,23 @@ class DenseGradBuckets:
             if id(p) not in self.seen:          # no gradient on this rank in this step: zeros
                 self._pack(p)
         self.works[b] = dist.all_reduce(self.flats[b], async_op=True)
+        dp_trace()("dense_issue", bucket=b, numel=self.flats[b].numel())
 
     def finish(self) -> None:
         if not self.armed:
             return
+        tr = dp_trace()
+        tr("dense_finish", issued=self.next, buckets=len(self.buckets))
         while self.next < len(self.buckets):
             self._launch(self.next)
             self.next += 1
+        if tr.f is not None and torch.cuda.is_available():
+            torch.cuda.synchronize()
+            tr("dense_drained")
         for b, w in enumerate(self.works):
             w.wait()
+            if tr.f is not None:
+                tr("dense_waited", bucket=b)
             self.flats[b].div_(float(self.world))          # p.grad are views of it
         self.works, self.flats = [], []
         self.armed = False
@@ -629,15 +683,18 @@ class SMTEngine:
             gas = max(1, int(total) // (int(micro) * self.world)) if (micro and total) else 1
         self.gradient_accumulation_steps = int(gas)
         self.max_grad_norm = float(cfg.get("gradient_clipping", 0.0) or 0.0)
-        if "wgrad_rounding" in cfg:
-            # "reference": the tile gradients rounded as smt.py:397-404 does (per-sample bf16 partials)
-            from .smt import smt as _smt
-            _smt.set_wgrad_rounding(cfg["wgrad_rounding"])
-        if "activation_policy" in cfg:
-            # "selective": SMT linears fed by a norm / SwiGLU keep no input blocks; the backward
-            # rebuilds them (smt.smt.set_activation_policy)
-            from .smt import smt as _smt
-            _smt.set_activation_policy(cfg["activation_policy"])
+        # this engine's own modes (None: the global smt.set_wgrad_rounding / set_activation_policy);
+        # linearZ reads them through the modules' gradient sinks, so they end with the engine.
+        # "wgrad_rounding": "reference" rounds the tile gradients as smt.py:397-404 does (per-sample
+        # bf16 partials); "activation_policy": "selective" keeps no input blocks for SMT linears fed by
+        # a norm / SwiGLU (the backward rebuilds them)
+        # Default: the reference's rounding on the bf16 tile path (its cost is within the bench's noise:
+        # the tile wgrad runs off the critical path, profiles/r04_*), "single" with fp8 weights (the
+        # MX-fp8 tile gradient sums e4m3 products over all rows: no per-sample bf16 partials exist)
+        from .smt import smt as _smt
+        self.wgrad_rounding = cfg.get("wgrad_rounding", "single" if cfg.get("fp8_linears") else ENGINE_WGRAD_ROUNDING)
+        self.activation_policy = cfg.get("activation_policy")
+        _smt.register_engine_modes(self, self.wgrad_rounding, self.activation_policy)
         self.micro_steps = 0
         self.global_steps = 0
         self.device = next(model.parameters()).device

@@ -25,6 +25,7 @@ No CPU path: every entry point raises without a ROCm device.
 from __future__ import annotations
 
 import os
+import threading
 import weakref
 from typing import Optional
 
@@ -266,6 +267,28 @@ FUSED_SWIGLU_FWD_QUANT = os.environ.get("SMT_FP8_FUSED_SWIGLU_FWD", "1") != "0"
 # gradient instead of only the row blocks its MX tile gradient reads (A/B, parity tests)
 PACK_SWIGLU_GRAD = os.environ.get("SMT_FP8_PACK_SWIGLU_GRAD", "1") != "0"
 
+# Packed row blocks are requested only by gate/up outputs whose sole consumer is known to be the
+# fused SwiGLU: fused_llama.fused_mlp_forward computes them inside this scope. Any other graph (a
+# hook, a custom MLP, a second reader of the gate output) gets the whole bf16 gradient, so a valid
+# graph never hits the summed-away guard of linearZ.backward.
+_sole_swiglu = threading.local()
+
+
+class sole_swiglu_consumer:
+    """Context manager: the SMT linears called inside feed only FusedSwiGLUFn."""
+
+    def __enter__(self):
+        _sole_swiglu.depth = getattr(_sole_swiglu, "depth", 0) + 1
+        return self
+
+    def __exit__(self, *exc):
+        _sole_swiglu.depth -= 1
+        return False
+
+
+def packed_rows_allowed() -> bool:
+    return PACK_SWIGLU_GRAD and getattr(_sole_swiglu, "depth", 0) > 0
+
 
 class MxRowsNeed(tuple):
     """``("mx_rows", tiles)``: an SMT module's request for only its MX tiles' row blocks of its bf16
@@ -284,7 +307,9 @@ def tag_group_output(y: torch.Tensor, reg, fw: "Fp8Weight", needs_bf16_grad) -> 
     tiles are read, which a producer may hand over packed). ``reg``: what :func:`register_group`
     returned."""
     if reg is not None:
-        y._smt_gout = (reg[0], fw.group_index, needs_bf16_grad)
+        # the last field: produced where the fused SwiGLU is known to be the only consumer
+        # (sole_swiglu_consumer), the condition for it to hand the gradients over pre-quantised
+        y._smt_gout = (reg[0], fw.group_index, needs_bf16_grad, getattr(_sole_swiglu, "depth", 0) > 0)
     return y
 
 
@@ -295,6 +320,10 @@ def swiglu_group(gate: torch.Tensor, up: torch.Tensor):
         return None
     tg, tu = gate.__dict__.get("_smt_gout"), up.__dict__.get("_smt_gout")
     if tg is None or tu is None or tg[0] is not tu[0] or (tg[1], tu[1]) != (0, 1) or len(tg[0].group.outs) != 2:
+        return None
+    if not (tg[3] and tu[3]):
+        # gate / up made outside fused_mlp_forward may have other consumers: autograd then sums their
+        # gradients, and the group quantises what arrives instead
         return None
     if gate.shape != up.shape or gate.shape[-1] > 16384:
         return None

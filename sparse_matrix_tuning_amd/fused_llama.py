@@ -396,7 +396,9 @@ def _grad_or_placeholder(like: torch.Tensor, grad, need) -> torch.Tensor:
 def fused_mlp_forward(self, x):
     """Drop-in for ``LlamaMLP.forward`` (SiLU activation). With an fp8 down_proj the SwiGLU also emits
     down_proj's quantised input; a frozen plain down_proj then never reads the bf16 activation."""
-    gate, up = self.gate_proj(x), self.up_proj(x)
+    from .fp8 import sole_swiglu_consumer
+    with sole_swiglu_consumer():             # gate / up feed only the SwiGLU below
+        gate, up = self.gate_proj(x), self.up_proj(x)
     d = self.down_proj
     if getattr(d.weight, "_smt_fp8", None) is not None and gate.shape[-1] <= 16384:
         from . import fp8

@@ -85,11 +85,41 @@ def activation_policy() -> str:
     return _activation_policy
 
 
+# Engines whose config names a mode of their own (``"wgrad_rounding"`` / ``"activation_policy"``)
+# keep it on the engine: linearZ reads it through the module's gradient sink, so one engine's
+# config never leaks into another model or a later test in the same process. The global setting
+# above is what modules without such an engine use. Live engines asking for "selective" are counted
+# so that the producers tag their outputs (tag_recompute) while any of them exists.
+_selective_engines = 0
+
+
+def _engine_mode(sink, attr: str):
+    eng = getattr(sink, "engine", None) if sink is not None else None
+    return getattr(eng, attr, None) if eng is not None else None
+
+
+def register_engine_modes(engine, wgrad_rounding_mode: Optional[str], policy: Optional[str]) -> None:
+    """Validate an engine's own modes (None: follow the global setting)."""
+    global _selective_engines
+    if wgrad_rounding_mode is not None and wgrad_rounding_mode not in WGRAD_ROUNDINGS:
+        raise ValueError(f"wgrad rounding {wgrad_rounding_mode!r}: one of {WGRAD_ROUNDINGS}")
+    if policy is not None and policy not in ACTIVATION_POLICIES:
+        raise ValueError(f"activation policy {policy!r}: one of {ACTIVATION_POLICIES}")
+    if policy == "selective":
+        import weakref
+        _selective_engines += 1
+
+        def _done():
+            global _selective_engines
+            _selective_engines -= 1
+        weakref.finalize(engine, _done)
+
+
 def tag_recompute(out: torch.Tensor, op: int, a2d: torch.Tensor, b2d: Optional[torch.Tensor] = None,
                   weight: Optional[torch.Tensor] = None, rstd: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Mark ``out`` (a norm's / SwiGLU's output) as rebuildable from the producer's operands (which
     the producer saves for its own backward anyway); read by linearZ under the "selective" policy."""
-    if _activation_policy == "selective":
+    if _activation_policy == "selective" or _selective_engines > 0:
         out._smt_recompute = (out._version, op, a2d, b2d, weight, rstd)
     return out
 
@@ -434,9 +464,12 @@ class linearZ(torch.autograd.Function):
             # smt.py:354-356 slices input[:, :, cols]; anything but 3-D fails there
             raise IndexError(f"too many indices for tensor of dimension {input.dim()}")
         ctx.tiles = tiles
-        # reference rounding: each of the input's B sequences (S rows) is one sample of smt.py:397-404
-        ctx.seq_len = int(input.shape[1]) if (_wgrad_rounding == "reference" and len(tiles)) else None
         ctx.sink = getattr(selected_weight, "_smt_grad_sink", None)
+        # the engine's own modes when its config names them, else the global ones
+        rounding = _engine_mode(ctx.sink, "wgrad_rounding") or _wgrad_rounding
+        policy = _engine_mode(ctx.sink, "activation_policy") or _activation_policy
+        # reference rounding: each of the input's B sequences (S rows) is one sample of smt.py:397-404
+        ctx.seq_len = int(input.shape[1]) if (rounding == "reference" and len(tiles)) else None
         ctx.packed = False
         ctx.mx = None
         ctx.mx_pos = None
@@ -447,6 +480,10 @@ class linearZ(torch.autograd.Function):
                 and input.device.type == "cuda"):
             # fp8 path: the tile weight gradient runs on MX-fp8 operands; keep only the input's
             # column blocks, quantised (half the bytes of the bf16 blocks)
+            if ctx.seq_len is not None:
+                # the MX kernel sums e4m3 products over all T rows: it has no per-sample bf16 partials
+                raise RuntimeError("linearZ: the reference wgrad rounding (smt.py:397-404) exists on the bf16 tile "
+                                   "path only; with fp8 weights set SMT_FP8_TILE_WGRAD=bf16 or use rounding 'single'")
             grp = fw.group
             x2d = _rows_ready(input.reshape(-1, weight.shape[1]))
             if grp is not None and grp.mx_union is not None:
@@ -459,7 +496,7 @@ class linearZ(torch.autograd.Function):
                 ctx.mx = _off_stream(ctx.sink, lambda: _hip.mx_quant_cols(x2d, cb_dev), x2d)
                 ctx.mx_pos = None
             saved = None
-        elif (_activation_policy == "selective" and ctx.needs_input_grad[1] and len(tiles)
+        elif (policy == "selective" and ctx.needs_input_grad[1] and len(tiles)
                 and input.device.type == "cuda" and _recompute_source(input) is not None):
             # rebuilt in the backward from the producer's saved operands: nothing kept here
             ctx.recompute = _recompute_source(input)
@@ -481,7 +518,7 @@ class linearZ(torch.autograd.Function):
             ctx.acc = fp8.register_group(input, fw, ctx)
             # the tile weight gradient reads the bf16 output gradient: ask the consumer for it (only
             # the row blocks the MX tiles read, packed, from a producer that can write them so)
-            need = fp8.MxRowsNeed(tiles) if ctx.mx is not None and fp8.PACK_SWIGLU_GRAD else True
+            need = fp8.MxRowsNeed(tiles) if ctx.mx is not None and fp8.packed_rows_allowed() else True
             ctx.mx_need = need if need is not True else None
             return fp8.tag_group_output(_dense_forward(input, weight), ctx.acc, fw, need)
         return _dense_forward(input, weight)

@@ -12,9 +12,9 @@ GPU parity tests drive the exact same sequence:
                                         D2H copy + CPU add per parameter)
 * :func:`select_and_convert`            fine_tune.py:257-384
 * :class:`ActivationHarvester`          fine_tune.py:584-709 (channel path: |x| of every targeted
-                                        linear's input summed over steps in fp64 HBM accumulators
-                                        by one HIP launch per hook; ONE all-reduce at selection
-                                        instead of one per hook per step)
+                                        linear's input summed over steps in fp32 HBM accumulators
+                                        by one HIP launch per hook; ranks summed in bf16 per hook
+                                        and step as the reference does)
 * :func:`select_and_convert_channels`   fine_tune.py:406-575
 """
 from __future__ import annotations
@@ -264,18 +264,46 @@ def select_and_convert(engine, harvester: GradHarvester, targeted_module_dims: d
         model = freeze_unselected_matrix_layer(model, selected_mlp, selected_att)
     engine.release()
     harvester.release()
-    model = convert_linear_layer_to_matrix_sparsity(model, selected_mlp, selected_att)
+    # fine_tune.py:336-337 converts without ``mixture`` in both branches
+    new_engine, opt, sched = _convert_and_initialize(model, selected_mlp, selected_att, False, w_decay,
+                                                     smt_lr, ft_learning_rate, smt_lr_warmup_steps,
+                                                     num_training_steps, ds_config)
+    return new_engine, opt, sched, selected_mlp, selected_att
+
+
+def _convert_and_initialize(model, selected_mlp, selected_att, mixture, w_decay, smt_lr, ft_learning_rate,
+                            smt_lr_warmup_steps, num_training_steps, ds_config):
+    """fine_tune.py:339-384: convert the frozen model's selected linears, rebuild the optimizer
+    groups, scheduler and engine."""
+    model = convert_linear_layer_to_matrix_sparsity(model, selected_mlp, selected_att, mixture=mixture)
     make_gradient_checkpointing_compatible(model)
     groups = get_optimizer_sparse_grouped_parameters(model, w_decay, smt_lr)
     if not groups:
-        raise RuntimeError("SMT selection produced no trainable tile (block budgets "
-                           f"attention={num_attention_blocks}, mlp={num_mlp_blocks})")
+        raise RuntimeError("SMT selection produced no trainable tile (selected "
+                           f"attention={sum(map(len, selected_att.values()))}, mlp={sum(map(len, selected_mlp.values()))})")
     opt = SMTFusedAdam(groups, lr=ft_learning_rate if ft_learning_rate is not None else smt_lr, betas=(0.9, 0.95))
     sched = torch.optim.lr_scheduler.LambdaLR(opt, linear_lr_lambda(smt_lr_warmup_steps, num_training_steps))
     torch.cuda.empty_cache()
     new_engine, opt, _, sched = initialize(model=model, optimizer=opt, config=ds_config or {"gradient_clipping": 1.0},
                                            lr_scheduler=sched)
-    return new_engine, opt, sched, selected_mlp, selected_att
+    return new_engine, opt, sched
+
+
+def reselect(engine, selected_mlp, selected_att, *, w_decay=0.0, smt_lr=9.865e-6, ft_learning_rate=None,
+             smt_lr_warmup_steps=0, num_training_steps=1000, ds_config: Optional[dict] = None):
+    """Swap an SMT engine's model over to another tile selection: merge every module's tiles back into
+    its W (convert_matrix_sparsity_to_linear_layer, smt.py:416-457), drop the engine's packed state and
+    weight copies, freeze / convert / initialise for the new selection (fine_tune.py:264-384). Used by
+    the bench to time a second selection of the same model. Returns ``(engine, optimizer, scheduler)``."""
+    from .engine import detach_transposed_weights
+    from .smt.smt import convert_matrix_sparsity_to_linear_layer
+    model = engine.module
+    engine.release()
+    detach_transposed_weights(model)
+    convert_matrix_sparsity_to_linear_layer(model)
+    model = freeze_unselected_matrix_layer(model, selected_mlp, selected_att)
+    return _convert_and_initialize(model, selected_mlp, selected_att, False, w_decay, smt_lr, ft_learning_rate,
+                                   smt_lr_warmup_steps, num_training_steps, ds_config)
 
 
 def _broadcast(selection, enabled: bool):
@@ -307,12 +335,25 @@ class ActivationHarvester:
     model feeds them the same inputs. Each hook is one ``smt_act_accumulate`` launch that keeps the
     reference's own state, the fp32 ``[B, S, in]`` sum of ``|x|`` over steps, in HBM (bit for bit the
     CPU ``+=``). Linears that read the same input tensor in one forward (q/k/v, gate/up) share one
-    accumulator instead of holding identical copies. Ranks are summed once, in :meth:`finalize`,
-    with one fp32 all-reduce of all accumulators (the reference all-reduces every hook's bf16 ``|x|``;
-    at world size 1 both are the identity)."""
+    accumulator instead of holding identical copies.
 
-    def __init__(self, model, num_mlp_channel: int, num_attention_channel: int):
+    Ranks (``rank_reduction``): ``"reference"`` (default) does what fine_tune.py:651-665 does on
+    every hook of every step: ``|x|`` in bf16, summed over ranks in bf16 by one all-reduce, then
+    added in fp32 -- so the accumulators, and the selection, are the reference's at any world size
+    (one all-reduce per distinct input: the reference's q/k/v hooks each all-reduce the same
+    ``|x|`` and get the same sum). ``"fp32_once"`` sums the fp32 accumulators once, in
+    :meth:`finalize` (one collective instead of one per input per step; it rounds differently from
+    the reference at world size > 1). At world size 1 both are the identity."""
+
+    RANK_REDUCTIONS = ("reference", "fp32_once")
+
+    def __init__(self, model, num_mlp_channel: int, num_attention_channel: int, rank_reduction: str = "reference"):
+        if rank_reduction not in self.RANK_REDUCTIONS:
+            raise ValueError(f"rank_reduction {rank_reduction!r}: one of {self.RANK_REDUCTIONS}")
+        import torch.distributed as dist
         self.model = model
+        self.rank_reduction = rank_reduction
+        self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
         self.activation: Dict[tuple, ChannelActivation] = {}
         self.attention_activation: Dict[tuple, ChannelActivation] = {}
         self._handles = []
@@ -352,6 +393,12 @@ class ActivationHarvester:
                 # the reference's `feat_dict[key] += x` needs equal shapes across steps too
                 raise RuntimeError(f"activation shape {tuple(x.shape)} differs from earlier steps "
                                    f"({tuple(ent.acc.shape)}) for {key}")
+            if self.world > 1 and self.rank_reduction == "reference":
+                # fine_tune.py:653-657: x = |x| (bf16), all_reduce (bf16 sum over ranks), then the fp32
+                # add; act_accumulate takes |.| of the non-negative sum again, which changes nothing
+                import torch.distributed as dist
+                x = x.abs()
+                dist.all_reduce(x)
             _hip.act_accumulate(x, ent.acc, assign=ent.steps == 0)
             ent.steps += 1
             self._last = (x_obj, ent)
@@ -376,6 +423,8 @@ class ActivationHarvester:
         self._reduced = True
         if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
             return
+        if self.rank_reduction == "reference":
+            return                          # every hook already summed its bf16 |x| over ranks
         seen, accs = set(), []
         for d in (self.activation, self.attention_activation):
             for e in d.values():

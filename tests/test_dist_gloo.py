@@ -201,3 +201,51 @@ def test_gloo_bucket_issue_order_is_rank_independent(world):
     for p in procs:
         p.join(timeout=60)
     assert res == {r: True for r in range(world)}
+
+
+def _mixed_dtype_worker(rank, world, port, q):
+    """A mixed-precision model (fp32 norm-like scale beside bf16 weights): each dtype
+    fills buckets of its own, and every p.grad comes back DP-averaged in its own dtype."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from sparse_matrix_tuning_amd.engine import DenseGradBuckets
+    torch.manual_seed(0)
+    lin1 = torch.nn.Linear(8, 16).to(torch.bfloat16)
+    scale = torch.nn.Parameter(torch.rand(16) + 0.5)     # fp32
+    lin2 = torch.nn.Linear(16, 4).to(torch.bfloat16)
+    params = list(lin1.parameters()) + [scale] + list(lin2.parameters())
+    buckets = DenseGradBuckets(params, bucket_elems=40, world=world)
+    ok = all(len({p.dtype for p in b}) == 1 for b in buckets.buckets)
+    ok &= sorted(p.numel() for b in buckets.buckets for p in b) == sorted(p.numel() for p in params)
+    x = torch.randn(5, 8, generator=torch.Generator().manual_seed(10 + rank)).to(torch.bfloat16)
+
+    def loss():
+        return lin2((lin1(x).float() * scale).to(torch.bfloat16)).float().pow(2).sum()
+    local = list(torch.autograd.grad(loss(), params))
+    buckets.arm()
+    loss().backward()
+    buckets.finish()
+    for p, g in zip(params, local):
+        got = [torch.zeros_like(g) for _ in range(world)]
+        dist.all_gather(got, g)
+        want = sum(t.float() for t in got) / world
+        ok &= p.grad.dtype == p.dtype
+        ok &= torch.allclose(p.grad.float(), want, rtol=2e-2, atol=1e-3)
+    buckets.remove()
+    q.put((rank, bool(ok)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_dense_buckets_mixed_dtypes():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mixed_dtype_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {r: True for r in range(world)}

@@ -379,8 +379,10 @@ def test_fused_swiglu_group_grad_bit_identical_to_unfused():
         f8.FUSED_SWIGLU_QUANT = fused
         try:
             x = x0.clone().requires_grad_()
-            gate = f8.Fp8LinearFn.apply(x, ws[0], fws[0], None)
-            up = f8.Fp8LinearFn.apply(x, ws[1], fws[1], None)
+            with f8.sole_swiglu_consumer():        # as fused_mlp_forward computes them
+                gate = f8.Fp8LinearFn.apply(x, ws[0], fws[0], None)
+                up = f8.Fp8LinearFn.apply(x, ws[1], fws[1], None)
+            assert (f8.swiglu_group(gate, up) is not None) == fused
             h = FusedSwiGLUFn.apply(gate, up)
             h.backward(dh)
             return x.grad
@@ -389,6 +391,52 @@ def test_fused_swiglu_group_grad_bit_identical_to_unfused():
 
     fused, plain = run(True), run(False)
     assert torch.equal(fused, plain)
+
+
+def test_gate_up_outside_fused_mlp_fall_back_to_full_gradients():
+    """packed gate/up row blocks (and the SwiGLU's pre-quantised group rows) are used only
+    where fused_mlp_forward makes the SwiGLU their sole consumer. A custom MLP whose gate output has a
+    second consumer trains without raising, and its tile and data gradients equal the fused MLP's."""
+    import bench
+    from collections import defaultdict
+    from sparse_matrix_tuning_amd import engine as eng
+    from sparse_matrix_tuning_amd import fused_llama
+    from sparse_matrix_tuning_amd.fused_llama import FusedSwiGLUFn, patch_llama
+
+    def custom_two(self, x):
+        gate, up = self.gate_proj(x), self.up_proj(x)
+        return self.down_proj(FusedSwiGLUFn.apply(gate, up) + 0 * gate)
+
+    def custom_one(self, x):
+        return self.down_proj(FusedSwiGLUFn.apply(self.gate_proj(x), self.up_proj(x)))
+
+    results = {}
+    for label, fwd in (("fused", None), ("one", custom_one), ("two", custom_two)):
+        cfg = dict(bench.MODELS["mini"], num_hidden_layers=1)
+        bench.MODELS["_p"] = cfg
+        try:
+            model = bench.build_model("_p", DEV)
+        finally:
+            del bench.MODELS["_p"]
+        patch_llama(model)
+        if fwd is not None:
+            for layer in model.model.layers:
+                layer.mlp.forward = fwd.__get__(layer.mlp, type(layer.mlp))
+        sel_att = defaultdict(list, {("q_proj", 0): [(1, 1)]})
+        sel_mlp = defaultdict(list, {("gate_proj", 0): [(3, 1), (0, 0)], ("up_proj", 0): [(1, 0)]})
+        smt.freeze_unselected_matrix_layer(model, sel_mlp, sel_att)
+        smt.convert_linear_layer_to_matrix_sparsity(model, sel_mlp, sel_att)
+        opt = eng.SMTFusedAdam(smt.get_optimizer_sparse_grouped_parameters(model, 0.0, 1e-3), lr=1e-3)
+        engine, *_ = eng.initialize(model=model, optimizer=opt, config={"fp8_linears": True})
+        ids = torch.randint(0, 4096, (2, 256), generator=torch.Generator().manual_seed(0)).to(DEV)
+        loss = engine(input_ids=ids, labels=ids, use_cache=False).loss
+        engine.backward(loss)                       # no RuntimeError for the two-consumer graph
+        torch.cuda.synchronize()
+        results[label] = (loss.item(), torch.cat([tg.grad.clone() for tg in engine.tile_groups]))
+        del engine, model, opt
+    assert results["one"][0] == results["fused"][0] == results["two"][0]
+    assert torch.equal(results["one"][1], results["fused"][1])
+    assert torch.equal(results["two"][1], results["fused"][1])
 
 
 @pytest.mark.parametrize("rows,cols", [(300, 14336), (17, 1024)])

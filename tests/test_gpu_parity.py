@@ -305,13 +305,53 @@ def test_engine_sink_grads_are_fp32_and_exact():
     W = nn.Parameter((torch.randn(512, 768) * 0.05).bfloat16().to(DEV))
     mod = smt.LinearLayer_MatrixSparsity(W, index_list=[(0, 2), (1, 0)])
     opt = SMTFusedAdam([mod.selected_weight], lr=1e-3)
-    engine, _, _, _ = initialize(model=mod, optimizer=opt, config={})
+    engine, _, _, _ = initialize(model=mod, optimizer=opt, config={"wgrad_rounding": "single"})
     x = torch.randn(2, 96, 768).bfloat16()
     g = torch.randn(2, 96, 512).bfloat16()
     engine.backward((mod(x.to(DEV)).float() * g.to(DEV).float()).sum())
     sink = mod.selected_weight._smt_grad_sink.buffer
     assert sink.dtype == torch.float32 and mod.selected_weight.grad is None
     assert _rel(sink, ref.tile_grads_fp64(g, x, [(0, 2), (1, 0)])) < 1e-5
+
+
+def test_engine_config_rounding_is_engine_scoped():
+    """an engine's ``"wgrad_rounding"`` rounds that engine's tile gradients -- by default
+     and with ``"reference"`` as smt.py:397-404 does (within 1e-3 of
+    oracle.linearz_backward), with ``"single"`` in fp32 over the batch (1e-5 of fp64 truth) -- and never
+    changes the global mode. An fp8 weight with MX tile gradients refuses the reference rounding
+    instead of silently ignoring it."""
+    from sparse_matrix_tuning_amd import fp8 as f8
+    torch.manual_seed(19)
+    tiles = [(0, 2), (1, 0)]
+    x = torch.randn(4, 128, 768).bfloat16()
+    g = torch.randn(4, 128, 512).bfloat16()
+    W0 = (torch.randn(512, 768) * 0.05).bfloat16()
+    truth = ref.tile_grads_fp64(g, x, tiles)
+    _gi, ref_gw = ref.linearz_backward(g, x, W0, tiles)
+    before = smt.wgrad_rounding()
+    bufs = {}
+    for key in ("reference", "single", None):
+        mod = smt.LinearLayer_MatrixSparsity(nn.Parameter(W0.to(DEV)), index_list=tiles)
+        opt = SMTFusedAdam([mod.selected_weight], lr=1e-3)
+        cfg = {} if key is None else {"wgrad_rounding": key}
+        engine, _, _, _ = initialize(model=mod, optimizer=opt, config=cfg)
+        assert smt.wgrad_rounding() == before
+        engine.backward((mod(x.to(DEV)).float() * g.to(DEV).float()).sum())
+        torch.cuda.synchronize()
+        bufs[key] = mod.selected_weight._smt_grad_sink.buffer.clone()
+    assert _rel(bufs["reference"], ref_gw) <= 1e-3
+    assert _rel(bufs["single"], truth) < 1e-5
+    assert not torch.equal(bufs["reference"], bufs["single"])
+    assert torch.equal(bufs[None], bufs["reference"])            # the engine's default
+    # fp8 + MX tile gradients + reference rounding: refused
+    W = nn.Parameter(W0.to(DEV), requires_grad=False)
+    W._smt_fp8 = f8.Fp8Weight(W)
+    if W._smt_fp8.mx_wgrad:
+        mod = smt.LinearLayer_MatrixSparsity(W, index_list=tiles)
+        opt = SMTFusedAdam([mod.selected_weight], lr=1e-3)
+        engine, _, _, _ = initialize(model=mod, optimizer=opt, config={"wgrad_rounding": "reference"})
+        with pytest.raises(RuntimeError, match="reference wgrad rounding"):
+            mod(x.to(DEV))
 
 
 # ------------------------------------------------------------------ end to end: mini LLaMA vs oracle

@@ -153,7 +153,10 @@ def _mini_engine(batch_tiles, seed=0):
     params = [m.selected_weight for m in model.modules() if isinstance(m, smt.LinearLayer_MatrixSparsity)]
     opt = eng.SMTFusedAdam(params, lr=1e-3)
     engine, *_ = eng.initialize(model=model, optimizer=opt,
-                                config={"gradient_clipping": 1.0, "wgrad_batch_tiles": batch_tiles})
+                                # single rounding: batched and per-module launches split T differently,
+                                # which fp32 sums absorb (1e-6) but a per-sample bf16 rounding may not
+                                config={"gradient_clipping": 1.0, "wgrad_batch_tiles": batch_tiles,
+                                        "wgrad_rounding": "single"})
 
     def fwd(x):
         for layer in model.layers:
