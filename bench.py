@@ -206,8 +206,15 @@ def spawn_ranks(n: int, argv) -> int:
     import subprocess
     cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
-    log("launching", n, "ranks:", " ".join(cmd))
-    proc = subprocess.Popen(cmd)
+    env = dict(os.environ)
+    n_dev = torch.cuda.device_count()       # counts devices without initialising one (this image)
+    if n > n_dev:
+        # ranks share a GPU (gloo rehearsals): one hardware queue per process. With the box's 4 per
+        # process, 4 processes on one card oversubscribe its hardware queues and a step stalls for
+        # 2-3 minutes (profiles/r04_b_dist4_*: GPU_MAX_HW_QUEUES=1 removes it, HSA_ENABLE_SDMA=0 does not)
+        env["GPU_MAX_HW_QUEUES"] = "1"
+    log("launching", n, "ranks:", " ".join(cmd), f"({n_dev} GPUs; GPU_MAX_HW_QUEUES={env.get('GPU_MAX_HW_QUEUES')})")
+    proc = subprocess.Popen(cmd, env=env)
 
     def forward(sig, _frame):
         if proc.poll() is None:
@@ -845,6 +852,10 @@ def main():
                          f"this node has {n_dev}")
     # one process per GPU; more ranks than GPUs (functional multi-rank runs on a 1-GPU box with gloo)
     # share devices round-robin
+    if world > n_dev and os.environ.get("GPU_MAX_HW_QUEUES") != "1":
+        log(f"warning: {world} ranks share {n_dev} GPU(s) with GPU_MAX_HW_QUEUES="
+            f"{os.environ.get('GPU_MAX_HW_QUEUES')}: hardware-queue oversubscription stalls steps (DESIGN §7); "
+            "bench.py --gpus N sets 1 when it starts the ranks itself")
     dev_index = local % max(1, n_dev)
     torch.cuda.set_device(dev_index)
     device = torch.device("cuda", dev_index)

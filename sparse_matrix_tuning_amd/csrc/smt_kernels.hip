@@ -100,14 +100,17 @@ __device__ __forceinline__ bf16x8_t tr_frag(const uint8_t* img, uint32_t k, uint
     return __builtin_bit_cast(bf16x8_t, both);
 }
 
-// Epilogue modes: partial slab (S > 1), or the final tile written directly (S == 1).
-enum WgradOut { kOutSlab = 0, kOutF32 = 1, kOutBF16 = 2 };
+// Epilogue modes: partial slab (S > 1), or the final tile written directly (S == 1). kOutSlabBF16:
+// the reference rounding's per-sample partial when one workgroup computes a whole sample (kps == 1):
+// rounded to bf16 in the epilogue, as smt.py:397-404 rounds it, so its slab takes half the bytes.
+enum WgradOut { kOutSlab = 0, kOutF32 = 1, kOutBF16 = 2, kOutSlabBF16 = 3 };
 
 // Where a workgroup's accumulators go: the fp32 partial slab (tile, s) of a split tile (S > 1), or
 // the final tile itself (S == 1; fp32 or bf16 per OUT).
 template <int OUT>
 __device__ __forceinline__ void* wgrad_dst(void* out_ptr, int tile, int s, int S) {
     if (OUT == kOutSlab) return static_cast<float*>(out_ptr) + (int64_t)(tile * S + s) * kTileElems;
+    if (OUT == kOutSlabBF16) return static_cast<uint16_t*>(out_ptr) + (int64_t)(tile * S + s) * kTileElems;
     if (OUT == kOutF32) return static_cast<float*>(out_ptr) + (int64_t)tile * kTileElems;
     return static_cast<uint16_t*>(out_ptr) + (int64_t)tile * kTileElems;
 }
@@ -130,6 +133,8 @@ __device__ __forceinline__ void wgrad_store(f32x16_t (&acc)[4][2], void* __restr
                 float v = acc[mb][nb][i];
                 if (OUT == kOutSlab) {
                     static_cast<float*>(dst)[m * kTile + n] = v;
+                } else if (OUT == kOutSlabBF16) {
+                    static_cast<uint16_t*>(dst)[m * kTile + n] = f32_to_bf16_bits(v);
                 } else if (OUT == kOutF32) {
                     float* out = static_cast<float*>(dst);
                     if (accumulate) v += out[m * kTile + n];
@@ -315,7 +320,8 @@ void wgrad_partial_kernel(const WgradModules mods, int64_t T, int64_t chunk, int
         __syncthreads();
     }
 
-    wgrad_store<OUT>(acc, OUT == kOutSlab ? wgrad_dst<kOutSlab>(slab, tile, s, S) : tt.out, wm, wn, lane, tt.accumulate);
+    wgrad_store<OUT>(acc, (OUT == kOutSlab || OUT == kOutSlabBF16) ? wgrad_dst<OUT>(slab, tile, s, S) : tt.out, wm, wn,
+                     lane, tt.accumulate);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -496,7 +502,8 @@ void wgrad_dma_kernel(const WgradModules mods, int64_t T, int64_t chunk, int S, 
         }
 #endif
     }
-    wgrad_store<OUT>(acc, OUT == kOutSlab ? wgrad_dst<kOutSlab>(slab, tile, s, S) : tt.out, wm, wn, lane, tt.accumulate);
+    wgrad_store<OUT>(acc, (OUT == kOutSlab || OUT == kOutSlabBF16) ? wgrad_dst<OUT>(slab, tile, s, S) : tt.out, wm, wn,
+                     lane, tt.accumulate);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -543,6 +550,8 @@ __device__ __forceinline__ void wgrad_store_q(f32x16_t (&acc)[2][2], void* __res
                 float v = acc[mb][nb][i];
                 if (OUT == kOutSlab) {
                     static_cast<float*>(dst)[m * kTile + n] = v;
+                } else if (OUT == kOutSlabBF16) {
+                    static_cast<uint16_t*>(dst)[m * kTile + n] = f32_to_bf16_bits(v);
                 } else if (OUT == kOutF32) {
                     float* out = static_cast<float*>(dst);
                     if (accumulate) v += out[m * kTile + n];
@@ -660,7 +669,7 @@ void wgrad_quarter_kernel(const WgradModules mods, int64_t T, int64_t chunk, int
                     acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mb], bfr[nb], acc[mb][nb], 0, 0, 0);
         }
     }
-    wgrad_store_q<OUT>(acc, OUT == kOutSlab ? wgrad_dst<kOutSlab>(slab, tile, s, S) : tt.out,
+    wgrad_store_q<OUT>(acc, (OUT == kOutSlab || OUT == kOutSlabBF16) ? wgrad_dst<OUT>(slab, tile, s, S) : tt.out,
                        qm * 128 + wm * 64, qn * 128 + wn * 64, lane, tt.accumulate);
 }
 
@@ -672,13 +681,25 @@ __device__ __forceinline__ float bf16_round(float v) { return bf16_bits_to_f32(f
 // the samples are summed in order in fp32 and the sum is rounded to bf16 once more (smt.py:397-404:
 // bf16 matmul per sample, then torch.sum(dim=0) of the bf16 partials, accumulated in fp32), before
 // the optional accumulation into the output (autograd's add into .grad).
-template <bool OUT_F32>
+template <bool OUT_F32, bool SLAB16 = false>
 __device__ __forceinline__ void wgrad_reduce_tile(const float* __restrict__ slab, int S, int kps, int tile,
                                                   void* __restrict__ tile_out, int accumulate) {
     const int e = (((blockIdx.x & 63) << 8) + threadIdx.x) * 4;
     const float* src = slab + (int64_t)tile * S * kTileElems + e;
     float4 sum;
-    if (kps <= 0) {
+    if (SLAB16) {
+        // kps == 1: every slab IS a sample's bf16-rounded partial (kOutSlabBF16); sum them in sample
+        // order in fp32 and round once more (the same arithmetic as the fp32-slab branch below)
+        const uint16_t* s16 = reinterpret_cast<const uint16_t*>(slab) + (int64_t)tile * S * kTileElems + e;
+        sum = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int s = 0; s < S; ++s) {
+            const uint2 v = *reinterpret_cast<const uint2*>(s16 + (int64_t)s * kTileElems);
+            sum.x += bf16_bits_to_f32(v.x & 0xffffu); sum.y += bf16_bits_to_f32(v.x >> 16);
+            sum.z += bf16_bits_to_f32(v.y & 0xffffu); sum.w += bf16_bits_to_f32(v.y >> 16);
+        }
+        sum.x = bf16_round(sum.x); sum.y = bf16_round(sum.y);
+        sum.z = bf16_round(sum.z); sum.w = bf16_round(sum.w);
+    } else if (kps <= 0) {
         sum = *reinterpret_cast<const float4*>(src);
         for (int s = 1; s < S; ++s) {
             const float4 v = *reinterpret_cast<const float4*>(src + (int64_t)s * kTileElems);
@@ -724,11 +745,11 @@ __device__ __forceinline__ void wgrad_reduce_tile(const float* __restrict__ slab
 }
 
 // 64 workgroups x 256 threads x 4 elements per tile; tile i's output = out + i tiles
-template <bool OUT_F32>
+template <bool OUT_F32, bool SLAB16 = false>
 __global__ __launch_bounds__(256)
 void wgrad_reduce_kernel(const float* __restrict__ slab, int S, int kps, void* __restrict__ out, int accumulate) {
     const int tile = blockIdx.x >> 6;
-    wgrad_reduce_tile<OUT_F32>(slab, S, kps, tile, static_cast<uint8_t*>(out) + (int64_t)tile * kTileElems * (OUT_F32 ? 4 : 2),
+    wgrad_reduce_tile<OUT_F32, SLAB16>(slab, S, kps, tile, static_cast<uint8_t*>(out) + (int64_t)tile * kTileElems * (OUT_F32 ? 4 : 2),
                                accumulate);
 }
 
@@ -746,13 +767,13 @@ void wgrad_reduce_mx_batch_kernel(const float* __restrict__ slab, int S, const W
 }
 
 // the same over a batch: each tile's output and accumulate flag from its module (wgrad_tile)
-template <bool OUT_F32>
+template <bool OUT_F32, bool SLAB16 = false>
 __global__ __launch_bounds__(256)
 void wgrad_reduce_batch_kernel(const float* __restrict__ slab, int S, int kps, const WgradModules mods,
                                const int32_t* __restrict__ tile_tab) {
     const int tile = blockIdx.x >> 6;
     const WgradTile tt = wgrad_tile<true, OUT_F32 ? 4 : 2>(mods, tile_tab, tile);
-    wgrad_reduce_tile<OUT_F32>(slab, S, kps, tile, tt.out, tt.accumulate);
+    wgrad_reduce_tile<OUT_F32, SLAB16>(slab, S, kps, tile, tt.out, tt.accumulate);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1022,7 +1043,8 @@ void wgrad_mx_kernel(const WgradMxModules mods, int64_t ldq, int64_t chunk, int 
                 acc[mb][nb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af[mb], bfr[nb], acc[mb][nb],
                                                                                0, 0, 0, as[mb], 0, bs[nb]);
     }
-    wgrad_store<OUT>(acc, OUT == kOutSlab ? wgrad_dst<kOutSlab>(slab, tile, s, S) : tt.out, wm, wn, lane, tt.accumulate);
+    wgrad_store<OUT>(acc, (OUT == kOutSlab || OUT == kOutSlabBF16) ? wgrad_dst<OUT>(slab, tile, s, S) : tt.out, wm, wn,
+                     lane, tt.accumulate);
 }
 
 // Quarter-tile MX variant for modules with few tiles (the fill-bound regime, as wgrad_quarter_kernel):
@@ -1147,7 +1169,7 @@ void wgrad_mx_quarter_kernel(const WgradMxModules mods, int64_t ldq, int64_t chu
                 acc[mb][nb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af[mb], bfr[nb], acc[mb][nb],
                                                                                0, 0, 0, as[mb], 0, bs[nb]);
     }
-    wgrad_store_q<OUT>(acc, OUT == kOutSlab ? wgrad_dst<kOutSlab>(slab, tile, s, S) : tt.out,
+    wgrad_store_q<OUT>(acc, (OUT == kOutSlab || OUT == kOutSlabBF16) ? wgrad_dst<OUT>(slab, tile, s, S) : tt.out,
                        qm * 128 + wm * 64, qn * 128 + wn * 64, lane, tt.accumulate);
 }
 
@@ -1907,6 +1929,10 @@ int wgrad_launch(const WgradModules& mods, int64_t T, int64_t max_ld, const int3
     static const int qslots = [] { const char* e = getenv("SMT_WGRAD_QSLOTS"); return (e && atoi(e) == 5) ? 5 : kQSlots; }();
     const bool dma = !force_reg && sp.chunk * max_ld * 2 < (int64_t)0x7fffffff;
     const bool quarter = dma && sp.quarter;
+    // reference rounding with one workgroup per sample piece (kps == 1): the LDS-DMA kernels round
+    // each sample's partial to bf16 themselves and write half-size slabs (SMT_WGRAD_SLAB16=0: fp32)
+    static const bool slab16_ok = [] { const char* e = getenv("SMT_WGRAD_SLAB16"); return !(e && atoi(e) == 0); }();
+    const bool slab16 = slab16_ok && dma && sp.seq > 0 && sp.kps == 1;
     float* slab = nullptr;
     if (use_slab) {
         const size_t need = (size_t)n_tiles * sp.S * kTileElems * sizeof(float);
@@ -1933,24 +1959,40 @@ int wgrad_launch(const WgradModules& mods, int64_t T, int64_t max_ld, const int3
         else SMT_WGRAD_LAUNCH(kOutBF16);
         return check_launch("wgrad kernel");
     }
-    SMT_WGRAD_LAUNCH(kOutSlab);
+    if (slab16) {
+        // the LDS-DMA kernels only (dma is true here)
+        if (quarter && qslots == 5) hipLaunchKernelGGL((wgrad_quarter_kernel<kOutSlabBF16, 5, BATCH>), qgrid, qblock, 0,
+                                                       stream, mods, T, sp.chunk, sp.S, sp.seq, sp.kps, n_tiles, tab,
+                                                       order, slab);
+        else if (quarter) hipLaunchKernelGGL((wgrad_quarter_kernel<kOutSlabBF16, kQSlots, BATCH>), qgrid, qblock, 0, stream,
+                                             mods, T, sp.chunk, sp.S, sp.seq, sp.kps, n_tiles, tab, order, slab);
+        else if (slots == 5) hipLaunchKernelGGL((wgrad_dma_kernel<kOutSlabBF16, 5, BATCH>), grid, block, 0, stream, mods, T,
+                                                sp.chunk, sp.S, sp.seq, sp.kps, n_tiles, tab, order, slab);
+        else hipLaunchKernelGGL((wgrad_dma_kernel<kOutSlabBF16, kDmaSlotsDefault, BATCH>), grid, block, 0, stream, mods, T,
+                                sp.chunk, sp.S, sp.seq, sp.kps, n_tiles, tab, order, slab);
+    } else {
+        SMT_WGRAD_LAUNCH(kOutSlab);
+    }
 #undef SMT_WGRAD_LAUNCH
     int rc = check_launch("wgrad kernel");
     if (rc) return rc;
     const dim3 rgrid(n_tiles * 64), rblock(256);
     const int kps = sp.seq > 0 ? sp.kps : 0;
-    if (BATCH) {
-        if (out_dtype == SMT_DTYPE_FP32)
-            hipLaunchKernelGGL(wgrad_reduce_batch_kernel<true>, rgrid, rblock, 0, stream, slab, sp.S, kps, mods, tab);
-        else
-            hipLaunchKernelGGL(wgrad_reduce_batch_kernel<false>, rgrid, rblock, 0, stream, slab, sp.S, kps, mods, tab);
+#define SMT_WGRAD_REDUCE(F32, S16)                                                                                 \
+    do {                                                                                                          \
+        if (BATCH) hipLaunchKernelGGL((wgrad_reduce_batch_kernel<F32, S16>), rgrid, rblock, 0, stream, slab, sp.S,  \
+                                      kps, mods, tab);                                                            \
+        else hipLaunchKernelGGL((wgrad_reduce_kernel<F32, S16>), rgrid, rblock, 0, stream, slab, sp.S, kps,          \
+                                mods.m[0].grad_tiles, mods.m[0].accumulate);                                      \
+    } while (0)
+    if (out_dtype == SMT_DTYPE_FP32) {
+        if (slab16) SMT_WGRAD_REDUCE(true, true);
+        else SMT_WGRAD_REDUCE(true, false);
     } else {
-        const smt_wgrad_module& m = mods.m[0];
-        if (out_dtype == SMT_DTYPE_FP32)
-            hipLaunchKernelGGL(wgrad_reduce_kernel<true>, rgrid, rblock, 0, stream, slab, sp.S, kps, m.grad_tiles, m.accumulate);
-        else
-            hipLaunchKernelGGL(wgrad_reduce_kernel<false>, rgrid, rblock, 0, stream, slab, sp.S, kps, m.grad_tiles, m.accumulate);
+        if (slab16) SMT_WGRAD_REDUCE(false, true);
+        else SMT_WGRAD_REDUCE(false, false);
     }
+#undef SMT_WGRAD_REDUCE
     return check_launch("wgrad_reduce_kernel");
 }
 

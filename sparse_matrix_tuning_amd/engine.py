@@ -366,13 +366,13 @@ class DPTrace:
             import time
             rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
             self.f = open(f"{prefix}.rank{rank}.jsonl", "a", buffering=1)
-            self._time, self._thread = time, threading
+            self._time, self._thread, self.rank = time, threading, rank
 
     def __call__(self, ev: str, **kw) -> None:
         if self.f is None:
             return
         import json
-        kw.update(ev=ev, t=round(self._time.time(), 6), cpu=round(self._time.process_time(), 4),
+        kw.update(ev=ev, rank=self.rank, t=round(self._time.time(), 6), cpu=round(self._time.process_time(), 4),
                   thread=self._thread.current_thread().name)
         self.f.write(json.dumps(kw) + "\n")
 

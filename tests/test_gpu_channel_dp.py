@@ -28,7 +28,7 @@ def test_channel_harvest_world2_matches_reference_rank_reduction(tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()),
            os.path.join(ROOT, "tests", "channel_dp_worker.py"), "--out", out]
-    r = subprocess.run(cmd, cwd=ROOT, env=dict(os.environ, PYTHONPATH=ROOT), capture_output=True, text=True,
+    r = subprocess.run(cmd, cwd=ROOT, env=dict(os.environ, PYTHONPATH=ROOT, GPU_MAX_HW_QUEUES="1"), capture_output=True, text=True,
                        timeout=400)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     res = torch.load(out, weights_only=True)

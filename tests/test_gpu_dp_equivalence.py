@@ -32,7 +32,8 @@ def _port():
 
 
 def _run(cmd, tmp):
-    env = dict(os.environ, PYTHONPATH=ROOT)
+    # ranks share cuda:0: one hardware queue per process (oversubscribed queues stall)
+    env = dict(os.environ, PYTHONPATH=ROOT, GPU_MAX_HW_QUEUES="1")
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
 

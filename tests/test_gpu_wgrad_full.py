@@ -16,6 +16,8 @@ bf16, then the batch sum): <= 1e-3 relative (north_star's bf16 tolerance), and
 (b) the default single-rounding mode: the direct difference printed and <= 1.5 x the reference's own
 error vs fp64 truth (the two differ by the reference's per-sample rounding, ~2.4e-3 at B = 16).
 """
+import os
+
 import pytest
 import torch
 
@@ -165,6 +167,26 @@ def test_reference_rounding_vs_restatement_at_bench_geometry(module, n):
               f"{d_rr:.2e}, default mode {d_single:.2e}; reference vs fp64 truth {ref_err:.2e}")
         assert d_rr <= 1e-3, (module, n, i, d_rr)
         assert d_single <= 1.5 * ref_err, (module, n, i, d_single, ref_err)
+
+
+def test_reference_rounding_bf16_slabs_bit_identical(tmp_path):
+    """With one workgroup per sample (kps == 1) the kernels round each sample's partial to bf16 in
+    their epilogue and write half-size slabs: bit-identical to rounding them in the reduce from fp32
+    slabs (SMT_WGRAD_SLAB16=0, a child process: the library reads the switch once)."""
+    import subprocess
+    import sys
+    from tests.wgrad_slab_worker import cases
+    mine = cases()
+    path = str(tmp_path / "fp32_slabs.pt")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tests", "wgrad_slab_worker.py"), path], cwd=root,
+                       env=dict(os.environ, SMT_WGRAD_SLAB16="0", PYTHONPATH=root), capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    theirs = torch.load(path, weights_only=True)
+    assert sorted(mine) == sorted(theirs)
+    for k in mine:
+        assert torch.equal(mine[k], theirs[k]), k
 
 
 def test_reference_rounding_rejects_partial_samples():
