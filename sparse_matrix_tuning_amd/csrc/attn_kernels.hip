@@ -2295,6 +2295,350 @@ void attn_dkdv_kernel(DkvArgs a) {
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// dK / dV, one wave per SIMD (runtime SMT_ATTN_DKV=2): the same 256-key block per workgroup, as 4
+// waves x 64 keys. Each wave holds dK^T and dV^T of its two 32-key blocks (4 x 64 fp32 accumulators:
+// 256 registers, MFMA-only, so they can live in the accumulation registers of the 512-register
+// file) and the K fragments of both blocks. Every Q / dO fragment read from LDS -- rows for S / dP,
+// transposed for dV / dK -- feeds the MFMAs of both key blocks, so a slice costs half the LDS-read
+// bytes per MFMA of DkvLean (whose 8 waves x 32 keys read every fragment once per 32 keys), and one
+// wave per SIMD has no partner wave to wait for at the barrier (MI355X_MICROARCH "Two waves per
+// SIMD"; cdna_hip_programming "Attention backward": 4 waves x 64 keys, 256 accumulator registers).
+// ------------------------------------------------------------------------------------------------
+constexpr int kDualKW = 64, kDualKWaves = kKB / kDualKW;
+#ifndef SMT_DKV_DUAL_ATTR
+#define SMT_DKV_DUAL_ATTR
+#endif
+// The 256 dK^T / dV^T accumulator registers are pinned to the accumulation registers (AGPRs) by
+// issuing their MFMAs from inline asm with "+a" operands: left to itself, hipcc put the S / dP chains
+// (64 registers, read by the softmax VALU) into AGPRs and spilled four accumulator tiles per slice.
+// The asm MFMAs are invisible to the compiler's hazard tracking, so each group starts with an s_nop
+// (VALU-written B operands), and the accumulators are read out only after a 24-wait-state pad.
+__device__ __forceinline__ void mfma4_agpr(f32x16_t& c0, f32x16_t& c1, f32x16_t& c2, f32x16_t& c3, bf16x8_t a01,
+                                           bf16x8_t b0, bf16x8_t b1, bf16x8_t a23, bf16x8_t b2, bf16x8_t b3) {
+    asm("s_nop 2\n\t"
+        "v_mfma_f32_32x32x16_bf16 %0, %4, %5, %0\n\t"
+        "v_mfma_f32_32x32x16_bf16 %1, %4, %6, %1\n\t"
+        "v_mfma_f32_32x32x16_bf16 %2, %7, %8, %2\n\t"
+        "v_mfma_f32_32x32x16_bf16 %3, %7, %9, %3"
+        : "+a"(c0), "+a"(c1), "+a"(c2), "+a"(c3)
+        : "v"(a01), "v"(b0), "v"(b1), "v"(a23), "v"(b2), "v"(b3));
+}
+// zero accumulators born in AGPRs (a zero-operand MFMA): a C++ zero would be materialised in VGPRs
+// for all 256 registers at once and copied over, spilling whatever else is live at that point
+__device__ __forceinline__ void zero_agpr(f32x16_t& c) {
+    const bf16x8_t z = __builtin_bit_cast(bf16x8_t, u32x4_t{0u, 0u, 0u, 0u});
+    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %1, 0" : "=a"(c) : "v"(z));
+}
+// S / dP (read by VALU) in arch VGPRs, the same way: C = 0 for the first k-step
+__device__ __forceinline__ void mfma4_vgpr0(f32x16_t& c0, f32x16_t& c1, f32x16_t& c2, f32x16_t& c3, bf16x8_t a01,
+                                            bf16x8_t b0, bf16x8_t b1, bf16x8_t a23, bf16x8_t b2, bf16x8_t b3) {
+    asm("v_mfma_f32_32x32x16_bf16 %0, %4, %5, 0\n\t"
+        "v_mfma_f32_32x32x16_bf16 %1, %4, %6, 0\n\t"
+        "v_mfma_f32_32x32x16_bf16 %2, %7, %8, 0\n\t"
+        "v_mfma_f32_32x32x16_bf16 %3, %7, %9, 0"
+        : "=&v"(c0), "=&v"(c1), "=&v"(c2), "=&v"(c3)
+        : "v"(a01), "v"(b0), "v"(b1), "v"(a23), "v"(b2), "v"(b3));
+}
+__device__ __forceinline__ void mfma4_vgpr(f32x16_t& c0, f32x16_t& c1, f32x16_t& c2, f32x16_t& c3, bf16x8_t a01,
+                                           bf16x8_t b0, bf16x8_t b1, bf16x8_t a23, bf16x8_t b2, bf16x8_t b3) {
+    asm("v_mfma_f32_32x32x16_bf16 %0, %4, %5, %0\n\t"
+        "v_mfma_f32_32x32x16_bf16 %1, %4, %6, %1\n\t"
+        "v_mfma_f32_32x32x16_bf16 %2, %7, %8, %2\n\t"
+        "v_mfma_f32_32x32x16_bf16 %3, %7, %9, %3"
+        : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3)
+        : "v"(a01), "v"(b0), "v"(b1), "v"(a23), "v"(b2), "v"(b3));
+}
+// 24 wait states between the last asm MFMA writing these registers and any other reader (the tie
+// keeps the pad between them)
+__device__ __forceinline__ void mfma_drain4(f32x16_t& c0, f32x16_t& c1, f32x16_t& c2, f32x16_t& c3) {
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3));
+}
+__device__ __forceinline__ void mfma_drain_agpr(f32x16_t (&d)[2][4], f32x16_t (&k)[2][4]) {
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7"
+                 : "+a"(d[0][0]), "+a"(d[0][1]), "+a"(d[0][2]), "+a"(d[0][3]), "+a"(d[1][0]), "+a"(d[1][1]),
+                   "+a"(d[1][2]), "+a"(d[1][3]), "+a"(k[0][0]), "+a"(k[0][1]), "+a"(k[0][2]), "+a"(k[0][3]),
+                   "+a"(k[1][0]), "+a"(k[1][1]), "+a"(k[1][2]), "+a"(k[1][3]));
+}
+// SMT_DKV_DUAL_FENCE: a scheduling fence after every k-step (1) or every second one (0)
+#ifndef SMT_DKV_DUAL_FENCE
+#define SMT_DKV_DUAL_FENCE 1
+#endif
+#ifndef SMT_DKV_DUAL_RING
+#define SMT_DKV_DUAL_RING 2
+#endif
+constexpr int kDkvDualRing = SMT_DKV_DUAL_RING;
+// LDS: the slice ring, the V image of the 256 keys, and the K rows of every wave's second key block
+// (its first block's K fragments stay in registers: 512 registers hold 256 accumulators + one block)
+constexpr int kKbImg = kDualKWaves * kKW * kRowB;        // 32 KiB
+static_assert(kDkvDualRing >= 2 && kDkvDualRing * kSliceBuf + kVImg + kKbImg <= 160 * 1024, "dK/dV dual ring");
+
+template <bool KMASK>
+struct DkvDual {
+    const DkvArgs& a;
+    uint8_t* lds;
+    bf16x8_t kf[8];                                        // K fragments of key block 0
+    f32x16_t dvt[2][4], dkt[2][4];
+    int G, lane, wave, hi, l32, k0, kw, n_sl, n_it, b, hk, per_slice;
+    int key[2];
+    bool kvalid[2];
+    uint32_t lds0;
+    uint32_t lo_row, lo_v0, lo_v1, lo_k1, lo_t0, lo_t4;
+
+    __device__ __forceinline__ DkvDual(const DkvArgs& a_, uint8_t* lds_) : a(a_), lds(lds_) {}
+
+    __device__ __forceinline__ void issue(int it) {            // Q and dO rows 8w .. 8w+7 of slice it
+        const int hh = it / n_sl, sl = n_sl - 1 - (it - hh * n_sl);
+        const int h = hk * G + hh;
+        const int s0 = k0 + sl * kSlice;
+        const uint32_t buf = lds0 + (uint32_t)((it % kDkvDualRing) * kSliceBuf);
+        const uint16_t* qb = a.q.p + b * a.q.sb + h * a.q.sh;
+        const uint16_t* db = a.dout.p + b * a.dout.sb + h * a.dout.sh;
+        dma_rows(uniform_rsrc(qb, (int64_t)a.S * a.q.ss * 2), a.q.ss, buf, s0, s0 + 8 * wave, 2, lane);
+        dma_rows(uniform_rsrc(db, (int64_t)a.S * a.dout.ss * 2), a.dout.ss, buf + (uint32_t)kSliceB, s0,
+                 s0 + 8 * wave, 2, lane);
+        if (wave < 2 && lane < 8) {
+            const float* row = (wave == 0 ? a.lse : a.delta) + ((int64_t)b * a.Hq + h) * a.S;
+            dma16(uniform_rsrc(row, (int64_t)a.S * 4), __builtin_amdgcn_readfirstlane(buf + 2 * kSliceB + 128 * wave),
+                  (s0 + 4 * lane) * 4);
+        }
+    }
+
+    // the slice's s0, or -1 when no q of the slice sees a key of the wave (both blocks skip it)
+    __device__ __forceinline__ int slice_s0(int it) const {
+        const int sl = n_sl - 1 - it % n_sl;               // descending q (see dkdv_block)
+        const int s0 = k0 + sl * kSlice;
+        return (s0 + kSlice - 1 < kw) ? -1 : s0;
+    }
+
+    // phase 1: S = Q K^T and dP = dO V^T of both key blocks; each Q / dO row fragment read once
+    template <int SLOT>
+    __device__ __forceinline__ void qk(f32x16_t (&s)[2], f32x16_t (&dp)[2]) {
+        constexpr int QI = SLOT * kSliceBuf, DI = QI + kSliceB;
+        const uint32_t lr = opaque(lo_row), lv0 = opaque(lo_v0), lv1 = opaque(lo_v1), lk1 = opaque(lo_k1);
+        // k-step ks's five fragments (Q row, dO row, K row of block 1, V rows of blocks 0 / 1) are read
+        // while k-step ks-1's four MFMAs run: one fence per k-step keeps that order
+        bf16x8_t f[2][5];
+        auto ld = [&](int ks, bf16x8_t (&g)[5]) {
+            g[0] = rowx<QI>(lds, lr, ks);
+            g[1] = rowx<DI>(lds, lr, ks);
+            g[2] = rowx<0>(lds, lk1, ks);
+            g[3] = rowx<0>(lds, lv0, ks);
+            g[4] = rowx<0>(lds, lv1, ks);
+        };
+        ld(0, f[0]);
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+            if (ks < 7) ld(ks + 1, f[(ks + 1) & 1]);
+            const bf16x8_t(&c)[5] = f[ks & 1];
+            if (ks == 0) mfma4_vgpr0(s[0], s[1], dp[0], dp[1], c[0], kf[ks], c[2], c[1], c[3], c[4]);
+            else mfma4_vgpr(s[0], s[1], dp[0], dp[1], c[0], kf[ks], c[2], c[1], c[3], c[4]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        mfma_drain4(s[0], s[1], dp[0], dp[1]);
+    }
+
+    // P and dS of key block j (rows q = s0 + (i&3) + 8(i>>2) + 4hi of register i), packed to the B
+    // fragments of the dV^T / dK^T products
+    __device__ __forceinline__ void probs(int j, int s0, const float* cst, const f32x16_t& s, const f32x16_t& dp,
+                                         bf16x8_t (&pf)[2], bf16x8_t (&sf)[2]) {
+        float pr[16], dsv[16];
+        const f32x2_t sl2v = {a.sl2, a.sl2};
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const float4 lz = *reinterpret_cast<const float4*>(cst + 8 * g + 4 * hi);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int i = 4 * g + 2 * h;
+                const f32x2_t l2 = h ? f32x2_t{lz.z, lz.w} : f32x2_t{lz.x, lz.y};
+                const f32x2_t e = __builtin_elementwise_fma(f32x2_t{s[i], s[i + 1]}, sl2v, -l2);
+                pr[i] = __builtin_amdgcn_exp2f(e.x);
+                pr[i + 1] = __builtin_amdgcn_exp2f(e.y);
+            }
+        }
+        const int kj = key[j];
+        if (s0 < kj - l32 + kKW - 1) {                     // the slice crosses this block's diagonal
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int q = s0 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+                if (kj > q) pr[i] = 0.f;
+            }
+        }
+        if (KMASK && !kvalid[j]) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) pr[i] = 0.f;
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const float4 dz = *reinterpret_cast<const float4*>(cst + 32 + 8 * g + 4 * hi);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int i = 4 * g + 2 * h;
+                const f32x2_t d2 = h ? f32x2_t{dz.z, dz.w} : f32x2_t{dz.x, dz.y};
+                const f32x2_t r = (f32x2_t{dp[i], dp[i + 1]} - d2) * f32x2_t{pr[i], pr[i + 1]};
+                dsv[i] = r.x;
+                dsv[i + 1] = r.y;
+            }
+        }
+        pack_b_frags(pr, pf[0], pf[1]);
+        pack_b_frags(dsv, sf[0], sf[1]);
+    }
+
+    // phase 2: dV^T += dO^T P and dK^T += Q^T dS of both blocks; each transposed fragment read once
+    template <int SLOT>
+    __device__ __forceinline__ void pv(int s0, const f32x16_t (&s)[2], const f32x16_t (&dp)[2]) {
+        constexpr int QI = SLOT * kSliceBuf, DI = QI + kSliceB;
+        const float* cst = reinterpret_cast<const float*>(lds + QI + 2 * kSliceB);
+        bf16x8_t pf[2][2], sf[2][2];
+        probs(0, s0, cst, s[0], dp[0], pf[0], sf[0]);
+        probs(1, s0, cst, s[1], dp[1], pf[1], sf[1]);
+        const uint32_t t0 = opaque(lo_t0), t4 = opaque(lo_t4);
+        // the transposed dO / Q fragments of step n+1 are read while step n's MFMAs run
+        bf16x8_t tf[2][2];
+        tf[0][0] = trx<DI>(lds, t0, t4, 0, 0);
+        tf[0][1] = trx<QI>(lds, t0, t4, 0, 0);
+#pragma unroll
+        for (int n = 0; n < 8; ++n) {
+            const int dt = n >> 1, kq = n & 1;
+            if (n < 7) {
+                tf[(n + 1) & 1][0] = trx<DI>(lds, t0, t4, (n + 1) & 1, (n + 1) >> 1);
+                tf[(n + 1) & 1][1] = trx<QI>(lds, t0, t4, (n + 1) & 1, (n + 1) >> 1);
+            }
+            mfma4_agpr(dvt[0][dt], dvt[1][dt], dkt[0][dt], dkt[1][dt], tf[n & 1][0], pf[0][kq], pf[1][kq], tf[n & 1][1],
+                       sf[0][kq], sf[1][kq]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+
+    template <int SLOT>
+    __device__ __forceinline__ void step(int it) {
+        constexpr int R = kDkvDualRing;
+        if (it + R - 1 < n_it) issue(it + R - 1);          // into the slot slice it-1 used
+        const int s0 = slice_s0(it);
+        if (s0 >= 0) {
+            f32x16_t s[2], dp[2];
+            qk<SLOT>(s, dp);
+            pv<SLOT>(s0, s, dp);
+        }
+        vm_wait_upto(per_slice * max(0, min(R - 2, n_it - 2 - it)));   // slice it+1 landed
+        __syncthreads();
+    }
+
+    template <int SLOT>
+    __device__ __forceinline__ void steps(int it0) {       // slices it0 .. it0+R-1, slot = compile-time
+        if (it0 + SLOT < n_it) {
+            step<SLOT>(it0 + SLOT);
+            if constexpr (SLOT + 1 < kDkvDualRing) steps<SLOT + 1>(it0);
+        }
+    }
+
+    __device__ __forceinline__ void run(int b_, int hk_, int kb) {
+        b = b_;
+        hk = hk_;
+        G = a.Hq / a.Hkv;
+        const int tid = threadIdx.x;
+        lane = tid & 63;
+        wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        hi = lane >> 5;
+        l32 = lane & 31;
+        k0 = kb * kKB;
+        kw = k0 + wave * kDualKW;
+        const uint16_t* kp = a.k.p + b * a.k.sb + hk * a.k.sh;
+        const uint16_t* vp = a.v.p + b * a.v.sb + hk * a.v.sh;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            key[j] = kw + kKW * j + l32;
+            kvalid[j] = !KMASK || (key[j] < a.S && key_bit(a.kmask[(int64_t)b * a.kmask_ld + (key[j] >> 6)], key[j]));
+        }
+        lds0 = lds_addr(lds);
+        // V rows of the wave's 64 keys into the image after the ring; K rows of its second key block
+        // into rows 32w .. 32w+31 of the K image after that
+        dma_rows(uniform_rsrc(vp, (int64_t)a.S * a.v.ss * 2), a.v.ss, lds0 + kDkvDualRing * kSliceBuf, k0, kw,
+                 kDualKW / 4, lane);
+        dma_rows(uniform_rsrc(kp, (int64_t)a.S * a.k.ss * 2), a.k.ss, lds0 + kDkvDualRing * kSliceBuf + kVImg,
+                 kw + kKW - kKW * wave, kw + kKW, kKW / 4, lane);
+        {
+            const uint32_t r = (uint32_t)l32;
+            lo_row = r * kRowB + ((16u * hi) ^ (swz(r) << 4));
+            // V rows wave*64 + 32j + l32 share row l32's swizzle (a multiple of 16 apart)
+            lo_v0 = lo_row + (uint32_t)(kDkvDualRing * kSliceBuf + wave * kDualKW * kRowB);
+            lo_v1 = lo_v0 + (uint32_t)(kKW * kRowB);
+            lo_k1 = lo_row + (uint32_t)(kDkvDualRing * kSliceBuf + kVImg + wave * kKW * kRowB);
+            const TrLane tl = tr_lane(lane);
+            lo_t0 = tl.krow * kRowB + (tl.feat_byte ^ (swz(tl.krow) << 4));
+            lo_t4 = (tl.krow + 4) * kRowB + (tl.feat_byte ^ (swz(tl.krow + 4) << 4));
+        }
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+            if (key[0] < a.S)
+                kf[ks] = *reinterpret_cast<const bf16x8_t*>(kp + (int64_t)key[0] * a.k.ss + 16 * ks + 8 * hi);
+            else
+                kf[ks] = __builtin_bit_cast(bf16x8_t, u32x4_t{0u, 0u, 0u, 0u});
+        }
+        n_sl = (a.S - k0 + kSlice - 1) / kSlice;
+        n_it = G * n_sl;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) {
+                zero_agpr(dvt[j][dt]);
+                zero_agpr(dkt[j][dt]);
+            }
+        per_slice = 4 + (wave < 2 ? 1 : 0);                // DMA instructions per slice (+ lse / delta)
+#pragma unroll
+        for (int i = 0; i < kDkvDualRing - 1; ++i)
+            if (i < n_it) issue(i);
+        vm_wait_all();
+        vm_wait_all_known();                               // the K fragments too (compiler-visible)
+        __syncthreads();
+        for (int it = 0; it < n_it; it += kDkvDualRing) steps<0>(it);
+        mfma_drain_agpr(dvt, dkt);                         // the asm MFMAs' results, before any read
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            if (key[j] < a.S) {
+                uint16_t* dkr = a.dk + b * a.dk_sb + hk * a.dk_sh + (int64_t)key[j] * a.dk_ss;
+                uint16_t* dvr = a.dv + b * a.dv_sb + hk * a.dv_sh + (int64_t)key[j] * a.dv_ss;
+#pragma unroll
+                for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const int d = 32 * dt + 8 * g + 4 * hi;
+                        uint2 w;
+                        w.x = pk_bf16(dkt[j][dt][4 * g] * a.scale, dkt[j][dt][4 * g + 1] * a.scale);
+                        w.y = pk_bf16(dkt[j][dt][4 * g + 2] * a.scale, dkt[j][dt][4 * g + 3] * a.scale);
+                        *reinterpret_cast<uint2*>(dkr + d) = w;
+                        w.x = pk_bf16(dvt[j][dt][4 * g], dvt[j][dt][4 * g + 1]);
+                        w.y = pk_bf16(dvt[j][dt][4 * g + 2], dvt[j][dt][4 * g + 3]);
+                        *reinterpret_cast<uint2*>(dvr + d) = w;
+                    }
+            }
+        }
+    }
+};
+
+template <bool KMASK>
+__global__ __launch_bounds__(kDualKWaves * 64, 1) SMT_DKV_DUAL_ATTR
+void attn_dkdv_dual_kernel(DkvArgs a) {
+    static_assert(kKB == 256 && kDualKWaves == 4, "dual dK/dV: 256-key blocks of 4 waves");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kDkvDualRing * kSliceBuf + kVImg + kKbImg];
+    const int nkb = (a.S + kKB - 1) / kKB;
+    const int total = ((nkb + 1) / 2) * a.Hkv * a.B;
+    const PairTask t = pair_task(xcd_logical(blockIdx.x, total), nkb, 1, a.Hkv);
+#pragma nounroll
+    for (int i = 0; i < t.n; ++i) {
+        if (i) __syncthreads();
+        DkvDual<KMASK> d(a, lds);
+        d.run(t.b, t.hk, t.blk[1 - i]);
+    }
+}
+
+// SMT_ATTN_DKV (runtime): 1 = attn_dkdv_kernel (DkvLean, 8 waves x 32 keys, default), 2 = the
+// one-wave-per-SIMD attn_dkdv_dual_kernel
+int dkv_impl() {
+    static const int v = [] { const char* e = getenv("SMT_ATTN_DKV"); return (e && atoi(e) == 2) ? 2 : 1; }();
+    return v;
+}
+
 inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 int check_tensor(const smt_attn_tensor* t, const char* what, const char* fn) {
@@ -2420,6 +2764,11 @@ int smt_attn_bwd_kmask(const smt_attn_tensor* q, const smt_attn_tensor* k, const
     ka.B = B; ka.Hq = Hq; ka.Hkv = Hkv; ka.S = S; ka.sl2 = sl2; ka.scale = shape->scale;
     const int64_t nkb = (S + kKB - 1) / kKB;
     const dim3 grid((unsigned)(((nkb + 1) / 2) * Hkv * B));
+    if (dkv_impl() == 2) {
+        if (key_mask) hipLaunchKernelGGL(attn_dkdv_dual_kernel<true>, grid, dim3(kDualKWaves * 64), 0, stream, ka);
+        else hipLaunchKernelGGL(attn_dkdv_dual_kernel<false>, grid, dim3(kDualKWaves * 64), 0, stream, ka);
+        return check_launch("attn_dkdv_dual_kernel");
+    }
     if (key_mask) hipLaunchKernelGGL(attn_dkdv_kernel<true>, grid, dim3(kDkvWaves * 64), 0, stream, ka);
     else hipLaunchKernelGGL(attn_dkdv_kernel<false>, grid, dim3(kDkvWaves * 64), 0, stream, ka);
     return check_launch("attn_dkdv_kernel");
