@@ -2349,6 +2349,29 @@ __device__ __forceinline__ void mfma4_vgpr(f32x16_t& c0, f32x16_t& c1, f32x16_t&
         : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3)
         : "v"(a01), "v"(b0), "v"(b1), "v"(a23), "v"(b2), "v"(b3));
 }
+// two-MFMA groups of the interleaved dual loop (one MFMA gap pair per softmax chunk)
+__device__ __forceinline__ void mfma2_vgpr0(f32x16_t& c0, f32x16_t& c1, bf16x8_t a0, bf16x8_t b0, bf16x8_t a1,
+                                            bf16x8_t b1) {
+    asm("v_mfma_f32_32x32x16_bf16 %0, %2, %3, 0\n\t"
+        "v_mfma_f32_32x32x16_bf16 %1, %4, %5, 0"
+        : "=&v"(c0), "=&v"(c1) : "v"(a0), "v"(b0), "v"(a1), "v"(b1));
+}
+__device__ __forceinline__ void mfma2_vgpr(f32x16_t& c0, f32x16_t& c1, bf16x8_t a0, bf16x8_t b0, bf16x8_t a1,
+                                           bf16x8_t b1) {
+    asm("v_mfma_f32_32x32x16_bf16 %0, %2, %3, %0\n\t"
+        "v_mfma_f32_32x32x16_bf16 %1, %4, %5, %1"
+        : "+v"(c0), "+v"(c1) : "v"(a0), "v"(b0), "v"(a1), "v"(b1));
+}
+__device__ __forceinline__ void mfma2_agpr(f32x16_t& c0, f32x16_t& c1, bf16x8_t a0, bf16x8_t b0, bf16x8_t a1,
+                                           bf16x8_t b1) {
+    asm("s_nop 2\n\t"
+        "v_mfma_f32_32x32x16_bf16 %0, %2, %3, %0\n\t"
+        "v_mfma_f32_32x32x16_bf16 %1, %4, %5, %1"
+        : "+a"(c0), "+a"(c1) : "v"(a0), "v"(b0), "v"(a1), "v"(b1));
+}
+__device__ __forceinline__ void mfma_drain2(f32x16_t& c0, f32x16_t& c1) {
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+v"(c0), "+v"(c1));
+}
 // 24 wait states between the last asm MFMA writing these registers and any other reader (the tie
 // keeps the pad between them)
 __device__ __forceinline__ void mfma_drain4(f32x16_t& c0, f32x16_t& c1, f32x16_t& c2, f32x16_t& c3) {
@@ -2373,7 +2396,12 @@ constexpr int kDkvDualRing = SMT_DKV_DUAL_RING;
 constexpr int kKbImg = kDualKWaves * kKW * kRowB;        // 32 KiB
 static_assert(kDkvDualRing >= 2 && kDkvDualRing * kSliceBuf + kVImg + kKbImg <= 160 * 1024, "dK/dV dual ring");
 
-template <bool KMASK>
+// V (SMT_ATTN_DKV 2 / 3): 2 = both key blocks' S / dP, then both softmaxes, then the dV / dK products
+// sharing every fragment read; 3 = the softmax of one block placed in the MFMA gaps of the other's
+// products (S1/dP1 beside softmax 0, dV0/dK0 beside softmax 1): one wave per SIMD has no partner wave
+// to hide the softmax behind, so the block pairs overlap inside the wave, at the price of reading the
+// Q / dO fragments once per block (1.4 instead of 0.9 KiB of LDS reads per MFMA)
+template <bool KMASK, int V = 2>
 struct DkvDual {
     const DkvArgs& a;
     uint8_t* lds;
@@ -2510,12 +2538,166 @@ struct DkvDual {
         }
     }
 
+    // one eighth of key block j's softmax (chunk c, compile-time): c 0-3: p of registers 4c..4c+3 (with
+    // the causal mask when DIAG); c 4-7: ds of registers 4(c-4)..; c 5 / 7 also pack P / dS
+    template <bool DIAG, int C>
+    __device__ __forceinline__ void soft_chunk(int j, int s0, const float4 (&lz)[4], const float4 (&dz)[4],
+                                               f32x16_t& s, f32x16_t& dp, bf16x8_t (&pf)[2], bf16x8_t (&sf)[2]) {
+        if constexpr (C < 4) {
+            const f32x2_t sl2v = {a.sl2, a.sl2};
+            const float4 l = lz[C];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int i = 4 * C + 2 * h;
+                const f32x2_t l2 = h ? f32x2_t{l.z, l.w} : f32x2_t{l.x, l.y};
+                const f32x2_t e = __builtin_elementwise_fma(f32x2_t{s[i], s[i + 1]}, sl2v, -l2);
+                float p0 = __builtin_amdgcn_exp2f(e.x), p1 = __builtin_amdgcn_exp2f(e.y);
+                if (DIAG) {
+                    const int q = s0 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+                    p0 = key[j] > q ? 0.f : p0;
+                    p1 = key[j] > q + 1 ? 0.f : p1;
+                }
+                if (KMASK) {
+                    p0 = kvalid[j] ? p0 : 0.f;
+                    p1 = kvalid[j] ? p1 : 0.f;
+                }
+                s[i] = p0;                                 // P replaces S in place
+                s[i + 1] = p1;
+            }
+        } else {
+            const float4 d = dz[C - 4];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int i = 4 * (C - 4) + 2 * h;
+                const f32x2_t d2 = h ? f32x2_t{d.z, d.w} : f32x2_t{d.x, d.y};
+                const f32x2_t r = (f32x2_t{dp[i], dp[i + 1]} - d2) * f32x2_t{s[i], s[i + 1]};
+                dp[i] = r.x;                               // dS replaces dP in place
+                dp[i + 1] = r.y;
+            }
+            if constexpr (C == 5) {
+                float pr[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) pr[i] = s[i];
+                pack_b_frags(pr, pf[0], pf[1]);
+            }
+            if constexpr (C == 7) {
+                float dsv[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) dsv[i] = dp[i];
+                pack_b_frags(dsv, sf[0], sf[1]);
+            }
+        }
+    }
+
+    template <bool DIAG, int C>
+    __device__ __forceinline__ void soft_chunks_from(int j, int s0, const float4 (&lz)[4], const float4 (&dz)[4],
+                                                     f32x16_t& s, f32x16_t& dp, bf16x8_t (&pf)[2], bf16x8_t (&sf)[2],
+                                                     int c) {
+        // (dispatch on the unrolled loop index)
+        if (c == C) soft_chunk<DIAG, C>(j, s0, lz, dz, s, dp, pf, sf);
+        if constexpr (C + 1 < 8) soft_chunks_from<DIAG, C + 1>(j, s0, lz, dz, s, dp, pf, sf, c);
+    }
+
+    // V = 3: S0/dP0; S1/dP1 || softmax 0; dV0/dK0 || softmax 1; dV1/dK1 (2 MFMAs per group)
+    template <int SLOT, bool DIAG>
+    __device__ __forceinline__ void slice3(int s0) {
+        constexpr int QI = SLOT * kSliceBuf, DI = QI + kSliceB;
+        const uint32_t lr = opaque(lo_row), lv0 = opaque(lo_v0), lv1 = opaque(lo_v1), lk1 = opaque(lo_k1);
+        const float* cst = reinterpret_cast<const float*>(lds + QI + 2 * kSliceB);
+        float4 lz[4], dz[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            lz[g] = *reinterpret_cast<const float4*>(cst + 8 * g + 4 * hi);
+            dz[g] = *reinterpret_cast<const float4*>(cst + 32 + 8 * g + 4 * hi);
+        }
+        f32x16_t s[2], dp[2];
+        bf16x8_t pf[2][2], sf[2][2];
+        // S0, dP0 (Q / dO rows, K0 in registers, V0 rows)
+        {
+            bf16x8_t f[2][3];
+            auto ld = [&](int ks, bf16x8_t (&g)[3]) {
+                g[0] = rowx<QI>(lds, lr, ks);
+                g[1] = rowx<DI>(lds, lr, ks);
+                g[2] = rowx<0>(lds, lv0, ks);
+            };
+            ld(0, f[0]);
+#pragma unroll
+            for (int ks = 0; ks < 8; ++ks) {
+                if (ks < 7) ld(ks + 1, f[(ks + 1) & 1]);
+                const bf16x8_t(&c)[3] = f[ks & 1];
+                if (ks == 0) mfma2_vgpr0(s[0], dp[0], c[0], kf[ks], c[1], c[2]);
+                else mfma2_vgpr(s[0], dp[0], c[0], kf[ks], c[1], c[2]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        // S1, dP1 (Q / dO rows again, K1 / V1 rows), softmax 0 in the gaps
+        {
+            bf16x8_t f[2][4];
+            auto ld = [&](int ks, bf16x8_t (&g)[4]) {
+                g[0] = rowx<QI>(lds, lr, ks);
+                g[1] = rowx<DI>(lds, lr, ks);
+                g[2] = rowx<0>(lds, lk1, ks);
+                g[3] = rowx<0>(lds, lv1, ks);
+            };
+            ld(0, f[0]);
+#pragma unroll
+            for (int ks = 0; ks < 8; ++ks) {
+                if (ks < 7) ld(ks + 1, f[(ks + 1) & 1]);
+                const bf16x8_t(&c)[4] = f[ks & 1];
+                if (ks == 0) mfma2_vgpr0(s[1], dp[1], c[0], c[2], c[1], c[3]);
+                else mfma2_vgpr(s[1], dp[1], c[0], c[2], c[1], c[3]);
+                if (ks == 0) mfma_drain2(s[0], dp[0]);     // S0 / dP0 final before the softmax reads them
+                soft_chunks_from<DIAG, 0>(0, s0, lz, dz, s[0], dp[0], pf[0], sf[0], ks);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        const uint32_t t0 = opaque(lo_t0), t4 = opaque(lo_t4);
+        // dV0, dK0 (transposed dO / Q), softmax 1 in the gaps
+        {
+            bf16x8_t tf[2][2];
+            tf[0][0] = trx<DI>(lds, t0, t4, 0, 0);
+            tf[0][1] = trx<QI>(lds, t0, t4, 0, 0);
+#pragma unroll
+            for (int n = 0; n < 8; ++n) {
+                const int dt = n >> 1, kq = n & 1;
+                if (n < 7) {
+                    tf[(n + 1) & 1][0] = trx<DI>(lds, t0, t4, (n + 1) & 1, (n + 1) >> 1);
+                    tf[(n + 1) & 1][1] = trx<QI>(lds, t0, t4, (n + 1) & 1, (n + 1) >> 1);
+                }
+                mfma2_agpr(dvt[0][dt], dkt[0][dt], tf[n & 1][0], pf[0][kq], tf[n & 1][1], sf[0][kq]);
+                if (n == 0) mfma_drain2(s[1], dp[1]);
+                soft_chunks_from<DIAG, 0>(1, s0, lz, dz, s[1], dp[1], pf[1], sf[1], n);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        // dV1, dK1 (the transposed fragments read again)
+        {
+            bf16x8_t tf[2][2];
+            tf[0][0] = trx<DI>(lds, t0, t4, 0, 0);
+            tf[0][1] = trx<QI>(lds, t0, t4, 0, 0);
+#pragma unroll
+            for (int n = 0; n < 8; ++n) {
+                const int dt = n >> 1, kq = n & 1;
+                if (n < 7) {
+                    tf[(n + 1) & 1][0] = trx<DI>(lds, t0, t4, (n + 1) & 1, (n + 1) >> 1);
+                    tf[(n + 1) & 1][1] = trx<QI>(lds, t0, t4, (n + 1) & 1, (n + 1) >> 1);
+                }
+                mfma2_agpr(dvt[1][dt], dkt[1][dt], tf[n & 1][0], pf[1][kq], tf[n & 1][1], sf[1][kq]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+    }
+
     template <int SLOT>
     __device__ __forceinline__ void step(int it) {
         constexpr int R = kDkvDualRing;
         if (it + R - 1 < n_it) issue(it + R - 1);          // into the slot slice it-1 used
         const int s0 = slice_s0(it);
-        if (s0 >= 0) {
+        if (V == 3 && s0 >= 0) {
+            // wave-uniform: the slice reaches below the diagonal of the wave's second block
+            if (s0 < kw + 2 * kKW - 1) slice3<SLOT, true>(s0);
+            else slice3<SLOT, false>(s0);
+        } else if (s0 >= 0) {
             f32x16_t s[2], dp[2];
             qk<SLOT>(s, dp);
             pv<SLOT>(s0, s, dp);
@@ -2616,7 +2798,7 @@ struct DkvDual {
     }
 };
 
-template <bool KMASK>
+template <bool KMASK, int V>
 __global__ __launch_bounds__(kDualKWaves * 64, 1) SMT_DKV_DUAL_ATTR
 void attn_dkdv_dual_kernel(DkvArgs a) {
     static_assert(kKB == 256 && kDualKWaves == 4, "dual dK/dV: 256-key blocks of 4 waves");
@@ -2627,15 +2809,19 @@ void attn_dkdv_dual_kernel(DkvArgs a) {
 #pragma nounroll
     for (int i = 0; i < t.n; ++i) {
         if (i) __syncthreads();
-        DkvDual<KMASK> d(a, lds);
+        DkvDual<KMASK, V> d(a, lds);
         d.run(t.b, t.hk, t.blk[1 - i]);
     }
 }
 
-// SMT_ATTN_DKV (runtime): 1 = attn_dkdv_kernel (DkvLean, 8 waves x 32 keys, default), 2 = the
-// one-wave-per-SIMD attn_dkdv_dual_kernel
+// SMT_ATTN_DKV (runtime): 1 = attn_dkdv_kernel (DkvLean, 8 waves x 32 keys, default), 2 / 3 = the
+// one-wave-per-SIMD attn_dkdv_dual_kernel (DkvDual V = 2 / 3)
 int dkv_impl() {
-    static const int v = [] { const char* e = getenv("SMT_ATTN_DKV"); return (e && atoi(e) == 2) ? 2 : 1; }();
+    static const int v = [] {
+        const char* e = getenv("SMT_ATTN_DKV");
+        const int x = e ? atoi(e) : 1;
+        return (x == 2 || x == 3) ? x : 1;
+    }();
     return v;
 }
 
@@ -2765,8 +2951,13 @@ int smt_attn_bwd_kmask(const smt_attn_tensor* q, const smt_attn_tensor* k, const
     const int64_t nkb = (S + kKB - 1) / kKB;
     const dim3 grid((unsigned)(((nkb + 1) / 2) * Hkv * B));
     if (dkv_impl() == 2) {
-        if (key_mask) hipLaunchKernelGGL(attn_dkdv_dual_kernel<true>, grid, dim3(kDualKWaves * 64), 0, stream, ka);
-        else hipLaunchKernelGGL(attn_dkdv_dual_kernel<false>, grid, dim3(kDualKWaves * 64), 0, stream, ka);
+        if (key_mask) hipLaunchKernelGGL((attn_dkdv_dual_kernel<true, 2>), grid, dim3(kDualKWaves * 64), 0, stream, ka);
+        else hipLaunchKernelGGL((attn_dkdv_dual_kernel<false, 2>), grid, dim3(kDualKWaves * 64), 0, stream, ka);
+        return check_launch("attn_dkdv_dual_kernel");
+    }
+    if (dkv_impl() == 3) {
+        if (key_mask) hipLaunchKernelGGL((attn_dkdv_dual_kernel<true, 3>), grid, dim3(kDualKWaves * 64), 0, stream, ka);
+        else hipLaunchKernelGGL((attn_dkdv_dual_kernel<false, 3>), grid, dim3(kDualKWaves * 64), 0, stream, ka);
         return check_launch("attn_dkdv_dual_kernel");
     }
     if (key_mask) hipLaunchKernelGGL(attn_dkdv_kernel<true>, grid, dim3(kDkvWaves * 64), 0, stream, ka);
