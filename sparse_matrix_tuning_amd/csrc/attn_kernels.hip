@@ -2296,19 +2296,8 @@ void attn_dkdv_kernel(DkvArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// dK / dV, one wave per SIMD (runtime SMT_ATTN_DKV=2): the same 256-key block per workgroup, as 4
-// waves x 64 keys. Each wave holds dK^T and dV^T of its two 32-key blocks (4 x 64 fp32 accumulators:
-// 256 registers, MFMA-only, so they can live in the accumulation registers of the 512-register
-// file) and the K fragments of both blocks. Every Q / dO fragment read from LDS -- rows for S / dP,
-// transposed for dV / dK -- feeds the MFMAs of both key blocks, so a slice costs half the LDS-read
-// bytes per MFMA of DkvLean (whose 8 waves x 32 keys read every fragment once per 32 keys), and one
-// wave per SIMD has no partner wave to wait for at the barrier (MI355X_MICROARCH "Two waves per
-// SIMD"; cdna_hip_programming "Attention backward": 4 waves x 64 keys, 256 accumulator registers).
+// asm MFMA helpers of the one-wave-per-SIMD kernels (DqDual, DkvDual)
 // ------------------------------------------------------------------------------------------------
-constexpr int kDualKW = 64, kDualKWaves = kKB / kDualKW;
-#ifndef SMT_DKV_DUAL_ATTR
-#define SMT_DKV_DUAL_ATTR
-#endif
 // The 256 dK^T / dV^T accumulator registers are pinned to the accumulation registers (AGPRs) by
 // issuing their MFMAs from inline asm with "+a" operands: left to itself, hipcc put the S / dP chains
 // (64 registers, read by the softmax VALU) into AGPRs and spilled four accumulator tiles per slice.
@@ -2383,6 +2372,313 @@ __device__ __forceinline__ void mfma_drain_agpr(f32x16_t (&d)[2][4], f32x16_t (&
                    "+a"(d[1][2]), "+a"(d[1][3]), "+a"(k[0][0]), "+a"(k[0][1]), "+a"(k[0][2]), "+a"(k[0][3]),
                    "+a"(k[1][0]), "+a"(k[1][1]), "+a"(k[1][2]), "+a"(k[1][3]));
 }
+
+// ------------------------------------------------------------------------------------------------
+// dQ, one wave per SIMD (runtime SMT_ATTN_DQ=2): a workgroup = 4 waves x 64 query rows (two 32-row
+// blocks per wave) of one (b, q head); 64-key K / V tiles through the same LDS-DMA ring as DqLean.
+// Per wave the Q and dO fragments of both blocks (128 registers) and the dQ^T accumulators of both
+// (128) sit in the 256 AGPRs (the asm MFMAs read them from there); every K / V fragment read from LDS
+// feeds both blocks (0.5 KiB of reads per MFMA instead of 1). Each tile is two halves of 32 keys, and
+// one half's softmax runs in the MFMA gaps of the next product: S/dP(h0); S/dP(h1) || softmax(h0);
+// dQ(h0) || softmax(h1); dQ(h1).
+// ------------------------------------------------------------------------------------------------
+constexpr int kDqDualQB = 256;
+
+// S^T / dP^T of both query blocks for one key k-step: A = the K / V row fragment (VGPRs), B = the
+// blocks' Q / dO fragments (AGPRs); accumulators in VGPRs (read by the softmax). FIRST: C = 0.
+template <bool FIRST>
+__device__ __forceinline__ void mfma4_qd(f32x16_t& sA, f32x16_t& sB, f32x16_t& dA, f32x16_t& dB, bf16x8_t kr,
+                                         bf16x8_t vr, bf16x8_t qa, bf16x8_t qb, bf16x8_t da, bf16x8_t db) {
+    if (FIRST)
+        asm("s_nop 4\n\t"
+            "v_mfma_f32_32x32x16_bf16 %0, %4, %6, 0\n\t"
+            "v_mfma_f32_32x32x16_bf16 %1, %4, %7, 0\n\t"
+            "v_mfma_f32_32x32x16_bf16 %2, %5, %8, 0\n\t"
+            "v_mfma_f32_32x32x16_bf16 %3, %5, %9, 0"
+            : "=&v"(sA), "=&v"(sB), "=&v"(dA), "=&v"(dB)
+            : "v"(kr), "v"(vr), "a"(qa), "a"(qb), "a"(da), "a"(db));
+    else
+        asm("v_mfma_f32_32x32x16_bf16 %0, %4, %6, %0\n\t"
+            "v_mfma_f32_32x32x16_bf16 %1, %4, %7, %1\n\t"
+            "v_mfma_f32_32x32x16_bf16 %2, %5, %8, %2\n\t"
+            "v_mfma_f32_32x32x16_bf16 %3, %5, %9, %3"
+            : "+v"(sA), "+v"(sB), "+v"(dA), "+v"(dB)
+            : "v"(kr), "v"(vr), "a"(qa), "a"(qb), "a"(da), "a"(db));
+}
+
+template <bool KMASK>
+struct DqDual {
+    const DqArgs& a;
+    uint8_t* lds;
+    bf16x8_t qf[2][8], df[2][8];
+    f32x16_t dq[2][4];
+    float lse[2], dlt[2];
+    int qlim[2];                                           // causal limit of the tile: qrow, or INT_MAX off the diagonal
+    const uint64_t* km;
+    __amdgpu_buffer_rsrc_t rk, rv;
+    uint32_t lds0, lo_row, lo_t0, lo_t4;
+    int lane, wave, hi, l32, qw, qrow[2], nt, last;
+
+    __device__ __forceinline__ DqDual(const DqArgs& a_, uint8_t* lds_) : a(a_), lds(lds_) {}
+
+    __device__ __forceinline__ void issue(int t) {            // K(t), V(t) into slot t & 1: 16 rows per wave
+        const uint32_t slot = lds0 + (uint32_t)((t & 1) * 2 * kTileB);
+        dma_rows(rk, a.k.ss, slot, t * kKV, t * kKV + 16 * wave, 4, lane);
+        dma_rows(rv, a.v.ss, slot + kTileB, t * kKV, t * kKV + 16 * wave, 4, lane);
+    }
+
+    // one eighth of the softmax of both query blocks over one 32-key half (chunk C, compile-time):
+    // C 0-3 the probabilities of registers 4C..4C+3 (in place of S), C 4-7 dS (in place of dP), C 7 packs
+    template <bool DIAG, int C>
+    __device__ __forceinline__ void soft_chunk(int k0h, f32x16_t (&s)[2], f32x16_t (&dp)[2], bf16x8_t (&sf)[2][2]) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            if constexpr (C < 4) {
+                const f32x2_t sl2v = {a.sl2, a.sl2}, lv = {-lse[j], -lse[j]};
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int i = 4 * C + 2 * h;
+                    const f32x2_t e = __builtin_elementwise_fma(f32x2_t{s[j][i], s[j][i + 1]}, sl2v, lv);
+                    float p0 = __builtin_amdgcn_exp2f(e.x), p1 = __builtin_amdgcn_exp2f(e.y);
+                    const int key = k0h + (i & 3) + 8 * (i >> 2) + 4 * hi;
+                    // branch-free causal mask (qlim = INT_MAX off the diagonal): one code path for every
+                    // tile, so the accumulators never take a second register assignment
+                    p0 = key > qlim[j] ? 0.f : p0;
+                    p1 = key + 1 > qlim[j] ? 0.f : p1;
+                    if (KMASK) {
+                        const uint64_t w = km[key >> 6];
+                        p0 = key_bit(w, key) ? p0 : 0.f;
+                        p1 = key_bit(w, key + 1) ? p1 : 0.f;
+                    }
+                    s[j][i] = p0;
+                    s[j][i + 1] = p1;
+                }
+            } else {
+                const f32x2_t dv = {dlt[j], dlt[j]};
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int i = 4 * (C - 4) + 2 * h;
+                    const f32x2_t r = (f32x2_t{dp[j][i], dp[j][i + 1]} - dv) * f32x2_t{s[j][i], s[j][i + 1]};
+                    dp[j][i] = r.x;
+                    dp[j][i + 1] = r.y;
+                }
+                if constexpr (C == 7) {
+                    float ds[16];
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) ds[i] = dp[j][i];
+                    pack_b_frags(ds, sf[j][0], sf[j][1]);
+                }
+            }
+        }
+    }
+    template <bool DIAG, int C>
+    __device__ __forceinline__ void soft_chunks_from(int c, int k0h, f32x16_t (&s)[2], f32x16_t (&dp)[2],
+                                                     bf16x8_t (&sf)[2][2]) {
+        if (c == C) soft_chunk<DIAG, C>(k0h, s, dp, sf);
+        if constexpr (C + 1 < 8) soft_chunks_from<DIAG, C + 1>(c, k0h, s, dp, sf);
+    }
+
+    // S^T, dP^T of key half H into s / dp; with SOFT, the other half's softmax chunk per k-step
+    template <int SLOT, int H, bool SOFT, bool DIAG>
+    __device__ __forceinline__ void qk(f32x16_t (&s)[2], f32x16_t (&dp)[2], int k0o, f32x16_t (&so)[2],
+                                       f32x16_t (&dpo)[2], bf16x8_t (&sfo)[2][2]) {
+        constexpr int KI = SLOT * 2 * kTileB + H * 32 * kRowB, VI = KI + kTileB;
+        const uint32_t lr = opaque(lo_row);
+        bf16x8_t f[2][2];
+        f[0][0] = rowx<KI>(lds, lr, 0);
+        f[0][1] = rowx<VI>(lds, lr, 0);
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+            if (ks < 7) {
+                f[(ks + 1) & 1][0] = rowx<KI>(lds, lr, ks + 1);
+                f[(ks + 1) & 1][1] = rowx<VI>(lds, lr, ks + 1);
+            }
+            if (ks == 0) mfma4_qd<true>(s[0], s[1], dp[0], dp[1], f[0][0], f[0][1], qf[0][0], qf[1][0], df[0][0], df[1][0]);
+            else mfma4_qd<false>(s[0], s[1], dp[0], dp[1], f[ks & 1][0], f[ks & 1][1], qf[0][ks], qf[1][ks], df[0][ks],
+                                 df[1][ks]);
+            if (SOFT) {
+                if (ks == 0) { mfma_drain2(so[0], so[1]); mfma_drain2(dpo[0], dpo[1]); }
+                soft_chunks_from<DIAG, 0>(ks, k0o, so, dpo, sfo);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+
+    // dQ^T += K^T dS^T over key half H; with SOFT, the other half's softmax chunk per step
+    template <int SLOT, int H, bool SOFT, bool DIAG>
+    __device__ __forceinline__ void dqp(const bf16x8_t (&sf)[2][2], int k0o, f32x16_t (&so)[2], f32x16_t (&dpo)[2],
+                                        bf16x8_t (&sfo)[2][2]) {
+        constexpr int KI = SLOT * 2 * kTileB;
+        const uint32_t t0 = opaque(lo_t0), t4 = opaque(lo_t4);
+        bf16x8_t tf[2];
+        tf[0] = trx<KI>(lds, t0, t4, 2 * H, 0);
+#pragma unroll
+        for (int n = 0; n < 8; ++n) {
+            const int dt = n >> 1, kst = n & 1;
+            if (n < 7) tf[(n + 1) & 1] = trx<KI>(lds, t0, t4, 2 * H + ((n + 1) & 1), (n + 1) >> 1);
+            mfma2_agpr(dq[0][dt], dq[1][dt], tf[n & 1], sf[0][kst], tf[n & 1], sf[1][kst]);
+            if (SOFT) {
+                if (n == 0) { mfma_drain2(so[0], so[1]); mfma_drain2(dpo[0], dpo[1]); }
+                soft_chunks_from<DIAG, 0>(n, k0o, so, dpo, sfo);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+
+    template <int SLOT, bool DIAG>
+    __device__ __forceinline__ void compute(int t) {
+        const int k0 = t * kKV;
+        f32x16_t s0[2], dp0[2], s1[2], dp1[2];
+        bf16x8_t sf0[2][2], sf1[2][2];
+        qk<SLOT, 0, false, DIAG>(s0, dp0, 0, s1, dp1, sf1);              // (no softmax beside it)
+        qk<SLOT, 1, true, DIAG>(s1, dp1, k0, s0, dp0, sf0);              // || softmax of half 0
+        dqp<SLOT, 0, true, DIAG>(sf0, k0 + 32, s1, dp1, sf1);            // || softmax of half 1
+        dqp<SLOT, 1, false, DIAG>(sf1, 0, s1, dp1, sf1);
+    }
+
+    template <int SLOT>
+    __device__ __forceinline__ void tile(int t) {
+        if (t + 1 < nt) issue(t + 1);
+        if (t <= last) {
+            qlim[0] = t == last ? qrow[0] : 0x7fffffff;
+            qlim[1] = t == last ? qrow[1] : 0x7fffffff;
+            compute<SLOT, false>(t);
+        }
+        vm_wait_all();
+        __syncthreads();
+    }
+
+    __device__ __forceinline__ void run(int b, int h, int hk, int qb) {
+        const int tid = threadIdx.x;
+        lane = tid & 63;
+        wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        hi = lane >> 5;
+        l32 = lane & 31;
+        const int q0 = qb * kDqDualQB;
+        qw = q0 + wave * 64;
+        const uint16_t* qp = a.q.p + b * a.q.sb + h * a.q.sh;
+        const uint16_t* dop = a.dout.p + b * a.dout.sb + h * a.dout.sh;
+        const uint16_t* op = a.o.p + b * a.o.sb + h * a.o.sh;
+        const uint16_t* kp = a.k.p + b * a.k.sb + hk * a.k.sh;
+        const uint16_t* vp = a.v.p + b * a.v.sb + hk * a.v.sh;
+        km = KMASK ? a.kmask + (int64_t)b * a.kmask_ld : nullptr;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            qrow[j] = qw + 32 * j + l32;
+            const bool qvalid = qrow[j] < a.S;
+            // Q / dO fragments straight into AGPRs (a load the compiler would otherwise keep in VGPRs and
+            // copy into AGPRs every tile). Rows past S read row S-1: their S^T / dS^T columns only reach
+            // their own dQ^T column, which is never stored.
+            const int64_t rr = qvalid ? qrow[j] : a.S - 1;
+#pragma unroll
+            for (int ks = 0; ks < 8; ++ks) {
+                const uint16_t* qa = qp + rr * a.q.ss + 16 * ks + 8 * hi;
+                const uint16_t* da = dop + rr * a.dout.ss + 16 * ks + 8 * hi;
+                asm volatile("global_load_dwordx4 %0, %1, off" : "=a"(qf[j][ks]) : "v"(qa) : "memory");
+                asm volatile("global_load_dwordx4 %0, %1, off" : "=a"(df[j][ks]) : "v"(da) : "memory");
+            }
+            float part = 0.f;
+#pragma unroll
+            for (int ks = 0; ks < 8; ++ks) {
+                // delta = rowsum(dO * O) of this row (SMT_DQ_DELTA, as DqLean), from a second (VGPR) read of dO
+                const u32x4_t ov = qvalid ? *reinterpret_cast<const u32x4_t*>(op + qrow[j] * a.o.ss + 16 * ks + 8 * hi)
+                                          : u32x4_t{0u, 0u, 0u, 0u};
+                const u32x4_t dv = qvalid ? *reinterpret_cast<const u32x4_t*>(dop + qrow[j] * a.dout.ss + 16 * ks + 8 * hi)
+                                          : u32x4_t{0u, 0u, 0u, 0u};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    part += __uint_as_float(ov[e] << 16) * __uint_as_float(dv[e] << 16);
+                    part += __uint_as_float(ov[e] & 0xffff0000u) * __uint_as_float(dv[e] & 0xffff0000u);
+                }
+            }
+            const int64_t srow = ((int64_t)b * a.Hq + h) * a.S + (qvalid ? qrow[j] : 0);
+            lse[j] = qvalid ? a.lse[srow] : 0.f;
+            dlt[j] = halves_sum(part);
+            if (qvalid && hi == 0) a.delta[srow] = dlt[j];
+        }
+        const int kv_end = min(a.S, q0 + kDqDualQB);
+        nt = (kv_end + kKV - 1) / kKV;
+        last = min(nt - 1, qw / kKV);                      // both blocks' diagonal: tile qw / 64
+        rk = uniform_rsrc(kp, (int64_t)a.S * a.k.ss * 2);
+        rv = uniform_rsrc(vp, (int64_t)a.S * a.v.ss * 2);
+        lds0 = lds_addr(lds);
+        {
+            const uint32_t r = (uint32_t)l32;
+            lo_row = r * kRowB + ((16u * hi) ^ (swz(r) << 4));
+            const TrLane tl = tr_lane(lane);
+            lo_t0 = tl.krow * kRowB + (tl.feat_byte ^ (swz(tl.krow) << 4));
+            lo_t4 = (tl.krow + 4) * kRowB + (tl.feat_byte ^ (swz(tl.krow + 4) << 4));
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) zero_agpr(dq[j][dt]);
+        if (nt > 0) issue(0);
+        vm_wait_all();
+        vm_wait_all_known();
+        __syncthreads();
+        for (int t = 0; t < nt; t += 2) {
+            tile<0>(t);
+            if (t + 1 < nt) tile<1>(t + 1);
+        }
+        f32x16_t (&dqa)[2][4] = dq;
+        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7"
+                     : "+a"(dqa[0][0]), "+a"(dqa[0][1]), "+a"(dqa[0][2]), "+a"(dqa[0][3]), "+a"(dqa[1][0]),
+                       "+a"(dqa[1][1]), "+a"(dqa[1][2]), "+a"(dqa[1][3]));
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            if (qrow[j] < a.S) {
+                uint16_t* out = a.dq + b * a.dq_sb + h * a.dq_sh + (int64_t)qrow[j] * a.dq_ss;
+#pragma unroll
+                for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const int d = 32 * dt + 8 * g + 4 * hi;
+                        uint2 w;
+                        w.x = pk_bf16(dq[j][dt][4 * g] * a.scale, dq[j][dt][4 * g + 1] * a.scale);
+                        w.y = pk_bf16(dq[j][dt][4 * g + 2] * a.scale, dq[j][dt][4 * g + 3] * a.scale);
+                        *reinterpret_cast<uint2*>(out + d) = w;
+                    }
+            }
+        }
+    }
+};
+
+template <bool KMASK>
+__global__ __launch_bounds__(256, 1)
+void attn_dq_dual_kernel(DqArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * 2 * kTileB];      // 64 KiB
+    const int nqb = (a.S + kDqDualQB - 1) / kDqDualQB;
+    const int G = a.Hq / a.Hkv;
+    const int total = nqb * a.Hq * a.B;
+    const int L = xcd_logical(blockIdx.x, total);
+    const int per_group = G * nqb;
+    const int grp = L / per_group;
+    const int rem = L - grp * per_group;
+    const int hk = grp % a.Hkv;
+    DqDual<KMASK> d(a, lds);
+    d.run(grp / a.Hkv, hk * G + rem % G, hk, nqb - 1 - rem / G);
+}
+
+int dq_impl() {
+    static const int v = [] { const char* e = getenv("SMT_ATTN_DQ"); return (e && atoi(e) == 2) ? 2 : 1; }();
+    return v;
+}
+
+// ------------------------------------------------------------------------------------------------
+// dK / dV, one wave per SIMD (runtime SMT_ATTN_DKV=2): the same 256-key block per workgroup, as 4
+// waves x 64 keys. Each wave holds dK^T and dV^T of its two 32-key blocks (4 x 64 fp32 accumulators:
+// 256 registers, MFMA-only, so they can live in the accumulation registers of the 512-register
+// file) and the K fragments of both blocks. Every Q / dO fragment read from LDS -- rows for S / dP,
+// transposed for dV / dK -- feeds the MFMAs of both key blocks, so a slice costs half the LDS-read
+// bytes per MFMA of DkvLean (whose 8 waves x 32 keys read every fragment once per 32 keys), and one
+// wave per SIMD has no partner wave to wait for at the barrier (MI355X_MICROARCH "Two waves per
+// SIMD"; cdna_hip_programming "Attention backward": 4 waves x 64 keys, 256 accumulator registers).
+// ------------------------------------------------------------------------------------------------
+constexpr int kDualKW = 64, kDualKWaves = kKB / kDualKW;
+#ifndef SMT_DKV_DUAL_ATTR
+#define SMT_DKV_DUAL_ATTR
+#endif
 // SMT_DKV_DUAL_FENCE: a scheduling fence after every k-step (1) or every second one (0)
 #ifndef SMT_DKV_DUAL_FENCE
 #define SMT_DKV_DUAL_FENCE 1
@@ -2935,11 +3231,19 @@ int smt_attn_bwd_kmask(const smt_attn_tensor* q, const smt_attn_tensor* k, const
     qa.lse = lse; qa.delta = delta_ws;
     qa.kmask = key_mask; qa.kmask_ld = key_mask_ld;
     qa.B = B; qa.Hq = Hq; qa.Hkv = Hkv; qa.S = S; qa.sl2 = sl2; qa.scale = shape->scale;
-    const int64_t nqb = (S + kDqQB - 1) / kDqQB;
-    const dim3 qgrid((unsigned)(nqb * Hq * B)), qblock(64 * kDqWaves);
-    if (key_mask) hipLaunchKernelGGL(attn_dq_kernel<true>, qgrid, qblock, 0, stream, qa);
-    else hipLaunchKernelGGL(attn_dq_kernel<false>, qgrid, qblock, 0, stream, qa);
-    if ((rc = check_launch("attn_dq_kernel"))) return rc;
+    if (dq_impl() == 2 && SMT_DQ_DELTA) {
+        const int64_t nqb2 = (S + kDqDualQB - 1) / kDqDualQB;
+        const dim3 g2((unsigned)(nqb2 * Hq * B)), b2(256);
+        if (key_mask) hipLaunchKernelGGL(attn_dq_dual_kernel<true>, g2, b2, 0, stream, qa);
+        else hipLaunchKernelGGL(attn_dq_dual_kernel<false>, g2, b2, 0, stream, qa);
+        if ((rc = check_launch("attn_dq_dual_kernel"))) return rc;
+    } else {
+        const int64_t nqb = (S + kDqQB - 1) / kDqQB;
+        const dim3 qgrid((unsigned)(nqb * Hq * B)), qblock(64 * kDqWaves);
+        if (key_mask) hipLaunchKernelGGL(attn_dq_kernel<true>, qgrid, qblock, 0, stream, qa);
+        else hipLaunchKernelGGL(attn_dq_kernel<false>, qgrid, qblock, 0, stream, qa);
+        if ((rc = check_launch("attn_dq_kernel"))) return rc;
+    }
 
     DkvArgs ka;
     ka.q = tns(q); ka.k = tns(k); ka.v = tns(v); ka.dout = tns(d_o);
