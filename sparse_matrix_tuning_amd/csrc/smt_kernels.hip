@@ -115,36 +115,71 @@ __device__ __forceinline__ void* wgrad_dst(void* out_ptr, int tile, int s, int S
     return static_cast<uint16_t*>(out_ptr) + (int64_t)tile * kTileElems;
 }
 
-// Epilogue: C/D map of 32x32x16 (col = lane&31, row = (i&3) + 8*(i>>2) + 4*(lane>>5)) into the
-// 256x256 destination `dst` (wgrad_dst): an fp32 slab, or the fp32 / bf16 output tile.
-template <int OUT>
-__device__ __forceinline__ void wgrad_store(f32x16_t (&acc)[4][2], void* __restrict__ dst,
-                                            int wm, int wn, int lane, int accumulate) {
-    const int col = lane & 31;
+// Epilogue of the wgrad kernels. They issue their MFMAs as x-slice x g-slice, so each accumulator
+// holds C^T: acc[mb][nb][i] = C[m][n] with m = wm0 + mb*32 + (lane&31), n = wn0 + nb*32 +
+// 8*(i>>2) + 4*(lane>>5) + (i&3), (wm0, wn0) = the wave's origin in the tile. Each lane then holds
+// runs of 4 consecutive columns of one row, so the stores are 16-B (fp32) or 8-B (bf16) vectors
+// instead of 16 scalar stores per accumulator -- the store tail is issue-bound (cdna_hip_programming
+// T21). For the bf16 slab the two half-waves' 4-column runs are paired by v_permlane32_swap into
+// 8-column rows: one 16-B store per lane per pair of runs.
+template <int OUT, int MB>
+__device__ __forceinline__ void wgrad_store_t(f32x16_t (&acc)[MB][2], void* __restrict__ dst,
+                                              int wm0, int wn0, int lane, int accumulate) {
+    const int r = lane & 31;
     const int h = lane >> 5;
 #pragma unroll
-    for (int mb = 0; mb < 4; ++mb)
+    for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
-        for (int nb = 0; nb < 2; ++nb)
+        for (int nb = 0; nb < 2; ++nb) {
+            const int m = wm0 + mb * 32 + r;
+            const int n0 = wn0 + nb * 32;
+            const f32x16_t& a = acc[mb][nb];
+            if (OUT == kOutSlabBF16) {
+                uint16_t* row = static_cast<uint16_t*>(dst) + m * kTile + n0;
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int m = wm * 128 + mb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-                const int n = wn * 64 + nb * 32 + col;
-                float v = acc[mb][nb][i];
-                if (OUT == kOutSlab) {
-                    static_cast<float*>(dst)[m * kTile + n] = v;
-                } else if (OUT == kOutSlabBF16) {
-                    static_cast<uint16_t*>(dst)[m * kTile + n] = f32_to_bf16_bits(v);
-                } else if (OUT == kOutF32) {
-                    float* out = static_cast<float*>(dst);
-                    if (accumulate) v += out[m * kTile + n];
-                    out[m * kTile + n] = v;
-                } else {
-                    uint16_t* out = static_cast<uint16_t*>(dst);
-                    if (accumulate) v += bf16_bits_to_f32(out[m * kTile + n]);
-                    out[m * kTile + n] = f32_to_bf16_bits(v);
+                for (int g = 0; g < 4; g += 2) {
+                    uint32_t lo0 = f32_to_bf16_bits(a[4 * g]) | ((uint32_t)f32_to_bf16_bits(a[4 * g + 1]) << 16);
+                    uint32_t lo1 = f32_to_bf16_bits(a[4 * g + 2]) | ((uint32_t)f32_to_bf16_bits(a[4 * g + 3]) << 16);
+                    uint32_t hi0 = f32_to_bf16_bits(a[4 * g + 4]) | ((uint32_t)f32_to_bf16_bits(a[4 * g + 5]) << 16);
+                    uint32_t hi1 = f32_to_bf16_bits(a[4 * g + 6]) | ((uint32_t)f32_to_bf16_bits(a[4 * g + 7]) << 16);
+                    // vdst = run g, src = run g+1: lanes 0-31 end with columns 8g..8g+7 of their row,
+                    // lanes 32-63 with columns 8(g+1)..8(g+1)+7
+                    const auto s0 = __builtin_amdgcn_permlane32_swap(lo0, hi0, false, false);
+                    const auto s1 = __builtin_amdgcn_permlane32_swap(lo1, hi1, false, false);
+                    uint4 w;
+                    w.x = s0[0]; w.y = s1[0]; w.z = s0[1]; w.w = s1[1];
+                    *reinterpret_cast<uint4*>(row + 8 * (g + h)) = w;
+                }
+            } else if (OUT == kOutSlab || OUT == kOutF32) {
+                float* row = static_cast<float*>(dst) + m * kTile + n0;
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    float4* p = reinterpret_cast<float4*>(row + 8 * g + 4 * h);
+                    float4 v = make_float4(a[4 * g], a[4 * g + 1], a[4 * g + 2], a[4 * g + 3]);
+                    if (OUT == kOutF32 && accumulate) {
+                        const float4 o = *p;
+                        v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+                    }
+                    *p = v;
+                }
+            } else {
+                uint16_t* row = static_cast<uint16_t*>(dst) + m * kTile + n0;
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    uint2* p = reinterpret_cast<uint2*>(row + 8 * g + 4 * h);
+                    float v0 = a[4 * g], v1 = a[4 * g + 1], v2 = a[4 * g + 2], v3 = a[4 * g + 3];
+                    if (accumulate) {
+                        const uint2 o = *p;
+                        v0 += bf16_bits_to_f32(o.x & 0xffffu); v1 += bf16_bits_to_f32(o.x >> 16);
+                        v2 += bf16_bits_to_f32(o.y & 0xffffu); v3 += bf16_bits_to_f32(o.y >> 16);
+                    }
+                    uint2 w;
+                    w.x = f32_to_bf16_bits(v0) | ((uint32_t)f32_to_bf16_bits(v1) << 16);
+                    w.y = f32_to_bf16_bits(v2) | ((uint32_t)f32_to_bf16_bits(v3) << 16);
+                    *p = w;
                 }
             }
+        }
 }
 
 // One tile of a wgrad launch: its operand column slices and its output. A launch covers the tiles
@@ -314,14 +349,14 @@ void wgrad_partial_kernel(const WgradModules mods, int64_t T, int64_t chunk, int
             for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
                 for (int nb = 0; nb < 2; ++nb)
-                    acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mb], bfr[nb], acc[mb][nb], 0, 0, 0);
+                    acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[nb], af[mb], acc[mb][nb], 0, 0, 0);
         }
         if (st + 1 < nst) swrite(buf ^ 1);
         __syncthreads();
     }
 
-    wgrad_store<OUT>(acc, (OUT == kOutSlab || OUT == kOutSlabBF16) ? wgrad_dst<OUT>(slab, tile, s, S) : tt.out, wm, wn,
-                     lane, tt.accumulate);
+    wgrad_store_t<OUT, 4>(acc, (OUT == kOutSlab || OUT == kOutSlabBF16) ? wgrad_dst<OUT>(slab, tile, s, S) : tt.out,
+                          wm * 128, wn * 64, lane, tt.accumulate);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -494,16 +529,18 @@ void wgrad_dma_kernel(const WgradModules mods, int64_t T, int64_t chunk, int S, 
 #pragma unroll
             for (int nb = 0; nb < 2; ++nb)
                 bfr[nb] = tr_frag(B, ks * 16 + krow, 2u * (wn * 64 + nb * 32) + feat_byte);
+            // x slice as A, g slice as B: the accumulators hold C^T, whose per-lane runs of 4
+            // consecutive columns give wgrad_store_t its vector stores
 #pragma unroll
             for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
                 for (int nb = 0; nb < 2; ++nb)
-                    acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mb], bfr[nb], acc[mb][nb], 0, 0, 0);
+                    acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[nb], af[mb], acc[mb][nb], 0, 0, 0);
         }
 #endif
     }
-    wgrad_store<OUT>(acc, (OUT == kOutSlab || OUT == kOutSlabBF16) ? wgrad_dst<OUT>(slab, tile, s, S) : tt.out, wm, wn,
-                     lane, tt.accumulate);
+    wgrad_store_t<OUT, 4>(acc, (OUT == kOutSlab || OUT == kOutSlabBF16) ? wgrad_dst<OUT>(slab, tile, s, S) : tt.out,
+                          wm * 128, wn * 64, lane, tt.accumulate);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -532,36 +569,6 @@ __device__ __forceinline__ bf16x8_t qtr_frag(const uint8_t* img, uint32_t k, uin
     s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(img + qimg_off(k + 4, byte_in_row)));
     const s16x8_t both = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
     return __builtin_bit_cast(bf16x8_t, both);
-}
-
-template <int OUT>
-__device__ __forceinline__ void wgrad_store_q(f32x16_t (&acc)[2][2], void* __restrict__ dst,
-                                              int m0, int n0, int lane, int accumulate) {
-    const int col = lane & 31;
-    const int h = lane >> 5;
-#pragma unroll
-    for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int m = m0 + mb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-                const int n = n0 + nb * 32 + col;
-                float v = acc[mb][nb][i];
-                if (OUT == kOutSlab) {
-                    static_cast<float*>(dst)[m * kTile + n] = v;
-                } else if (OUT == kOutSlabBF16) {
-                    static_cast<uint16_t*>(dst)[m * kTile + n] = f32_to_bf16_bits(v);
-                } else if (OUT == kOutF32) {
-                    float* out = static_cast<float*>(dst);
-                    if (accumulate) v += out[m * kTile + n];
-                    out[m * kTile + n] = v;
-                } else {
-                    uint16_t* out = static_cast<uint16_t*>(dst);
-                    if (accumulate) v += bf16_bits_to_f32(out[m * kTile + n]);
-                    out[m * kTile + n] = f32_to_bf16_bits(v);
-                }
-            }
 }
 
 template <int OUT, int QS, bool BATCH>
@@ -666,11 +673,11 @@ void wgrad_quarter_kernel(const WgradModules mods, int64_t T, int64_t chunk, int
             for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
                 for (int nb = 0; nb < 2; ++nb)
-                    acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mb], bfr[nb], acc[mb][nb], 0, 0, 0);
+                    acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[nb], af[mb], acc[mb][nb], 0, 0, 0);
         }
     }
-    wgrad_store_q<OUT>(acc, (OUT == kOutSlab || OUT == kOutSlabBF16) ? wgrad_dst<OUT>(slab, tile, s, S) : tt.out,
-                       qm * 128 + wm * 64, qn * 128 + wn * 64, lane, tt.accumulate);
+    wgrad_store_t<OUT, 2>(acc, (OUT == kOutSlab || OUT == kOutSlabBF16) ? wgrad_dst<OUT>(slab, tile, s, S) : tt.out,
+                          qm * 128 + wm * 64, qn * 128 + wn * 64, lane, tt.accumulate);
 }
 
 __device__ __forceinline__ float bf16_round(float v) { return bf16_bits_to_f32(f32_to_bf16_bits(v)); }
@@ -1040,11 +1047,11 @@ void wgrad_mx_kernel(const WgradMxModules mods, int64_t ldq, int64_t chunk, int 
         for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
             for (int nb = 0; nb < 2; ++nb)
-                acc[mb][nb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af[mb], bfr[nb], acc[mb][nb],
-                                                                               0, 0, 0, as[mb], 0, bs[nb]);
+                acc[mb][nb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(bfr[nb], af[mb], acc[mb][nb],
+                                                                               0, 0, 0, bs[nb], 0, as[mb]);
     }
-    wgrad_store<OUT>(acc, (OUT == kOutSlab || OUT == kOutSlabBF16) ? wgrad_dst<OUT>(slab, tile, s, S) : tt.out, wm, wn,
-                     lane, tt.accumulate);
+    wgrad_store_t<OUT, 4>(acc, (OUT == kOutSlab || OUT == kOutSlabBF16) ? wgrad_dst<OUT>(slab, tile, s, S) : tt.out,
+                          wm * 128, wn * 64, lane, tt.accumulate);
 }
 
 // Quarter-tile MX variant for modules with few tiles (the fill-bound regime, as wgrad_quarter_kernel):
@@ -1166,11 +1173,11 @@ void wgrad_mx_quarter_kernel(const WgradMxModules mods, int64_t ldq, int64_t chu
         for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
             for (int nb = 0; nb < 2; ++nb)
-                acc[mb][nb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af[mb], bfr[nb], acc[mb][nb],
-                                                                               0, 0, 0, as[mb], 0, bs[nb]);
+                acc[mb][nb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(bfr[nb], af[mb], acc[mb][nb],
+                                                                               0, 0, 0, bs[nb], 0, as[mb]);
     }
-    wgrad_store_q<OUT>(acc, (OUT == kOutSlab || OUT == kOutSlabBF16) ? wgrad_dst<OUT>(slab, tile, s, S) : tt.out,
-                       qm * 128 + wm * 64, qn * 128 + wn * 64, lane, tt.accumulate);
+    wgrad_store_t<OUT, 2>(acc, (OUT == kOutSlab || OUT == kOutSlabBF16) ? wgrad_dst<OUT>(slab, tile, s, S) : tt.out,
+                          qm * 128 + wm * 64, qn * 128 + wn * 64, lane, tt.accumulate);
 }
 
 // ------------------------------------------------------------------------------------------------
