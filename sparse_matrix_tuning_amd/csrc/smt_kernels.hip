@@ -1620,6 +1620,62 @@ void column_gather_kernel(const uint16_t* __restrict__ x, int64_t ld_x, int64_t 
     }
 }
 
+// The same gather with the rows staged by LDS-DMA (buffer_load ... lds): a row is ppr 1 KiB pieces
+// (one wave instruction each; the last may run past n_in into the row's padding or the next row,
+// bytes the gather never indexes; past the last row's n_in elements the descriptor returns zeros). All R * ppr
+// pieces of a workgroup are in flight at once without passing through registers (the round-3
+// attempt to issue a thread's loads ahead in registers ran 1.65x slower). Each thread then loads
+// its 8 output indices once and gathers them from every staged row.
+template <int R>
+__global__ __launch_bounds__(256)
+void column_gather_dma_kernel(const uint16_t* __restrict__ x, int64_t ld_x, int64_t n_in, int64_t T, int ppr,
+                              const int32_t* __restrict__ cols, int32_t n_cols, uint16_t* __restrict__ out,
+                              int64_t ld_out) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t cg_lds[];          // [R][ppr * 1 KiB]
+    const int64_t t0 = (int64_t)blockIdx.x * R;
+    const int rows = (int)(T - t0 < R ? T - t0 : R);
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // the descriptor ends at the last row's n_in-th element: a piece running past it reads zeros,
+    // never memory past a column-slice view's allocation
+    const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(x + t0 * ld_x, (int64_t)(rows - 1) * ld_x * 2 + n_in * 2);
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(cg_lds));
+    const int row_stride = ppr * 1024;
+    for (int p = wave; p < rows * ppr; p += 4) {
+        const int r = p / ppr, c = p - r * ppr;
+        dma16(rs, __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)(r * row_stride + c * 1024)),
+              (int)(r * ld_x * 2 + c * 1024 + lane * 16));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int64_t vec_per_row = ld_out >> 3;
+    for (int64_t v = tid; v < vec_per_row; v += 256) {
+        const int j0 = (int)(v * 8);
+        int idx[8];
+        if (j0 + 8 <= n_cols) {
+            const int4 a = *reinterpret_cast<const int4*>(cols + j0);
+            const int4 b = *reinterpret_cast<const int4*>(cols + j0 + 4);
+            idx[0] = a.x; idx[1] = a.y; idx[2] = a.z; idx[3] = a.w;
+            idx[4] = b.x; idx[5] = b.y; idx[6] = b.z; idx[7] = b.w;
+        } else {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) idx[q] = j0 + q < n_cols ? cols[j0 + q] : -1;
+        }
+        for (int r = 0; r < rows; ++r) {
+            const uint16_t* br = reinterpret_cast<const uint16_t*>(cg_lds + r * row_stride);
+            uint32_t w[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t lo = idx[2 * q] >= 0 ? br[idx[2 * q]] : 0u;
+                const uint32_t hi = idx[2 * q + 1] >= 0 ? br[idx[2 * q + 1]] : 0u;
+                w[q] = lo | (hi << 16);
+            }
+            *reinterpret_cast<uint4*>(out + (t0 + r) * ld_out + j0) = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+    }
+}
+
 // Transposed tile scatter: Wt[c*256 + j, r*256 + k] = tile[k, j] for every descriptor (weight = the
 // transposed copy Wt = W^T of a frozen W, ld_weight its row stride, (row_block, col_block) = the
 // tile's (r, c) in W, flat_offset = the tile in the bf16 source). Keeps the transposed copies that
@@ -2419,6 +2475,29 @@ int smt_column_gather(const void* x, int64_t ld_x, int64_t n_in, int64_t T, cons
     const int rows = row_bytes * 4 <= 65536 ? 4 : row_bytes * 2 <= 65536 ? 2 : 1;
     if (row_bytes > 65536) return fail(SMT_E_INVALID, "smt_column_gather: rows of %lld elements exceed the LDS stage", (long long)n_in);
     if (n_cols > 0 && ((uintptr_t)cols_dev & 15)) return fail(SMT_E_ALIGN, "smt_column_gather: cols not 16-byte aligned");
+    // SMT_CGATHER_IMPL: 1 = rows staged through registers; 2 (default) / 3 = LDS-DMA staging of 4 / 8
+    // rows per workgroup (8 while they fit the CU's 160 KiB)
+    static const int impl = [] { const char* e = getenv("SMT_CGATHER_IMPL"); const int v = e ? atoi(e) : 2;
+                                 return (v == 1 || v == 3) ? v : 2; }();
+    const int64_t ppr = (n_in * 2 + 1023) / 1024;
+    if (impl != 1 && ppr * 1024 * 4 <= 65536 && ld_x * 2 * 8 < 0x7fffffffLL) {
+        const int R = (impl == 3 && ppr * 1024 * 8 <= 160 * 1024) ? 8 : 4;
+        const int64_t nb = (T + R - 1) / R;
+        if (nb > 0x7fffffffLL) return fail(SMT_E_INVALID, "smt_column_gather: too large");
+        const size_t lds = (size_t)(R * ppr * 1024);
+        if (lds > 65536) {
+            static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(column_gather_dma_kernel<8>),
+                                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            if (attr != hipSuccess) return fail(SMT_E_LAUNCH, "smt_column_gather: LDS attribute: %s", hipGetErrorString(attr));
+        }
+        if (R == 8) hipLaunchKernelGGL(column_gather_dma_kernel<8>, dim3((unsigned)nb), dim3(256), lds, stream,
+                                       static_cast<const uint16_t*>(x), ld_x, n_in, T, (int)ppr, cols_dev, n_cols,
+                                       static_cast<uint16_t*>(out), ld_out);
+        else hipLaunchKernelGGL(column_gather_dma_kernel<4>, dim3((unsigned)nb), dim3(256), lds, stream,
+                                static_cast<const uint16_t*>(x), ld_x, n_in, T, (int)ppr, cols_dev, n_cols,
+                                static_cast<uint16_t*>(out), ld_out);
+        return check_launch("column_gather_dma_kernel");
+    }
     const int64_t blocks = (T + rows - 1) / rows;
     if (blocks > 0x7fffffffLL) return fail(SMT_E_INVALID, "smt_column_gather: too large");
     hipLaunchKernelGGL(column_gather_kernel, dim3((unsigned)blocks), dim3(256), (size_t)(rows * row_bytes), stream,

@@ -77,6 +77,20 @@ def test_column_gather_ragged_row_width(T, k, in_f):
     assert not out[:, k:].any()
 
 
+@pytest.mark.parametrize("T,k,off,in_f", [(9, 300, 304, 1000), (33, 1713, 8, 5112)])   # 16-B aligned views
+def test_column_gather_of_a_column_slice_view(T, k, off, in_f):
+    """x = a column slice at an offset of a wider buffer (its last row ends before the buffer does):
+    the LDS-DMA staging reads whole 1 KiB pieces, bounded at the last row's n_in-th element."""
+    torch.manual_seed(5)
+    ld = off + in_f + 8
+    buf = torch.randn(T, ld).bfloat16().to(DEV)
+    x = buf[:, off:off + in_f]
+    idx = torch.randperm(in_f)[:k].tolist()
+    out = _hip.column_gather(x, _hip.index_table(idx, DEV), k, -(-k // 256) * 256)
+    assert torch.equal(out[:, :k].cpu(), x.cpu()[:, idx])
+    assert not out[:, k:].any()
+
+
 @pytest.mark.parametrize("strategy", ["mean_abs", "abs_mean", "L1", "L2"])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_act_accumulate_and_channel_scores_bit_exact(strategy, dtype):
