@@ -2781,6 +2781,341 @@ int dq_impl() {
 }
 
 // ------------------------------------------------------------------------------------------------
+// Forward, one wave per SIMD, software-pipelined across key tiles (runtime SMT_ATTN_FWD=4; no key
+// mask). A workgroup = 4 waves x 64 query rows (row blocks 0 / 1 of 32 per wave) of one (b, q head);
+// Q fragments (both blocks) and the O^T accumulators live in the 256 AGPRs (asm loads / asm MFMAs);
+// 64-key K / V tiles in a 4-slot LDS-DMA ring, tile k+2 in flight while k and k-1 are read. Each key
+// tile is two 32-key halves, and every MFMA phase of a step carries one half of a softmax, so the
+// VALU work is spread over all MFMA gaps (at most ~5 single-issue instructions hide per gap):
+//   P1: S(h0, k)           || softmax b-part of (h1, k-1)   (exponentials, sums, P packing)
+//   P2: O += V(h0) P(h0, k-1) || softmax a-part of (h0, k)   (causal mask, row max, exponentials)
+//   P3: S(h1, k)           || softmax b-part of (h0, k)
+//   P4: O += V(h1) P(h1, k-1) || softmax a-part of (h1, k)
+// There is no O rescale in the loop (hipcc cannot keep 128 AGPR accumulators in place through a
+// read-modify-write: it spilled). Instead each row's exponent base is its first half-tile's max and
+// stays there: P = 2^(s - m) may exceed 1, which bf16 and fp32 carry exactly as far as 2^127 (a power
+// of two shifts no rounding). Should a later score exceed the base by more than kPwThr (2^64 headroom
+// left), the workgroup runs the tiles a second time from the rows' true maxima, tracked in pass one.
+// ------------------------------------------------------------------------------------------------
+constexpr int kPwQB = 256, kPwRing = 4;
+constexpr float kPwThr = 64.f;
+
+// S^T of both row blocks for one k-step of a 32-key half: A = the K row fragment, B = the blocks'
+// Q fragments (AGPRs); accumulators in VGPRs (read by the softmax). FIRST: C = 0.
+template <bool FIRST>
+__device__ __forceinline__ void mfma2_qs(f32x16_t& sA, f32x16_t& sB, bf16x8_t kr, bf16x8_t qa, bf16x8_t qb) {
+    if (FIRST)
+        asm("s_nop 1\n\t"
+            "v_mfma_f32_32x32x16_bf16 %0, %2, %3, 0\n\t"
+            "v_mfma_f32_32x32x16_bf16 %1, %2, %4, 0"
+            : "=&v"(sA), "=&v"(sB) : "v"(kr), "a"(qa), "a"(qb));
+    else
+        asm("v_mfma_f32_32x32x16_bf16 %0, %2, %3, %0\n\t"
+            "v_mfma_f32_32x32x16_bf16 %1, %2, %4, %1"
+            : "+v"(sA), "+v"(sB) : "v"(kr), "a"(qa), "a"(qb));
+}
+
+// mfma2_agpr without the leading pad: the forward's P operands are packed a whole phase earlier and
+// its V^T fragments come from LDS, so no VALU write is within reach of these MFMAs
+__device__ __forceinline__ void mfma2_agpr_np(f32x16_t& c0, f32x16_t& c1, bf16x8_t a0, bf16x8_t b0, bf16x8_t a1,
+                                              bf16x8_t b1) {
+    asm("v_mfma_f32_32x32x16_bf16 %0, %2, %3, %0\n\t"
+        "v_mfma_f32_32x32x16_bf16 %1, %4, %5, %1"
+        : "+a"(c0), "+a"(c1) : "v"(a0), "v"(b0), "v"(a1), "v"(b1));
+}
+
+struct FwdPw {
+    const FwdArgs& a;
+    uint8_t* lds;
+    bf16x8_t qf[2][8];                 // [block][k-step], AGPRs
+    f32x16_t o[2][4];                  // O^T [block][32-feature tile], AGPRs
+    f32x16_t s[2][2];                  // [half][block]: scores, then probabilities in place
+    bf16x8_t pf[2][2][2];              // [half][block][16-key step]: P^T packed as the PV B operand
+    float m[2], l[2], mx[2], mt[2], ps[2];
+    int bad;                           // a score beyond the exponent base's headroom (second pass)
+    __amdgpu_buffer_rsrc_t rk, rv;
+    uint32_t lds0, lo_row, lo_t0, lo_t4;
+    int lane, wave, hi, l32, qw, qrow[2], nt, last;
+
+    __device__ __forceinline__ FwdPw(const FwdArgs& a_, uint8_t* lds_) : a(a_), lds(lds_) {}
+
+    __device__ __forceinline__ uint32_t slot_off(int t) const { return (uint32_t)((t & (kPwRing - 1)) * 2 * kTileB); }
+
+    __device__ __forceinline__ void issue(int t) {            // K(t), V(t): 16 rows of each per wave
+        const uint32_t slot = lds0 + slot_off(t);
+        dma_rows(rk, a.k.ss, slot, t * kKV, t * kKV + 16 * wave, 4, lane);
+        dma_rows(rv, a.v.ss, slot + kTileB, t * kKV, t * kKV + 16 * wave, 4, lane);
+    }
+
+    // one sixteenth of the softmax of half H (both blocks), chunk C compile-time; keys k0h .. k0h+31
+    template <bool DIAG, int H, int C>
+    __device__ __forceinline__ void chunk(int k0h) {
+        f32x16_t& s0 = s[H][0];
+        f32x16_t& s1 = s[H][1];
+        if constexpr (C == 0 || C == 2) {                      // causal mask (diagonal tile) + max, part 1
+            constexpr int j = C / 2;
+            f32x16_t& x = s[H][j];
+            if (DIAG) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int key = k0h + (i & 3) + 8 * (i >> 2) + 4 * hi;
+                    x[i] = key > qrow[j] ? kNegInf : x[i];
+                }
+            }
+            float t = max3f(x[0], x[1], x[2]);
+            t = max3f(t, x[3], x[4]);
+            t = max3f(t, x[5], x[6]);
+            mt[j] = max3f(t, x[7], x[8]);
+        } else if constexpr (C == 1 || C == 3) {               // max, part 2
+            constexpr int j = C / 2;
+            const f32x16_t& x = s[H][j];
+            float t = max3f(mt[j], x[9], x[10]);
+            t = max3f(t, x[11], x[12]);
+            mt[j] = max3f(t, x[13], fmaxf(x[14], x[15]));
+        } else if constexpr (C == 4) {                         // row max over the half; the base fixed
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const float mtile = other_half_max(mt[j]) * a.sl2;
+                mx[j] = fmaxf(mx[j], mtile);
+                const bool first = m[j] == kNegInf;            // the row's first half-tile sets the base
+                bad |= (int)(!first && mtile > m[j] + kPwThr);
+                m[j] = first ? mtile : m[j];
+            }
+        } else if constexpr (C >= 5 && C <= 12) {              // 4 exponentials + their partial sum
+            constexpr int j = (C - 5) / 4, i0 = 4 * ((C - 5) % 4);
+            f32x16_t& x = s[H][j];
+            const float nm = -m[j];
+#pragma unroll
+            for (int i = i0; i < i0 + 4; ++i) x[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(x[i], a.sl2, nm));
+            const float q = (x[i0] + x[i0 + 1]) + (x[i0 + 2] + x[i0 + 3]);
+            ps[j] = i0 == 0 ? q : ps[j] + q;
+        } else if constexpr (C == 13 || C == 14) {             // running sum, P packed for the PV product
+            constexpr int j = C - 13;
+            l[j] += ps[j];
+            float p[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) p[i] = s[H][j][i];
+            pack_b_frags(p, pf[H][j][0], pf[H][j][1]);
+        }
+        (void)s0; (void)s1;
+    }
+    template <bool DIAG, int H, int C>
+    __device__ __forceinline__ void chunks_from(int c, int k0h) {
+        if (c == C) chunk<DIAG, H, C>(k0h);
+        if constexpr (C + 1 < 16) chunks_from<DIAG, H, C + 1>(c, k0h);
+    }
+
+    // S(H) over the K tile at slot offset sk, with softmax chunks C0 .. C0+7 of half SH beside it
+    template <int H, bool SM, bool DIAG, int SH, int C0>
+    __device__ __forceinline__ void qk(uint32_t sk, int k0s) {
+        constexpr int KI = H * 32 * kRowB;
+        const uint32_t lr = opaque(lo_row) + sk;
+        bf16x8_t f[3];                                     // K fragments two k-steps ahead (fenced)
+        f[0] = rowx<KI>(lds, lr, 0);
+        f[1] = rowx<KI>(lds, lr, 1);
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+            if (ks + 2 < 8) f[(ks + 2) % 3] = rowx<KI>(lds, lr, ks + 2);
+            __builtin_amdgcn_sched_barrier(0);
+            if (ks == 0) mfma2_qs<true>(s[H][0], s[H][1], f[0], qf[0][0], qf[1][0]);
+            else mfma2_qs<false>(s[H][0], s[H][1], f[ks % 3], qf[0][ks], qf[1][ks]);
+            if (SM) chunks_from<DIAG, SH, C0>(C0 + ks, k0s);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+
+    // O^T += V^T(H) P^T(H) over the V tile at slot offset sv, with softmax chunks beside it. DRAIN:
+    // the softmax half's scores were just written by MFMAs (24 wait states before its first read)
+    template <int H, bool SM, bool DIAG, int SH, int C0, bool DRAIN>
+    __device__ __forceinline__ void pv(uint32_t sv, int k0s) {
+        constexpr int VI = kTileB;
+        const uint32_t t0 = opaque(lo_t0) + sv, t4 = opaque(lo_t4) + sv;
+        bf16x8_t tf[3];                                    // V^T fragments two steps ahead (fenced)
+        tf[0] = trx<VI>(lds, t0, t4, 2 * H, 0);
+        tf[1] = trx<VI>(lds, t0, t4, 2 * H + 1, 0);
+#pragma unroll
+        for (int n = 0; n < 8; ++n) {
+            const int dt = n >> 1, kst = n & 1;
+            if (n + 2 < 8) tf[(n + 2) % 3] = trx<VI>(lds, t0, t4, 2 * H + ((n + 2) & 1), (n + 2) >> 1);
+            __builtin_amdgcn_sched_barrier(0);
+            mfma2_agpr_np(o[0][dt], o[1][dt], tf[n % 3], pf[H][0][kst], tf[n % 3], pf[H][1][kst]);
+            if (SM) {
+                if (DRAIN && n == 0) mfma_drain2(s[SH][0], s[SH][1]);
+                chunks_from<DIAG, SH, C0>(C0 + n, k0s);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    // the softmax chunks alone (no product beside them: the first and the drain steps)
+    template <bool DIAG, int SH, int C0, bool DRAIN>
+    __device__ __forceinline__ void sm_only(int k0s) {
+        if (DRAIN) mfma_drain2(s[SH][0], s[SH][1]);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            chunks_from<DIAG, SH, C0>(C0 + c, k0s);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+
+    // step k: S(k) and the softmax of tile k's halves; O += V(k-1) P(k-1). QK: tile k exists for this
+    // wave (k <= last); PV: k >= 1; DIAG: k == last
+    template <bool QK, bool PV, bool DIAG>
+    __device__ __forceinline__ void step(int k) {
+        const uint32_t sk = slot_off(k), sv = slot_off(k - 1);
+        const int k0 = k * kKV, kp = (k - 1) * kKV;
+        // P1: S(h0, k) || b-part of the previous tile's h1 softmax
+        if (QK && PV) qk<0, true, false, 1, 8>(sk, kp + 32);
+        else if (QK) qk<0, false, false, 1, 8>(sk, 0);
+        else if (PV) sm_only<false, 1, 8, false>(kp + 32);
+        // P2: O += V(h0, k-1) P(h0, k-1) || a-part of (h0, k)
+        if (PV && QK) pv<0, true, DIAG, 0, 0, true>(sv, k0);
+        else if (PV) pv<0, false, false, 0, 0, false>(sv, 0);
+        else sm_only<DIAG, 0, 0, true>(k0);
+        // P3: S(h1, k) || b-part of (h0, k)
+        if (QK) qk<1, true, DIAG, 0, 8>(sk, k0);
+        // P4: O += V(h1, k-1) P(h1, k-1) || a-part of (h1, k)
+        if (PV && QK) pv<1, true, DIAG, 1, 0, true>(sv, k0 + 32);
+        else if (PV) pv<1, false, false, 1, 0, false>(sv, 0);
+        else if (QK) sm_only<DIAG, 1, 0, true>(k0 + 32);
+    }
+
+    // ring bookkeeping of step k (every wave, the same count of barriers): tile k+2 into the slot
+    // tile k-2 used, then tile k+1 landed, barrier
+    __device__ __forceinline__ void ring_pre(int k) {
+        if (k + 2 < nt) issue(k + 2);
+    }
+    __device__ __forceinline__ void ring_post(int k) {
+        if (k + 2 < nt) vm_wait_upto(8);
+        else vm_wait_all();
+        __syncthreads();
+    }
+
+    template <int j>
+    __device__ __forceinline__ void store(int b, int h) {
+        const float l_tot = halves_sum(l[j]);
+        if (qrow[j] >= a.S) return;
+        const float inv = 1.f / l_tot;
+        uint16_t* op = a.o + b * a.o_sb + h * a.o_sh + (int64_t)qrow[j] * a.o_ss;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int d = 32 * dt + 8 * g + 4 * hi;
+                uint2 w;
+                w.x = pk_bf16(o[j][dt][4 * g] * inv, o[j][dt][4 * g + 1] * inv);
+                w.y = pk_bf16(o[j][dt][4 * g + 2] * inv, o[j][dt][4 * g + 3] * inv);
+                *reinterpret_cast<uint2*>(op + d) = w;
+            }
+        if (hi == 0) a.lse[((int64_t)b * a.Hq + h) * a.S + qrow[j]] = m[j] + __log2f(l_tot);
+    }
+
+    __device__ __forceinline__ void run(int b, int h, int hk, int qb) {
+        const int tid = threadIdx.x;
+        lane = tid & 63;
+        wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        hi = lane >> 5;
+        l32 = lane & 31;
+        const int q0 = qb * kPwQB;
+        qw = q0 + wave * 64;
+        const uint16_t* qp = a.q.p + b * a.q.sb + h * a.q.sh;
+        const uint16_t* kp = a.k.p + b * a.k.sb + hk * a.k.sh;
+        const uint16_t* vp = a.v.p + b * a.v.sb + hk * a.v.sh;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            qrow[j] = qw + 32 * j + l32;
+            // rows past S read row S-1: their scores only reach their own O column, never stored
+            const int64_t rr = qrow[j] < a.S ? qrow[j] : a.S - 1;
+#pragma unroll
+            for (int ks = 0; ks < 8; ++ks) {
+                const uint16_t* qa = qp + rr * a.q.ss + 16 * ks + 8 * hi;
+                asm volatile("global_load_dwordx4 %0, %1, off" : "=a"(qf[j][ks]) : "v"(qa) : "memory");
+            }
+            m[j] = kNegInf;
+            mx[j] = kNegInf;
+        }
+        const int kv_end = min(a.S, q0 + kPwQB);
+        nt = (kv_end + kKV - 1) / kKV;
+        last = min(nt - 1, qw / kKV);                      // both blocks' diagonal tile (qw % 64 == 0)
+        rk = uniform_rsrc(kp, (int64_t)a.S * a.k.ss * 2);
+        rv = uniform_rsrc(vp, (int64_t)a.S * a.v.ss * 2);
+        lds0 = lds_addr(lds);
+        {
+            const uint32_t r = (uint32_t)l32;
+            lo_row = r * kRowB + ((16u * hi) ^ (swz(r) << 4));
+            const TrLane tl = tr_lane(lane);
+            lo_t0 = tl.krow * kRowB + (tl.feat_byte ^ (swz(tl.krow) << 4));
+            lo_t4 = (tl.krow + 4) * kRowB + (tl.feat_byte ^ (swz(tl.krow + 4) << 4));
+        }
+        for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            l[j] = 0.f;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) zero_agpr(o[j][dt]);
+        }
+        bad = 0;
+        issue(0);
+        if (nt > 1) issue(1);
+        vm_wait_all();
+        __syncthreads();
+        // this wave's steps 0 .. last+1; the workgroup's ring runs steps 0 .. nt (the last wave's)
+        int k = 0;
+        ring_pre(0);
+        if (last == 0) step<true, false, true>(0);
+        else step<true, false, false>(0);
+        ring_post(0);
+        for (k = 1; k < last; ++k) {
+            ring_pre(k);
+            step<true, true, false>(k);
+            ring_post(k);
+        }
+        if (last > 0) {
+            ring_pre(last);
+            step<true, true, true>(last);
+            ring_post(last);
+        }
+        k = last + 1;
+        ring_pre(k);
+        step<false, true, false>(k);
+        if (k < nt) ring_post(k);
+        for (++k; k <= nt; ++k) {                          // ring duty only
+            ring_pre(k);
+            if (k < nt) ring_post(k);
+        }
+        // every wave's steps are done (the last barrier of the ring, or this one) before a second pass
+        // re-fills the ring from tile 0
+        if (!__syncthreads_or(bad)) break;
+        m[0] = mx[0];
+        m[1] = mx[1];
+        }
+        mfma_drain_agpr(o, o);
+        store<0>(b, h);
+        store<1>(b, h);
+    }
+};
+
+__global__ __launch_bounds__(256, 1)
+void attn_fwd_pw_kernel(FwdArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kPwRing * 2 * kTileB];         // 128 KiB
+    const int nqb = (a.S + kPwQB - 1) / kPwQB;
+    const int G = a.Hq / a.Hkv;
+    const int total = nqb * a.Hq * a.B;
+    const int L = xcd_logical(blockIdx.x, total);
+    const int per_group = G * nqb;
+    const int grp = L / per_group;
+    const int rem = L - grp * per_group;
+    const int hk = grp % a.Hkv;
+    FwdPw f(a, lds);
+    f.run(grp / a.Hkv, hk * G + rem % G, hk, nqb - 1 - rem / G);
+}
+
+// SMT_ATTN_FWD (runtime): 4 = attn_fwd_pw_kernel for unmasked batches; otherwise attn_fwd_kernel
+int fwd_impl() {
+    static const int v = [] { const char* e = getenv("SMT_ATTN_FWD"); return (e && atoi(e) == 4) ? 4 : 0; }();
+    return v;
+}
+
+// ------------------------------------------------------------------------------------------------
 // dK / dV, one wave per SIMD (runtime SMT_ATTN_DKV=2): the same 256-key block per workgroup, as 4
 // waves x 64 keys. Each wave holds dK^T and dV^T of its two 32-key blocks (4 x 64 fp32 accumulators:
 // 256 registers, MFMA-only, so they can live in the accumulation registers of the 512-register
@@ -3294,6 +3629,13 @@ int smt_attn_fwd_kmask(const smt_attn_tensor* q, const smt_attn_tensor* k, const
     a.kmask = key_mask; a.kmask_ld = key_mask_ld;
     a.B = shape->B; a.Hq = shape->Hq; a.Hkv = shape->Hkv; a.S = shape->S;
     a.sl2 = shape->scale * 1.4426950408889634f;
+    if (!key_mask && fwd_impl() == 4) {
+        const int64_t nqb = (shape->S + kPwQB - 1) / kPwQB;
+        const int64_t blocks = nqb * shape->Hq * shape->B;
+        if (blocks > 0x7fffffffLL) return fail(-1, "%s: too many blocks", fn);
+        hipLaunchKernelGGL(attn_fwd_pw_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, a);
+        return check_launch("attn_fwd_pw_kernel");
+    }
     if (SMT_ATTN_FWD_IMPL == 3) {
         const int64_t nqb = (shape->S + kDualQB - 1) / kDualQB;
         const int64_t blocks = nqb * shape->Hq * shape->B;

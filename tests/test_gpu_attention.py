@@ -72,6 +72,32 @@ def test_flash_attention_matches_fp32_reference(B, Hq, Hkv, S, layout):
     assert (lse - rlse).abs().max().item() < 2e-3
 
 
+def test_flash_attention_score_far_above_the_first_tiles():
+    """A late key whose score beats every earlier one by ~95 in log2 units: kernels that fix each row's
+    exponent base early (the one-wave-per-SIMD forward, SMT_ATTN_FWD=4) must take their second pass;
+    the others move their running max. Output, gradients and lse as the main test."""
+    torch.manual_seed(11)
+    B, Hq, Hkv, S, D = 1, 4, 2, 512, 128
+    mk = lambda H: torch.randn(B, S, H, D, device=DEV).bfloat16().transpose(1, 2)
+    q, k, v = mk(Hq), mk(Hkv), mk(Hkv)
+    q = (q.float() * 0.25 + 0.5).bfloat16()                    # a common positive direction
+    k = k.clone()
+    k[:, :, 400] = 12.0                                         # q.k ~ 768 -> ~68 natural, ~98 log2 units
+    q, k, v = (t.detach().requires_grad_(True) for t in (q, k, v))
+    g = torch.randn(B, S, Hq, D, device=DEV).bfloat16()
+    o = flash_attention(q, k, v)
+    lse = o.grad_fn.saved_tensors[4].clone()
+    o.backward(g)
+    ro, rdq, rdk, rdv, rlse = _ref(q, k, v, g, D ** -0.5)
+    so, sdq, sdk, sdv = _sdpa_bf16(q, k, v, g)
+    assert torch.isfinite(o).all() and torch.isfinite(lse).all()
+    for name, mine, sdpa, ref in (("o", o, so, ro), ("dq", q.grad, sdq, rdq), ("dk", k.grad, sdk, rdk),
+                                  ("dv", v.grad, sdv, rdv)):
+        e, es = _rel(mine, ref), _rel(sdpa, ref)
+        assert e <= max(8e-3, 1.5 * es), (name, e, es)
+    assert (lse - rlse).abs().max().item() < 2e-3 * max(1.0, rlse.abs().max().item() / 64)
+
+
 def test_flash_attention_rejects_unsupported():
     q = torch.zeros(1, 2, 64, 64, device=DEV, dtype=torch.bfloat16)
     with pytest.raises(NotImplementedError):
