@@ -2831,7 +2831,7 @@ struct FwdPw {
     f32x16_t o[2][4];                  // O^T [block][32-feature tile], AGPRs
     f32x16_t s[2][2];                  // [half][block]: scores, then probabilities in place
     bf16x8_t pf[2][2][2];              // [half][block][16-key step]: P^T packed as the PV B operand
-    float m[2], l[2], mx[2], mt[2], ps[2];
+    float m[2], l[2], mx[2], mt[2], ps[2], mq[2][3];
     int bad;                           // a score beyond the exponent base's headroom (second pass)
     __amdgpu_buffer_rsrc_t rk, rv;
     uint32_t lds0, lo_row, lo_t0, lo_t4;
@@ -2848,11 +2848,42 @@ struct FwdPw {
     }
 
     // one sixteenth of the softmax of half H (both blocks), chunk C compile-time; keys k0h .. k0h+31
+    // The softmax of one half (both blocks) in 16 chunks, each beside one MFMA pair. With one wave per
+    // SIMD nothing else fills the gap while a VALU result is awaited, so a chunk holds independent
+    // operations only: the max trees are split into independent triples, and the 8 groups of 4
+    // scores (g = 4j + i/4) run as a pipeline (chunk 5 + n: fma of group n, exp of group n-1, sums
+    // of group n-2).
+    template <int G>
+    __device__ __forceinline__ void grp_fma(int H) {
+        if constexpr (G >= 0 && G < 8) {
+            constexpr int j = G / 4, i0 = 4 * (G % 4);
+            f32x16_t& x = s[H][j];
+            const float nm = -m[j];
+#pragma unroll
+            for (int i = i0; i < i0 + 4; ++i) x[i] = __builtin_fmaf(x[i], a.sl2, nm);
+        }
+    }
+    template <int G>
+    __device__ __forceinline__ void grp_exp(int H) {
+        if constexpr (G >= 0 && G < 8) {
+            constexpr int j = G / 4, i0 = 4 * (G % 4);
+            f32x16_t& x = s[H][j];
+#pragma unroll
+            for (int i = i0; i < i0 + 4; ++i) x[i] = __builtin_amdgcn_exp2f(x[i]);
+        }
+    }
+    template <int G>
+    __device__ __forceinline__ void grp_sum(int H) {
+        if constexpr (G >= 0 && G < 8) {
+            constexpr int j = G / 4, i0 = 4 * (G % 4);
+            const f32x16_t& x = s[H][j];
+            const float q = (x[i0] + x[i0 + 1]) + (x[i0 + 2] + x[i0 + 3]);
+            ps[j] = i0 == 0 ? q : ps[j] + q;
+        }
+    }
     template <bool DIAG, int H, int C>
     __device__ __forceinline__ void chunk(int k0h) {
-        f32x16_t& s0 = s[H][0];
-        f32x16_t& s1 = s[H][1];
-        if constexpr (C == 0 || C == 2) {                      // causal mask (diagonal tile) + max, part 1
+        if constexpr (C == 0 || C == 2) {                      // causal mask (diagonal tile) + 3 triples
             constexpr int j = C / 2;
             f32x16_t& x = s[H][j];
             if (DIAG) {
@@ -2862,45 +2893,52 @@ struct FwdPw {
                     x[i] = key > qrow[j] ? kNegInf : x[i];
                 }
             }
-            float t = max3f(x[0], x[1], x[2]);
-            t = max3f(t, x[3], x[4]);
-            t = max3f(t, x[5], x[6]);
-            mt[j] = max3f(t, x[7], x[8]);
-        } else if constexpr (C == 1 || C == 3) {               // max, part 2
+            mq[j][0] = max3f(x[0], x[1], x[2]);
+            mq[j][1] = max3f(x[3], x[4], x[5]);
+            mq[j][2] = max3f(x[6], x[7], x[8]);
+        } else if constexpr (C == 1 || C == 3) {               // 2 more triples, then the tree
             constexpr int j = C / 2;
             const f32x16_t& x = s[H][j];
-            float t = max3f(mt[j], x[9], x[10]);
-            t = max3f(t, x[11], x[12]);
-            mt[j] = max3f(t, x[13], fmaxf(x[14], x[15]));
+            const float t3 = max3f(x[9], x[10], x[11]);
+            const float t4 = max3f(x[12], x[13], x[14]);
+            const float u = max3f(mq[j][0], mq[j][1], mq[j][2]);
+            mt[j] = max3f(u, max3f(t3, t4, x[15]), u);
         } else if constexpr (C == 4) {                         // row max over the half; the base fixed
+            float mtile[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) mtile[j] = other_half_max(mt[j]) * a.sl2;
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
-                const float mtile = other_half_max(mt[j]) * a.sl2;
-                mx[j] = fmaxf(mx[j], mtile);
+                mx[j] = fmaxf(mx[j], mtile[j]);
                 const bool first = m[j] == kNegInf;            // the row's first half-tile sets the base
-                bad |= (int)(!first && mtile > m[j] + kPwThr);
-                m[j] = first ? mtile : m[j];
+                bad |= (int)(!first && mtile[j] > m[j] + kPwThr);
+                m[j] = first ? mtile[j] : m[j];
             }
-        } else if constexpr (C >= 5 && C <= 12) {              // 4 exponentials + their partial sum
-            constexpr int j = (C - 5) / 4, i0 = 4 * ((C - 5) % 4);
-            f32x16_t& x = s[H][j];
-            const float nm = -m[j];
+        } else if constexpr (C >= 5 && C <= 14) {              // the group pipeline
+            constexpr int n = C - 5;
+            grp_fma<n>(H);
+            grp_exp<n - 1>(H);
+            grp_sum<n - 2>(H);
+            if constexpr (n == 5) l[0] += ps[0];               // block 0's groups 0-3 summed at n = 5
+            if constexpr (n == 6) {
+                float p[16];
 #pragma unroll
-            for (int i = i0; i < i0 + 4; ++i) x[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(x[i], a.sl2, nm));
-            const float q = (x[i0] + x[i0 + 1]) + (x[i0 + 2] + x[i0 + 3]);
-            ps[j] = i0 == 0 ? q : ps[j] + q;
-        } else if constexpr (C == 13 || C == 14) {             // running sum, P packed for the PV product
-            constexpr int j = C - 13;
-            l[j] += ps[j];
+                for (int i = 0; i < 16; ++i) p[i] = s[H][0][i];
+                pack_b_frags(p, pf[H][0][0], pf[H][0][1]);
+            }
+            if constexpr (n == 9) l[1] += ps[1];
+        } else {                                               // C == 15: block 1 packed
             float p[16];
 #pragma unroll
-            for (int i = 0; i < 16; ++i) p[i] = s[H][j][i];
-            pack_b_frags(p, pf[H][j][0], pf[H][j][1]);
+            for (int i = 0; i < 16; ++i) p[i] = s[H][1][i];
+            pack_b_frags(p, pf[H][1][0], pf[H][1][1]);
         }
-        (void)s0; (void)s1;
     }
     template <bool DIAG, int H, int C>
     __device__ __forceinline__ void chunks_from(int c, int k0h) {
+#ifdef SMT_PW_DIAG_NO_SOFTMAX
+        return;                                            // diagnostic build: the loop skeleton alone
+#endif
         if (c == C) chunk<DIAG, H, C>(k0h);
         if constexpr (C + 1 < 16) chunks_from<DIAG, H, C + 1>(c, k0h);
     }
