@@ -1008,26 +1008,31 @@ def main():
 
     # ---- the tile wgrad alone (its roofline): the same steps with the wgrad stream joined ----
     overlapped = {"bf16": w, "mx": w_mx}
-    if engine.wgrad_stream is not None and args.roofline_steps > 0:
+
+    def isolated_wgrad(n_steps, offset):
+        """Timer summaries of the tile wgrad over n_steps SMT steps with the wgrad stream joined."""
         side = engine.wgrad_stream
         engine.wgrad_stream = None
         for tg in engine.tile_groups:
             if tg.buckets is not None:
                 tg.buckets.side_stream = None
-        iso = batches(args.roofline_steps, B, S, vocab, rank, device, offset=70000)
+        iso = batches(n_steps, B, S, vocab, rank, device, offset=offset)
         timer.records, mx_timer.records = [], []
         timer.enabled = mx_timer.enabled = True
         for b in iso:
             step(b)
         torch.cuda.synchronize()
         timer.enabled = mx_timer.enabled = False
-        w, w_mx = timer.summary(), mx_timer.summary()
-        log(f"roofline steps done ({args.roofline_steps}, wgrad stream joined)")
         engine.wgrad_stream = side
         for tg in engine.tile_groups:
             if tg.buckets is not None:
                 tg.buckets.side_stream = side
         del iso
+        return timer.summary(), mx_timer.summary()
+
+    if engine.wgrad_stream is not None and args.roofline_steps > 0:
+        w, w_mx = isolated_wgrad(args.roofline_steps, 70000)
+        log(f"roofline steps done ({args.roofline_steps}, wgrad stream joined)")
 
     # ---- the selective activation policy: GEMM outputs, attention O / LSE resident; the SMT linears'
     # RMSNorm / SwiGLU input blocks rebuilt in the backward (smt.set_activation_policy) ----
@@ -1071,6 +1076,20 @@ def main():
         engine.wgrad_rounding = headline_rounding
         alt_round_mode["wgrad_rounding"] = WGRAD_ROUNDING_NOTE[alt]
         alt_round_mode["median_step_vs_headline"] = round(alt_round_mode["median_ms_per_step"] / (med * 1e3), 4)
+        if engine.wgrad_stream is not None and args.roofline_steps > 0:
+            # the tile wgrad kernel alone under this rounding, as the headline's roofline is measured
+            engine.wgrad_rounding = alt
+            wa, _wm = isolated_wgrad(args.roofline_steps, 35000)
+            engine.wgrad_rounding = headline_rounding
+            if wa and wa["seconds"] > 0:
+                avg_a = wa["seconds"] / wa["launches"]
+                uniq_a = wa["unique_bytes"] / wa["launches"]
+                traffic_a, tsrc_a = pmc_traffic(args, alt)
+                alt_round_mode["wgrad_kernel"] = {
+                    "launches": wa["launches"], "avg_launch_us": round(avg_a * 1e6, 2),
+                    "algorithmic_bytes_per_launch": round(uniq_a),
+                    "hbm_frac_on_algorithmic_bytes": round(uniq_a / avg_a / 1e9 / PEAK_HBM_GBS, 4),
+                    "traffic": traffic_a, "traffic_source": tsrc_a}
         log(f"{alt} rounding: {alt_round_mode['value']} tokens/s (median step x{alt_round_mode['median_step_vs_headline']})")
 
     # ---- the reference's memory policy (per-layer recompute), same engine and tiles ----
