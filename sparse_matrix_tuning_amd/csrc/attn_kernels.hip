@@ -2953,7 +2953,9 @@ struct FwdPw {
         f[1] = rowx<KI>(lds, lr, 1);
 #pragma unroll
         for (int ks = 0; ks < 8; ++ks) {
+#ifndef SMT_PW_DIAG_NO_LDS
             if (ks + 2 < 8) f[(ks + 2) % 3] = rowx<KI>(lds, lr, ks + 2);
+#endif
             __builtin_amdgcn_sched_barrier(0);
             if (ks == 0) mfma2_qs<true>(s[H][0], s[H][1], f[0], qf[0][0], qf[1][0]);
             else mfma2_qs<false>(s[H][0], s[H][1], f[ks % 3], qf[0][ks], qf[1][ks]);
@@ -2974,7 +2976,9 @@ struct FwdPw {
 #pragma unroll
         for (int n = 0; n < 8; ++n) {
             const int dt = n >> 1, kst = n & 1;
+#ifndef SMT_PW_DIAG_NO_LDS
             if (n + 2 < 8) tf[(n + 2) % 3] = trx<VI>(lds, t0, t4, 2 * H + ((n + 2) & 1), (n + 2) >> 1);
+#endif
             __builtin_amdgcn_sched_barrier(0);
             mfma2_agpr_np(o[0][dt], o[1][dt], tf[n % 3], pf[H][0][kst], tf[n % 3], pf[H][1][kst]);
             if (SM) {
@@ -3020,12 +3024,18 @@ struct FwdPw {
     // ring bookkeeping of step k (every wave, the same count of barriers): tile k+2 into the slot
     // tile k-2 used, then tile k+1 landed, barrier
     __device__ __forceinline__ void ring_pre(int k) {
+#ifndef SMT_PW_DIAG_NO_DMA
         if (k + 2 < nt) issue(k + 2);
+#endif
     }
     __device__ __forceinline__ void ring_post(int k) {
+#ifndef SMT_PW_DIAG_NO_DMA
         if (k + 2 < nt) vm_wait_upto(8);
         else vm_wait_all();
+#endif
+#ifndef SMT_PW_DIAG_NO_BARRIER
         __syncthreads();
+#endif
     }
 
     template <int j>
