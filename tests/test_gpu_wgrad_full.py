@@ -135,8 +135,8 @@ def _restatement(go, x, sel):
     return ref.linearz_tile_grads(gs, xs, diag), ref.tile_grads_fp64(gs, xs, diag)
 
 
-@pytest.mark.parametrize("module,n", [("k_proj", 4), ("down_proj", 8), ("q_proj", 27), ("gate_proj", 67),
-                                      ("down_proj", 436)])
+@pytest.mark.parametrize("module,n", [("k_proj", 4), ("down_proj", 8), ("q_proj", 27), ("q_proj", 54),
+                                      ("gate_proj", 67), ("down_proj", 436)])
 def test_reference_rounding_vs_restatement_at_bench_geometry(module, n):
     out_f, in_f = SHAPES[module]
     go, x = _operands(out_f, in_f, seed=100 + n)
@@ -169,24 +169,58 @@ def test_reference_rounding_vs_restatement_at_bench_geometry(module, n):
         assert d_single <= 1.5 * ref_err, (module, n, i, d_single, ref_err)
 
 
+def _slab_worker(tmp_path, name, **env):
+    """tests/wgrad_slab_worker.py in a child process with the given library switches (read once per
+    process) -> its {case: tile gradients}."""
+    import subprocess
+    import sys
+    path = str(tmp_path / f"{name}.pt")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tests", "wgrad_slab_worker.py"), path], cwd=root,
+                       env=dict(os.environ, PYTHONPATH=root, **env), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return torch.load(path, weights_only=True)
+
+
 def test_reference_rounding_bf16_slabs_bit_identical(tmp_path):
     """With one workgroup per sample (kps == 1) the kernels round each sample's partial to bf16 in
     their epilogue and write half-size slabs: bit-identical to rounding them in the reduce from fp32
     slabs (SMT_WGRAD_SLAB16=0, a child process: the library reads the switch once)."""
-    import subprocess
-    import sys
     from tests.wgrad_slab_worker import cases
     mine = cases()
-    path = str(tmp_path / "fp32_slabs.pt")
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    r = subprocess.run([sys.executable, os.path.join(root, "tests", "wgrad_slab_worker.py"), path], cwd=root,
-                       env=dict(os.environ, SMT_WGRAD_SLAB16="0", PYTHONPATH=root), capture_output=True, text=True,
-                       timeout=300)
-    assert r.returncode == 0, r.stderr[-3000:]
-    theirs = torch.load(path, weights_only=True)
+    theirs = _slab_worker(tmp_path, "fp32_slabs", SMT_WGRAD_SLAB16="0")
     assert sorted(mine) == sorted(theirs)
     for k in mine:
         assert torch.equal(mine[k], theirs[k]), k
+
+
+def test_reference_rounding_batch_vs_restatement():
+    """The engine's launch: three modules in one batch with the reference rounding
+    (smt_tile_wgrad_batch_seq), 54 tiles (the bench's typical launch: 864 workgroups), one module
+    accumulating; sampled tiles against oracle.linearz_tile_grads."""
+    items, checks, lists = [], [], []
+    for k, (name, n) in enumerate((("q_proj", 18), ("k_proj", 12), ("gate_proj", 24))):
+        out_f, in_f = SHAPES[name]
+        go, x = _operands(out_f, in_f, seed=40 + k)
+        tiles = _tiles(out_f, in_f, n, seed=50 + k)
+        acc = k == 1
+        base = (torch.randn(n * 256, 256, device=DEV) * 1e-2).bfloat16()
+        out = base.clone() if acc else torch.empty(n * 256, 256, dtype=torch.bfloat16, device=DEV)
+        items.append((go, x, out, acc))
+        lists.append(tiles)
+        checks.append((go, x, tiles, out, base, acc))
+    tab, order = _hip.wgrad_batch_table(lists, DEV)
+    _hip.tile_wgrad_batch(items, tab, order, seq_len=S)
+    torch.cuda.synchronize()
+    for go, x, tiles, out, base, acc in checks:
+        pick = [0, len(tiles) - 1]
+        want, _truth_ = _restatement(go, x, [tiles[i] for i in pick])
+        for k, i in enumerate(pick):
+            w = want[k * 256:(k + 1) * 256]
+            if acc:
+                w = (base[i * 256:(i + 1) * 256].cpu().float() + w.float()).bfloat16()
+            d = _rel(out[i * 256:(i + 1) * 256].cpu(), w)
+            assert d <= 1e-3, (tiles[i], acc, d)
 
 
 def test_reference_rounding_rejects_partial_samples():
