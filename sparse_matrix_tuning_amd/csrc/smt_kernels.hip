@@ -699,7 +699,8 @@ __device__ __forceinline__ void wgrad_reduce_tile(const float* __restrict__ slab
         // order in fp32 and round once more (the same arithmetic as the fp32-slab branch below)
         const uint16_t* s16 = reinterpret_cast<const uint16_t*>(slab) + (int64_t)tile * S * kTileElems + e;
         sum = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int s = 0; s < S; ++s) {
+#pragma unroll 8
+        for (int s = 0; s < S; ++s) {                      // unrolled: several slab loads in flight
             const uint2 v = *reinterpret_cast<const uint2*>(s16 + (int64_t)s * kTileElems);
             sum.x += bf16_bits_to_f32(v.x & 0xffffu); sum.y += bf16_bits_to_f32(v.x >> 16);
             sum.z += bf16_bits_to_f32(v.y & 0xffffu); sum.w += bf16_bits_to_f32(v.y >> 16);
@@ -708,12 +709,14 @@ __device__ __forceinline__ void wgrad_reduce_tile(const float* __restrict__ slab
         sum.z = bf16_round(sum.z); sum.w = bf16_round(sum.w);
     } else if (kps <= 0) {
         sum = *reinterpret_cast<const float4*>(src);
+#pragma unroll 4
         for (int s = 1; s < S; ++s) {
             const float4 v = *reinterpret_cast<const float4*>(src + (int64_t)s * kTileElems);
             sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
         }
     } else {
         sum = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 4
         for (int s0 = 0; s0 < S; s0 += kps) {
             float4 part = *reinterpret_cast<const float4*>(src + (int64_t)s0 * kTileElems);
             for (int j = 1; j < kps; ++j) {
