@@ -65,6 +65,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--pattern", default="spread", choices=("spread", "rowblock"))
     ap.add_argument("--g-width", type=int, default=None, help="override every module's out features")
+    ap.add_argument("--seq-len", type=int, default=0, help="reference rounding: T / seq_len samples")
     ap.add_argument("--tag", default=os.environ.get("SMT_HIP_LIB", "default"))
     args = ap.parse_args()
     dev = torch.device("cuda")
@@ -84,7 +85,7 @@ def main():
 
     def run_all():
         for items, tab, order, *_ in prepared:
-            _hip.tile_wgrad_batch(items, tab, order)
+            _hip.tile_wgrad_batch(items, tab, order, seq_len=args.seq_len or None)
 
     run_all()
     torch.cuda.synchronize()
@@ -94,7 +95,7 @@ def main():
     for _ in range(args.iters):
         for i, (items, tab, order, *_r) in enumerate(prepared):
             ev[i][0].record(s)
-            _hip.tile_wgrad_batch(items, tab, order)
+            _hip.tile_wgrad_batch(items, tab, order, seq_len=args.seq_len or None)
             ev[i][1].record(s)
         torch.cuda.synchronize()
         for i in range(len(prepared)):
@@ -108,7 +109,9 @@ def main():
     distinct = sum(p[4] for p in prepared)
     per_tile = sum(p[5] for p in prepared)
     tiles = sum(p[3] for p in prepared)
-    print(json.dumps({"tag": os.path.basename(args.tag), "T": args.T, "launches": launches,
+    print(json.dumps({"tag": os.path.basename(args.tag), "env": {k: v for k, v in os.environ.items()
+                                                                    if k.startswith("SMT_WGRAD")},
+                      "seq_len": args.seq_len, "T": args.T, "launches": launches,
                       "tiles_per_launch": round(tiles / launches, 1),
                       "avg_launch_us": round(t / launches * 1e6, 2),
                       "distinct_gb_per_launch": round(distinct / launches / 1e9, 4),
