@@ -278,6 +278,9 @@ void rmsnorm_fwd_reg_kernel(const uint16_t* __restrict__ x, int64_t ldx, const u
 
 // Backward without weight grad; with ADD the gradient reaching the norm's input by the residual path
 // is added as autograd would: dx = bf16(bf16(dx_norm) + dres).
+#ifndef SMT_NORM_BWD_PRELOAD
+#define SMT_NORM_BWD_PRELOAD 1
+#endif
 template <int CPL, bool ADD, bool QUANT = false>
 __global__ __launch_bounds__(256, CPL <= 10 ? 2 : 1)        // two waves per SIMD up to hidden 5120
 void rmsnorm_bwd_reg_kernel(const uint16_t* __restrict__ dy, int64_t lddy, const uint16_t* __restrict__ x, int64_t ldx,
@@ -294,6 +297,14 @@ void rmsnorm_bwd_reg_kernel(const uint16_t* __restrict__ dy, int64_t lddy, const
     // instead of one (at CPL 8 the fp32 copies fit two waves, and the packing only adds ALU work)
     constexpr bool PACK = CPL > 8;
     typename RowReg<PACK>::T xr[CPL], gr[CPL];
+    // up to CPL 8 the residual gradient's row is loaded with x and dy (32 more registers): issued
+    // in the second pass, each load waited behind the dx stores issued before it (vmcnt counts both)
+    constexpr bool PRE = ADD && !PACK && SMT_NORM_BWD_PRELOAD;
+    uint4 drr[PRE ? CPL : 1];
+    if constexpr (PRE) {
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) drr[k] = *reinterpret_cast<const uint4*>(dres + row * lddr + (lane + 64 * k) * 8);
+    }
     float dot = 0.f;
 #pragma unroll
     for (int k = 0; k < CPL; ++k) {
@@ -309,6 +320,12 @@ void rmsnorm_bwd_reg_kernel(const uint16_t* __restrict__ dy, int64_t lddy, const
         }
         gr[k] = RowReg<PACK>::put(gw);
     }
+    if constexpr (PRE) {
+        // opaque from here on: hipcc would otherwise re-issue (rematerialise) the read-only loads in pass 2
+#pragma unroll
+        for (int k = 0; k < CPL; ++k)
+            asm volatile("" : "+v"(drr[k].x), "+v"(drr[k].y), "+v"(drr[k].z), "+v"(drr[k].w));
+    }
     dot = wave_sum_f(dot);
     const float coef = r * r * r * dot / (float)H;
     if constexpr (PACK) asm volatile("" ::: "memory");   // the residual-gradient loads stay in this pass
@@ -320,7 +337,9 @@ void rmsnorm_bwd_reg_kernel(const uint16_t* __restrict__ dy, int64_t lddy, const
 #pragma unroll
         for (int j = 0; j < 8; ++j) o.v[j] = r * gw.v[j] - xv.v[j] * coef;
         if (ADD) {
-            const F8 dr = ld8(dres + row * lddr + c * 8);
+            F8 dr;
+            if constexpr (PRE) dr = unpack8(drr[k]);
+            else dr = ld8(dres + row * lddr + c * 8);
 #pragma unroll
             for (int j = 0; j < 8; ++j) o.v[j] = rbf(o.v[j]) + dr.v[j];
         }
