@@ -53,7 +53,7 @@ def main():
             out.backward(g)
         tot = timed(fb, a.iters)
         bwd = tot - fwd
-        print(json.dumps({"impl": impl, "B": B, "Hq": Hq, "Hkv": Hkv, "S": S, "fwd_ms": round(fwd, 3),
+        print(json.dumps({"impl": impl, "env": {k: v for k, v in os.environ.items() if k.startswith("SMT_ATTN")}, "B": B, "Hq": Hq, "Hkv": Hkv, "S": S, "fwd_ms": round(fwd, 3),
                           "bwd_ms": round(bwd, 3), "fwd_tflops": round(fl / fwd / 1e9, 1),
                           "bwd_tflops": round(2.5 * fl / bwd / 1e9, 1)}), flush=True)
 
