@@ -223,6 +223,30 @@ def test_reference_rounding_batch_vs_restatement():
             assert d <= 1e-3, (tiles[i], acc, d)
 
 
+@pytest.mark.parametrize("n", [12, 60])
+def test_reference_rounding_odd_sample_count(n):
+    """Five samples of 640 rows: 12 tiles cut each sample into pieces (kps > 1, fp32 slabs, the
+    reduce's per-sample loop), 60 tiles give one workgroup per sample (bf16 slabs, the reduce's
+    unrolled sample loop with a remainder); sampled tiles vs oracle.linearz_tile_grads."""
+    Bo, So = 5, 640
+    out_f, in_f = SHAPES["q_proj"]
+    g = torch.Generator(device=DEV).manual_seed(7 + n)
+    x = torch.randn(Bo * So, in_f, generator=g, device=DEV).bfloat16()
+    go = (torch.randn(Bo * So, out_f, generator=g, device=DEV) * 1e-2).bfloat16()
+    tiles = _tiles(out_f, in_f, n, seed=70 + n)
+    out = torch.empty(n * 256, 256, dtype=torch.bfloat16, device=DEV)
+    _hip.tile_wgrad(go, x, _hip.tile_table(tiles, DEV), out, order=_hip.order_table(tiles, DEV), seq_len=So)
+    torch.cuda.synchronize()
+    pick = [0, n // 2, n - 1]
+    sel = [tiles[i] for i in pick]
+    gs = torch.cat([go[:, r * 256:(r + 1) * 256] for r, _c in sel], 1).view(Bo, So, -1).cpu()
+    xs = torch.cat([x[:, c * 256:(c + 1) * 256] for _r, c in sel], 1).view(Bo, So, -1).cpu()
+    want = ref.linearz_tile_grads(gs, xs, [(k, k) for k in range(len(sel))])
+    for k, i in enumerate(pick):
+        d = _rel(out[i * 256:(i + 1) * 256].cpu(), want[k * 256:(k + 1) * 256])
+        assert d <= 1e-3, (tiles[i], d)
+
+
 def test_reference_rounding_rejects_partial_samples():
     go, x = _operands(1024, 1024, seed=1)
     table = _hip.tile_table([(0, 0)], DEV)
