@@ -13,6 +13,14 @@ has not run yet will be executed by the running backward (``torch._C._will_engin
 So a consumer whose output does not reach the loss, a partial ``torch.autograd.grad``, or separate
 backward calls over different consumers never strand a contribution: each backward pass hands over
 exactly the sum of the consumers it ran. A tensor with one consumer takes the plain path.
+
+Joint product (q/k/v): when a consumer's output gradient is a column slice of a wider row-major
+buffer and its weight operand the transpose of a column slice of an equally wide transposed copy
+(the flash attention's joint [dq | dk | dv] gradient and the engine's joint q/k/v W^T), its product
+is deferred to the last consumer. If the deferred slices then tile both buffers at the same column
+offsets, the sum is ONE GEMM over the whole width (fewer, larger GEMMs and no C re-reads; one bf16
+rounding of the fp32 sum instead of one per consumer); otherwise the deferred products run one by
+one as before.
 """
 from __future__ import annotations
 
@@ -22,8 +30,11 @@ from typing import List, Optional
 import torch
 
 
+JOINT_PRODUCTS = 0          # joint GEMMs issued by _flush (diagnostics / tests)
+
+
 class SharedInputGrad:
-    __slots__ = ("version", "nodes", "done", "buf")
+    __slots__ = ("version", "nodes", "done", "buf", "pending")
 
     def __init__(self, version: int):
         self.version = version
@@ -32,6 +43,7 @@ class SharedInputGrad:
         self.nodes: List[weakref.ref] = []
         self.done: List[bool] = []
         self.buf: Optional[torch.Tensor] = None
+        self.pending: List[tuple] = []              # deferred (g2, mat) of joint-slice consumers
 
     @property
     def consumers(self) -> int:
@@ -80,13 +92,53 @@ def input_grad(slot: Optional[_Slot], grad_output: torch.Tensor, mat: torch.Tens
     if acc is None or acc.consumers <= 1:
         out = torch.matmul(g2, mat)
         return out.view(*lead, out.shape[-1])
-    if acc.buf is None:
+    if _joint_slice(g2, mat):
+        acc.pending.append((g2, mat))
+    elif acc.buf is None:
         acc.buf = torch.matmul(g2, mat)
     else:
         acc.buf.addmm_(g2, mat)
     acc.done[slot.index] = True
     if _others_pending(acc, slot.index):
         return None
+    if acc.pending:
+        _flush(acc)
     buf, acc.buf = acc.buf, None
     acc.done = [False] * len(acc.done)           # a later backward over the same graph starts afresh
     return buf.view(*lead, buf.shape[-1])
+
+
+def _joint_slice(g2: torch.Tensor, mat: torch.Tensor) -> bool:
+    """g2 [T, out] a column slice of a wider row-major buffer (row stride C > out), mat [out, in] the
+    transpose of a column slice of an [in, C] row-major transposed copy."""
+    C = g2.stride(0)
+    return (g2.dim() == 2 and g2.stride(1) == 1 and C > g2.shape[1] and mat.dim() == 2
+            and mat.stride(0) == 1 and mat.stride(1) == C and mat.dtype == g2.dtype)
+
+
+def _flush(acc: SharedInputGrad) -> None:
+    """Add the deferred products into ``acc.buf``: one GEMM over the whole width when the deferred
+    slices tile the gradient buffer and the transposed copy at the same column offsets."""
+    items, acc.pending = acc.pending, []
+    g0, m0 = items[0]
+    C = g0.stride(0)
+    og, ow = min(g.storage_offset() for g, _ in items), min(m.storage_offset() for _, m in items)
+    spans = sorted((g.storage_offset() - og, g.shape[1], m.storage_offset() - ow) for g, m in items)
+    joint = (all(g.untyped_storage().data_ptr() == g0.untyped_storage().data_ptr() and g.shape[0] == g0.shape[0]
+                 and g.stride(0) == C for g, _ in items)
+             and all(m.untyped_storage().data_ptr() == m0.untyped_storage().data_ptr() and m.shape[1] == m0.shape[1]
+                     for _, m in items)
+             and all(a == c for a, _w, c in spans)
+             and all(spans[i][0] + spans[i][1] == spans[i + 1][0] for i in range(len(spans) - 1))
+             and spans[0][0] == 0 and spans[-1][0] + spans[-1][1] == C)
+    if joint:
+        global JOINT_PRODUCTS
+        JOINT_PRODUCTS += 1
+        gj = torch.as_strided(g0, (g0.shape[0], C), (C, 1), og)
+        mj = torch.as_strided(m0, (C, m0.shape[1]), (1, C), ow)
+        items = [(gj, mj)]
+    for g, m in items:
+        if acc.buf is None:
+            acc.buf = torch.matmul(g, m)
+        else:
+            acc.buf.addmm_(g, m)

@@ -179,12 +179,42 @@ def attach_fp8_weights(model: torch.nn.Module, part_module_name=(".layers",)) ->
     return added
 
 
-def attach_transposed_weights(model: torch.nn.Module) -> int:
+def _attach_joint_qkv(model: torch.nn.Module) -> int:
+    """q/k/v_proj of one attention module (matrix-SMT or plain frozen linears over one input): their
+    transposed copies as column slices [q | k | v] of ONE [in, q + k + v] copy, and the attention
+    module marked (``_smt_joint_qkv_grad``) so that smt_flash hands back [dq | dk | dv] as slices of
+    one buffer: dgrad.py then runs the three data gradients as one GEMM. Returns the bytes added."""
+    added = 0
+    for m in model.modules():
+        lin = [getattr(m, n, None) for n in ("q_proj", "k_proj", "v_proj")]
+        if not all(isinstance(x, LinearLayer_MatrixSparsity) or type(x) is torch.nn.Linear for x in lin):
+            continue
+        ws = [x.weight for x in lin]
+        if (not all(_transposable(w) for w in ws) or len({w.shape[1] for w in ws}) != 1
+                or any(getattr(w, a, None) is not None for w in ws for a in ("_smt_weight_t", "_smt_fp8"))
+                or any(x.bias is not None for x in lin)):
+            continue
+        joint = torch.empty(ws[0].shape[1], sum(w.shape[0] for w in ws), dtype=ws[0].dtype, device=ws[0].device)
+        off = 0
+        for x, w in zip(lin, ws):
+            view = joint[:, off:off + w.shape[0]]
+            view.copy_(w.detach().t())
+            w._smt_weight_t = view
+            off += w.shape[0]
+            if type(x) is torch.nn.Linear:
+                x.forward = _frozen_linear_forward.__get__(x, type(x))
+        m._smt_joint_qkv_grad = True
+        added += joint.numel() * joint.element_size()
+    return added
+
+
+def attach_transposed_weights(model: torch.nn.Module, joint_qkv: bool = True) -> int:
     """Give every frozen bf16 linear weight of ``model`` (SMT modules and plain ``nn.Linear``) a
     transposed contiguous copy ``weight._smt_weight_t`` for the TN data-gradient GEMM, and route
     plain frozen ``nn.Linear`` forwards through :class:`FrozenLinearFn`. Weights that carry fp8
-    copies are skipped. Returns the bytes added."""
-    added = 0
+    copies are skipped. ``joint_qkv``: q/k/v_proj share one copy (:func:`_attach_joint_qkv`).
+    Returns the bytes added."""
+    added = _attach_joint_qkv(model) if joint_qkv else 0
     for m in model.modules():
         if isinstance(m, (LinearLayer_MatrixSparsity, LinearLayer_ChannelSparsity)) or type(m) is torch.nn.Linear:
             w = m.weight
@@ -203,6 +233,8 @@ def attach_transposed_weights(model: torch.nn.Module) -> int:
 def detach_transposed_weights(model: torch.nn.Module) -> None:
     """Undo :func:`attach_transposed_weights`."""
     for m in model.modules():
+        if "_smt_joint_qkv_grad" in m.__dict__:
+            del m.__dict__["_smt_joint_qkv_grad"]
         w = getattr(m, "weight", None)
         for attr in ("_smt_weight_t", "_smt_fp8"):
             if isinstance(w, torch.Tensor) and hasattr(w, attr):
@@ -721,7 +753,10 @@ class SMTEngine:
                 # SMT phase: every linear weight is frozen (tiles change only through the epilogue;
                 # the channel path's rows through LinearLayer_ChannelSparsity.sync_weight, which keeps
                 # W^T in step)
-                self.transposed_bytes = attach_transposed_weights(model)
+                # "joint_qkv_dgrad" (default on; SMT_JOINT_QKV=0 for A/B runs): q/k/v_proj's data
+                # gradients as one GEMM over smt_flash's joint [dq | dk | dv] (dgrad.py)
+                joint = cfg.get("joint_qkv_dgrad", os.environ.get("SMT_JOINT_QKV", "1") != "0")
+                self.transposed_bytes = attach_transposed_weights(model, joint_qkv=joint)
             for group in optimizer.param_groups:
                 mods = [owner[id(p)] for p in group["params"] if id(p) in owner]
                 dense = [p for p in group["params"] if id(p) not in owner and p.requires_grad]

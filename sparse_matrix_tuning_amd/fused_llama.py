@@ -264,9 +264,10 @@ def _rope_desc(inp: torch.Tensor, out: torch.Tensor) -> _hip.RopeTensor:
     return _hip.RopeTensor(inp.data_ptr(), out.data_ptr(), sb, sh, ss, ob, oh, os_, inp.shape[1], 0)
 
 
-def _rope_launch(fn_name, q, k, cos, sin, q_layout=None, k_layout=None):
+def _rope_launch(fn_name, q, k, cos, sin, q_layout=None, k_layout=None, in_place=False):
     """Launch the fused rope kernel on q and k; outputs take ``*_layout`` = (shape, stride) (default:
-    the input's own layout: [B, S, H, D] storage under the [B, H, S, D] view for HF q/k)."""
+    the input's own layout: [B, S, H, D] storage under the [B, H, S, D] view for HF q/k), or
+    overwrite q and k (``in_place``: every thread reads its element pairs before writing them)."""
     B, _Hq, S, D = q.shape
     if cos.dim() != 3 or cos.stride(-1) != 1 or cos.shape != sin.shape or cos.stride() != sin.stride():
         cos, sin = cos.contiguous(), sin.contiguous()
@@ -276,8 +277,11 @@ def _rope_launch(fn_name, q, k, cos, sin, q_layout=None, k_layout=None):
     k = _rope_ready(k)
     qs, qst = q_layout or (q.shape, q.stride())
     ks, kst = k_layout or (k.shape, k.stride())
-    qo = torch.empty_strided(qs, qst, dtype=q.dtype, device=q.device)
-    ko = torch.empty_strided(ks, kst, dtype=k.dtype, device=k.device)
+    if in_place:
+        qo, ko = q, k
+    else:
+        qo = torch.empty_strided(qs, qst, dtype=q.dtype, device=q.device)
+        ko = torch.empty_strided(ks, kst, dtype=k.dtype, device=k.device)
     dq, dk = _rope_desc(q, qo), _rope_desc(k, ko)
     lib = _hip.load()
     rc = getattr(lib, fn_name)(ctypes.byref(dq), ctypes.byref(dk), cos.data_ptr(), sin.data_ptr(), cos.stride(0),
@@ -312,7 +316,11 @@ class FusedRoPEFn(torch.autograd.Function):
             dqo = torch.zeros(ql[0], dtype=torch.bfloat16, device=cos.device)
         if dko is None:
             dko = torch.zeros(kl[0], dtype=torch.bfloat16, device=cos.device)
-        dq, dk = _rope_launch("smt_rope_bwd", dqo, dko, cos, sin, ql, kl)
+        # the flash attention's joint [dq | dk | dv] gradient (FlashAttnFn joint): rotate the q / k
+        # slices in place, so q_proj and k_proj receive slices of the one buffer (dgrad's joint GEMM)
+        joint = (getattr(dqo, "_smt_joint", False) and getattr(dko, "_smt_joint", False)
+                 and _rope_ready(dqo) is dqo and _rope_ready(dko) is dko)
+        dq, dk = _rope_launch("smt_rope_bwd", dqo, dko, cos, sin, ql, kl, in_place=joint)
         return dq, dk, None, None
 
 
@@ -509,7 +517,7 @@ class FlashAttnFn(torch.autograd.Function):
     ``key_mask``: optional :class:`KeyMask` (padded batches)."""
 
     @staticmethod
-    def forward(ctx, q, k, v, scale, key_mask=None):
+    def forward(ctx, q, k, v, scale, key_mask=None, joint=False):
         for t, n in ((q, "q"), (k, "k"), (v, "v")):
             _need(t, "flash attention " + n)
         B, Hq, S, D = q.shape
@@ -537,6 +545,7 @@ class FlashAttnFn(torch.autograd.Function):
         _hip._check(rc, "smt_attn_fwd")
         ctx.save_for_backward(q, k, v, o, lse, key_mask.bits if key_mask is not None else None)
         ctx.scale = float(scale)
+        ctx.joint = bool(joint)
         return o
 
     @staticmethod
@@ -546,9 +555,18 @@ class FlashAttnFn(torch.autograd.Function):
         Hkv = k.shape[1]
         do = do if (do.stride(-1) == 1 and not any(s % 8 for s in do.stride()[:3]) and do.data_ptr() % 16 == 0) \
             else do.contiguous()
-        dq = torch.empty_strided(q.shape, q.stride(), dtype=q.dtype, device=q.device)
-        dk = torch.empty_strided(k.shape, k.stride(), dtype=k.dtype, device=k.device)
-        dv = torch.empty_strided(v.shape, v.stride(), dtype=v.dtype, device=v.device)
+        if ctx.joint:
+            # one [B, S, (Hq + 2 Hkv) D] buffer holding [dq | dk | dv] row by row: q/k/v_proj's data
+            # gradients then run as one GEMM (dgrad.py, the engine's joint transposed copy)
+            J = torch.empty(B, S, (Hq + 2 * Hkv) * D, dtype=q.dtype, device=q.device)
+            dq = J[:, :, :Hq * D].view(B, S, Hq, D).transpose(1, 2)
+            dk = J[:, :, Hq * D:(Hq + Hkv) * D].view(B, S, Hkv, D).transpose(1, 2)
+            dv = J[:, :, (Hq + Hkv) * D:].view(B, S, Hkv, D).transpose(1, 2)
+            dq._smt_joint = dk._smt_joint = True
+        else:
+            dq = torch.empty_strided(q.shape, q.stride(), dtype=q.dtype, device=q.device)
+            dk = torch.empty_strided(k.shape, k.stride(), dtype=k.dtype, device=k.device)
+            dv = torch.empty_strided(v.shape, v.stride(), dtype=v.dtype, device=v.device)
         delta = torch.empty(B, Hq, S, dtype=torch.float32, device=q.device)
         shape = _hip.AttnShape(B, Hq, Hkv, S, ctx.scale, 0)
         T = _attn_tensor
@@ -559,13 +577,14 @@ class FlashAttnFn(torch.autograd.Function):
                                             km.data_ptr() if km is not None else None,
                                             km.shape[1] if km is not None else 0, ctypes.byref(shape), _stream(q))
         _hip._check(rc, "smt_attn_bwd")
-        return dq, dk, dv, None, None
+        return dq, dk, dv, None, None, None
 
 
-def flash_attention(q, k, v, scale=None, key_mask: "KeyMask" = None):
+def flash_attention(q, k, v, scale=None, key_mask: "KeyMask" = None, joint: bool = False):
     """Causal attention ``[B, Hq, S, 128]`` x ``[B, Hkv, S, 128]`` -> ``[B, S, Hq, 128]``; with
-    ``key_mask`` the keys it clears take no part (padded batches)."""
-    return FlashAttnFn.apply(q, k, v, scale if scale is not None else q.shape[-1] ** -0.5, key_mask)
+    ``key_mask`` the keys it clears take no part (padded batches). ``joint``: the gradients of q, k
+    and v go out as slices of one ``[B, S, (Hq + 2 Hkv) * 128]`` buffer (same values)."""
+    return FlashAttnFn.apply(q, k, v, scale if scale is not None else q.shape[-1] ** -0.5, key_mask, joint)
 
 
 def smt_flash_attention_forward(module, query, key, value, attention_mask, dropout=0.0, scaling=None,
@@ -580,7 +599,9 @@ def smt_flash_attention_forward(module, query, key, value, attention_mask, dropo
         raise NotImplementedError("smt_flash attention: dropout is not supported")
     if is_causal is False or not getattr(module, "is_causal", True):
         raise NotImplementedError("smt_flash attention: causal attention only")
-    return flash_attention(query, key, value, scaling, attention_mask), None
+    # the engine marks attention modules whose q/k/v_proj share a joint transposed copy
+    return flash_attention(query, key, value, scaling, attention_mask,
+                           joint=getattr(module, "_smt_joint_qkv_grad", False)), None
 
 
 def smt_flash_mask(batch_size, q_length, kv_length, q_offset=0, kv_offset=0, mask_function=None,

@@ -442,6 +442,51 @@ def test_shared_input_data_gradients_accumulate_once():
         assert _rel(xi.grad, truth) < 5e-3, transposed
 
 
+def test_joint_qkv_data_gradient_is_one_gemm():
+    """q/k/v_proj over one input with a joint transposed copy (engine.attach_transposed_weights) and
+    output gradients that are slices of one [dq | dk | dv] buffer (what smt_flash hands back when the
+    attention module is marked): one joint GEMM (dgrad.JOINT_PRODUCTS), the input gradient within
+    bf16 rounding of the fp64 sum and of the per-consumer path; a partial backward (k dropped) and
+    separate gradient tensors take the per-consumer path."""
+    from sparse_matrix_tuning_amd import dgrad
+    from sparse_matrix_tuning_amd.engine import attach_transposed_weights, detach_transposed_weights
+    torch.manual_seed(14)
+    net = nn.Module()
+    Ws = [nn.Parameter((torch.randn(o, 512) * 0.05).bfloat16().to(DEV), requires_grad=False) for o in (512, 256)]
+    net.q_proj = smt.LinearLayer_MatrixSparsity(Ws[0], index_list=[(1, 1)])
+    net.k_proj = smt.LinearLayer_MatrixSparsity(Ws[1], index_list=[(0, 0)])
+    net.v_proj = nn.Linear(512, 256, bias=False).to(DEV).bfloat16().requires_grad_(False)
+    mods = (net.q_proj, net.k_proj, net.v_proj)
+    x = torch.randn(2, 96, 512).bfloat16().to(DEV)
+    J = torch.randn(2, 96, 1024).bfloat16().to(DEV)
+    gs = [J[..., :512], J[..., 512:768], J[..., 768:]]
+    truth = sum(g.double() @ m.weight.detach().double() for g, m in zip(gs, mods))
+
+    def run(grads, keep=(0, 1, 2)):
+        xi = x.clone().requires_grad_(True)
+        outs = [m(xi) for m in mods]
+        torch.autograd.backward([outs[i] for i in keep], [grads[i] for i in keep])
+        return xi.grad
+
+    assert attach_transposed_weights(net) == 512 * 1024 * 2
+    assert net._smt_joint_qkv_grad
+    wt = [m.weight._smt_weight_t for m in mods]
+    assert all(w.untyped_storage().data_ptr() == wt[0].untyped_storage().data_ptr() for w in wt)
+    n0 = dgrad.JOINT_PRODUCTS
+    joint = run(gs)
+    assert dgrad.JOINT_PRODUCTS == n0 + 1
+    assert _rel(joint, truth) < 5e-3
+    sep = run([g.contiguous() for g in gs])                 # separate tensors: per-consumer products
+    assert dgrad.JOINT_PRODUCTS == n0 + 1
+    assert _rel(joint, sep) < 1e-2
+    part = run(gs, keep=(0, 2))                              # k dropped: the deferred q, v run one by one
+    assert dgrad.JOINT_PRODUCTS == n0 + 1
+    want = gs[0].double() @ mods[0].weight.detach().double() + gs[2].double() @ mods[2].weight.detach().double()
+    assert _rel(part, want) < 5e-3
+    detach_transposed_weights(net)
+    assert not hasattr(net, "_smt_joint_qkv_grad")
+
+
 def test_shared_input_consumer_off_the_loss_keeps_the_others_gradient():
     """one of q/k/v's outputs does not reach the loss; the input gradient is
     still the sum of the two consumers that ran (SMT modules and a frozen nn.Linear, with and without
