@@ -2,6 +2,7 @@
 three GEMMs accumulating through the C operand (what dgrad.py issues: v, then k and q with
 addmm_, on the transposed copies as TN products) vs one joint GEMM over [dq | dk | dv] (T x 6144)
 and the joint transposed copy (4096 x 6144). Interleaved rounds, HIP events."""
+import argparse
 import json
 
 import torch
@@ -20,29 +21,33 @@ def timeit(fn, iters=30):
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--outs", default="4096,1024,1024", help="consumer widths (gate/up: 14336,14336)")
+    outs = tuple(int(v) for v in ap.parse_args().outs.split(","))
     dev = torch.device("cuda", 0)
-    T, H, outs = 32768, 4096, (4096, 1024, 1024)
+    T, H = 32768, 4096
     g = torch.Generator(device=dev).manual_seed(0)
     J = (torch.randn(T, sum(outs), device=dev, generator=g) * 0.01).bfloat16()
     Wt = (torch.randn(H, sum(outs), device=dev, generator=g) * 0.02).bfloat16()      # joint W^T [in, out]
-    offs = [0, outs[0], outs[0] + outs[1], sum(outs)]
-    gs = [J[:, offs[i]:offs[i + 1]].contiguous() for i in range(3)]                 # today's separate grads
-    gv = [J[:, offs[i]:offs[i + 1]] for i in range(3)]                              # views of J
-    wts = [Wt[:, offs[i]:offs[i + 1]].contiguous() for i in range(3)]               # today's separate copies
+    offs = [sum(outs[:i]) for i in range(len(outs) + 1)]
+    n = len(outs)
+    gs = [J[:, offs[i]:offs[i + 1]].contiguous() for i in range(n)]                 # today's separate grads
+    gv = [J[:, offs[i]:offs[i + 1]] for i in range(n)]                              # views of J
+    wts = [Wt[:, offs[i]:offs[i + 1]].contiguous() for i in range(n)]               # today's separate copies
     mats = [w.t() for w in wts]                                                     # (W^T)^T: TN
-    mats_j = [Wt[:, offs[i]:offs[i + 1]].t() for i in range(3)]
+    mats_j = [Wt[:, offs[i]:offs[i + 1]].t() for i in range(n)]
 
-    def sep(gl, ml):
-        buf = torch.matmul(gl[2], ml[2])
-        buf.addmm_(gl[1], ml[1])
-        buf.addmm_(gl[0], ml[0])
+    def sep(gl, ml):                                # backward order: the last consumer first
+        buf = torch.matmul(gl[-1], ml[-1])
+        for i in range(n - 2, -1, -1):
+            buf.addmm_(gl[i], ml[i])
         return buf
 
     def joint():
         return torch.matmul(J, Wt.t())
 
     ref = sep(gs, mats).float()
-    res = {"joint_rel": ((joint().float() - ref).norm() / ref.norm()).item()}
+    res = {"outs": list(outs), "joint_rel": ((joint().float() - ref).norm() / ref.norm()).item()}
     for r in range(3):
         res[f"sep_ms_{r}"] = round(timeit(lambda: sep(gs, mats)), 4)
         res[f"sep_views_ms_{r}"] = round(timeit(lambda: sep(gv, mats_j)), 4)
