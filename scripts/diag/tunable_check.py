@@ -10,7 +10,7 @@ import torch.nn.functional as F
 
 T = 16 * 2048
 SHAPES = {"q/o": (4096, 4096), "k/v": (4096, 1024), "gate/up": (4096, 14336), "down": (14336, 4096),
-          "lm_head": (4096, 128256)}
+          "lm_head": (4096, 128256), "qkv_joint": (4096, 6144)}
 
 
 def main():
@@ -30,9 +30,21 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / n
+        # the data gradient on the transposed copy (g @ (W^T)^T, engine.FrozenLinearFn)
+        gs = [torch.randn(T, fout, device=dev, dtype=torch.bfloat16) for _ in range(3)]
+        wt = w.t().contiguous()
+        for i in range(3):
+            torch.matmul(gs[i], wt.t())
+        torch.cuda.synchronize()
+        e0.record()
+        for i in range(n):
+            torch.matmul(gs[i % 3], wt.t())
+        e1.record()
+        torch.cuda.synchronize()
+        ms_d = e0.elapsed_time(e1) / n
         print(json.dumps({"tag": tag, "shape": name, "in": fin, "out": fout, "ms": round(ms, 4),
-                          "tflops": round(2 * T * fin * fout / ms / 1e9, 1)}), flush=True)
-        del xs, w
+                          "tflops": round(2 * T * fin * fout / ms / 1e9, 1), "dgrad_ms": round(ms_d, 4)}), flush=True)
+        del xs, w, gs, wt
         torch.cuda.empty_cache()
 
 

@@ -11,6 +11,7 @@ import torch.nn.functional as F
 T = 16 * 2048
 H, I, KV, V = 4096, 14336, 1024, 128256
 SHAPES = [(H, H), (H, KV), (H, I), (I, H), (H, V)]      # (in, out): q/o, k/v, gate/up, down, lm_head
+JOINT = [(H, H + 2 * KV)]                                 # the joint q/k/v data gradient (dgrad.py)
 
 
 def main():
@@ -25,6 +26,13 @@ def main():
         torch.cuda.synchronize()
         print(f"tuned in={fin} out={fout}", flush=True)
         del x, w, g, wt
+    for fin, fout in JOINT:
+        g = torch.randn(T, fout, device=dev, dtype=torch.bfloat16)
+        wt = torch.randn(fin, fout, device=dev, dtype=torch.bfloat16) * 0.02
+        torch.matmul(g, wt.t())              # data gradient only
+        torch.cuda.synchronize()
+        print(f"tuned joint dgrad in={fin} out={fout}", flush=True)
+        del g, wt
 
 
 if __name__ == "__main__":
