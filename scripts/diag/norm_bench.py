@@ -50,7 +50,25 @@ def main():
         rc = lib.smt_add_rmsnorm_fwd(P(x), H, P(dres), H, P(w), P(h), H, P(y), H, P(rs), T, H, 1e-5, st)
         assert rc == 0
 
-    out = {"lib": os.path.basename(os.environ.get("SMT_HIP_LIB", "default"))}
+    from sparse_matrix_tuning_amd import fused_llama as fl
+    B, S, D = 16, 2048, 128
+    qh = torch.randn(B, S, 32 * D, device=dev, generator=g).bfloat16().view(B, S, 32, D).transpose(1, 2)
+    kh = torch.randn(B, S, 8 * D, device=dev, generator=g).bfloat16().view(B, S, 8, D).transpose(1, 2)
+    cs = torch.randn(B, S, D, device=dev, generator=g).bfloat16()
+    sn = torch.randn(B, S, D, device=dev, generator=g).bfloat16()
+    rope_out = []
+
+    def rope():
+        rope_out[:] = fl._rope_launch("smt_rope_fwd", qh, kh, cs, sn)
+
+    out = {"lib": os.path.basename(os.environ.get("SMT_HIP_LIB", "default")),
+           "env": {k: v for k, v in os.environ.items() if k.startswith("SMT_ROPE")}}
+    t = timeit(rope)
+    hs = hashlib.sha256()
+    for o in rope_out:
+        hs.update(o.contiguous().view(torch.int16).cpu().numpy().tobytes())
+    out["rope_fwd"] = {"us": round(t * 1e6, 1), "tb_s": round(2 * B * S * 40 * D * 2 / t / 1e12, 2),
+                       "checksum": hs.hexdigest()[:12]}
     for name, fn, nbytes, outs in (("rmsnorm_bwd_add", bwd, 4 * T * H * 2, (dx,)),
                                    ("add_rmsnorm_fwd", fwd, 4 * T * H * 2, (h, y))):
         t = timeit(fn)

@@ -447,6 +447,50 @@ __device__ __forceinline__ void rope_row(const RopeT& t, const uint16_t* cos, co
     st8(op + half + d, ohi);
 }
 
+// Head-grouped variant: a thread rotates the same (s, 8-pair chunk) of kRopeHG consecutive heads, so
+// its cos / sin chunks (4 x 16 B) are loaded once per group instead of once per head (the loads per
+// element pair drop from 6 to 2.5). blockIdx.y = b * (q groups + k groups) + group.
+constexpr int kRopeHG = 8;
+template <bool BWD>
+__global__ __launch_bounds__(256)
+void rope_hg_kernel(RopeT q, RopeT k, const uint16_t* __restrict__ cos, const uint16_t* __restrict__ sin,
+                    int64_t cb, int64_t cs, int S, int D) {
+    const int qg = q.H / kRopeHG, groups = qg + k.H / kRopeHG;
+    const int y = blockIdx.y;
+    const int64_t b = y / groups;
+    const int g = y - (int)b * groups;
+    const RopeT& t = g < qg ? q : k;
+    const int h0 = (g < qg ? g : g - qg) * kRopeHG;
+    const int half = D >> 1;
+    const int cpr = half >> 3;
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    const int s = idx / cpr;
+    if (s >= S) return;
+    const int d = (idx - s * cpr) * 8;
+    const uint16_t* cp = cos + b * cb + (int64_t)s * cs;
+    const uint16_t* sp = sin + b * cb + (int64_t)s * cs;
+    const F8 clo = ld8(cp + d), chi = ld8(cp + half + d), slo = ld8(sp + d), shi = ld8(sp + half + d);
+#pragma unroll 4
+    for (int h = h0; h < h0 + kRopeHG; ++h) {
+        const uint16_t* ip = t.in + b * t.sb + h * t.sh + (int64_t)s * t.ss;
+        uint16_t* op = t.out + b * t.ob + h * t.oh + (int64_t)s * t.os;
+        const F8 lo = ld8(ip + d), hi = ld8(ip + half + d);
+        F8 olo, ohi;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (!BWD) {
+                olo.v[j] = rbf(lo.v[j] * clo.v[j]) + rbf(-hi.v[j] * slo.v[j]);
+                ohi.v[j] = rbf(hi.v[j] * chi.v[j]) + rbf(lo.v[j] * shi.v[j]);
+            } else {
+                olo.v[j] = rbf(lo.v[j] * clo.v[j]) + rbf(hi.v[j] * shi.v[j]);
+                ohi.v[j] = rbf(hi.v[j] * chi.v[j]) - rbf(lo.v[j] * slo.v[j]);
+            }
+        }
+        st8(op + d, olo);
+        st8(op + half + d, ohi);
+    }
+}
+
 template <bool BWD>
 __global__ __launch_bounds__(256)
 void rope_kernel(RopeT q, RopeT k, const uint16_t* __restrict__ cos, const uint16_t* __restrict__ sin,
@@ -916,6 +960,17 @@ static int rope(bool bwd, const smt_rope_tensor* q, const smt_rope_tensor* k, co
     if (rows > 65535 || per_row > 0x7fffffffLL - 255)
         return fail(-1, "smt_rope: %lld (batch x heads) rows of %lld chunks exceed the grid", (long long)rows,
                     (long long)per_row);
+    static const bool hg_on = [] { const char* e = getenv("SMT_ROPE_HG"); return !(e && atoi(e) == 0); }();
+    if (hg_on && q->heads % kRopeHG == 0 && k->heads % kRopeHG == 0) {
+        const dim3 hgrid((unsigned)((per_row + 255) / 256), (unsigned)(B * (q->heads + k->heads) / kRopeHG));
+        if (bwd)
+            hipLaunchKernelGGL(rope_hg_kernel<true>, hgrid, dim3(256), 0, stream, tq, tk, (const uint16_t*)cos,
+                               (const uint16_t*)sin, cos_sb, cos_ss, S, D);
+        else
+            hipLaunchKernelGGL(rope_hg_kernel<false>, hgrid, dim3(256), 0, stream, tq, tk, (const uint16_t*)cos,
+                               (const uint16_t*)sin, cos_sb, cos_ss, S, D);
+        return check_launch("rope_hg_kernel");
+    }
     const dim3 grid((unsigned)((per_row + 255) / 256), (unsigned)rows);
     if (bwd)
         hipLaunchKernelGGL(rope_kernel<true>, grid, dim3(256), 0, stream, tq, tk, (const uint16_t*)cos,

@@ -67,9 +67,11 @@ def _hf_qk(B=2, S=96, Hq=8, Hk=2, D=128):
     return q, k, cos, sin
 
 
-def test_rope_bit_exact_vs_eager_forward_and_backward():
+@pytest.mark.parametrize("Hq,Hk", [(8, 2), (32, 8)])
+def test_rope_bit_exact_vs_eager_forward_and_backward(Hq, Hk):
+    """(32, 8): LLaMA-3-8B's heads, the head-grouped kernel (cos / sin once per 8 heads)."""
     torch.manual_seed(1)
-    q, k, cos, sin = _hf_qk()
+    q, k, cos, sin = _hf_qk(Hq=Hq, Hk=Hk)
     qe, ke = q.clone().requires_grad_(True), k.clone().requires_grad_(True)
     oq_e, ok_e = fl.eager_apply_rotary_pos_emb(qe, ke, cos, sin)
     qf, kf = q.clone().requires_grad_(True), k.clone().requires_grad_(True)
