@@ -23,6 +23,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import weakref
 
 import torch
 from torch import nn
@@ -223,6 +224,22 @@ class FusedAddRMSNormFn(torch.autograd.Function):
 
 
 _RESIDUAL_NORM = os.environ.get("SMT_FUSED_RESIDUAL_NORM", "1") != "0"
+# SMT_FUSED_LAYER_TAIL=0: the MLP residual add stays a separate add before the next layer's input norm
+_LAYER_TAIL = os.environ.get("SMT_FUSED_LAYER_TAIL", "1") != "0"
+
+
+def _recomputed(layer) -> bool:
+    """transformers' per-layer gradient checkpointing is active for ``layer`` (its forward runs again
+    in the backward; the fused tail below must then not span it)."""
+    return bool(getattr(layer, "gradient_checkpointing", False) and layer.training)
+
+
+def _attn_quant(attn, H):
+    """(quant, need_y) of a norm feeding this attention's q/k/v (fp8 consumers), as below."""
+    if H in (1024, 2048, 4096, 8192) and all(hasattr(attn, n) for n in ("q_proj", "k_proj", "v_proj")):
+        from .fp8 import norm_consumers
+        return norm_consumers(attn.q_proj, attn.k_proj, attn.v_proj)
+    return (False, True)
 
 
 def fused_decoder_layer_forward(self, hidden_states, attention_mask=None, position_ids=None, past_key_values=None,
@@ -239,7 +256,13 @@ def fused_decoder_layer_forward(self, hidden_states, attention_mask=None, positi
         q1 = norm_consumers(attn.q_proj, attn.k_proj, attn.v_proj)
         if hasattr(mlp, "gate_proj") and hasattr(mlp, "up_proj"):
             q2 = norm_consumers(mlp.gate_proj, mlp.up_proj)
-    if _RESIDUAL_NORM:
+    # the previous layer may have normalised this input already (its fused tail, below): same values
+    # as the input norm computes here, and its backward sums the residual gradient the same way
+    st = hidden_states.__dict__.pop("_smt_normed", None)
+    if (st is not None and st[0] is norm1.weight and st[1] == q1 and st[3] == hidden_states._version
+            and not _recomputed(self)):
+        residual, hidden_states = hidden_states, st[2]
+    elif _RESIDUAL_NORM:
         hidden_states, residual = FusedRMSNormResFn.apply(hidden_states, norm1.weight, norm1.variance_epsilon, *q1)
     else:
         residual = hidden_states
@@ -250,6 +273,18 @@ def fused_decoder_layer_forward(self, hidden_states, attention_mask=None, positi
     norm = self.post_attention_layernorm
     residual, hidden_states = FusedAddRMSNormFn.apply(hidden_states, residual, norm.weight, norm.variance_epsilon, *q2)
     hidden_states = self.mlp(hidden_states)
+    ref = self.__dict__.get("_smt_next_layer")
+    nxt = ref() if ref is not None else None
+    if _LAYER_TAIL and _RESIDUAL_NORM and nxt is not None and not _recomputed(self) and not _recomputed(nxt):
+        # the MLP residual add fused with the NEXT layer's input RMSNorm (one add+norm pass instead of
+        # an add and a norm): the layer still returns h = residual + mlp_out, with the normalised h
+        # attached for the next layer, which uses it only if it receives this very tensor unchanged
+        qn = _attn_quant(nxt.self_attn, H)
+        if not qn[0]:
+            n1 = nxt.input_layernorm
+            h, y = FusedAddRMSNormFn.apply(hidden_states, residual, n1.weight, n1.variance_epsilon, *qn)
+            h.__dict__["_smt_normed"] = (n1.weight, qn, y, h._version)
+            return h
     return residual + hidden_states
 
 
@@ -688,6 +723,11 @@ def patch_llama(model: nn.Module, attention: bool = True, loss: bool = True) -> 
                 raise NotImplementedError(f"fused MLP: SiLU activation only (got {type(act).__name__})")
             m.forward = fused_mlp_forward.__get__(m, type(m))
             counts["mlp"] += 1
+        elif isinstance(m, nn.ModuleList) and len(m) > 1 and all(isinstance(x, ml.LlamaDecoderLayer) for x in m):
+            # each decoder layer's fused tail normalises for the layer after it (a weak reference:
+            # not a submodule)
+            for i in range(len(m) - 1):
+                m[i].__dict__["_smt_next_layer"] = weakref.ref(m[i + 1])
     ml.apply_rotary_pos_emb = fused_apply_rotary_pos_emb
     return counts
 
@@ -704,3 +744,4 @@ def unpatch_llama(model: nn.Module = None) -> None:
         for m in model.modules():
             if isinstance(m, (ml.LlamaRMSNorm, ml.LlamaMLP, ml.LlamaDecoderLayer)) and "forward" in m.__dict__:
                 del m.__dict__["forward"]
+            m.__dict__.pop("_smt_next_layer", None)

@@ -124,6 +124,43 @@ def test_patched_mini_llama_matches_eager():
     assert worst < 5e-2, worst
 
 
+def test_layer_tail_fusion_is_bit_identical():
+    """The MLP residual add fused with the next layer's input RMSNorm (fused_decoder_layer_forward's
+    tail): loss, every parameter gradient (full fine-tuning: the norm weights too) and the hidden
+    states bit-identical to the separate add + norm; with per-layer recompute on every other layer
+    the tail is not used across a recomputed layer and the results are still identical."""
+    import bench
+
+    def run(tail, ckpt_every_other=False):
+        torch.manual_seed(3)
+        model = bench.build_model("mini", DEV)
+        ids = torch.randint(0, 4096, (2, 256), device=DEV, generator=torch.Generator(device=DEV).manual_seed(4))
+        old = fl._LAYER_TAIL
+        fl._LAYER_TAIL = tail
+        try:
+            fl.patch_llama(model)
+            if ckpt_every_other:
+                model.gradient_checkpointing_enable(gradient_checkpointing_kwargs={"use_reentrant": False})
+                for i, layer in enumerate(model.model.layers):
+                    layer.gradient_checkpointing = i % 2 == 1
+            out = model(input_ids=ids, labels=ids, use_cache=False, output_hidden_states=True)
+            out.loss.backward()
+        finally:
+            fl._LAYER_TAIL = old
+            fl.unpatch_llama(model)
+        return (out.loss.detach(), [h.detach() for h in out.hidden_states],
+                {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None})
+
+    for ckpt in (False, True):
+        l0, h0, g0 = run(False, ckpt)
+        l1, h1, g1 = run(True, ckpt)
+        assert torch.equal(l0, l1), ckpt
+        assert all(torch.equal(a, b) for a, b in zip(h0, h1)), ckpt
+        assert sorted(g0) == sorted(g1)
+        for n in g0:
+            assert torch.equal(g0[n], g1[n]), (ckpt, n)
+
+
 @pytest.mark.parametrize("H", [4096, 512])
 @pytest.mark.parametrize("weight_grad", [False, True])
 def test_fused_add_rmsnorm_vs_eager(H, weight_grad):
