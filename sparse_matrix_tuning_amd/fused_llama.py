@@ -307,7 +307,8 @@ def _rope_launch(fn_name, q, k, cos, sin, q_layout=None, k_layout=None, in_place
     if cos.dim() != 3 or cos.stride(-1) != 1 or cos.shape != sin.shape or cos.stride() != sin.stride():
         cos, sin = cos.contiguous(), sin.contiguous()
     if cos.shape[0] != B:
-        cos, sin = cos.expand(B, -1, -1).contiguous(), sin.expand(B, -1, -1).contiguous()
+        # HF's position embeddings are [1, S, D] for a batch: a zero batch stride instead of B copies
+        cos, sin = cos.expand(B, -1, -1), sin.expand(B, -1, -1)
     q = _rope_ready(q)
     k = _rope_ready(k)
     qs, qst = q_layout or (q.shape, q.stride())
