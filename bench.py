@@ -100,6 +100,11 @@ def parse():
     ap.add_argument("--ref-mode-steps", type=int, default=None,
                     help="after the timed steps, also time this many steps with gradient checkpointing "
                          "(reported under 'grad_ckpt_mode'; default: as many as --steps; 0 disables)")
+    ap.add_argument("--views-steps", type=int, default=None,
+                    help="also time this many steps with the 'views' activation policy (SMT linears keep their "
+                         "whole input, as the reference's ctx.list1 views do, instead of packed copies of the "
+                         "column blocks their tiles read); reported under 'views_mode'; default: as many as "
+                         "--steps; 0 disables")
     ap.add_argument("--selective-steps", type=int, default=None,
                     help="after the timed steps, also time this many steps with the 'selective' activation "
                          "policy (SMT linears fed by RMSNorm / SwiGLU keep no input blocks; the backward rebuilds "
@@ -141,7 +146,11 @@ def parse():
                          "chip with the data-gradient GEMM)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0, help="0 disables the CPU leg")
     ap.add_argument("--out", default=None, help="also write the JSON line here")
-    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm) or gloo (functional tests)")
+    ap.add_argument("--dist-backend", default=None,
+                    help="nccl (= RCCL on ROCm; the default with N > 1) or gloo (functional tests). Given with "
+                         "one rank, a world-1 process group of that backend is created and the engine runs its "
+                         "DP exchange anyway (engine config dp_exchange: always), so the line measures the "
+                         "step with the RCCL all-reduces in it")
     args = ap.parse_args()
     default_ratio = (0.0043 if args.fp8 else 0.00356) if args.model == "llama3-8b" else 0.03
     args.att_ratio = default_ratio if args.att_ratio is None else args.att_ratio
@@ -150,6 +159,8 @@ def parse():
         args.ref_mode_steps = args.steps
     if args.selective_steps is None:
         args.selective_steps = args.steps
+    if args.views_steps is None:
+        args.views_steps = args.steps
     if args.half_resident_steps is None:
         args.half_resident_steps = min(args.steps, 20)
     if args.ref_rounding_steps is None:
@@ -846,7 +857,9 @@ def main():
         launch_check(args, world, rank)
         return
     n_dev = torch.cuda.device_count()
-    if args.dist_backend == "nccl" and world > n_dev:
+    dist_backend = args.dist_backend or "nccl"
+    pg1 = world == 1 and args.dist_backend is not None     # a world-1 group: the exchange runs anyway
+    if dist_backend == "nccl" and world > n_dev:
         # RCCL needs one GPU per rank: never report N ranks that shared fewer devices as N GPUs
         raise SystemExit(f"bench.py: {world} ranks with the nccl (RCCL) backend need {world} GPUs; "
                          f"this node has {n_dev}")
@@ -859,12 +872,14 @@ def main():
     dev_index = local % max(1, n_dev)
     torch.cuda.set_device(dev_index)
     device = torch.device("cuda", dev_index)
-    if world > 1:
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=device)
+    if world > 1 or pg1:
+        kw = {} if (world > 1 or "MASTER_ADDR" in os.environ) else {"store": dist.HashStore(), "rank": 0,
+                                                                  "world_size": 1}
+        if dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=device, **kw)
         else:
-            dist.init_process_group(args.dist_backend)
-    backend = dist.get_backend() if world > 1 else None
+            dist.init_process_group(dist_backend, **kw)
+    backend = dist.get_backend() if dist.is_initialized() else None
     devices_used = n_dev if world > n_dev else world
 
     from sparse_matrix_tuning_amd import _hip
@@ -905,7 +920,8 @@ def main():
     log(f"num_total_blocks={total_blocks} attention budget={n_att} mlp budget={n_mlp}")
 
     # ---- warm-up: full fine-tuning + gradient harvest (fine_tune.py:710-775) ----
-    ds_config = {"gradient_clipping": 1.0, "train_micro_batch_size_per_gpu": B, "train_batch_size": B * world}
+    ds_config = {"gradient_clipping": 1.0, "train_micro_batch_size_per_gpu": B, "train_batch_size": B * world,
+                 "dp_exchange": "always" if pg1 else "auto"}
     smt_config = dict(ds_config, fp8_linears=bool(args.fp8), overlap_wgrad=not args.no_overlap_wgrad,
                       wgrad_batch_tiles=args.wgrad_batch_tiles)
     from sparse_matrix_tuning_amd.smt.smt import _NO_DECAY
@@ -1063,6 +1079,20 @@ def main():
                                         "(smt_colblock_recompute in the backward)")
         _smt.set_activation_policy(old_policy)
         log(f"selective policy: {selective_mode['value']} tokens/s at {selective_mode['peak_hbm_gb']} GB")
+
+    # ---- the "views" activation policy: the SMT linears keep their whole input,
+    # as the reference's ctx.list1 views do (smt.py:351-358), instead of the packed copies of the
+    # column blocks their tiles read (smt_colblock_gather on the wgrad stream, beside the GEMMs) ----
+    views_mode = None
+    if args.views_steps > 0 and not args.grad_ckpt and not args.fp8:
+        from sparse_matrix_tuning_amd.smt import smt as _smt
+        old_policy = _smt.set_activation_policy("views")
+        views_mode = policy_point(args.views_steps, 65000, "views")
+        views_mode["kept"] = "every SMT linear's whole input (no column-block copies)"
+        views_mode["median_step_vs_headline"] = round(views_mode["median_ms_per_step"] / (med * 1e3), 4)
+        _smt.set_activation_policy(old_policy)
+        log(f"views policy: {views_mode['value']} tokens/s at {views_mode['peak_hbm_gb']} GB "
+            f"(median step x{views_mode['median_step_vs_headline']})")
 
     # ---- the other tile-gradient rounding, same engine and tiles: the headline
     # runs the engine's default, the reference's per-sample bf16 partials (smt.py:397-404); this point
@@ -1254,6 +1284,7 @@ def main():
                           "band": sel_timer.reports},
             "grad_ckpt_mode": ckpt_mode, "grad_ckpt_half_resident_mode": half_mode,
             "selective_mode": selective_mode,
+            "views_mode": views_mode,
             "wgrad_rounding_alt_mode": alt_round_mode,
             "raw_harvest_mode": raw_mode,
             "tile_distribution": tile_distribution(sel_mlp, sel_att),
@@ -1275,7 +1306,7 @@ def main():
         if args.out:
             with open(args.out, "w") as f:
                 f.write(line + "\n")
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

@@ -211,17 +211,43 @@ def channel_hook_accumulate(feat: dict, key, x: torch.Tensor) -> None:
         feat[key] += a
 
 
-def channel_hook_accumulate_ranks(feat: dict, key, xs: Sequence[torch.Tensor]) -> None:
+def bf16_rank_sum(xs: Sequence[torch.Tensor], order=None) -> torch.Tensor:
+    """The bf16 sum over ranks of a bf16 ``all_reduce`` (fine_tune.py:655-657), every addition rounded
+    to bf16 as a collective's bf16 reduction does: ``order`` is a list of rank indices summed left to
+    right (default ``range(len(xs))``) or ``"pairwise"`` (a balanced tree: (x0 + x1) + (x2 + x3) ...).
+    For two ranks every order gives the same bits (bf16 addition is commutative); from three ranks on
+    the result depends on the order, which is the collective library's (NCCL / RCCL / gloo) internal
+    choice -- per element, since ring algorithms start each chunk's reduction at a different rank."""
+    xs = [x.to(torch.float32) for x in xs]
+    rnd = lambda t: t.to(torch.bfloat16).to(torch.float32)
+    if order == "pairwise":
+        level = xs
+        while len(level) > 1:
+            nxt = [rnd(level[i] + level[i + 1]) for i in range(0, len(level) - 1, 2)]
+            if len(level) % 2:
+                nxt.append(level[-1])
+            level = nxt
+        return level[0]
+    order = list(range(len(xs))) if order is None else list(order)
+    if sorted(order) != list(range(len(xs))):
+        raise ValueError(f"order {order} is not a permutation of {len(xs)} ranks")
+    acc = xs[order[0]]
+    for r in order[1:]:
+        acc = rnd(acc + xs[r])
+    return acc
+
+
+def channel_hook_accumulate_ranks(feat: dict, key, xs: Sequence[torch.Tensor], order=None) -> None:
     """fine_tune.py:651-665 cache_input_hook at world size len(xs): every rank's ``|x|`` in bf16,
-    ``all_reduce`` (sum) in bf16 -- restated for two ranks, where the collective's one addition is
-    ``bf16(fp32(a) + fp32(b))`` whatever its order -- then fp32 on the CPU, first step assigns, later
-    steps ``+=``. Rank counts above 2 depend on the collective's summation order (external)."""
+    ``all_reduce`` (sum) in bf16, then fp32 on the CPU, first step assigns, later steps ``+=``. For two
+    ranks the collective's one addition is ``bf16(fp32(a) + fp32(b))`` whatever its order; from three
+    ranks on the caller names the summation order (:func:`bf16_rank_sum`): the reference's result
+    then depends on its collective's internal order (external, unpinned)."""
     if len(xs) == 1:
         return channel_hook_accumulate(feat, key, xs[0])
-    if len(xs) != 2:
-        raise NotImplementedError("the bf16 rank sum is restated for two ranks")
-    a, b = (x.detach().cpu().abs() for x in xs)
-    s = (a.to(torch.float32) + b.to(torch.float32)).to(torch.bfloat16).to(torch.float32)
+    if len(xs) > 2 and order is None:
+        raise NotImplementedError("above two ranks the bf16 rank sum depends on the collective's order: name one")
+    s = bf16_rank_sum([x.detach().cpu().abs() for x in xs], order)
     if key not in feat:
         feat[key] = s
     else:

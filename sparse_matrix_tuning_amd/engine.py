@@ -46,10 +46,6 @@ from . import _hip, dgrad
 from .smt.smt import LinearLayer_ChannelSparsity, LinearLayer_MatrixSparsity
 
 TILE_ELEMS = _hip.TILE_ELEMS
-# the engine's tile-gradient rounding unless its config names one (smt.WGRAD_ROUNDINGS): the
-# reference's per-sample bf16 partials (smt.py:397-404), so the trained tiles follow the reference's
-# arithmetic; "single" keeps fp32 over the whole batch (closer to exact, 1e-5 of fp64 in the sink)
-ENGINE_WGRAD_ROUNDING = os.environ.get("SMT_ENGINE_WGRAD_ROUNDING", "reference")
 
 
 class SMTFusedAdam(torch.optim.Optimizer):
@@ -456,6 +452,7 @@ class TileGradBuckets:
         self.armed = False
         self.side_stream = None                # the engine's wgrad stream (where the kernels run)
         self.comm_stream = None                # the collectives are issued from here (device buffers)
+        self.issued = 0                        # collectives issued since construction (diagnostics)
 
     def arm(self) -> None:
         self.pending = [b[2] for b in self.buckets]
@@ -486,6 +483,7 @@ class TileGradBuckets:
         flat = self.buffer[start:end]
         if flat.device.type != "cuda":
             self.works[b] = dist.all_reduce(flat, async_op=True)
+            self.issued += 1
             return
         if self.comm_stream is None:
             self.comm_stream = torch.cuda.Stream(flat.device)
@@ -496,6 +494,7 @@ class TileGradBuckets:
         self.comm_stream.wait_event(ev)
         with torch.cuda.stream(self.comm_stream):
             self.works[b] = dist.all_reduce(flat, async_op=True)
+        self.issued += 1
 
     def finish(self) -> None:
         if not self.armed:
@@ -551,6 +550,7 @@ class DenseGradBuckets:
         self.armed = False
         self.works: list = []
         self.flats: list = []
+        self.issued = 0                          # collectives issued since construction (diagnostics)
 
     def arm(self) -> None:
         self.pending = [len(b) for b in self.buckets]
@@ -605,6 +605,7 @@ class DenseGradBuckets:
             if id(p) not in self.seen:          # no gradient on this rank in this step: zeros
                 self._pack(p)
         self.works[b] = dist.all_reduce(self.flats[b], async_op=True)
+        self.issued += 1
         dp_trace()("dense_issue", bucket=b, numel=self.flats[b].numel())
 
     def finish(self) -> None:
@@ -707,7 +708,16 @@ class SMTEngine:
         self.lr_scheduler = lr_scheduler
         cfg = dict(config or {})
         self.config = cfg
-        self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+        pg = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size() if pg else 1
+        # "dp_exchange": "auto" (default) runs the DP exchange (bucketed all-reduce of the tile and, in
+        # the warm-up, dense gradients) when there is more than one rank; "always" whenever a process
+        # group exists, also at world 1 -- the RCCL collectives and their stream / event ordering then
+        # run on a single GPU (the result equals the run without a process group bit for bit)
+        self.dp_exchange = cfg.get("dp_exchange", "auto")
+        if self.dp_exchange not in ("auto", "always"):
+            raise ValueError(f"dp_exchange {self.dp_exchange!r}: 'auto' or 'always'")
+        self.exchange = pg and (self.world > 1 or self.dp_exchange == "always")
         micro = cfg.get("train_micro_batch_size_per_gpu")
         total = cfg.get("train_batch_size")
         gas = cfg.get("gradient_accumulation_steps")
@@ -715,16 +725,18 @@ class SMTEngine:
             gas = max(1, int(total) // (int(micro) * self.world)) if (micro and total) else 1
         self.gradient_accumulation_steps = int(gas)
         self.max_grad_norm = float(cfg.get("gradient_clipping", 0.0) or 0.0)
-        # this engine's own modes (None: the global smt.set_wgrad_rounding / set_activation_policy);
-        # linearZ reads them through the modules' gradient sinks, so they end with the engine.
-        # "wgrad_rounding": "reference" rounds the tile gradients as smt.py:397-404 does (per-sample
-        # bf16 partials); "activation_policy": "selective" keeps no input blocks for SMT linears fed by
-        # a norm / SwiGLU (the backward rebuilds them)
-        # Default: the reference's rounding on the bf16 tile path (its cost is within the bench's noise:
-        # the tile wgrad runs off the critical path, profiles/r04_*), "single" with fp8 weights (the
-        # MX-fp8 tile gradient sums e4m3 products over all rows: no per-sample bf16 partials exist)
+        # this engine's own modes; linearZ reads them through the modules' gradient sinks, so they
+        # end with the engine. "wgrad_rounding": "reference" rounds the tile gradients as
+        # smt.py:397-404 does (per-sample bf16 partials), "single" sums in fp32 over the whole batch;
+        # without the key the engine takes the global mode (smt.set_wgrad_rounding /
+        # SMT_WGRAD_ROUNDING, "reference" by default) when it is created, and "single" with fp8
+        # weights (the MX-fp8 tile gradient sums e4m3 products over all rows: no per-sample bf16
+        # partials exist). "activation_policy" (None: the global smt.set_activation_policy):
+        # "selective" keeps no input blocks for SMT linears fed by a norm / SwiGLU (the backward
+        # rebuilds them)
         from .smt import smt as _smt
-        self.wgrad_rounding = cfg.get("wgrad_rounding", "single" if cfg.get("fp8_linears") else ENGINE_WGRAD_ROUNDING)
+        self.wgrad_rounding = cfg.get("wgrad_rounding",
+                                      "single" if cfg.get("fp8_linears") else _smt.wgrad_rounding())
         self.activation_policy = cfg.get("activation_policy")
         _smt.register_engine_modes(self, self.wgrad_rounding, self.activation_policy)
         self.micro_steps = 0
@@ -764,7 +776,7 @@ class SMTEngine:
                     if any(m.weight.dtype != torch.bfloat16 for m in mods):
                         raise NotImplementedError("SMT engine: bf16 models only")
                     self.tile_groups.append(_TileGroup(group, mods, self.device, self,
-                                                       self.reduce_bucket_size if self.world > 1 else None))
+                                                       self.reduce_bucket_size if self.exchange else None))
                 if dense:
                     self.dense_groups.append((group, dense))
         self._set_mx_unions()
@@ -788,7 +800,7 @@ class SMTEngine:
                 tg.buckets.side_stream = self.wgrad_stream
         dense_params = [p for _g, ps in self.dense_groups for p in ps]
         self.dense_buckets = (DenseGradBuckets(dense_params, self.reduce_bucket_size, self.world)
-                              if self.world > 1 and dense_params else None)
+                              if self.exchange and dense_params else None)
 
     def _set_mx_unions(self) -> None:
         """fp8 groups (q/k/v, gate/up) whose members run MX-fp8 tile gradients share one quantised
@@ -843,7 +855,7 @@ class SMTEngine:
         if self.gradient_accumulation_steps > 1:
             loss = loss / self.gradient_accumulation_steps
         boundary = self.is_gradient_accumulation_boundary()
-        exchange = boundary and self.world > 1
+        exchange = boundary and self.exchange
         if exchange:
             for tg in self.tile_groups:
                 tg.buckets.arm()                # tile buckets all-reduce while backward runs

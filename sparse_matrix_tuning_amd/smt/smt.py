@@ -16,11 +16,15 @@ Differences from the reference, all deliberate:
 
 * no process-group initialisation or rank query at import (smt.py:20-21);
 * no ``print_rank_0`` spam;
-* by default the wgrad sums the whole batch in fp32 and rounds once, where the reference rounds
-  every per-sample ``[256, 256]`` partial to bf16 before summing (smt.py:397-404), so tile
-  gradients are closer to exact than the reference's. :func:`set_wgrad_rounding("reference")`
-  (or ``SMT_WGRAD_ROUNDING=reference``, or the engine config key ``"wgrad_rounding"``) reproduces
-  the reference's rounding instead (``smt_tile_wgrad_batch_seq``; tests/test_gpu_wgrad_full.py).
+* the tile-gradient rounding follows the reference by default: every per-sample ``[256, 256]``
+  partial is rounded to bf16 and the partials are summed in sample order (smt.py:397-404,
+  ``smt_tile_wgrad_batch_seq``; tests/test_gpu_wgrad_full.py). :func:`set_wgrad_rounding("single")`
+  (or ``SMT_WGRAD_ROUNDING=single``) sums the whole batch in fp32 and rounds once instead, which is
+  closer to exact than the reference. Those two are the global switch; an engine's config key
+  ``"wgrad_rounding"`` overrides it for that engine's modules only (an engine without the key takes
+  the global mode at its creation, and "single" for fp8 weights). The MX-fp8 tile gradient (config 5)
+  sums e4m3 products over all rows and has no per-sample partials: the global mode does not apply to
+  it, and an engine that asks for "reference" on it raises.
 
 There is no CPU or eager-PyTorch path: a module built on CPU tensors raises. ``meta`` tensors are
 accepted for shape-only construction (used by the CPU tests of the conversion logic).
@@ -40,10 +44,11 @@ Block_dimension = 256
 
 _LAYER_PATTERN = re.compile(r'model\.layers\.(\d+)\.')
 
-# Tile-gradient rounding of linearZ.backward: "single" (fp32 over the whole batch, one rounding) or
-# "reference" (smt.py:397-404: every per-sample partial rounded to bf16, then the batch sum)
+# Tile-gradient rounding of linearZ.backward: "reference" (the default, smt.py:397-404: every
+# per-sample partial rounded to bf16, then the batch sum) or "single" (fp32 over the whole batch, one
+# rounding)
 WGRAD_ROUNDINGS = ("single", "reference")
-_wgrad_rounding = os.environ.get("SMT_WGRAD_ROUNDING", "single")
+_wgrad_rounding = os.environ.get("SMT_WGRAD_ROUNDING", "reference")
 if _wgrad_rounding not in WGRAD_ROUNDINGS:
     raise ValueError(f"SMT_WGRAD_ROUNDING={_wgrad_rounding!r}: one of {WGRAD_ROUNDINGS}")
 
@@ -65,8 +70,10 @@ def wgrad_rounding() -> str:
 # of it): "resident" (the input, or a packed copy of its column blocks when the tiles touch at most
 # half of them), "selective" (when the input is an RMSNorm's or SwiGLU's output produced by
 # fused_llama, nothing: the backward rebuilds the column blocks from the producer's own saved
-# operands with smt_colblock_recompute; bit-identical tile gradients)
-ACTIVATION_POLICIES = ("resident", "selective")
+# operands with smt_colblock_recompute), "views" (the input itself, always: the reference's views
+# of it, which keep the whole input alive, and no copy). Tile gradients are bit-identical under all
+# three (same operands, same kernel, same order).
+ACTIVATION_POLICIES = ("resident", "selective", "views")
 _activation_policy = os.environ.get("SMT_ACTIVATION_POLICY", "resident")
 if _activation_policy not in ACTIVATION_POLICIES:
     raise ValueError(f"SMT_ACTIVATION_POLICY={_activation_policy!r}: one of {ACTIVATION_POLICIES}")
@@ -466,7 +473,8 @@ class linearZ(torch.autograd.Function):
         ctx.tiles = tiles
         ctx.sink = getattr(selected_weight, "_smt_grad_sink", None)
         # the engine's own modes when its config names them, else the global ones
-        rounding = _engine_mode(ctx.sink, "wgrad_rounding") or _wgrad_rounding
+        engine_rounding = _engine_mode(ctx.sink, "wgrad_rounding")
+        rounding = engine_rounding or _wgrad_rounding
         policy = _engine_mode(ctx.sink, "activation_policy") or _activation_policy
         # reference rounding: each of the input's B sequences (S rows) is one sample of smt.py:397-404
         ctx.seq_len = int(input.shape[1]) if (rounding == "reference" and len(tiles)) else None
@@ -480,10 +488,12 @@ class linearZ(torch.autograd.Function):
                 and input.device.type == "cuda"):
             # fp8 path: the tile weight gradient runs on MX-fp8 operands; keep only the input's
             # column blocks, quantised (half the bytes of the bf16 blocks)
-            if ctx.seq_len is not None:
+            if engine_rounding == "reference":
                 # the MX kernel sums e4m3 products over all T rows: it has no per-sample bf16 partials
                 raise RuntimeError("linearZ: the reference wgrad rounding (smt.py:397-404) exists on the bf16 tile "
                                    "path only; with fp8 weights set SMT_FP8_TILE_WGRAD=bf16 or use rounding 'single'")
+            # the global mode is the bf16 tiles' (the reference has no fp8 path whose rounding to follow)
+            ctx.seq_len = None
             grp = fw.group
             x2d = _rows_ready(input.reshape(-1, weight.shape[1]))
             if grp is not None and grp.mx_union is not None:
@@ -502,7 +512,7 @@ class linearZ(torch.autograd.Function):
             ctx.recompute = _recompute_source(input)
             saved = None
             ctx.packed = True
-        elif (ctx.needs_input_grad[1] and len(tiles) and input.device.type == "cuda"
+        elif (policy != "views" and ctx.needs_input_grad[1] and len(tiles) and input.device.type == "cuda"
                 and 2 * len(tiles.column_blocks()) <= in_blocks):
             cb_dev, _ = tiles.packed_tables(input.device)
             x2d = _rows_ready(input.reshape(-1, weight.shape[1]))

@@ -12,6 +12,10 @@ step (fused clip + AdamW), of a 2-layer mini-LLaMA (fused HIP ops, smt_flash att
 * ``acc``: 1 rank, the same two micro-batches as 2 gradient-accumulation micro-steps;
 * ``big``: 1 rank, the concatenated micro-batch of 4.
 
+``--pg nccl --exchange always`` (with ``big``, under ``torch.distributed.run --nproc-per-node 1``): a
+world-1 RCCL process group and the engine's ``"dp_exchange": "always"``, so the bucketed RCCL
+all-reduces of the dense warm-up gradients and the tile gradients run (identities at world 1).
+
 ``--fp8``: the SMT phase on the fp8 path (e4m3 decoder GEMMs, MX-fp8 tile weight gradients).
 
 Writes the post-warm-up weights, the selection, the tile optimizer state and the SMT modules'
@@ -35,13 +39,19 @@ def main():
     ap.add_argument("--mode", choices=("dp", "acc", "big"), required=True)
     ap.add_argument("--out", required=True)
     ap.add_argument("--fp8", action="store_true", help="SMT phase on the fp8 path (MX-fp8 tile gradients)")
+    ap.add_argument("--pg", default=None, help="process-group backend (default: gloo when WORLD_SIZE > 1)")
+    ap.add_argument("--exchange", default="auto", choices=("auto", "always"), help="the engine's dp_exchange")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
-    if world > 1:
-        dist.init_process_group("gloo")
+    if world > 1 or args.pg:
+        backend = args.pg or "gloo"
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     import bench
     from sparse_matrix_tuning_amd import trainer
@@ -68,7 +78,8 @@ def main():
 
     micro = 4 if args.mode == "big" else 2
     ds = {"gradient_clipping": 1.0, "train_micro_batch_size_per_gpu": micro, "train_batch_size": 4,
-          "reduce_bucket_size": 300000}                 # several buckets on this small model
+          "reduce_bucket_size": 300000,                 # several buckets on this small model
+          "dp_exchange": args.exchange}
     dims = trainer.get_targeted_module_dims(model)
     n_att, n_mlp = trainer.block_budgets(trainer.count_total_blocks(model), 0.05, 0.05)
     opt = SMTFusedAdam(model.parameters(), lr=1e-3, betas=(0.9, 0.95))
@@ -80,6 +91,7 @@ def main():
             harvester.harvest()                          # the DP-averaged (accumulated) gradients
         engine.step()
     warm = {n: p.detach().cpu().clone() for n, p in model.named_parameters()}
+    dense_issued = engine.dense_buckets.issued if engine.dense_buckets is not None else 0
     engine, opt, sched, sel_mlp, sel_att = trainer.select_and_convert(
         engine, harvester, dims, n_att, n_mlp, calculate_strategy="abs_mean", smt_lr=1e-3, num_training_steps=10,
         ds_config=dict(ds, fp8_linears=args.fp8))
@@ -94,10 +106,13 @@ def main():
            "master": tg.master.cpu(), "exp_avg": tg.exp_avg.cpu(), "exp_avg_sq": tg.exp_avg_sq.cpu(),
            "W": {n: m.weight.detach().cpu().clone() for n, m in model.named_modules()
                  if isinstance(m, LinearLayer_MatrixSparsity)},
-           "buckets": len(tg.buckets.buckets) if tg.buckets is not None else 0}
+           "buckets": len(tg.buckets.buckets) if tg.buckets is not None else 0,
+           "tile_issued": tg.buckets.issued if tg.buckets is not None else 0, "dense_issued": dense_issued,
+           "backend": dist.get_backend() if dist.is_initialized() else None,
+           "world": dist.get_world_size() if dist.is_initialized() else 1}
     if rank == 0:
         torch.save(out, args.out)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

@@ -73,9 +73,8 @@ def test_flash_attention_matches_fp32_reference(B, Hq, Hkv, S, layout):
 
 
 def test_flash_attention_score_far_above_the_first_tiles():
-    """A late key whose score beats every earlier one by ~95 in log2 units: kernels that fix each row's
-    exponent base early (the one-wave-per-SIMD forward, SMT_ATTN_FWD=4) must take their second pass;
-    the others move their running max. Output, gradients and lse as the main test."""
+    """A late key whose score beats every earlier one by ~95 in log2 units: the forward's deferred
+    running max must move (a rescale of O and l). Output, gradients and lse as the main test."""
     torch.manual_seed(11)
     B, Hq, Hkv, S, D = 1, 4, 2, 512, 128
     mk = lambda H: torch.randn(B, S, H, D, device=DEV).bfloat16().transpose(1, 2)

@@ -99,3 +99,36 @@ def test_dp2_equals_gradient_accumulation_fp8_mx(tmp_path):
         assert torch.equal(dp[k], acc[k]), k
     for n in acc["W"]:
         assert torch.equal(dp["W"][n], acc["W"][n]), n
+
+
+def test_rccl_world1_exchange_bit_identical_to_no_process_group(tmp_path):
+    """the engine's DP exchange through RCCL itself. One rank under
+    torch.distributed.run with the nccl backend (= RCCL) and ``"dp_exchange": "always"``: the dense
+    warm-up gradients and the packed tile gradients go through the bucketed all-reduces (issued from the
+    comm stream behind per-bucket events; RCCL's ``Work.wait()`` orders the current stream instead of
+    blocking the host as gloo's does). At world 1 the sum is the identity, so the state must equal the
+    run without a process group bit for bit (``fine_tune.py:81``, ``smt.py:20``: the reference's NCCL)."""
+    outs = {}
+    for mode in ("plain", "rccl"):
+        out = str(tmp_path / f"{mode}.pt")
+        if mode == "rccl":
+            cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                   "--master-addr", "127.0.0.1", "--master-port", str(_port()), WORKER, "--mode", "big",
+                   "--pg", "nccl", "--exchange", "always", "--out", out]
+        else:
+            cmd = [sys.executable, WORKER, "--mode", "big", "--out", out]
+        env = dict(os.environ, PYTHONPATH=ROOT)
+        r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
+        assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+        outs[mode] = torch.load(out, weights_only=True)
+    plain, rccl = outs["plain"], outs["rccl"]
+    assert rccl["backend"] == "nccl" and rccl["world"] == 1 and plain["backend"] is None
+    assert rccl["buckets"] > 1 and rccl["tile_issued"] == rccl["buckets"]     # one SMT step, every bucket
+    assert rccl["dense_issued"] > 1 and plain["tile_issued"] == plain["dense_issued"] == 0
+    for n in plain["warm"]:
+        assert torch.equal(rccl["warm"][n], plain["warm"][n]), n
+    assert rccl["sel_mlp"] == plain["sel_mlp"] and rccl["sel_att"] == plain["sel_att"]
+    for k in ("master", "exp_avg", "exp_avg_sq"):
+        assert torch.equal(rccl[k], plain[k]), k
+    for n in plain["W"]:
+        assert torch.equal(rccl["W"][n], plain["W"][n]), n

@@ -83,6 +83,31 @@ def test_rope_bit_exact_vs_eager_forward_and_backward(Hq, Hk):
     assert torch.equal(qf.grad, qe.grad) and torch.equal(kf.grad, ke.grad)
 
 
+@pytest.mark.parametrize("Hq,Hk", [(8, 2), (32, 8)])
+def test_rope_shared_cos_sin_zero_batch_stride(Hq, Hk):
+    """HF hands one [1, S, D] cos / sin for the whole batch: the fused RoPE reads it with a zero
+    batch stride (fused_llama._rope_launch) instead of B materialised copies -- bit-identical to the
+    copies, forward and backward, for B = 4."""
+    torch.manual_seed(3)
+    B = 4
+    q, k, cos, sin = _hf_qk(B=B, Hq=Hq, Hk=Hk)
+    cos1, sin1 = cos[:1].clone(), sin[:1].clone()           # [1, S, D], as LlamaRotaryEmbedding returns
+    outs = []
+    for c, s in ((cos, sin), (cos1, sin1)):
+        qf, kf = q.clone().requires_grad_(True), k.clone().requires_grad_(True)
+        oq, ok = fl.fused_apply_rotary_pos_emb(qf, kf, c, s)
+        gq = torch.arange(oq.numel(), device=DEV).remainder(97).view_as(oq).bfloat16() / 97
+        gk = torch.arange(ok.numel(), device=DEV).remainder(89).view_as(ok).bfloat16() / 89
+        (oq.float() * gq.float()).sum().add((ok.float() * gk.float()).sum()).backward()
+        outs.append((oq, ok, qf.grad, kf.grad))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    # and both equal transformers' own rotary on the [1, S, D] embeddings
+    qe, ke = q.clone(), k.clone()
+    oq_e, ok_e = fl.eager_apply_rotary_pos_emb(qe, ke, cos1, sin1)
+    assert torch.equal(outs[1][0], oq_e) and torch.equal(outs[1][1], ok_e)
+
+
 def test_swiglu_vs_eager():
     torch.manual_seed(2)
     g = (torch.randn(4, 100, 1536, device=DEV) * 3).bfloat16()

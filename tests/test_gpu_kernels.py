@@ -254,7 +254,9 @@ def test_linearz_packed_input_grads_bit_identical():
     assert y.grad_fn.packed
     y.backward(g)
     direct = torch.empty(len(tiles) * 256, 256, dtype=torch.bfloat16, device=DEV)
-    _hip.tile_wgrad(g.reshape(-1, out_f), x.detach().reshape(-1, in_f), _hip.tile_table(tiles, torch.device(DEV)), direct)
+    seq = S if smt.wgrad_rounding() == "reference" else None     # the module's rounding (smt.py:397-404)
+    _hip.tile_wgrad(g.reshape(-1, out_f), x.detach().reshape(-1, in_f), _hip.tile_table(tiles, torch.device(DEV)), direct,
+                    seq_len=seq)
     assert torch.equal(mod.selected_weight.grad, direct)
     assert torch.equal(x.grad, torch.matmul(g, W.detach()))
     wide = [(0, c) for c in range(5)]                   # 5 of 8 blocks -> the input itself is saved

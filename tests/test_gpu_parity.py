@@ -342,7 +342,19 @@ def test_engine_config_rounding_is_engine_scoped():
     assert _rel(bufs["reference"], ref_gw) <= 1e-3
     assert _rel(bufs["single"], truth) < 1e-5
     assert not torch.equal(bufs["reference"], bufs["single"])
-    assert torch.equal(bufs[None], bufs["reference"])            # the engine's default
+    assert torch.equal(bufs[None], bufs[before])                 # no key: the global mode
+    # an engine without the key takes the global mode at its creation
+    old = smt.set_wgrad_rounding("single" if before == "reference" else "reference")
+    try:
+        mod = smt.LinearLayer_MatrixSparsity(nn.Parameter(W0.to(DEV)), index_list=tiles)
+        engine, _, _, _ = initialize(model=mod, optimizer=SMTFusedAdam([mod.selected_weight], lr=1e-3), config={})
+        assert engine.wgrad_rounding == smt.wgrad_rounding() != before
+        engine.backward((mod(x.to(DEV)).float() * g.to(DEV).float()).sum())
+        torch.cuda.synchronize()
+        other = "single" if before == "reference" else "reference"
+        assert torch.equal(mod.selected_weight._smt_grad_sink.buffer, bufs[other])
+    finally:
+        smt.set_wgrad_rounding(old)
     # fp8 + MX tile gradients + reference rounding: refused
     W = nn.Parameter(W0.to(DEV), requires_grad=False)
     W._smt_fp8 = f8.Fp8Weight(W)
@@ -352,6 +364,38 @@ def test_engine_config_rounding_is_engine_scoped():
         engine, _, _, _ = initialize(model=mod, optimizer=opt, config={"wgrad_rounding": "reference"})
         with pytest.raises(RuntimeError, match="reference wgrad rounding"):
             mod(x.to(DEV))
+
+
+def test_autograd_tile_grads_follow_the_reference_rounding_without_engine():
+    """the unchanged drop-in (fine_tune.py + DeepSpeed FusedAdam, no SMT engine)
+    gets bf16 ``selected_weight.grad`` from autograd. By default those are rounded as smt.py:397-404
+    rounds them (per-sample bf16 partials summed in sample order), within north_star's 1e-3 of the
+    reference algorithm at B = 16, where the single rounding lands 2-3e-3 away."""
+    assert smt.wgrad_rounding() == os.environ.get("SMT_WGRAD_ROUNDING", "reference")
+    torch.manual_seed(23)
+    tiles = [(1, 2), (0, 0), (3, 1), (1, 0)]
+    W0 = (torch.randn(1024, 768) * 0.05).bfloat16()
+    x = torch.randn(16, 256, 768).bfloat16()
+    g = torch.randn(16, 256, 1024).bfloat16()
+    _gi, ref_gw = ref.linearz_backward(g, x, W0, tiles)
+    got = {}
+    for mode in ("reference", "single"):
+        old = smt.set_wgrad_rounding(mode)
+        try:
+            mod = smt.LinearLayer_MatrixSparsity(nn.Parameter(W0.to(DEV)), index_list=tiles)
+            xd = x.to(DEV).requires_grad_(True)
+            (mod(xd).float() * g.to(DEV).float()).sum().backward()
+            torch.cuda.synchronize()
+            gw = mod.selected_weight.grad
+            assert gw.dtype == torch.bfloat16 and gw.shape == ref_gw.shape
+            got[mode] = gw.cpu()
+            assert _rel(xd.grad.cpu(), g.float() @ W0.float()) < 1e-2
+        finally:
+            smt.set_wgrad_rounding(old)
+    err_ref, err_single = _rel(got["reference"], ref_gw), _rel(got["single"], ref_gw)
+    print(f"\nvs oracle.linearz_backward at B 16: reference rounding {err_ref:.2e}, single {err_single:.2e}")
+    assert err_ref <= 1e-3
+    assert err_single > 2 * err_ref
 
 
 # ------------------------------------------------------------------ end to end: mini LLaMA vs oracle

@@ -60,7 +60,7 @@ def _build(device, cfg_dict):
 def test_layer_loss_and_tile_grads_vs_reference_restatement(case, rounding):
     """Also the direct product-vs-restatement difference of every module's tile gradients
     (oracle.linearz_backward on the module's own operands): <= 1e-3 with the reference-rounding mode
-    (smt.set_wgrad_rounding("reference")), <= 1.5 x the reference's own error by default."""
+    (the default), <= 1.5 x the reference's own error with smt.set_wgrad_rounding("single")."""
     old = smt.set_wgrad_rounding(rounding)
     try:
         _layer_case(case, rounding)

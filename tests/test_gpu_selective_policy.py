@@ -127,17 +127,20 @@ def test_selective_policy_same_tile_grads_less_memory():
         ids = torch.randint(1, CFG["vocab_size"], (2, 1024), generator=gen).to(DEV)
         loss_r, grads_r, held_r = _step(model, ids, "resident")
         loss_s, grads_s, held_s = _step(model, ids, "selective")
+        loss_v, grads_v, held_v = _step(model, ids, "views")
         loss_r2, grads_r2, _ = _step(model, ids, "resident")
     finally:
         fl.unpatch_llama()
-    print(f"\nsaved for backward: resident {held_r / 1e6:.1f} MB, selective {held_s / 1e6:.1f} MB")
+    print(f"\nsaved for backward: resident {held_r / 1e6:.1f} MB, selective {held_s / 1e6:.1f} MB, "
+          f"views {held_v / 1e6:.1f} MB")
     assert torch.equal(loss_r, loss_r2)               # the step itself is deterministic
-    assert torch.equal(loss_r, loss_s)
-    assert grads_r.keys() == grads_s.keys() and len(grads_r) == 8
+    assert torch.equal(loss_r, loss_s) and torch.equal(loss_r, loss_v)
+    assert grads_r.keys() == grads_s.keys() == grads_v.keys() and len(grads_r) == 8
     for n in grads_r:
         assert torch.equal(grads_r[n], grads_r2[n]), n
         assert torch.equal(grads_r[n], grads_s[n]), n
-    assert held_s < held_r
+        assert torch.equal(grads_r[n], grads_v[n]), n
+    assert held_s < held_r < held_v                   # views keep whole inputs (the reference's ctx.list1)
 
 
 def test_selective_policy_detects_in_place_change():
