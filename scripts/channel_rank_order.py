@@ -85,8 +85,19 @@ def main():
             a = {(k, c) for k, v in sel["sequential"].items() for c in v}
             b = {(k, c) for k, v in sel[name].items() for c in v}
             same_lists = all(list(sel[name].get(k, [])) == list(v) for k, v in sel["sequential"].items())
+            # the per-key order (the row order of selected_weight, smt.py:196-204): positions that moved
+            moved, disp = 0, 0
+            for k, v in sel["sequential"].items():
+                other = list(sel[name].get(k, []))
+                pos = {c: i for i, c in enumerate(other)}
+                for i, c in enumerate(v):
+                    if i >= len(other) or other[i] != c:
+                        moved += 1
+                    if c in pos:
+                        disp = max(disp, abs(pos[c] - i))
             w[name] = {"acc_elements_differing": diff, "acc_fraction_differing": diff / tot,
                        "acc_max_rel_diff": rel, "selected_channels_differing": len(a ^ b) // 2,
+                       "positions_moved": moved, "max_displacement": disp,
                        "selection_identical": a == b and same_lists}
         w["seconds"] = round(time.time() - t0, 1)
         results["worlds"][str(world)] = w

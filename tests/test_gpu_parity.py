@@ -56,8 +56,10 @@ def test_linearz_apply_with_python_index_list():
     x = torch.randn(3, 40, 512).bfloat16().to(DEV).requires_grad_(True)
     y = smt.linearZ.apply(x, sw, [(2, 1), (0, 0)], W)
     y.sum().backward()
-    truth = ref.tile_grads_fp64(torch.ones(3, 40, 768).bfloat16(), x.detach().cpu(), [(2, 1), (0, 0)])
-    assert _rel(sw.grad, truth) < 2e-3
+    g1 = torch.ones(3, 40, 768).bfloat16()
+    truth = ref.tile_grads_fp64(g1, x.detach().cpu(), [(2, 1), (0, 0)])
+    ref_err = _rel(ref.linearz_tile_grads(g1, x.detach().cpu(), [(2, 1), (0, 0)]), truth)
+    assert _rel(sw.grad, truth) <= max(1e-3, 1.1 * ref_err)
     assert sw.grad.dtype == torch.bfloat16
 
 
@@ -519,10 +521,15 @@ def test_joint_qkv_data_gradient_is_one_gemm():
     n0 = dgrad.JOINT_PRODUCTS
     joint = run(gs)
     assert dgrad.JOINT_PRODUCTS == n0 + 1
-    assert _rel(joint, truth) < 5e-3
+    # the joint sum is rounded to bf16 once (unit roundoff 2^-8); the reference's autograd rounds each
+    # consumer's product and each running sum (three roundings): the joint gradient is within one
+    # rounding of exact, closer to it than the per-consumer path, and within three roundings of it
     sep = run([g.contiguous() for g in gs])                 # separate tensors: per-consumer products
     assert dgrad.JOINT_PRODUCTS == n0 + 1
-    assert _rel(joint, sep) < 1e-2
+    e_joint, e_sep, d = _rel(joint, truth), _rel(sep, truth), _rel(joint, sep)
+    print(f"\nq/k/v data gradient vs fp64: joint {e_joint:.2e}, per consumer {e_sep:.2e}; joint vs per consumer {d:.2e}")
+    assert e_joint <= 2 ** -8 and e_joint < e_sep
+    assert d <= 3 * 2 ** -8
     part = run(gs, keep=(0, 2))                              # k dropped: the deferred q, v run one by one
     assert dgrad.JOINT_PRODUCTS == n0 + 1
     want = gs[0].double() @ mods[0].weight.detach().double() + gs[2].double() @ mods[2].weight.detach().double()
