@@ -46,3 +46,56 @@ def test_engine_mode_values_validated():
         smt.register_engine_modes(_Eng(), "double", None)
     with pytest.raises(ValueError):
         smt.register_engine_modes(_Eng(), None, "offload")
+
+
+def test_default_rounding_is_the_reference():
+    """without SMT_WGRAD_ROUNDING the global tile-gradient rounding is the
+    reference's (smt.py:397-404); "views" is an accepted activation policy."""
+    import os
+    assert smt.wgrad_rounding() == os.environ.get("SMT_WGRAD_ROUNDING", "reference")
+    assert "views" in smt.ACTIVATION_POLICIES
+    old = smt.set_activation_policy("views")
+    assert smt.set_activation_policy(old) == "views"
+
+
+def _dp_exchange_worker(q):
+    """One process, a world-1 gloo group: an engine with dp_exchange "always" arms the dense buckets
+    and all-reduces them (the identity at world 1); "auto" does not; an unknown value raises."""
+    import torch.distributed as dist
+    try:
+        dist.init_process_group("gloo", store=dist.HashStore(), rank=0, world_size=1)
+        from sparse_matrix_tuning_amd.engine import SMTFusedAdam, initialize
+        res = {}
+        for mode in ("auto", "always"):
+            torch.manual_seed(0)
+            net = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.Linear(32, 4))
+            opt = SMTFusedAdam(net.parameters(), lr=1e-3)
+            eng, *_ = initialize(model=net, optimizer=opt, config={"dp_exchange": mode, "reduce_bucket_size": 100})
+            x = torch.randn(8, 16)
+            eng.backward(eng(x).square().sum())
+            grads = [p.grad.clone() for p in net.parameters()]
+            res[mode] = (eng.exchange, eng.dense_buckets.issued if eng.dense_buckets else 0, grads)
+        ok = (res["auto"][:2] == (False, 0) and res["always"][0] and res["always"][1] > 1
+              and all(torch.equal(a, b) for a, b in zip(res["auto"][2], res["always"][2])))
+        try:
+            initialize(model=net, optimizer=SMTFusedAdam(net.parameters(), lr=1e-3), config={"dp_exchange": "never"})
+            ok = False
+        except ValueError:
+            pass
+        q.put(bool(ok))
+    except Exception as e:          # reported to the parent
+        q.put(repr(e))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_dp_exchange_always_at_world_one_gloo():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_dp_exchange_worker, args=(q,))
+    p.start()
+    res = q.get(timeout=120)
+    p.join(timeout=60)
+    assert res is True, res
