@@ -11,7 +11,7 @@ mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 R=${RANKS:-4}
 ARGS="--gpus $R --dist-backend gloo --model mini --full-ft-steps ${FT:-3} --steps 6 --warmup 1 --cpu-baseline-seconds 0 \
-  --selective-steps 0 --ref-mode-steps 0 --ref-rounding-steps 0 --raw-harvest-steps 0 --roofline-steps 0"
+  --selective-steps 0 --views-steps 0 --ref-mode-steps 0 --ref-rounding-steps 0 --raw-harvest-steps 0 --roofline-steps 0"
 for v in "$@"; do
   case $v in
     base) ENVS="" ;;

@@ -457,8 +457,10 @@ class linearZ(torch.autograd.Function):
     slices (``ctx.list1``, smt.py:351-358), which hold the whole input alive. Here, when the tiles
     touch at most half of the input's 256-column blocks, one ``smt_colblock_gather`` launch packs
     exactly those blocks into a ``[T, n_cb*256]`` copy and the input itself is not saved (for a
-    down_proj with ~14 tiles that is 14 of its 56 blocks); otherwise the input is saved as is.
-    The tile gradients are bit-identical either way (same operands, same kernel, same order).
+    down_proj with ~14 tiles that is 14 of its 56 blocks); otherwise the input is saved as is. Under
+    the "views" activation policy the input is always saved as is (the reference's own choice), and
+    under "selective" a norm's / SwiGLU's output is not saved at all (rebuilt in the backward). The
+    tile gradients are bit-identical every way (same operands, same kernel, same order).
 
     If ``selected_weight`` carries an engine gradient sink (``_smt_grad_sink``), the fp32 tile
     gradients are written straight into the engine's packed buffer and ``None`` is returned for
