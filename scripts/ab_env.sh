@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of kernel environment knobs on one box: the bench's wgrad roofline (kernel alone) per setting.
-#   TAG=x VARIANTS="base SMT_WGRAD_SLOTS=5" bash scripts/ab_env.sh
+#   TAG=x VARIANTS="base SMT_JOINT_QKV=0" bash scripts/ab_env.sh
 set -o pipefail
 OUT=gpurun_out/${TAG:-abenv}
 mkdir -p $OUT

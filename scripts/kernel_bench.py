@@ -40,7 +40,7 @@ def main():
     ap.add_argument("--tiles", type=int, nargs="*", default=[1, 8, 27, 64, 128, 256])
     ap.add_argument("--patterns", nargs="*", default=["random", "clustered"])
     ap.add_argument("--orders", nargs="*", type=int, default=[0, 1])
-    ap.add_argument("--tag", default=os.environ.get("SMT_WGRAD_SLOTS", "5"))
+    ap.add_argument("--tag", default="default")
     ap.add_argument("--mx", action="store_true", help="time smt_mx_quant_cols + smt_tile_wgrad_mx instead")
     ap.add_argument("--xblock", action="store_true",
                     help="x from the block-major copy linearZ saves (smt_colblock_gather), as in training")

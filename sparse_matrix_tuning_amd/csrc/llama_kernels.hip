@@ -277,10 +277,8 @@ void rmsnorm_fwd_reg_kernel(const uint16_t* __restrict__ x, int64_t ldx, const u
 }
 
 // Backward without weight grad; with ADD the gradient reaching the norm's input by the residual path
-// is added as autograd would: dx = bf16(bf16(dx_norm) + dres).
-#ifndef SMT_NORM_BWD_PRELOAD
-#define SMT_NORM_BWD_PRELOAD 1
-#endif
+// is added as autograd would: dx = bf16(bf16(dx_norm) + dres). The residual gradient is loaded up
+// front, beside the row's other loads (profiles/r04_v_norm_bwd_preload_ab.jsonl: 193-197 -> 189-190 us).
 template <int CPL, bool ADD, bool QUANT = false>
 __global__ __launch_bounds__(256, CPL <= 10 ? 2 : 1)        // two waves per SIMD up to hidden 5120
 void rmsnorm_bwd_reg_kernel(const uint16_t* __restrict__ dy, int64_t lddy, const uint16_t* __restrict__ x, int64_t ldx,
@@ -299,7 +297,7 @@ void rmsnorm_bwd_reg_kernel(const uint16_t* __restrict__ dy, int64_t lddy, const
     typename RowReg<PACK>::T xr[CPL], gr[CPL];
     // up to CPL 8 the residual gradient's row is loaded with x and dy (32 more registers): issued
     // in the second pass, each load waited behind the dx stores issued before it (vmcnt counts both)
-    constexpr bool PRE = ADD && !PACK && SMT_NORM_BWD_PRELOAD;
+    constexpr bool PRE = ADD && !PACK;
     uint4 drr[PRE ? CPL : 1];
     if constexpr (PRE) {
 #pragma unroll
@@ -960,8 +958,9 @@ static int rope(bool bwd, const smt_rope_tensor* q, const smt_rope_tensor* k, co
     if (rows > 65535 || per_row > 0x7fffffffLL - 255)
         return fail(-1, "smt_rope: %lld (batch x heads) rows of %lld chunks exceed the grid", (long long)rows,
                     (long long)per_row);
-    static const bool hg_on = [] { const char* e = getenv("SMT_ROPE_HG"); return !(e && atoi(e) == 0); }();
-    if (hg_on && q->heads % kRopeHG == 0 && k->heads % kRopeHG == 0) {
+    // cos / sin loaded once per kRopeHG heads (profiles/r04_nn_rope_hg_ab.jsonl: 141 -> 125 us); one
+    // head per thread when the head counts are not multiples of it
+    if (q->heads % kRopeHG == 0 && k->heads % kRopeHG == 0) {
         const dim3 hgrid((unsigned)((per_row + 255) / 256), (unsigned)(B * (q->heads + k->heads) / kRopeHG));
         if (bwd)
             hipLaunchKernelGGL(rope_hg_kernel<true>, hgrid, dim3(256), 0, stream, tq, tk, (const uint16_t*)cos,

@@ -397,21 +397,12 @@ typedef __attribute__((address_space(3))) uint8_t lds_u8_t;
 // purpose: hipcc then does not see an LDS write it cannot disambiguate from the ring slot being read
 // (with the builtin it puts s_waitcnt vmcnt(0) before every ds_read, draining the 2-deep pipeline);
 // completion is tracked by the hand-counted vmcnt in the loop. M0 is saved / restored inside the
-// statement (cdna_hip_programming §5.7).
-// SMT_DMA_NT=1: the operand stream with the non-temporal cache policy (A/B builds; measured the same
-// as the default policy on the bench's batched launches: profiles/r02_wgrad_nt_ab.jsonl)
-#ifndef SMT_DMA_NT
-#define SMT_DMA_NT 0
-#endif
-#if SMT_DMA_NT
-#define SMT_DMA_POLICY " nt lds"
-#else
-#define SMT_DMA_POLICY " lds"
-#endif
+// statement (cdna_hip_programming §5.7). Default cache policy: the non-temporal one measured the same
+// on the bench's batched launches (profiles/r02_wgrad_nt_ab.jsonl).
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, uint32_t lds_base, int voff) {
     uint32_t keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
-                 "buffer_load_dwordx4 %1, %2, 0 offen" SMT_DMA_POLICY "\n\ts_mov_b32 m0, %0"
+                 "buffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(lds_base) : "memory");
 }
 
@@ -468,11 +459,7 @@ void wgrad_dma_kernel(const WgradModules mods, int64_t T, int64_t chunk, int S, 
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
         const int k = 4 * wave + 2 * j + (lane >> 5);
-#ifdef SMT_WGRAD_DIAG_NOSWZ
-        const int lb = 16 * (lane & 31);                         // diagnostic build only (wrong tiles)
-#else
         const int lb = (16 * (lane & 31)) ^ ((k & 3) << 6);
-#endif
         voff_g[j] = (int)(k * ldg * 2) + lb;
         voff_x[j] = (int)(k * ldx * 2) + lb;
     }
@@ -517,7 +504,6 @@ void wgrad_dma_kernel(const WgradModules mods, int64_t T, int64_t chunk, int S, 
         }
         __builtin_amdgcn_s_barrier();                              // every wave's DMA for stage st landed
         __builtin_amdgcn_sched_barrier(0);
-#ifndef SMT_WGRAD_DIAG_NOMFMA
         const uint8_t* A = lds + (st % SLOTS) * kDmaSlotBytes;
         const uint8_t* B = A + kDmaImg;
 #pragma unroll
@@ -537,7 +523,6 @@ void wgrad_dma_kernel(const WgradModules mods, int64_t T, int64_t chunk, int S, 
                 for (int nb = 0; nb < 2; ++nb)
                     acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[nb], af[mb], acc[mb][nb], 0, 0, 0);
         }
-#endif
     }
     wgrad_store_t<OUT, 4>(acc, (OUT == kOutSlab || OUT == kOutSlabBF16) ? wgrad_dst<OUT>(slab, tile, s, S) : tt.out,
                           wm * 128, wn * 64, lane, tt.accumulate);
@@ -1894,13 +1879,11 @@ void channel_aten_levels_kernel(const float* __restrict__ chunks, int S, int C, 
 // S splits of `chunk` rows each; seq > 0: the reference-rounding split (kps pieces per seq-row sample)
 struct WgradSplit { int S; int64_t chunk; bool quarter; int64_t seq; int kps; };
 
-// Quarter-tile kernel for modules with at most this many tiles (SMT_WGRAD_QUARTER_MAX; 0 disables).
-// Measured at T = 32768 (profiles/r02_wgrad_quarter.jsonl): 1.1-1.2x faster than the full-tile
-// kernel at 1-8 tiles, even at 16, slower from 27.
-int quarter_max_tiles() {
-    static const int v = [] { const char* e = getenv("SMT_WGRAD_QUARTER_MAX"); return e ? atoi(e) : 8; }();
-    return v;
-}
+// Quarter-tile kernel for modules with at most this many tiles. Measured at T = 32768
+// (profiles/r02_wgrad_quarter.jsonl): 1.1-1.2x faster than the full-tile kernel at 1-8 tiles, even
+// at 16, slower from 27.
+constexpr int kQuarterMaxTiles = 8;
+int quarter_max_tiles() { return kQuarterMaxTiles; }
 
 // row_bytes: operand bytes per T row of one tile (1 KiB bf16, 512 B MX-fp8)
 WgradSplit wgrad_split(int64_t T, int32_t n_tiles, bool allow_quarter = true, double row_bytes = 1024.0) {
@@ -1988,12 +1971,9 @@ int wgrad_launch(const WgradModules& mods, int64_t T, int64_t max_ld, const int3
     const bool use_slab = sp.S > 1 || sp.seq > 0;       // reference rounding always reduces
     const dim3 grid(n_tiles * sp.S), block(kWgThreads);
     const dim3 qgrid(n_tiles * sp.S * 4), qblock(kQThreads);
-    static const bool force_reg = [] { const char* e = getenv("SMT_WGRAD_IMPL"); return e && strcmp(e, "reg") == 0; }();
-    // SMT_WGRAD_SLOTS=5: the 3-in-flight ring (A/B runs); default 4 (2 stages in flight)
-    static const int slots = [] { const char* e = getenv("SMT_WGRAD_SLOTS"); return (e && atoi(e) == 5) ? 5 : kDmaSlotsDefault; }();
-    // SMT_WGRAD_QSLOTS=5: the quarter kernel with 3 stages in flight (80 KiB LDS per workgroup)
-    static const int qslots = [] { const char* e = getenv("SMT_WGRAD_QSLOTS"); return (e && atoi(e) == 5) ? 5 : kQSlots; }();
-    const bool dma = !force_reg && sp.chunk * max_ld * 2 < (int64_t)0x7fffffff;
+    // the LDS-DMA kernels address a split's rows with 32-bit buffer offsets; past that, the
+    // register-staged kernel (64-bit addresses)
+    const bool dma = sp.chunk * max_ld * 2 < (int64_t)0x7fffffff;
     const bool quarter = dma && sp.quarter;
     // reference rounding with one workgroup per sample piece (kps == 1): the LDS-DMA kernels round
     // each sample's partial to bf16 themselves and write half-size slabs (SMT_WGRAD_SLAB16=0: fp32)
@@ -2011,12 +1991,8 @@ int wgrad_launch(const WgradModules& mods, int64_t T, int64_t max_ld, const int3
     do {                                                                                                          \
         if (!dma) hipLaunchKernelGGL((wgrad_partial_kernel<OUT, BATCH>), grid, block, 0, stream, mods, T, sp.chunk, \
                                      sp.S, sp.seq, sp.kps, n_tiles, tab, order, slab);                           \
-        else if (quarter && qslots == 5) hipLaunchKernelGGL((wgrad_quarter_kernel<OUT, 5, BATCH>), qgrid, qblock, 0, \
-                                     stream, mods, T, sp.chunk, sp.S, sp.seq, sp.kps, n_tiles, tab, order, slab);\
         else if (quarter) hipLaunchKernelGGL((wgrad_quarter_kernel<OUT, kQSlots, BATCH>), qgrid, qblock, 0, stream,  \
                                      mods, T, sp.chunk, sp.S, sp.seq, sp.kps, n_tiles, tab, order, slab);        \
-        else if (slots == 5) hipLaunchKernelGGL((wgrad_dma_kernel<OUT, 5, BATCH>), grid, block, 0, stream, mods, T,  \
-                                     sp.chunk, sp.S, sp.seq, sp.kps, n_tiles, tab, order, slab);                 \
         else hipLaunchKernelGGL((wgrad_dma_kernel<OUT, kDmaSlotsDefault, BATCH>), grid, block, 0, stream, mods, T,   \
                                 sp.chunk, sp.S, sp.seq, sp.kps, n_tiles, tab, order, slab);                      \
     } while (0)
@@ -2027,13 +2003,8 @@ int wgrad_launch(const WgradModules& mods, int64_t T, int64_t max_ld, const int3
     }
     if (slab16) {
         // the LDS-DMA kernels only (dma is true here)
-        if (quarter && qslots == 5) hipLaunchKernelGGL((wgrad_quarter_kernel<kOutSlabBF16, 5, BATCH>), qgrid, qblock, 0,
-                                                       stream, mods, T, sp.chunk, sp.S, sp.seq, sp.kps, n_tiles, tab,
-                                                       order, slab);
-        else if (quarter) hipLaunchKernelGGL((wgrad_quarter_kernel<kOutSlabBF16, kQSlots, BATCH>), qgrid, qblock, 0, stream,
-                                             mods, T, sp.chunk, sp.S, sp.seq, sp.kps, n_tiles, tab, order, slab);
-        else if (slots == 5) hipLaunchKernelGGL((wgrad_dma_kernel<kOutSlabBF16, 5, BATCH>), grid, block, 0, stream, mods, T,
-                                                sp.chunk, sp.S, sp.seq, sp.kps, n_tiles, tab, order, slab);
+        if (quarter) hipLaunchKernelGGL((wgrad_quarter_kernel<kOutSlabBF16, kQSlots, BATCH>), qgrid, qblock, 0, stream,
+                                        mods, T, sp.chunk, sp.S, sp.seq, sp.kps, n_tiles, tab, order, slab);
         else hipLaunchKernelGGL((wgrad_dma_kernel<kOutSlabBF16, kDmaSlotsDefault, BATCH>), grid, block, 0, stream, mods, T,
                                 sp.chunk, sp.S, sp.seq, sp.kps, n_tiles, tab, order, slab);
     } else {
@@ -2180,23 +2151,13 @@ int smt_mx_quant_cols(const void* x, int64_t ld_x, int64_t T, const int32_t* blo
     if (!x || !blocks_dev || !q || !scales) return fail(SMT_E_INVALID, "smt_mx_quant_cols: null pointer");
     if (!aligned16(x) || (ld_x & 7) || !aligned16(q))
         return fail(SMT_E_ALIGN, "smt_mx_quant_cols: 16-byte aligned rows required (ld %% 8 == 0)");
-    // SMT_MX_QUANT_ROWS = 32 | 64 (default) | 128 rows per workgroup (A/B runs)
-    static const int rows = [] { const char* e = getenv("SMT_MX_QUANT_ROWS"); const int v = e ? atoi(e) : 64;
-                                 return (v == 32 || v == 128) ? v : 64; }();
+    // 64 rows per workgroup (32 and 128 measured no faster)
+    constexpr int rows = 64;
     const int64_t wgs = (ldq + rows - 1) / rows;
     if (wgs > 65535) return fail(SMT_E_INVALID, "smt_mx_quant_cols: T too large");
-    if (rows == 32)
-        hipLaunchKernelGGL(mx_quant_cols_kernel<32>, dim3(n_blocks, (unsigned)wgs), dim3(256), 0, stream,
-                           static_cast<const uint16_t*>(x), ld_x, T, blocks_dev, ldq, static_cast<uint8_t*>(q),
-                           static_cast<uint8_t*>(scales));
-    else if (rows == 64)
-        hipLaunchKernelGGL(mx_quant_cols_kernel<64>, dim3(n_blocks, (unsigned)wgs), dim3(256), 0, stream,
-                           static_cast<const uint16_t*>(x), ld_x, T, blocks_dev, ldq, static_cast<uint8_t*>(q),
-                           static_cast<uint8_t*>(scales));
-    else
-        hipLaunchKernelGGL(mx_quant_cols_kernel<128>, dim3(n_blocks, (unsigned)wgs), dim3(256), 0, stream,
-                           static_cast<const uint16_t*>(x), ld_x, T, blocks_dev, ldq, static_cast<uint8_t*>(q),
-                           static_cast<uint8_t*>(scales));
+    hipLaunchKernelGGL(mx_quant_cols_kernel<rows>, dim3(n_blocks, (unsigned)wgs), dim3(256), 0, stream,
+                       static_cast<const uint16_t*>(x), ld_x, T, blocks_dev, ldq, static_cast<uint8_t*>(q),
+                       static_cast<uint8_t*>(scales));
     return check_launch("mx_quant_cols_kernel");
 }
 
@@ -2478,27 +2439,18 @@ int smt_column_gather(const void* x, int64_t ld_x, int64_t n_in, int64_t T, cons
     const int rows = row_bytes * 4 <= 65536 ? 4 : row_bytes * 2 <= 65536 ? 2 : 1;
     if (row_bytes > 65536) return fail(SMT_E_INVALID, "smt_column_gather: rows of %lld elements exceed the LDS stage", (long long)n_in);
     if (n_cols > 0 && ((uintptr_t)cols_dev & 15)) return fail(SMT_E_ALIGN, "smt_column_gather: cols not 16-byte aligned");
-    // SMT_CGATHER_IMPL: 1 = rows staged through registers; 2 (default) / 3 = LDS-DMA staging of 4 / 8
-    // rows per workgroup (8 while they fit the CU's 160 KiB)
-    static const int impl = [] { const char* e = getenv("SMT_CGATHER_IMPL"); const int v = e ? atoi(e) : 2;
-                                 return (v == 1 || v == 3) ? v : 2; }();
+    // LDS-DMA staging of 4 rows per workgroup (profiles/r04_h_column_gather_ab.jsonl: 82 us against 120
+    // for register staging and 90 for 8 rows); register staging where the rows do not fit the 64 KiB
+    // stage or the 32-bit buffer offsets
     const int64_t ppr = (n_in * 2 + 1023) / 1024;
-    if (impl != 1 && ppr * 1024 * 4 <= 65536 && ld_x * 2 * 8 < 0x7fffffffLL) {
-        const int R = (impl == 3 && ppr * 1024 * 8 <= 160 * 1024) ? 8 : 4;
+    if (ppr * 1024 * 4 <= 65536 && ld_x * 2 * 8 < 0x7fffffffLL) {
+        constexpr int R = 4;
         const int64_t nb = (T + R - 1) / R;
         if (nb > 0x7fffffffLL) return fail(SMT_E_INVALID, "smt_column_gather: too large");
         const size_t lds = (size_t)(R * ppr * 1024);
-        if (lds > 65536) {
-            static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(column_gather_dma_kernel<8>),
-                                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            if (attr != hipSuccess) return fail(SMT_E_LAUNCH, "smt_column_gather: LDS attribute: %s", hipGetErrorString(attr));
-        }
-        if (R == 8) hipLaunchKernelGGL(column_gather_dma_kernel<8>, dim3((unsigned)nb), dim3(256), lds, stream,
-                                       static_cast<const uint16_t*>(x), ld_x, n_in, T, (int)ppr, cols_dev, n_cols,
-                                       static_cast<uint16_t*>(out), ld_out);
-        else hipLaunchKernelGGL(column_gather_dma_kernel<4>, dim3((unsigned)nb), dim3(256), lds, stream,
-                                static_cast<const uint16_t*>(x), ld_x, n_in, T, (int)ppr, cols_dev, n_cols,
-                                static_cast<uint16_t*>(out), ld_out);
+        hipLaunchKernelGGL(column_gather_dma_kernel<R>, dim3((unsigned)nb), dim3(256), lds, stream,
+                           static_cast<const uint16_t*>(x), ld_x, n_in, T, (int)ppr, cols_dev, n_cols,
+                           static_cast<uint16_t*>(out), ld_out);
         return check_launch("column_gather_dma_kernel");
     }
     const int64_t blocks = (T + rows - 1) / rows;
