@@ -226,13 +226,32 @@ def attach_transposed_weights(model: torch.nn.Module, joint_qkv: bool = True) ->
     return added
 
 
+def attach_channel_gather_groups(model: torch.nn.Module) -> int:
+    """q/k/v_proj channel modules (LinearLayer_ChannelSparsity with channels) of one attention module
+    gather their partial inputs in ONE launch (smt.ChannelGatherGroup): each member's frozen weight
+    carries ``_smt_cgather = (group, member)``. Returns the number of groups."""
+    from .smt.smt import ChannelGatherGroup
+    n = 0
+    for m in model.modules():
+        lin = [getattr(m, name, None) for name in ("q_proj", "k_proj", "v_proj")]
+        mem = [x for x in lin if isinstance(x, LinearLayer_ChannelSparsity) and len(x.channels)
+               and x.selected_weight.requires_grad and x.weight.device.type == "cuda"]
+        if len(mem) < 2 or len({x.weight.shape[1] for x in mem}) != 1:
+            continue
+        grp = ChannelGatherGroup([x.channels for x in mem], mem[0].weight.device)
+        for i, x in enumerate(mem):
+            x.weight._smt_cgather = (grp, i)
+        n += 1
+    return n
+
+
 def detach_transposed_weights(model: torch.nn.Module) -> None:
-    """Undo :func:`attach_transposed_weights`."""
+    """Undo :func:`attach_transposed_weights` (and :func:`attach_channel_gather_groups`)."""
     for m in model.modules():
         if "_smt_joint_qkv_grad" in m.__dict__:
             del m.__dict__["_smt_joint_qkv_grad"]
         w = getattr(m, "weight", None)
-        for attr in ("_smt_weight_t", "_smt_fp8"):
+        for attr in ("_smt_weight_t", "_smt_fp8", "_smt_cgather"):
             if isinstance(w, torch.Tensor) and hasattr(w, attr):
                 delattr(w, attr)
         if type(m) is torch.nn.Linear and "forward" in m.__dict__:
@@ -750,6 +769,7 @@ class SMTEngine:
         self._dense_state = {}
         self.transposed_bytes = 0
         self.fp8_bytes = 0
+        self.channel_gather_groups = 0
         if optimizer is not None:
             owner = {}
             channel_rows = False
@@ -769,6 +789,9 @@ class SMTEngine:
                 # gradients as one GEMM over smt_flash's joint [dq | dk | dv] (dgrad.py)
                 joint = cfg.get("joint_qkv_dgrad", os.environ.get("SMT_JOINT_QKV", "1") != "0")
                 self.transposed_bytes = attach_transposed_weights(model, joint_qkv=joint)
+            if channel_rows and cfg.get("shared_channel_gather", os.environ.get("SMT_SHARED_CGATHER", "1") != "0"):
+                # the channel path's q/k/v read one input: one partial-input gather per layer
+                self.channel_gather_groups = attach_channel_gather_groups(model)
             for group in optimizer.param_groups:
                 mods = [owner[id(p)] for p in group["params"] if id(p) in owner]
                 dense = [p for p in group["params"] if id(p) not in owner and p.requires_grad]

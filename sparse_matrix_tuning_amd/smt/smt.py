@@ -824,6 +824,37 @@ def _as_channel_index(index) -> ChannelIndex:
     return index if isinstance(index, ChannelIndex) else ChannelIndex(index)
 
 
+class ChannelGatherGroup:
+    """Channel modules that read ONE input (q/k/v_proj of a layer): their partial inputs
+    ``x[:, :, index_list]`` (smt.py:225-233) come from one ``smt_column_gather`` launch into a joint
+    ``[T, sum of padded widths]`` buffer, the members' blocks side by side, and each member keeps a
+    column-slice view of it. The input rows are read once instead of once per member (a whole row is
+    fetched either way: the selected channels touch every 64-B granule). A column index of -1 in the
+    joint table writes a zero: each member's block is zero-padded to whole 256-column blocks exactly
+    as its own gather pads it, so the tile gradients are bit-identical."""
+
+    def __init__(self, channels: Sequence[ChannelIndex], device: torch.device):
+        cols, self.offsets, off = [], [], 0
+        for ch in channels:
+            cols.extend(ch.index_list)
+            cols.extend([-1] * (ch.padded - len(ch)))
+            self.offsets.append((off, ch.padded))
+            off += ch.padded
+        self.width = off
+        self.table = _hip.index_table(cols, device)
+
+    def partial(self, input: torch.Tensor, x2: torch.Tensor, member: int) -> torch.Tensor:
+        """Member ``member``'s ``[T, padded]`` partial input: a view of the joint gather of ``input``,
+        made by the first member that asks for it (cached on the input tensor while its version holds)."""
+        cache = input.__dict__.get("_smt_cgather")
+        if cache is None or cache[0] is not self or cache[1] != input._version:
+            joint = _hip.column_gather(x2, self.table, self.width, self.width)
+            cache = (self, input._version, joint)
+            input.__dict__["_smt_cgather"] = cache
+        off, width = self.offsets[member]
+        return cache[2][:, off:off + width]
+
+
 class LinearLayer_ChannelSparsity(torch.nn.Module):
     """smt.py:185-214: frozen dense ``W`` (aliased) plus the trainable rows
     ``selected_weight[i, :] = W[index_list[i], :]``; every forward writes the rows back into ``W``
@@ -896,7 +927,12 @@ class linearChannel(torch.autograd.Function):
         partial = None
         if ctx.needs_input_grad[1] and len(ch):
             x2 = _rows_ready(input.reshape(-1, input.shape[-1]))
-            partial = _hip.column_gather(x2, ch.device_table(x2.device), len(ch), ch.padded)
+            grp = getattr(weight, "_smt_cgather", None)
+            if grp is not None and grp[0].offsets[grp[1]][1] == ch.padded:
+                # q/k/v of a layer: one gather for the group (engine.attach_channel_gather_groups)
+                partial = grp[0].partial(input, x2, grp[1])
+            else:
+                partial = _hip.column_gather(x2, ch.device_table(x2.device), len(ch), ch.padded)
         ctx.save_for_backward(partial, weight)
         # q/k/v share their input: their data gradients accumulate in one buffer (dgrad.py)
         ctx.acc = dgrad.register(input, ctx)

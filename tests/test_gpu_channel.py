@@ -414,3 +414,54 @@ def test_channel_engine_transposed_copies_follow_the_rows():
     for a, b in zip(g1, g0):
         assert _rel(a, b) < 1e-2
     assert _rel(r1, r0) < 1e-2
+
+
+def test_channel_qkv_share_one_column_gather():
+    """Under the engine q/k/v_proj channel modules of one attention module gather their partial inputs
+    (smt.py:225-233) in ONE column-gather launch into a joint buffer (engine.attach_channel_gather_groups);
+    each member's partial is a zero-padded column slice of it. Tile gradients and the trained rows are
+    bit-identical to the per-module gathers (shared_channel_gather off)."""
+    from sparse_matrix_tuning_amd import _hip
+    from sparse_matrix_tuning_amd.engine import SMTFusedAdam, initialize
+
+    def run(shared):
+        torch.manual_seed(31)
+        net = nn.Module()
+        net.attn = nn.Module()
+        Ws = [nn.Parameter((torch.randn(512, 512) * 0.05).bfloat16().to(DEV), requires_grad=False) for _ in range(3)]
+        idx = ([5, 300, 17, 260, 511], list(range(0, 512, 2)) + [1, 3], [42])     # 5, 258 (ragged), 1 channels
+        for name, W, ix in zip(("q_proj", "k_proj", "v_proj"), Ws, idx):
+            setattr(net.attn, name, smt.LinearLayer_ChannelSparsity(W, index_list=ix))
+        mods = [net.attn.q_proj, net.attn.k_proj, net.attn.v_proj]
+        opt = SMTFusedAdam([m.selected_weight for m in mods], lr=1e-2)
+        engine, *_ = initialize(model=net, optimizer=opt, config={"shared_channel_gather": shared})
+        assert engine.channel_gather_groups == (1 if shared else 0)
+        calls = []
+        real = _hip.column_gather
+
+        def counting(*a, **k):
+            calls.append(a[2])
+            return real(*a, **k)
+        _hip.column_gather = counting
+        try:
+            x = torch.randn(2, 64, 512).bfloat16().to(DEV)
+            grads = []
+            for _ in range(2):
+                xi = x.clone().requires_grad_(True)
+                loss = sum(m(xi).float().pow(2).mean() for m in mods)
+                engine.backward(loss)
+                grads.append([m.selected_weight.grad.clone() for m in mods])
+                engine.step()
+        finally:
+            _hip.column_gather = real
+        return calls, grads, [m.selected_weight.detach().clone() for m in mods]
+
+    calls_s, grads_s, rows_s = run(True)
+    calls_p, grads_p, rows_p = run(False)
+    assert len(calls_s) == 2 and calls_s[0] == 256 + 512 + 256          # one joint gather per forward
+    assert len(calls_p) == 6
+    for gs, gp in zip(grads_s, grads_p):
+        for a, b in zip(gs, gp):
+            assert torch.equal(a, b)
+    for a, b in zip(rows_s, rows_p):
+        assert torch.equal(a, b)
