@@ -834,6 +834,7 @@ class ChannelGatherGroup:
     as its own gather pads it, so the tile gradients are bit-identical."""
 
     def __init__(self, channels: Sequence[ChannelIndex], device: torch.device):
+        self.members = list(channels)          # the ChannelIndex objects the joint table was built from
         cols, self.offsets, off = [], [], 0
         for ch in channels:
             cols.extend(ch.index_list)
@@ -928,7 +929,7 @@ class linearChannel(torch.autograd.Function):
         if ctx.needs_input_grad[1] and len(ch):
             x2 = _rows_ready(input.reshape(-1, input.shape[-1]))
             grp = getattr(weight, "_smt_cgather", None)
-            if grp is not None and grp[0].offsets[grp[1]][1] == ch.padded:
+            if grp is not None and grp[0].members[grp[1]] is ch:
                 # q/k/v of a layer: one gather for the group (engine.attach_channel_gather_groups)
                 partial = grp[0].partial(input, x2, grp[1])
             else:
