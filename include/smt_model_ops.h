@@ -96,6 +96,8 @@ int smt_colblock_recompute(int32_t op, const void* a, int64_t ld_a, const void* 
  *           0 where label[r] == ignore_index, NaN where the label is outside [0, vocab).
  * Backward: dlogits[r, j] = bf16((exp(logits[r, j] - lse[r]) - [j == label[r]]) * scale[0]),
  *           0 on ignored rows. `scale` is a device float (d loss / normaliser), so no host sync.
+ *           `dlogits` may be `logits` itself (ld_d == ld): every element is read and then written
+ *           by the same thread (the fused LM head + loss runs it in place over a chunk's logits).
  * vocab % 8 == 0, 16-byte aligned rows. */
 int smt_ce_fwd(const void* logits, int64_t ld, const int64_t* labels, int64_t rows, int64_t vocab,
                int64_t ignore_index, float* lse, float* loss, hipStream_t stream);

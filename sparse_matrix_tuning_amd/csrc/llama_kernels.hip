@@ -668,9 +668,11 @@ __device__ __forceinline__ F8 ce_grad8(const F8& v, int64_t col0, int64_t lab, f
 }
 
 __global__ __launch_bounds__(kCeThreads)
-void ce_bwd_kernel(const uint16_t* __restrict__ logits, int64_t ld, const int64_t* __restrict__ labels,
+void ce_bwd_kernel(const uint16_t* logits, int64_t ld, const int64_t* __restrict__ labels,
                    const float* __restrict__ lse, const float* __restrict__ scale, int64_t V, int64_t ignore_index,
-                   uint16_t* __restrict__ dlogits, int64_t ldd) {
+                   uint16_t* dlogits, int64_t ldd) {
+    // logits and dlogits may alias (in place): no __restrict__ on them; each thread reads its 8-element
+    // chunks before it writes the same chunks, and no two threads touch one chunk
     const int64_t row = blockIdx.x;
     const int64_t lab = labels[row];
     const float w = (lab == ignore_index) ? 0.f : scale[0];
@@ -795,6 +797,7 @@ int smt_ce_bwd(const void* logits, int64_t ld, const int64_t* labels, const floa
     if (!aligned16(logits) || !aligned16(dlogits) || (ld & 7) || (ld_d & 7))
         return fail(-2, "smt_ce_bwd: 16-byte aligned rows required");
     if (rows > 0x7fffffffLL) return fail(-1, "smt_ce_bwd: too many rows");
+    if (dlogits == logits && ld_d != ld) return fail(-1, "smt_ce_bwd: in place needs ld_d == ld");
     hipLaunchKernelGGL(ce_bwd_kernel, dim3((unsigned)rows), dim3(kCeThreads), 0, stream, (const uint16_t*)logits, ld,
                        labels, lse, scale, vocab, ignore_index, (uint16_t*)dlogits, ld_d);
     return check_launch("ce_bwd_kernel");

@@ -496,16 +496,138 @@ def fused_causal_lm_loss(logits, labels, vocab_size, num_items_in_batch=None, ig
     """Drop-in for ``transformers.loss.loss_utils.ForCausalLMLoss`` (the loss of
     ``LlamaForCausalLM.forward``): labels shifted left by one with ``ignore_index`` padding, mean over
     non-ignored tokens, or sum / ``num_items_in_batch``."""
-    if shift_labels is None:
-        labels = nn.functional.pad(labels, (0, 1), value=ignore_index)
-        shift_labels = labels[..., 1:]
     logits2d = logits.reshape(-1, vocab_size)
-    shift = shift_labels.reshape(-1).to(logits2d.device)
+    shift = _shifted_labels(labels, ignore_index, shift_labels).to(logits2d.device)
     if num_items_in_batch is None:
         denom = (shift != ignore_index).sum().to(torch.float32)
     else:
         denom = torch.as_tensor(num_items_in_batch, device=logits2d.device).to(torch.float32)
     return FusedCrossEntropyFn.apply(logits2d, shift, ignore_index, denom)
+
+
+def _shifted_labels(labels, ignore_index, shift_labels):
+    """ForCausalLMLoss's label shift: position s is scored against token s + 1, the last position
+    against ``ignore_index``."""
+    if shift_labels is None:
+        labels = nn.functional.pad(labels, (0, 1), value=ignore_index)
+        shift_labels = labels[..., 1:]
+    return shift_labels.reshape(-1)
+
+
+# ------------------------------------------------------------------------------------------------
+# LM head + causal-LM cross entropy, row chunk by row chunk
+# ------------------------------------------------------------------------------------------------
+LM_HEAD_CHUNK_ROWS = int(os.environ.get("SMT_LM_HEAD_CHUNK_ROWS", "4096"))
+
+
+class FusedLMHeadLossFn(torch.autograd.Function):
+    """``lm_head`` (frozen, no bias) followed by :class:`FusedCrossEntropyFn`, without the full
+    ``[T, V]`` logits. At B 16 x S 2048 x V 128256 the unfused pair keeps the bf16 logits (8.4 GB)
+    for the loss backward and allocates the same again for ``dlogits`` at the start of the backward,
+    when every activation of the step is still alive: that 16.8 GB is the SMT step's peak HBM.
+
+    Here each chunk of ``LM_HEAD_CHUNK_ROWS`` rows runs, inside the forward: the logits GEMM
+    (``hidden @ W^T``), the row log-sum-exp (``smt_ce_fwd``), and (when ``hidden`` needs a gradient)
+    ``dlogits`` for a unit upstream gradient written over the chunk's logits (``smt_ce_bwd`` in
+    place; each element is read and written by one thread) and the data gradient ``dlogits @ W``
+    (TN on the engine's transposed copy when there is one, as :class:`..engine.FrozenLinearFn` runs
+    it). Only ``dh [T, H]`` (268 MB) is kept; the backward scales it by the upstream gradient.
+
+    Per row this is the unfused arithmetic: the same GEMM products, the same kernels and, for the
+    upstream gradient 1 that ``loss.backward()`` gives (``engine.backward`` with one accumulation
+    step), the same ``dlogits`` scale ``1 / denom``. Any other upstream gradient is applied to the
+    bf16 ``dh`` (one more rounding than folding it into ``dlogits`` first, exact for powers of
+    two). Whether hipBLASLt picks the same kernel for a chunk's GEMM shape as for the whole batch's
+    decides bit-identity of the logits and ``dh``; tests/test_gpu_cross_entropy.py checks it."""
+
+    @staticmethod
+    def forward(ctx, hidden, weight, weight_t, labels, ignore_index, denom, chunk_rows):
+        _need(hidden, "lm head loss")
+        _need(weight, "lm head loss")
+        h2 = _rows2d(hidden)
+        N, H = h2.shape
+        V = weight.shape[0]
+        if weight.shape[1] != H:
+            raise ValueError(f"lm head loss: weight {tuple(weight.shape)} for hidden size {H}")
+        if V % 8:
+            raise ValueError(f"lm head loss: vocabulary {V} is not a multiple of 8")
+        labels = labels.to(device=hidden.device, dtype=torch.int64).contiguous()
+        if labels.numel() != N:
+            raise ValueError(f"lm head loss: {labels.numel()} labels for {N} rows")
+        need_dh = bool(ctx.needs_input_grad[0])
+        lib = _hip.load()
+        stream = _stream(hidden)
+        lse = torch.empty(N, dtype=torch.float32, device=hidden.device)
+        rows = torch.empty(N, dtype=torch.float32, device=hidden.device)
+        dh = torch.empty((N, H), dtype=hidden.dtype, device=hidden.device) if need_dh else None
+        scale = (1.0 / denom.to(torch.float32)).reshape(1).contiguous()
+        C = max(1, min(int(chunk_rows), N))
+        buf = torch.empty((C, V), dtype=hidden.dtype, device=hidden.device)
+        w_dgrad = weight_t.t() if weight_t is not None else weight
+        for r0 in range(0, N, C):
+            c = min(C, N - r0)
+            lg = buf[:c]
+            torch.mm(h2[r0:r0 + c], weight.t(), out=lg)
+            rc = lib.smt_ce_fwd(lg.data_ptr(), lg.stride(0), labels[r0:].data_ptr(), c, V, int(ignore_index),
+                                lse[r0:].data_ptr(), rows[r0:].data_ptr(), stream)
+            _hip._check(rc, "smt_ce_fwd")
+            if need_dh:
+                rc = lib.smt_ce_bwd(lg.data_ptr(), lg.stride(0), labels[r0:].data_ptr(), lse[r0:].data_ptr(),
+                                    scale.data_ptr(), c, V, int(ignore_index), lg.data_ptr(), lg.stride(0), stream)
+                _hip._check(rc, "smt_ce_bwd")
+                torch.mm(lg, w_dgrad, out=dh[r0:r0 + c])
+        del buf
+        if need_dh:
+            ctx.save_for_backward(dh)
+        ctx.shape = hidden.shape
+        return rows.sum() / denom
+
+    @staticmethod
+    def backward(ctx, dloss):
+        (dh,) = ctx.saved_tensors
+        return torch.mul(dh, dloss.float()).view(ctx.shape), None, None, None, None, None, None
+
+
+def fused_lm_head_loss(hidden, lm_head: nn.Linear, labels, num_items_in_batch=None, ignore_index=-100,
+                       shift_labels=None, chunk_rows=None):
+    """``ForCausalLMLoss(lm_head(hidden), labels)`` through :class:`FusedLMHeadLossFn`."""
+    shift = _shifted_labels(labels, ignore_index, shift_labels).to(hidden.device)
+    if num_items_in_batch is None:
+        denom = (shift != ignore_index).sum().to(torch.float32)
+    else:
+        denom = torch.as_tensor(num_items_in_batch, device=hidden.device).to(torch.float32)
+    wt = getattr(lm_head.weight, "_smt_weight_t", None)
+    return FusedLMHeadLossFn.apply(hidden, lm_head.weight, wt, shift, ignore_index, denom,
+                                   LM_HEAD_CHUNK_ROWS if chunk_rows is None else chunk_rows)
+
+
+def _fusable_lm_head(head) -> bool:
+    w = getattr(head, "weight", None)
+    return (type(head) is nn.Linear and head.bias is None and isinstance(w, torch.Tensor) and not w.requires_grad
+            and w.device.type == "cuda" and w.dtype == torch.bfloat16 and getattr(w, "_smt_fp8", None) is None)
+
+
+def fused_causal_lm_forward(self, input_ids=None, attention_mask=None, position_ids=None, past_key_values=None,
+                            inputs_embeds=None, labels=None, use_cache=None, logits_to_keep=0, **kwargs):
+    """Drop-in for ``LlamaForCausalLM.forward``. With labels, a frozen bias-free bf16 ``lm_head`` and
+    the fused loss patched in, the loss comes from :func:`fused_lm_head_loss` and the output carries
+    ``logits=None`` (``fine_tune.py:710-711`` reads only ``outputs.loss``); anything else runs
+    transformers' own forward."""
+    if (labels is None or not _fusable_lm_head(self.lm_head) or not isinstance(logits_to_keep, int)
+            or logits_to_keep != 0 or kwargs.get("return_dict") is False
+            or getattr(self, "loss_function", None) is not fused_causal_lm_loss):
+        return type(self).forward(self, input_ids=input_ids, attention_mask=attention_mask, position_ids=position_ids,
+                                  past_key_values=past_key_values, inputs_embeds=inputs_embeds, labels=labels,
+                                  use_cache=use_cache, logits_to_keep=logits_to_keep, **kwargs)
+    kwargs.pop("return_dict", None)
+    from transformers.modeling_outputs import CausalLMOutputWithPast
+    outputs = self.model(input_ids=input_ids, attention_mask=attention_mask, position_ids=position_ids,
+                         past_key_values=past_key_values, inputs_embeds=inputs_embeds, use_cache=use_cache, **kwargs)
+    loss = fused_lm_head_loss(outputs.last_hidden_state, self.lm_head, labels,
+                              num_items_in_batch=kwargs.get("num_items_in_batch"),
+                              shift_labels=kwargs.get("shift_labels"))
+    return CausalLMOutputWithPast(loss=loss, logits=None, past_key_values=outputs.past_key_values,
+                                  hidden_states=outputs.hidden_states, attentions=outputs.attentions)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -691,18 +813,25 @@ def eager_apply_rotary_pos_emb(*a, **k):
     return _ml() and _EAGER["rope"](*a, **k)
 
 
-def patch_llama(model: nn.Module, attention: bool = True, loss: bool = True) -> dict:
+def patch_llama(model: nn.Module, attention: bool = True, loss: bool = True, lm_head_loss: bool = None) -> dict:
     """Route a transformers LLaMA model's RMSNorm / RoPE / SwiGLU / attention-residual add (and, with ``attention``, its
     attention; with ``loss``, its causal-LM loss) through the fused kernels. RoPE is patched at
     module level (``modeling_llama.apply_rotary_pos_emb``, looked up by ``LlamaAttention.forward`` at
     call time); attention by switching ``config._attn_implementation`` to the registered
-    ``smt_flash``; the loss through the model's ``loss_function`` attribute.
+    ``smt_flash``; the loss through the model's ``loss_function`` attribute. ``lm_head_loss``
+    (default: ``SMT_LM_HEAD_LOSS``, on): with ``loss``, the model's forward runs a frozen LM head and
+    the loss together, chunk by chunk, without the full logits (:func:`fused_causal_lm_forward`).
     Returns counts of patched modules. Idempotent."""
     ml = _ml()
-    counts = {"rmsnorm": 0, "mlp": 0, "rope": 1, "attention": 0, "loss": 0, "decoder": 0}
+    counts = {"rmsnorm": 0, "mlp": 0, "rope": 1, "attention": 0, "loss": 0, "decoder": 0, "lm_head_loss": 0}
+    if lm_head_loss is None:
+        lm_head_loss = os.environ.get("SMT_LM_HEAD_LOSS", "1") != "0"
     if loss and hasattr(type(model), "loss_function"):
         model.loss_function = fused_causal_lm_loss
         counts["loss"] = 1
+        if lm_head_loss and isinstance(model, ml.LlamaForCausalLM):
+            model.forward = fused_causal_lm_forward.__get__(model, type(model))
+            counts["lm_head_loss"] = 1
     if attention:
         cfg = getattr(model, "config", None)
         if cfg is None:
@@ -742,6 +871,8 @@ def unpatch_llama(model: nn.Module = None) -> None:
     if model is not None:
         if "_loss_function" in model.__dict__:
             del model.__dict__["_loss_function"]
+        if "forward" in model.__dict__:
+            del model.__dict__["forward"]
         for m in model.modules():
             if isinstance(m, (ml.LlamaRMSNorm, ml.LlamaMLP, ml.LlamaDecoderLayer)) and "forward" in m.__dict__:
                 del m.__dict__["forward"]

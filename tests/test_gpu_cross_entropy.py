@@ -86,3 +86,169 @@ def test_cross_entropy_rejects_fp32_logits():
     with pytest.raises(RuntimeError):
         fl.fused_causal_lm_loss(torch.randn(1, 4, 1024, device=DEV), torch.zeros(1, 4, dtype=torch.long, device=DEV),
                                 vocab_size=1024)
+
+
+# ------------------------------------------------------------------------------------------------
+# LM head + loss, chunk by chunk (fl.FusedLMHeadLossFn): against the unfused pair it replaces,
+# lm_head (F.linear; data gradient on the transposed copy, as engine.FrozenLinearFn) followed by
+# fused_causal_lm_loss. Same kernels and scale per row, so the loss and dh agree to the GEMM
+# kernel choice for the chunk shape (printed: bit-identical or not); asserted: loss within 1e-6,
+# dh within one bf16 rounding step for all but 0.1 % of the elements.
+# ------------------------------------------------------------------------------------------------
+class _Head:
+    def __init__(self, w, wt):
+        self.weight = w
+        if wt is not None:
+            w._smt_weight_t = wt
+
+
+def _head_operands(B, S, H, V, seed, transposed=True):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    h = (torch.randn(B, S, H, device=DEV, generator=g)).bfloat16()
+    w = (torch.randn(V, H, device=DEV, generator=g) * H ** -0.5 * 2).bfloat16()
+    wt = w.t().contiguous() if transposed else None
+    labels = torch.randint(0, V, (B, S), device=DEV, generator=g)
+    return h, w, wt, labels
+
+
+def _unfused_head(h, w, wt, labels, num_items=None, dloss=1.0):
+    from sparse_matrix_tuning_amd.engine import FrozenLinearFn
+    x = h.detach().clone().requires_grad_(True)
+    logits = FrozenLinearFn.apply(x, w, wt, None) if wt is not None else torch.nn.functional.linear(x, w)
+    loss = fl.fused_causal_lm_loss(logits, labels, vocab_size=w.shape[0], num_items_in_batch=num_items)
+    (loss * dloss).backward()
+    return loss.detach(), x.grad
+
+
+def _fused_head(h, w, wt, labels, chunk, num_items=None, dloss=1.0):
+    x = h.detach().clone().requires_grad_(True)
+    w2 = w.detach().clone()              # a fresh tensor to carry this run's transposed copy
+    loss = fl.fused_lm_head_loss(x, _Head(w2, wt), labels, num_items_in_batch=num_items, chunk_rows=chunk)
+    (loss * dloss).backward()
+    return loss.detach(), x.grad
+
+
+def _close_bf16(a, b):
+    diff = (a.float() - b.float()).abs()
+    bad = (diff > b.float().abs() * 2 ** -7 + 1e-12).float().mean().item()
+    rel = ((a.float() - b.float()).norm() / b.float().norm()).item()
+    return bad < 1e-3 and rel < 4e-3, (bad, rel)
+
+
+@pytest.mark.parametrize("B,S,H,V,chunk,transposed", [
+    (2, 100, 256, 4096, 64, True),          # 200 rows: chunks of 64, 64, 64, 8
+    (2, 100, 256, 4096, 64, False),         # no transposed copy: dh = dlogits @ W (NN)
+    (1, 2048, 4096, 128256, 4096, True),    # the 8B head, one sample; one chunk
+    (1, 2048, 4096, 128256, 512, True),     # the 8B head, 4 chunks
+])
+def test_lm_head_loss_matches_unfused(B, S, H, V, chunk, transposed):
+    h, w, wt, labels = _head_operands(B, S, H, V, seed=B * S + V + chunk, transposed=transposed)
+    labels[0, : S // 7] = -100
+    lu, gu = _unfused_head(h, w, wt, labels)
+    lf, gf = _fused_head(h, w, wt, labels, chunk)
+    print(f"loss bit-identical {torch.equal(lu, lf)}, dh bit-identical {torch.equal(gu, gf)}")
+    assert abs(lf.item() - lu.item()) <= 1e-6 * abs(lu.item()), (lf.item(), lu.item())
+    ok, why = _close_bf16(gf, gu)
+    assert ok, why
+
+
+def test_lm_head_loss_upstream_gradient_and_num_items():
+    """dloss = 0.5 (exact either way: a power of two), 1/3 (fused: applied to the bf16 dh, one more
+    rounding; bounded against the fp64 truth at 1.5x the unfused error), and num_items_in_batch."""
+    B, S, H, V = 2, 64, 512, 8192
+    h, w, wt, labels = _head_operands(B, S, H, V, seed=11)
+    n = torch.tensor(100, device=DEV)
+    lu, gu = _unfused_head(h, w, wt, labels, n, dloss=0.5)
+    lf, gf = _fused_head(h, w, wt, labels, 48, n, dloss=0.5)
+    assert abs(lf.item() - lu.item()) <= 1e-6 * abs(lu.item())
+    ok, why = _close_bf16(gf, gu)
+    assert ok, why
+    # fp64 truth of d(loss / 3)/dh
+    x = h.double().reshape(-1, H).requires_grad_(True)
+    shift = torch.nn.functional.pad(labels, (0, 1), value=-100)[..., 1:].reshape(-1)
+    logit = x @ w.double().t()
+    truth_loss = torch.nn.functional.cross_entropy(logit, shift, ignore_index=-100, reduction="sum") / 100.0
+    (truth_loss / 3).backward()
+    truth = x.grad.view(B, S, H)
+    _lu, gu3 = _unfused_head(h, w, wt, labels, n, dloss=1 / 3)
+    _lf, gf3 = _fused_head(h, w, wt, labels, 48, n, dloss=1 / 3)
+    eu = ((gu3.double() - truth).norm() / truth.norm()).item()
+    ef = ((gf3.double() - truth).norm() / truth.norm()).item()
+    print(f"dloss 1/3: unfused {eu:.3e}, fused {ef:.3e} from fp64")
+    assert ef <= max(1.5 * eu, 4e-3), (ef, eu)
+
+
+def test_lm_head_loss_never_holds_the_full_logits():
+    """Peak memory of forward + backward above the operands: one chunk of logits and dh, not the
+    [T, V] logits and dlogits of the unfused pair."""
+    B, S, H, V, chunk = 4, 2048, 1024, 32768, 1024
+    h, w, wt, labels = _head_operands(B, S, H, V, seed=5)
+    full = B * S * V * 2
+
+    def peak(fn):
+        torch.cuda.synchronize()
+        base = torch.cuda.memory_allocated()
+        torch.cuda.reset_peak_memory_stats()
+        out = fn()
+        torch.cuda.synchronize()
+        p = torch.cuda.max_memory_allocated() - base
+        del out
+        return p
+
+    pu = peak(lambda: _unfused_head(h, w, wt, labels))
+    pf = peak(lambda: _fused_head(h, w, wt, labels, chunk))
+    print(f"peak above operands: unfused {pu / 2 ** 20:.0f} MiB, fused {pf / 2 ** 20:.0f} MiB")
+    assert pu >= 2 * full
+    assert pf <= chunk * V * 2 + 3 * B * S * H * 2 + (1 << 22) + w.numel() * 2, pf
+
+
+def test_lm_head_loss_without_grad_is_the_loss_only():
+    B, S, H, V = 2, 64, 256, 4096
+    h, w, wt, labels = _head_operands(B, S, H, V, seed=3)
+    lu, _ = _unfused_head(h, w, wt, labels)
+    with torch.no_grad():
+        lf = fl.fused_lm_head_loss(h, _Head(w.clone(), wt), labels, chunk_rows=40)
+    assert not lf.requires_grad
+    assert abs(lf.item() - lu.item()) <= 1e-6 * abs(lu.item())
+
+
+def test_patched_model_fuses_a_frozen_head_only():
+    """patch_llama's forward: a frozen head gives the fused loss (logits None) with the unfused loss
+    and the same trainable gradients; labels None, or a trainable head, run transformers' forward."""
+    import bench
+    torch.manual_seed(3)
+    model = bench.build_model("mini", DEV)
+    model.lm_head.weight.requires_grad_(False)
+    ids = torch.randint(0, 4096, (2, 256), device=DEV, generator=torch.Generator(device=DEV).manual_seed(4))
+
+    def run(fused):
+        model.zero_grad(set_to_none=True)
+        counts = fl.patch_llama(model, lm_head_loss=fused)
+        try:
+            out = model(input_ids=ids, labels=ids, use_cache=False)
+            out.loss.backward()
+            no_labels = model(input_ids=ids[:, :16], use_cache=False)
+        finally:
+            fl.unpatch_llama(model)
+        assert "forward" not in model.__dict__
+        return counts, out, no_labels, {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None}
+
+    c0, o0, n0, g0 = run(False)
+    c1, o1, n1, g1 = run(True)
+    assert c0["lm_head_loss"] == 0 and c1["lm_head_loss"] == 1
+    assert o0.logits is not None and o1.logits is None
+    assert n1.logits is not None and torch.equal(n0.logits, n1.logits)
+    assert abs(o1.loss.item() - o0.loss.item()) <= 1e-6 * abs(o0.loss.item())
+    assert sorted(g0) == sorted(g1) and "lm_head.weight" not in g1
+    for n in g0:
+        ok, why = _close_bf16(g1[n], g0[n])
+        assert ok, (n, why)
+    # a trainable head: transformers' forward (logits returned, the head gets its gradient)
+    model.lm_head.weight.requires_grad_(True)
+    fl.patch_llama(model)
+    try:
+        out = model(input_ids=ids, labels=ids, use_cache=False)
+        out.loss.backward()
+    finally:
+        fl.unpatch_llama(model)
+    assert out.logits is not None and model.lm_head.weight.grad is not None

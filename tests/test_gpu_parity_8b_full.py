@@ -97,9 +97,15 @@ def _probe(model):
                 out.register_hook(grab("dh", i))
         handles.append(layer.mlp.down_proj.register_forward_hook(down_out))
 
-    def head(_m, inp, out):
-        inp[0].register_hook(grab("dy_final"))
+    def norm_out(_m, _inp, out):
+        if out.requires_grad:
+            out.register_hook(grab("dy_final"))
+    handles.append(model.model.norm.register_forward_hook(norm_out))
+
+    def head(_m, _inp, out):
         out.register_hook(grab("dlogits"))
+    # the product's fused LM head + loss (fused_llama.FusedLMHeadLossFn) never calls lm_head and never
+    # holds dL/dlogits as one tensor: that row is the host's and the truth's only
     handles.append(model.lm_head.register_forward_hook(head))
     return rec, handles
 
@@ -225,7 +231,8 @@ def test_llama3_8b_full_depth_vs_fp32_truth_and_reference_restatement():
     table = {"loss": {k: r["loss"] for k, r in (("product", prod), ("host", host), ("truth", truth))},
              "top": {}, "layers": [], "modules": []}
     for key in ("dlogits", "dy_final"):
-        table["top"][key] = {"product": _rel(prod[key], truth[key]), "host": _rel(host[key], truth[key])}
+        table["top"][key] = {"product": _rel(prod[key], truth[key]) if key in prod else None,
+                             "host": _rel(host[key], truth[key])}
     L = len(truth["h"])
     for i in range(L):
         table["layers"].append({
@@ -245,7 +252,8 @@ def test_llama3_8b_full_depth_vs_fp32_truth_and_reference_restatement():
     lo = table["loss"]
     print(f"\nloss: product {lo['product']:.6f}  host {lo['host']:.6f}  fp32 truth {lo['truth']:.6f}")
     for k, v in table["top"].items():
-        print(f"{k:>9}: product {v['product']:.3e}  host {v['host']:.3e}  (relative to the fp32 truth)")
+        pv = "  n/a    " if v["product"] is None else f"{v['product']:.3e}"
+        print(f"{k:>9}: product {pv}  host {v['host']:.3e}  (relative to the fp32 truth)")
     print("layer   h: product   host    dL/dh: product   host")
     for r in table["layers"]:
         print(f"{r['layer']:5d}   {r['h_product']:.3e} {r['h_host']:.3e}     {r['dh_product']:.3e} {r['dh_host']:.3e}")
