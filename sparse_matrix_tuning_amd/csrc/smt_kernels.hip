@@ -100,37 +100,6 @@ __device__ __forceinline__ bf16x8_t tr_frag(const uint8_t* img, uint32_t k, uint
     return __builtin_bit_cast(bf16x8_t, both);
 }
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base, int64_t bytes) {
-    // every descriptor input made provably wave-uniform (T20): no waterfall loops
-    const uint64_t a = (uint64_t)(uintptr_t)base;
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-    const int n = __builtin_amdgcn_readfirstlane((int)bytes);
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
-}
-
-// Split-K partial slabs are stored WRITE-THROUGH (sc1: the line leaves the XCD's L2 as it is written,
-// MI355X_MICROARCH fence/store table) instead of as plain stores. The slabs' only reader is the reduce
-// launch, and a dependent kernel boundary first writes back every dirty L2 line of its predecessor
-// (guide price list, row "boundary": + B / 6 TB/s): 117 MB of per-sample bf16 partials per reference-
-// rounding launch is ~20 us of write-back between the two kernels, which write-through moves into the
-// wgrad kernel's own run, beside its operand stream. SMT_WGRAD_SLAB_SC1=0 builds the plain stores.
-#ifndef SMT_WGRAD_SLAB_SC1
-#define SMT_WGRAD_SLAB_SC1 1
-#endif
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ void slab_store16(__amdgpu_buffer_rsrc_t rsrc, void* base, uint32_t byte_off, uint4 v) {
-#if SMT_WGRAD_SLAB_SC1
-    (void)base;
-    u32x4_t w = {v.x, v.y, v.z, v.w};
-    __builtin_amdgcn_raw_buffer_store_b128(w, rsrc, (int)byte_off, 0, 16);    // aux 16 = sc1
-#else
-    (void)rsrc;
-    *reinterpret_cast<uint4*>(static_cast<uint8_t*>(base) + byte_off) = v;
-#endif
-}
-
 // Epilogue modes: partial slab (S > 1), or the final tile written directly (S == 1). kOutSlabBF16:
 // the reference rounding's per-sample partial when one workgroup computes a whole sample (kps == 1):
 // rounded to bf16 in the epilogue, as smt.py:397-404 rounds it, so its slab takes half the bytes.
@@ -158,8 +127,6 @@ __device__ __forceinline__ void wgrad_store_t(f32x16_t (&acc)[MB][2], void* __re
                                               int wm0, int wn0, int lane, int accumulate) {
     const int r = lane & 31;
     const int h = lane >> 5;
-    // the slab of this (tile, split): one descriptor over its 256 x 256 elements
-    const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(dst, (int64_t)kTileElems * (OUT == kOutSlabBF16 ? 2 : 4));
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
@@ -168,7 +135,7 @@ __device__ __forceinline__ void wgrad_store_t(f32x16_t (&acc)[MB][2], void* __re
             const int n0 = wn0 + nb * 32;
             const f32x16_t& a = acc[mb][nb];
             if (OUT == kOutSlabBF16) {
-                const uint32_t row = (uint32_t)(m * kTile + n0) * 2u;
+                uint16_t* row = static_cast<uint16_t*>(dst) + m * kTile + n0;
 #pragma unroll
                 for (int g = 0; g < 4; g += 2) {
                     uint32_t lo0 = f32_to_bf16_bits(a[4 * g]) | ((uint32_t)f32_to_bf16_bits(a[4 * g + 1]) << 16);
@@ -181,16 +148,9 @@ __device__ __forceinline__ void wgrad_store_t(f32x16_t (&acc)[MB][2], void* __re
                     const auto s1 = __builtin_amdgcn_permlane32_swap(lo1, hi1, false, false);
                     uint4 w;
                     w.x = s0[0]; w.y = s1[0]; w.z = s0[1]; w.w = s1[1];
-                    slab_store16(rs, dst, row + 16u * (uint32_t)(g + h), w);
+                    *reinterpret_cast<uint4*>(row + 8 * (g + h)) = w;
                 }
-            } else if (OUT == kOutSlab) {
-                const uint32_t row = (uint32_t)(m * kTile + n0) * 4u;
-#pragma unroll
-                for (int g = 0; g < 4; ++g)
-                    slab_store16(rs, dst, row + 4u * (uint32_t)(8 * g + 4 * h),
-                                 make_uint4(__float_as_uint(a[4 * g]), __float_as_uint(a[4 * g + 1]),
-                                            __float_as_uint(a[4 * g + 2]), __float_as_uint(a[4 * g + 3])));
-            } else if (OUT == kOutF32) {
+            } else if (OUT == kOutSlab || OUT == kOutF32) {
                 float* row = static_cast<float*>(dst) + m * kTile + n0;
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
@@ -450,6 +410,14 @@ __device__ __forceinline__ uint32_t lds_addr(const uint8_t* p) {
     return (uint32_t)(uintptr_t)(const lds_u8_t*)p;
 }
 
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base, int64_t bytes) {
+    // every descriptor input made provably wave-uniform (T20): no waterfall loops
+    const uint64_t a = (uint64_t)(uintptr_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    const int n = __builtin_amdgcn_readfirstlane((int)bytes);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
+}
 
 template <int OUT, int SLOTS, bool BATCH>
 __global__ __launch_bounds__(kWgThreads, 1)
