@@ -245,13 +245,35 @@ def attach_channel_gather_groups(model: torch.nn.Module) -> int:
     return n
 
 
+def attach_column_block_groups(model: torch.nn.Module) -> int:
+    """q/k/v_proj of an attention module and gate/up_proj of an MLP read one input: the members with
+    trainable tiles keep ONE packed copy of the union of the column blocks their tiles read
+    (smt.ColumnBlockGroup on each member's frozen weight, ``_smt_cb_group``) instead of one copy each.
+    Same operands, so the tile gradients are bit-identical. Returns the number of groups."""
+    from .smt.smt import ColumnBlockGroup
+    n = 0
+    for m in model.modules():
+        for names in (("q_proj", "k_proj", "v_proj"), ("gate_proj", "up_proj")):
+            mem = [getattr(m, x, None) for x in names]
+            mem = [x for x in mem if isinstance(x, LinearLayer_MatrixSparsity) and len(x.tiles)
+                   and x.selected_weight.requires_grad and x.weight.device.type == "cuda"]
+            if len(mem) < 2 or len({x.weight.shape[1] for x in mem}) != 1:
+                continue
+            grp = ColumnBlockGroup({c for x in mem for c in x.tiles.column_blocks()}, mem[0].weight.device)
+            for x in mem:
+                x.weight._smt_cb_group = grp
+            n += 1
+    return n
+
+
 def detach_transposed_weights(model: torch.nn.Module) -> None:
-    """Undo :func:`attach_transposed_weights` (and :func:`attach_channel_gather_groups`)."""
+    """Undo :func:`attach_transposed_weights` (and :func:`attach_channel_gather_groups`,
+    :func:`attach_column_block_groups`)."""
     for m in model.modules():
         if "_smt_joint_qkv_grad" in m.__dict__:
             del m.__dict__["_smt_joint_qkv_grad"]
         w = getattr(m, "weight", None)
-        for attr in ("_smt_weight_t", "_smt_fp8", "_smt_cgather"):
+        for attr in ("_smt_weight_t", "_smt_fp8", "_smt_cgather", "_smt_cb_group"):
             if isinstance(w, torch.Tensor) and hasattr(w, attr):
                 delattr(w, attr)
         if type(m) is torch.nn.Linear and "forward" in m.__dict__:
@@ -332,7 +354,8 @@ class WgradBatcher:
         """bf16 path: ``g2`` the output gradient [T, out], ``x2`` the saved input (row-major, or the
         block-major packed copy when ``packed``); ``seq_len``: the reference's per-sample rounding
         (smt.smt.set_wgrad_rounding)."""
-        self._add(sink, "bf16", (g2, x2, tiles, bool(packed), seq_len), (g2, x2), len(tiles))
+        self._add(sink, "bf16", (g2, x2, tiles, packed if isinstance(packed, dict) else bool(packed), seq_len),
+                  (g2, x2), len(tiles))
 
     def add_mx(self, sink: "_GradSink", g2: torch.Tensor, rb_dev: torch.Tensor, mx, tiles, col_pos=None) -> None:
         """fp8 path: ``g2`` is quantised into its MX row blocks ``rb_dev`` at launch time; ``mx`` is
@@ -368,9 +391,11 @@ class WgradBatcher:
         kind = pending[0][1]
         dev = pending[0][2][0].device
         if kind == "bf16":
-            key = ("bf16", dev.index) + tuple((id(p[2][2]), p[2][3]) for p in pending)
+            # packed: False / True (the module's own copy) or a ColumnBlockGroup's position map
+            key = ("bf16", dev.index) + tuple((id(p[2][2]), id(p[2][3]) if isinstance(p[2][3], dict) else p[2][3])
+                                              for p in pending)
             ktiles = lambda: [p[2][2].kernel_tiles(p[2][3]) for p in pending]
-            ids = [p[2][2] for p in pending]
+            ids = [(p[2][2], p[2][3]) for p in pending]
         else:
             key = ("mx", dev.index) + tuple((id(p[2][3]), id(p[2][4])) for p in pending)
             ktiles = lambda: [p[2][3].mx_kernel_tiles(p[2][4]) for p in pending]
@@ -770,6 +795,7 @@ class SMTEngine:
         self.transposed_bytes = 0
         self.fp8_bytes = 0
         self.channel_gather_groups = 0
+        self.column_block_groups = 0
         if optimizer is not None:
             owner = {}
             channel_rows = False
@@ -789,6 +815,9 @@ class SMTEngine:
                 # gradients as one GEMM over smt_flash's joint [dq | dk | dv] (dgrad.py)
                 joint = cfg.get("joint_qkv_dgrad", os.environ.get("SMT_JOINT_QKV", "1") != "0")
                 self.transposed_bytes = attach_transposed_weights(model, joint_qkv=joint)
+            if owner and cfg.get("shared_input_blocks", True):
+                # q/k/v (gate/up) keep one packed copy of their shared input's column blocks
+                self.column_block_groups = attach_column_block_groups(model)
             if channel_rows and cfg.get("shared_channel_gather", os.environ.get("SMT_SHARED_CGATHER", "1") != "0"):
                 # the channel path's q/k/v read one input: one partial-input gather per layer
                 self.channel_gather_groups = attach_channel_gather_groups(model)

@@ -33,6 +33,7 @@ from __future__ import annotations
 
 import os
 import re
+import weakref
 from typing import Iterable, List, Optional, Sequence, Tuple
 
 import torch
@@ -203,9 +204,16 @@ class TileIndex:
             seen.setdefault(c, len(seen))
         return list(seen)
 
-    def packed_tables(self, device: torch.device):
+    def packed_tables(self, device: torch.device, col_pos: Optional[dict] = None):
         """Device tables for the packed-input backward: int32 [n_cb] column blocks and the int32
-        [n, 2] table of (row_block, position of the column block in the packed input)."""
+        [n, 2] table of (row_block, position of the column block in the packed input). With
+        ``col_pos`` the positions in a :class:`ColumnBlockGroup`'s shared copy (the group's blocks)."""
+        if col_pos is not None:
+            key = ("packed_grp", id(col_pos), device.type, device.index)
+            e = self._dev.get(key)
+            if e is None or e[0] is not col_pos:
+                e = self._dev[key] = (col_pos, (None, _hip.tile_table(self.kernel_tiles(col_pos), device)))
+            return e[1]
         key = ("packed", device.type, device.index)
         t = self._dev.get(key)
         if t is None:
@@ -216,10 +224,17 @@ class TileIndex:
             self._dev[key] = t
         return t
 
-    def kernel_tiles(self, packed: bool) -> List[Tuple[int, int]]:
+    def kernel_tiles(self, packed) -> List[Tuple[int, int]]:
         """The ``(row_block, col_block)`` list as the wgrad kernel addresses the input: for the
-        block-major packed input of ``colblock_gather`` the column block is its position there."""
-        key = ("ktiles", packed)
+        block-major packed input of ``colblock_gather`` the column block is its position there
+        (``packed`` True: this module's own copy; a dict: a group's column-block positions)."""
+        if isinstance(packed, dict):
+            key = ("ktiles_grp", id(packed))
+            e = self._dev.get(key)
+            if e is None or e[0] is not packed:
+                e = self._dev[key] = (packed, [(r, packed[c]) for r, c in self.index_list])
+            return e[1]
+        key = ("ktiles", bool(packed))
         t = self._dev.get(key)
         if t is None:
             if packed:
@@ -328,6 +343,33 @@ class TileIndex:
 
 def _as_tile_index(index) -> TileIndex:
     return index if isinstance(index, TileIndex) else TileIndex(index)
+
+
+class ColumnBlockGroup:
+    """SMT linears that read ONE input (q/k/v_proj of an attention module, gate/up_proj of an MLP)
+    keep one packed copy of the union of the input's column blocks their tiles read, instead of
+    one copy per member: the members' blocks overlap (at the 8B bench point q/k/v read ~19 blocks of
+    their 16-block input between them, ~12 distinct). The engine sets it on the members' frozen
+    weights (``weight._smt_cb_group``); the first member's forward gathers the union, the others
+    reuse that copy (same input object and version), and each member's tile table indexes it. Only
+    weak references are held here: the members' saved tensors own the copy, so it is freed with
+    the last member's backward, as the per-member copies were."""
+
+    def __init__(self, col_blocks, device: torch.device):
+        self.col_blocks = sorted({int(c) for c in col_blocks})
+        self.pos = {c: i for i, c in enumerate(self.col_blocks)}
+        self.cb_dev = torch.tensor(self.col_blocks, dtype=torch.int32).to(device)
+        self._cache = None              # (weakref to the input, its version, weakref to the copy)
+
+    def packed_input(self, x: torch.Tensor, x2d: torch.Tensor, sink) -> torch.Tensor:
+        c = self._cache
+        if c is not None and c[0]() is x and c[1] == x._version:
+            p = c[2]()
+            if p is not None:
+                return p
+        p = _off_stream(sink, lambda: _hip.colblock_gather(x2d, self.cb_dev), x2d)
+        self._cache = (weakref.ref(x), x._version, weakref.ref(p))
+        return p
 
 
 # ------------------------------------------------------------------------------------------------
@@ -457,7 +499,9 @@ class linearZ(torch.autograd.Function):
     slices (``ctx.list1``, smt.py:351-358), which hold the whole input alive. Here, when the tiles
     touch at most half of the input's 256-column blocks, one ``smt_colblock_gather`` launch packs
     exactly those blocks into a ``[T, n_cb*256]`` copy and the input itself is not saved (for a
-    down_proj with ~14 tiles that is 14 of its 56 blocks); otherwise the input is saved as is. Under
+    down_proj with ~14 tiles that is 14 of its 56 blocks); otherwise the input is saved as is.
+    Members of a :class:`ColumnBlockGroup` (q/k/v_proj, gate/up_proj under the engine) share ONE
+    packed copy of the union of their blocks, or the input itself when the union covers it. Under
     the "views" activation policy the input is always saved as is (the reference's own choice), and
     under "selective" a norm's / SwiGLU's output is not saved at all (rebuilt in the backward). The
     tile gradients are bit-identical every way (same operands, same kernel, same order).
@@ -515,6 +559,17 @@ class linearZ(torch.autograd.Function):
             saved = None
             ctx.packed = True
         elif (policy != "views" and ctx.needs_input_grad[1] and len(tiles) and input.device.type == "cuda"
+                and getattr(weight, "_smt_cb_group", None) is not None
+                and len(weight._smt_cb_group.col_blocks) < in_blocks
+                and all(c in weight._smt_cb_group.pos for c in tiles.column_blocks())):
+            # one packed copy of the group's union of column blocks, shared with the other members
+            grp = weight._smt_cb_group
+            x2d = _rows_ready(input.reshape(-1, weight.shape[1]))
+            saved = grp.packed_input(input, x2d, ctx.sink)
+            ctx.packed = grp.pos
+        elif (policy != "views" and ctx.needs_input_grad[1] and len(tiles) and input.device.type == "cuda"
+                and (getattr(weight, "_smt_cb_group", None) is None
+                     or not all(c in weight._smt_cb_group.pos for c in tiles.column_blocks()))
                 and 2 * len(tiles.column_blocks()) <= in_blocks):
             cb_dev, _ = tiles.packed_tables(input.device)
             x2d = _rows_ready(input.reshape(-1, weight.shape[1]))
@@ -587,7 +642,8 @@ class linearZ(torch.autograd.Function):
                 x2 = _recompute_blocks(ctx.recompute, cb_dev)
                 ctx.recompute = None
             elif ctx.packed:
-                x2, table = saved, tiles.packed_tables(dev)[1]
+                x2 = saved
+                table = tiles.packed_tables(dev, ctx.packed if isinstance(ctx.packed, dict) else None)[1]
             else:
                 x2, table = _rows_ready(saved.reshape(-1, weight.shape[1])), tiles.device_table(dev)
             sink = ctx.sink
