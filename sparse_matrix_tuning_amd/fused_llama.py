@@ -521,24 +521,29 @@ LM_HEAD_CHUNK_ROWS = int(os.environ.get("SMT_LM_HEAD_CHUNK_ROWS", "4096"))
 
 
 class FusedLMHeadLossFn(torch.autograd.Function):
-    """``lm_head`` (frozen, no bias) followed by :class:`FusedCrossEntropyFn`, without the full
-    ``[T, V]`` logits. At B 16 x S 2048 x V 128256 the unfused pair keeps the bf16 logits (8.4 GB)
-    for the loss backward and allocates the same again for ``dlogits`` at the start of the backward,
-    when every activation of the step is still alive: that 16.8 GB is the SMT step's peak HBM.
+    """``lm_head`` (no bias) followed by :class:`FusedCrossEntropyFn`, without the full ``[T, V]``
+    logits. At B 16 x S 2048 x V 128256 the unfused pair keeps the bf16 logits (8.4 GB) for the loss
+    backward and allocates the same again for ``dlogits`` at the start of the backward, when every
+    activation of the step is still alive: that 16.8 GB is the SMT step's peak HBM (and the
+    full fine-tuning warm-up's).
 
     Here each chunk of ``LM_HEAD_CHUNK_ROWS`` rows runs, inside the forward: the logits GEMM
-    (``hidden @ W^T``), the row log-sum-exp (``smt_ce_fwd``), and (when ``hidden`` needs a gradient)
-    ``dlogits`` for a unit upstream gradient written over the chunk's logits (``smt_ce_bwd`` in
-    place; each element is read and written by one thread) and the data gradient ``dlogits @ W``
-    (TN on the engine's transposed copy when there is one, as :class:`..engine.FrozenLinearFn` runs
-    it). Only ``dh [T, H]`` (268 MB) is kept; the backward scales it by the upstream gradient.
+    (``hidden @ W^T``), the row log-sum-exp (``smt_ce_fwd``), and (when ``hidden`` or ``W`` needs a
+    gradient) ``dlogits`` for a unit upstream gradient written over the chunk's logits
+    (``smt_ce_bwd`` in place; each element is read and written by one thread), the data gradient
+    ``dlogits @ W`` (TN on the engine's transposed copy when there is one, as
+    :class:`..engine.FrozenLinearFn` runs it) and, for a trainable head (the warm-up), the chunk's
+    ``dlogits^T @ hidden`` added into an fp32 ``[V, H]`` accumulator (hipBLASLt bf16 x bf16 -> fp32,
+    beta 1), rounded to bf16 once after the last chunk. Only ``dh [T, H]`` (268 MB) and ``dW``
+    are kept; the backward scales them by the upstream gradient.
 
     Per row this is the unfused arithmetic: the same GEMM products, the same kernels and, for the
     upstream gradient 1 that ``loss.backward()`` gives (``engine.backward`` with one accumulation
     step), the same ``dlogits`` scale ``1 / denom``. Any other upstream gradient is applied to the
-    bf16 ``dh`` (one more rounding than folding it into ``dlogits`` first, exact for powers of
-    two). Whether hipBLASLt picks the same kernel for a chunk's GEMM shape as for the whole batch's
-    decides bit-identity of the logits and ``dh``; tests/test_gpu_cross_entropy.py checks it."""
+    bf16 ``dh`` / ``dW`` (one more rounding than folding it into ``dlogits`` first, exact for powers
+    of two). Whether hipBLASLt picks the same kernel for a chunk's GEMM shape as for the whole batch's
+    decides bit-identity of the logits and ``dh``; ``dW`` sums the same fp32 products in chunk order
+    before its one rounding. tests/test_gpu_cross_entropy.py checks both."""
 
     @staticmethod
     def forward(ctx, hidden, weight, weight_t, labels, ignore_index, denom, chunk_rows):
@@ -555,6 +560,7 @@ class FusedLMHeadLossFn(torch.autograd.Function):
         if labels.numel() != N:
             raise ValueError(f"lm head loss: {labels.numel()} labels for {N} rows")
         need_dh = bool(ctx.needs_input_grad[0])
+        need_dw = bool(ctx.needs_input_grad[1])
         lib = _hip.load()
         stream = _stream(hidden)
         lse = torch.empty(N, dtype=torch.float32, device=hidden.device)
@@ -564,28 +570,42 @@ class FusedLMHeadLossFn(torch.autograd.Function):
         C = max(1, min(int(chunk_rows), N))
         buf = torch.empty((C, V), dtype=hidden.dtype, device=hidden.device)
         w_dgrad = weight_t.t() if weight_t is not None else weight
+        acc = torch.empty((V, H), dtype=torch.float32, device=hidden.device) if need_dw else None
         for r0 in range(0, N, C):
             c = min(C, N - r0)
             lg = buf[:c]
-            torch.mm(h2[r0:r0 + c], weight.t(), out=lg)
+            hc = h2[r0:r0 + c]
+            torch.mm(hc, weight.t(), out=lg)
             rc = lib.smt_ce_fwd(lg.data_ptr(), lg.stride(0), labels[r0:].data_ptr(), c, V, int(ignore_index),
                                 lse[r0:].data_ptr(), rows[r0:].data_ptr(), stream)
             _hip._check(rc, "smt_ce_fwd")
-            if need_dh:
+            if need_dh or need_dw:
                 rc = lib.smt_ce_bwd(lg.data_ptr(), lg.stride(0), labels[r0:].data_ptr(), lse[r0:].data_ptr(),
                                     scale.data_ptr(), c, V, int(ignore_index), lg.data_ptr(), lg.stride(0), stream)
                 _hip._check(rc, "smt_ce_bwd")
+            if need_dh:
                 torch.mm(lg, w_dgrad, out=dh[r0:r0 + c])
+            if need_dw:
+                if r0 == 0:
+                    torch.mm(lg.t(), hc, out_dtype=torch.float32, out=acc)
+                else:
+                    torch.addmm(acc, lg.t(), hc, out_dtype=torch.float32, out=acc)
         del buf
-        if need_dh:
-            ctx.save_for_backward(dh)
+        dw = None
+        if need_dw:
+            dw = acc.to(weight.dtype)
+            del acc
+        ctx.save_for_backward(dh, dw)
         ctx.shape = hidden.shape
         return rows.sum() / denom
 
     @staticmethod
     def backward(ctx, dloss):
-        (dh,) = ctx.saved_tensors
-        return torch.mul(dh, dloss.float()).view(ctx.shape), None, None, None, None, None, None
+        dh, dw = ctx.saved_tensors
+        scale = dloss.float()
+        gh = torch.mul(dh, scale).view(ctx.shape) if dh is not None else None
+        gw = torch.mul(dw, scale) if dw is not None else None
+        return gh, gw, None, None, None, None, None
 
 
 def fused_lm_head_loss(hidden, lm_head: nn.Linear, labels, num_items_in_batch=None, ignore_index=-100,
@@ -603,14 +623,15 @@ def fused_lm_head_loss(hidden, lm_head: nn.Linear, labels, num_items_in_batch=No
 
 def _fusable_lm_head(head) -> bool:
     w = getattr(head, "weight", None)
-    return (type(head) is nn.Linear and head.bias is None and isinstance(w, torch.Tensor) and not w.requires_grad
+    return (type(head) is nn.Linear and head.bias is None and isinstance(w, torch.Tensor)
             and w.device.type == "cuda" and w.dtype == torch.bfloat16 and getattr(w, "_smt_fp8", None) is None)
 
 
 def fused_causal_lm_forward(self, input_ids=None, attention_mask=None, position_ids=None, past_key_values=None,
                             inputs_embeds=None, labels=None, use_cache=None, logits_to_keep=0, **kwargs):
-    """Drop-in for ``LlamaForCausalLM.forward``. With labels, a frozen bias-free bf16 ``lm_head`` and
-    the fused loss patched in, the loss comes from :func:`fused_lm_head_loss` and the output carries
+    """Drop-in for ``LlamaForCausalLM.forward``. With labels, a bias-free bf16 ``lm_head`` (frozen in the
+    SMT phase, trainable in the warm-up) and the fused loss patched in, the loss comes from
+    :func:`fused_lm_head_loss` and the output carries
     ``logits=None`` (``fine_tune.py:710-711`` reads only ``outputs.loss``); anything else runs
     transformers' own forward."""
     if (labels is None or not _fusable_lm_head(self.lm_head) or not isinstance(logits_to_keep, int)
@@ -819,8 +840,8 @@ def patch_llama(model: nn.Module, attention: bool = True, loss: bool = True, lm_
     module level (``modeling_llama.apply_rotary_pos_emb``, looked up by ``LlamaAttention.forward`` at
     call time); attention by switching ``config._attn_implementation`` to the registered
     ``smt_flash``; the loss through the model's ``loss_function`` attribute. ``lm_head_loss``
-    (default: ``SMT_LM_HEAD_LOSS``, on): with ``loss``, the model's forward runs a frozen LM head and
-    the loss together, chunk by chunk, without the full logits (:func:`fused_causal_lm_forward`).
+    (default: ``SMT_LM_HEAD_LOSS``, on): with ``loss``, the model's forward runs the LM head and the
+    loss together, chunk by chunk, without the full logits (:func:`fused_causal_lm_forward`).
     Returns counts of patched modules. Idempotent."""
     ml = _ml()
     counts = {"rmsnorm": 0, "mlp": 0, "rope": 1, "attention": 0, "loss": 0, "decoder": 0, "lm_head_loss": 0}

@@ -152,6 +152,26 @@ def test_lm_head_loss_matches_unfused(B, S, H, V, chunk, transposed):
     assert ok, why
 
 
+@pytest.mark.parametrize("B,S,H,V,chunk", [(2, 100, 256, 4096, 64), (1, 2048, 4096, 128256, 512)])
+def test_lm_head_loss_trainable_head_matches_unfused(B, S, H, V, chunk):
+    """The warm-up's trainable head: dW from an fp32 accumulator over the chunks (one bf16 rounding)
+    against autograd's one GEMM over all rows; dh and the loss as for a frozen head."""
+    h, w, _wt, labels = _head_operands(B, S, H, V, seed=B + S + chunk, transposed=False)
+    labels[0, S // 3: S // 3 + 9] = -100
+    x0, w0 = h.detach().clone().requires_grad_(True), w.detach().clone().requires_grad_(True)
+    lu = fl.fused_causal_lm_loss(torch.nn.functional.linear(x0, w0), labels, vocab_size=V)
+    lu.backward()
+    x1, w1 = h.detach().clone().requires_grad_(True), w.detach().clone().requires_grad_(True)
+    lf = fl.fused_lm_head_loss(x1, _Head(w1, None), labels, chunk_rows=chunk)
+    lf.backward()
+    print(f"loss bit-identical {torch.equal(lu, lf)}, dh bit-identical {torch.equal(x0.grad, x1.grad)}, "
+          f"dW bit-identical {torch.equal(w0.grad, w1.grad)}")
+    assert abs(lf.item() - lu.item()) <= 1e-6 * abs(lu.item())
+    for a, b in ((x1.grad, x0.grad), (w1.grad, w0.grad)):
+        ok, why = _close_bf16(a, b)
+        assert ok, why
+
+
 def test_lm_head_loss_upstream_gradient_and_num_items():
     """dloss = 0.5 (exact either way: a power of two), 1/3 (fused: applied to the bf16 dh, one more
     rounding; bounded against the fp64 truth at 1.5x the unfused error), and num_items_in_batch."""
@@ -212,9 +232,10 @@ def test_lm_head_loss_without_grad_is_the_loss_only():
     assert abs(lf.item() - lu.item()) <= 1e-6 * abs(lu.item())
 
 
-def test_patched_model_fuses_a_frozen_head_only():
-    """patch_llama's forward: a frozen head gives the fused loss (logits None) with the unfused loss
-    and the same trainable gradients; labels None, or a trainable head, run transformers' forward."""
+def test_patched_model_fuses_the_head():
+    """patch_llama's forward: a frozen head (SMT phase) and a trainable one (warm-up) give the fused
+    loss (logits None) with the unfused loss and the same gradients; labels None runs transformers'
+    forward."""
     import bench
     torch.manual_seed(3)
     model = bench.build_model("mini", DEV)
@@ -243,12 +264,13 @@ def test_patched_model_fuses_a_frozen_head_only():
     for n in g0:
         ok, why = _close_bf16(g1[n], g0[n])
         assert ok, (n, why)
-    # a trainable head: transformers' forward (logits returned, the head gets its gradient)
+    # a trainable head (the warm-up): fused too, and the head gets its gradient
     model.lm_head.weight.requires_grad_(True)
-    fl.patch_llama(model)
-    try:
-        out = model(input_ids=ids, labels=ids, use_cache=False)
-        out.loss.backward()
-    finally:
-        fl.unpatch_llama(model)
-    assert out.logits is not None and model.lm_head.weight.grad is not None
+    c2, o2, _n2, g2 = run(False)
+    c3, o3, _n3, g3 = run(True)
+    assert o2.logits is not None and o3.logits is None
+    assert abs(o3.loss.item() - o2.loss.item()) <= 1e-6 * abs(o2.loss.item())
+    assert sorted(g2) == sorted(g3) and "lm_head.weight" in g3
+    for n in g2:
+        ok, why = _close_bf16(g3[n], g2[n])
+        assert ok, (n, why)

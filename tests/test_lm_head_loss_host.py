@@ -14,7 +14,7 @@ def test_shifted_labels_follow_for_causal_lm_loss():
     assert fl._shifted_labels(labels, -100, explicit).tolist() == [9] * 4 + [8] * 4
 
 
-def test_only_frozen_bias_free_bf16_device_heads_fuse():
+def test_only_bias_free_bf16_device_heads_fuse():
     head = nn.Linear(16, 32, bias=False).bfloat16()
     head.weight.requires_grad_(False)
     assert not fl._fusable_lm_head(head)                 # host tensor: transformers' forward
@@ -24,8 +24,8 @@ def test_only_frozen_bias_free_bf16_device_heads_fuse():
     biased = nn.Linear(16, 32, bias=True)
     biased.weight.requires_grad_(False)
     assert not fl._fusable_lm_head(biased)
-    trainable = nn.Linear(16, 32, bias=False)
-    assert not fl._fusable_lm_head(trainable)
+    fp32 = nn.Linear(16, 32, bias=False)
+    assert not fl._fusable_lm_head(fp32)
     assert not fl._fusable_lm_head(nn.Identity())
 
 
