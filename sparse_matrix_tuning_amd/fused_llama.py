@@ -518,6 +518,11 @@ def _shifted_labels(labels, ignore_index, shift_labels):
 # LM head + causal-LM cross entropy, row chunk by row chunk
 # ------------------------------------------------------------------------------------------------
 LM_HEAD_CHUNK_ROWS = int(os.environ.get("SMT_LM_HEAD_CHUNK_ROWS", "4096"))
+# a trainable head (the warm-up) adds each chunk's dlogits^T @ hidden into an fp32 [V, H] accumulator:
+# longer chunks mean fewer, longer-K GEMMs (4096-row chunks: 8 x 4.37 ms at the 8B head,
+# profiles/r05_k_kernel_stats.csv). The chunk buffer is transient in the forward, below the warm-up's
+# peak (the backward's bf16 gradients of every parameter).
+LM_HEAD_DW_CHUNK_ROWS = int(os.environ.get("SMT_LM_HEAD_DW_CHUNK_ROWS", "16384"))
 
 
 class FusedLMHeadLossFn(torch.autograd.Function):
@@ -567,7 +572,7 @@ class FusedLMHeadLossFn(torch.autograd.Function):
         rows = torch.empty(N, dtype=torch.float32, device=hidden.device)
         dh = torch.empty((N, H), dtype=hidden.dtype, device=hidden.device) if need_dh else None
         scale = (1.0 / denom.to(torch.float32)).reshape(1).contiguous()
-        C = max(1, min(int(chunk_rows), N))
+        C = max(1, min(max(int(chunk_rows), LM_HEAD_DW_CHUNK_ROWS if need_dw else 0), N))
         buf = torch.empty((C, V), dtype=hidden.dtype, device=hidden.device)
         w_dgrad = weight_t.t() if weight_t is not None else weight
         acc = torch.empty((V, H), dtype=torch.float32, device=hidden.device) if need_dw else None

@@ -153,9 +153,11 @@ def test_lm_head_loss_matches_unfused(B, S, H, V, chunk, transposed):
 
 
 @pytest.mark.parametrize("B,S,H,V,chunk", [(2, 100, 256, 4096, 64), (1, 2048, 4096, 128256, 512)])
-def test_lm_head_loss_trainable_head_matches_unfused(B, S, H, V, chunk):
+def test_lm_head_loss_trainable_head_matches_unfused(B, S, H, V, chunk, monkeypatch):
     """The warm-up's trainable head: dW from an fp32 accumulator over the chunks (one bf16 rounding)
-    against autograd's one GEMM over all rows; dh and the loss as for a frozen head."""
+    against autograd's one GEMM over all rows; dh and the loss as for a frozen head. (The chunk floor
+    for a trainable head is lifted so that several chunks accumulate.)"""
+    monkeypatch.setattr(fl, "LM_HEAD_DW_CHUNK_ROWS", 0)
     h, w, _wt, labels = _head_operands(B, S, H, V, seed=B + S + chunk, transposed=False)
     labels[0, S // 3: S // 3 + 9] = -100
     x0, w0 = h.detach().clone().requires_grad_(True), w.detach().clone().requires_grad_(True)
