@@ -251,6 +251,11 @@ def attach_column_block_groups(model: torch.nn.Module) -> int:
     (smt.ColumnBlockGroup on each member's frozen weight, ``_smt_cb_group``) instead of one copy each.
     Same operands, so the tile gradients are bit-identical. Returns the number of groups."""
     from .smt.smt import ColumnBlockGroup
+    for m in model.modules():
+        # groups of an earlier selection (the frozen W objects outlive the SMT modules) are dropped
+        w = getattr(m, "weight", None)
+        if isinstance(w, torch.Tensor) and hasattr(w, "_smt_cb_group"):
+            delattr(w, "_smt_cb_group")
     n = 0
     for m in model.modules():
         for names in (("q_proj", "k_proj", "v_proj"), ("gate_proj", "up_proj")):
