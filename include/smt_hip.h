@@ -156,14 +156,16 @@ int smt_tile_wgrad(const void* grad_out, int64_t ld_grad_out,
  */
 #define SMT_WGRAD_MAX_MODULES 16
 typedef struct smt_wgrad_module {
-    const void* grad_out;           /* bf16 [T, ld_grad_out]                                       */
-    const void* x;                  /* bf16; block c at x + c * x_block_stride, rows of ld_x        */
+    const void* grad_out;           /* [T, ld_grad_out] of operand_dtype                            */
+    const void* x;                  /* block c at x + c * x_block_stride, rows of ld_x              */
     int64_t ld_grad_out;
     int64_t ld_x;
     int64_t x_block_stride;
     void* grad_tiles;               /* this module's [n_m*256, 256] output of out_dtype            */
     int32_t accumulate;             /* add to grad_tiles instead of overwriting                     */
-    int32_t reserved;
+    int32_t operand_dtype;          /* ABI v11 (was reserved, 0): SMT_DTYPE_BF16 (0), _FP16 or _FP32,
+                                       one per launch -- the reference's --dtype (fine_tune.py:955-959).
+                                       out_dtype is that dtype (16-bit operands) or SMT_DTYPE_FP32    */
 } smt_wgrad_module;                 /* 56 bytes                                                     */
 
 /* Workspace bytes smt_tile_wgrad_batch needs for T rows and n_tiles tiles over all its modules. */
@@ -179,6 +181,8 @@ size_t smt_wgrad_batch_workspace_bytes(int64_t T, int32_t n_tiles);
  * entries, passed to the kernels by value. Batching makes one launch of the ~8 tiles a module of a
  * spread selection carries plus those of its neighbours: fewer split-K slabs per tile and one launch
  * instead of several (the engine batches consecutive backward calls).
+ * Operands bf16 or fp16 (the 16-bit kernels: bf16 / f16 MFMA, fp32 accumulation) or fp32 (exact f32
+ * MFMA, v_mfma_f32_32x32x2_f32), per the modules' operand_dtype (ABI v11); smt_tile_wgrad is bf16.
  */
 int smt_tile_wgrad_batch(const smt_wgrad_module* modules, int32_t n_modules, int64_t T,
                          const int32_t* tile_tab_dev, const int32_t* order_dev, int32_t n_tiles,
@@ -193,7 +197,9 @@ size_t smt_wgrad_seq_workspace_bytes(int64_t T, int64_t seq_len, int32_t n_tiles
  * each tile's gradient is computed exactly as smt.py:397-404 rounds it: one [256, 256] product per
  * sample accumulated in fp32 and rounded to bf16 (torch.matmul of bf16), the B bf16 partials summed in
  * fp32 in sample order and rounded to bf16 (torch.sum(dim=0)), then, with accumulate, added to the
- * output (autograd's accumulation into .grad). An fp32 output holds that bf16 value exactly. T must be
+ * output (autograd's accumulation into .grad). An fp32 output holds that bf16 value exactly. fp16
+ * operands round to fp16 in the same places; for fp32 operands the roundings are the identity (each
+ * sample's fp32 partial, summed in sample order in fp32). T must be
  * a whole number of samples (SMT_E_INVALID otherwise). Deterministic; about n_samples / S times the
  * default mode's fp32 slab traffic.
  */

@@ -24,6 +24,7 @@ SCORE_MEAN_ABS, SCORE_ABS_MEAN, SCORE_L1, SCORE_L2 = 0, 1, 2, 3
 ADAM_DEEPSPEED, ADAM_TORCH = 0, 1
 
 _DT = {torch.bfloat16: DTYPE_BF16, torch.float32: DTYPE_FP32, torch.float16: DTYPE_FP16}
+ABI_VERSION = 11            # include/smt_hip.h: smt_wgrad_module.operand_dtype (v11)
 
 # Every function the headers declare (include/smt_hip.h, smt_model_ops.h, smt_attention.h); tests check the
 # library exports each of them.
@@ -57,7 +58,7 @@ class WgradModule(ctypes.Structure):
     """smt_wgrad_module (include/smt_hip.h): one module of a batched tile wgrad."""
     _fields_ = [("grad_out", ctypes.c_void_p), ("x", ctypes.c_void_p), ("ld_grad_out", ctypes.c_int64),
                 ("ld_x", ctypes.c_int64), ("x_block_stride", ctypes.c_int64), ("grad_tiles", ctypes.c_void_p),
-                ("accumulate", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("accumulate", ctypes.c_int32), ("operand_dtype", ctypes.c_int32)]
 
 
 class WgradMxModule(ctypes.Structure):
@@ -210,6 +211,9 @@ def load(build_if_missing: bool = False) -> ctypes.CDLL:
                 fn = getattr(lib, name)
                 fn.restype = res
                 fn.argtypes = args
+            if lib.smt_abi_version() != ABI_VERSION:
+                raise RuntimeError(f"{path} implements C ABI v{lib.smt_abi_version()}, this package v{ABI_VERSION}: "
+                                   "rebuild it (`python -c 'import __graft_entry__ as g; g.build()'`)")
             _lib = lib
     return _lib
 
@@ -297,8 +301,14 @@ def tile_wgrad(grad_out2d: torch.Tensor, x: torch.Tensor, tile_rc: torch.Tensor,
     input, row-major [T, in] (X_c = its c-th 256-column block), or the block-major [n_cb, T, 256]
     copy of ``colblock_gather`` (X_c = x[c]). ``order``: optional device int32 schedule permutation
     (speed only). ``seq_len``: the reference's rounding (``smt_tile_wgrad_batch_seq``): T is
-    T / seq_len samples, each sample's partial rounded to bf16 before the batch sum."""
-    if seq_len:
+    T / seq_len samples, each sample's partial rounded to bf16 before the batch sum. Operands bf16,
+    fp16 or fp32 (the reference's --dtype; fp16 / fp32 go through the batched entry point with one
+    module), ``out`` the operand dtype or fp32."""
+    if grad_out2d.dtype != torch.bfloat16 and grad_out2d.shape[0] == 0:
+        if not accumulate:
+            out.zero_()
+        return out
+    if seq_len or grad_out2d.dtype != torch.bfloat16:
         n = tile_rc.shape[0]
         tab = torch.zeros(n, 4, dtype=torch.int32, device=tile_rc.device)
         tab[:, 1:3] = tile_rc
@@ -364,16 +374,21 @@ def tile_wgrad_batch(items: Sequence[tuple], tile_tab: torch.Tensor, order: Opti
     dev = _require_device(tile_tab, order, *[t for it in items for t in it[:3]])
     T = items[0][0].shape[0]
     out_dtype = items[0][2].dtype
+    op_dtype = items[0][0].dtype
+    if op_dtype not in (torch.bfloat16, torch.float16, torch.float32):
+        raise NotImplementedError(f"tile_wgrad_batch: operands bf16, fp16 or fp32 (got {op_dtype})")
+    if out_dtype not in (op_dtype, torch.float32) or out_dtype == torch.float64:
+        raise ValueError(f"tile_wgrad_batch: {op_dtype} operands give {op_dtype} or fp32 tiles (got {out_dtype})")
     mods = (WgradModule * len(items))()
     for i, (g, x, out, acc) in enumerate(items):
-        if g.dtype != torch.bfloat16 or x.dtype != torch.bfloat16:
-            raise NotImplementedError("tile_wgrad_batch: bf16 operands only")
+        if g.dtype != op_dtype or x.dtype != op_dtype:
+            raise NotImplementedError(f"tile_wgrad_batch: one operand dtype per launch (got {g.dtype}, {x.dtype})")
         if g.dim() != 2 or g.shape[0] != T or g.stride(1) != 1:
             raise ValueError("tile_wgrad_batch: every grad_out must be [T, features] with the same T")
-        if out.dtype != out_dtype or out.dtype not in (torch.bfloat16, torch.float32) or not out.is_contiguous():
-            raise ValueError("tile_wgrad_batch: outputs must be contiguous and all bf16 or all fp32")
+        if out.dtype != out_dtype or not out.is_contiguous():
+            raise ValueError("tile_wgrad_batch: outputs must be contiguous and of one dtype")
         ld_x, xbs = _wgrad_x_layout(x, T, "tile_wgrad_batch")
-        mods[i] = WgradModule(_ptr(g), _ptr(x), g.stride(0), ld_x, xbs, _ptr(out), int(bool(acc)), 0)
+        mods[i] = WgradModule(_ptr(g), _ptr(x), g.stride(0), ld_x, xbs, _ptr(out), int(bool(acc)), _DT[op_dtype])
     if tile_tab.dtype != torch.int32 or tile_tab.dim() != 2 or tile_tab.shape[1] != 4:
         raise ValueError("tile_wgrad_batch: tile_tab must be int32 [n, 4]")
     n = tile_tab.shape[0]

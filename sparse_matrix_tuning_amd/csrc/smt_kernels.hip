@@ -67,6 +67,30 @@ __device__ __forceinline__ float half_bits_to_f32(uint16_t h) {
     return (float)__builtin_bit_cast(_Float16, h);
 }
 
+// Operand formats of the tile wgrad. The reference runs linearZ in the model's dtype
+// (fine_tune.py:955-959 --dtype bf16 | fp16 | fp32; deepspeed_helpers.py:53-61), so the per-sample
+// partials are rounded to that dtype (smt.py:397-404). FMT 0 = bf16, 1 = fp16 (the same 16-bit
+// staging, transposed reads and slabs; only the MFMA and the roundings differ), 2 = fp32 operands
+// (wgrad_f32_kernel; "rounding" a partial to fp32 is the identity).
+constexpr int kFmtBF16 = 0, kFmtF16 = 1, kFmtF32 = 2;
+
+__device__ __forceinline__ uint16_t f32_to_half_bits(float f) {
+    const _Float16 h = (_Float16)f;                        // round to nearest even, overflow to inf
+    return __builtin_bit_cast(uint16_t, h);
+}
+
+template <int FMT>
+__device__ __forceinline__ uint16_t to16(float f) { return FMT == kFmtF16 ? f32_to_half_bits(f) : f32_to_bf16_bits(f); }
+
+template <int FMT>
+__device__ __forceinline__ float from16(uint32_t b) {
+    return FMT == kFmtF16 ? half_bits_to_f32((uint16_t)b) : bf16_bits_to_f32(b);
+}
+
+// a partial rounded to the operand dtype (fp32 operands: unchanged)
+template <int FMT>
+__device__ __forceinline__ float round_op(float v) { return FMT == kFmtF32 ? v : from16<FMT>(to16<FMT>(v)); }
+
 // ------------------------------------------------------------------------------------------------
 // Per-tile weight gradient (smt.py:397-404):
 //   C[m][n] = sum_t g[t][r*256+m] * x[t][c*256+n],  m,n in [0,256)
@@ -89,6 +113,18 @@ static_assert(kChunksPerThread == 4, "staging geometry");
 
 __device__ __forceinline__ uint32_t img_off(uint32_t k, uint32_t byte_in_row) {
     return k * kRowBytes + (byte_in_row ^ ((k & 3u) << 6));
+}
+
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+
+// one 32x32x16 MFMA on 16-bit fragments in operand format FMT (the fragments are raw 16-bit lanes)
+template <int FMT>
+__device__ __forceinline__ f32x16_t mfma16(const bf16x8_t& a, const bf16x8_t& b, const f32x16_t& c) {
+    if constexpr (FMT == kFmtF16)
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b),
+                                                      c, 0, 0, 0);
+    else
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
 __device__ __forceinline__ bf16x8_t tr_frag(const uint8_t* img, uint32_t k, uint32_t byte_in_row) {
@@ -122,7 +158,7 @@ __device__ __forceinline__ void* wgrad_dst(void* out_ptr, int tile, int s, int S
 // instead of 16 scalar stores per accumulator -- the store tail is issue-bound (cdna_hip_programming
 // T21). For the bf16 slab the two half-waves' 4-column runs are paired by v_permlane32_swap into
 // 8-column rows: one 16-B store per lane per pair of runs.
-template <int OUT, int MB>
+template <int OUT, int MB, int FMT = kFmtBF16>
 __device__ __forceinline__ void wgrad_store_t(f32x16_t (&acc)[MB][2], void* __restrict__ dst,
                                               int wm0, int wn0, int lane, int accumulate) {
     const int r = lane & 31;
@@ -138,10 +174,10 @@ __device__ __forceinline__ void wgrad_store_t(f32x16_t (&acc)[MB][2], void* __re
                 uint16_t* row = static_cast<uint16_t*>(dst) + m * kTile + n0;
 #pragma unroll
                 for (int g = 0; g < 4; g += 2) {
-                    uint32_t lo0 = f32_to_bf16_bits(a[4 * g]) | ((uint32_t)f32_to_bf16_bits(a[4 * g + 1]) << 16);
-                    uint32_t lo1 = f32_to_bf16_bits(a[4 * g + 2]) | ((uint32_t)f32_to_bf16_bits(a[4 * g + 3]) << 16);
-                    uint32_t hi0 = f32_to_bf16_bits(a[4 * g + 4]) | ((uint32_t)f32_to_bf16_bits(a[4 * g + 5]) << 16);
-                    uint32_t hi1 = f32_to_bf16_bits(a[4 * g + 6]) | ((uint32_t)f32_to_bf16_bits(a[4 * g + 7]) << 16);
+                    uint32_t lo0 = to16<FMT>(a[4 * g]) | ((uint32_t)to16<FMT>(a[4 * g + 1]) << 16);
+                    uint32_t lo1 = to16<FMT>(a[4 * g + 2]) | ((uint32_t)to16<FMT>(a[4 * g + 3]) << 16);
+                    uint32_t hi0 = to16<FMT>(a[4 * g + 4]) | ((uint32_t)to16<FMT>(a[4 * g + 5]) << 16);
+                    uint32_t hi1 = to16<FMT>(a[4 * g + 6]) | ((uint32_t)to16<FMT>(a[4 * g + 7]) << 16);
                     // vdst = run g, src = run g+1: lanes 0-31 end with columns 8g..8g+7 of their row,
                     // lanes 32-63 with columns 8(g+1)..8(g+1)+7
                     const auto s0 = __builtin_amdgcn_permlane32_swap(lo0, hi0, false, false);
@@ -170,12 +206,12 @@ __device__ __forceinline__ void wgrad_store_t(f32x16_t (&acc)[MB][2], void* __re
                     float v0 = a[4 * g], v1 = a[4 * g + 1], v2 = a[4 * g + 2], v3 = a[4 * g + 3];
                     if (accumulate) {
                         const uint2 o = *p;
-                        v0 += bf16_bits_to_f32(o.x & 0xffffu); v1 += bf16_bits_to_f32(o.x >> 16);
-                        v2 += bf16_bits_to_f32(o.y & 0xffffu); v3 += bf16_bits_to_f32(o.y >> 16);
+                        v0 += from16<FMT>(o.x & 0xffffu); v1 += from16<FMT>(o.x >> 16);
+                        v2 += from16<FMT>(o.y & 0xffffu); v3 += from16<FMT>(o.y >> 16);
                     }
                     uint2 w;
-                    w.x = f32_to_bf16_bits(v0) | ((uint32_t)f32_to_bf16_bits(v1) << 16);
-                    w.y = f32_to_bf16_bits(v2) | ((uint32_t)f32_to_bf16_bits(v3) << 16);
+                    w.x = to16<FMT>(v0) | ((uint32_t)to16<FMT>(v1) << 16);
+                    w.y = to16<FMT>(v2) | ((uint32_t)to16<FMT>(v3) << 16);
                     *p = w;
                 }
             }
@@ -233,7 +269,7 @@ __device__ __forceinline__ void wgrad_span(int s, int64_t T, int64_t chunk, int6
     }
 }
 
-template <int OUT, bool BATCH>
+template <int OUT, bool BATCH, int FMT = kFmtBF16>
 __global__ __launch_bounds__(kWgThreads, 2)
 void wgrad_partial_kernel(const WgradModules mods, int64_t T, int64_t chunk, int S, int64_t seq, int kps, int n_tiles,
                           const int32_t* __restrict__ tile_tab, const int32_t* __restrict__ order,
@@ -349,13 +385,13 @@ void wgrad_partial_kernel(const WgradModules mods, int64_t T, int64_t chunk, int
             for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
                 for (int nb = 0; nb < 2; ++nb)
-                    acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[nb], af[mb], acc[mb][nb], 0, 0, 0);
+                    acc[mb][nb] = mfma16<FMT>(bfr[nb], af[mb], acc[mb][nb]);
         }
         if (st + 1 < nst) swrite(buf ^ 1);
         __syncthreads();
     }
 
-    wgrad_store_t<OUT, 4>(acc, (OUT == kOutSlab || OUT == kOutSlabBF16) ? wgrad_dst<OUT>(slab, tile, s, S) : tt.out,
+    wgrad_store_t<OUT, 4, FMT>(acc, (OUT == kOutSlab || OUT == kOutSlabBF16) ? wgrad_dst<OUT>(slab, tile, s, S) : tt.out,
                           wm * 128, wn * 64, lane, tt.accumulate);
 }
 
@@ -419,7 +455,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base,
     return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
 }
 
-template <int OUT, int SLOTS, bool BATCH>
+template <int OUT, int SLOTS, bool BATCH, int FMT = kFmtBF16>
 __global__ __launch_bounds__(kWgThreads, 1)
 void wgrad_dma_kernel(const WgradModules mods, int64_t T, int64_t chunk, int S, int64_t seq, int kps, int n_tiles,
                       const int32_t* __restrict__ tile_tab, const int32_t* __restrict__ order,
@@ -521,10 +557,10 @@ void wgrad_dma_kernel(const WgradModules mods, int64_t T, int64_t chunk, int S, 
             for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
                 for (int nb = 0; nb < 2; ++nb)
-                    acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[nb], af[mb], acc[mb][nb], 0, 0, 0);
+                    acc[mb][nb] = mfma16<FMT>(bfr[nb], af[mb], acc[mb][nb]);
         }
     }
-    wgrad_store_t<OUT, 4>(acc, (OUT == kOutSlab || OUT == kOutSlabBF16) ? wgrad_dst<OUT>(slab, tile, s, S) : tt.out,
+    wgrad_store_t<OUT, 4, FMT>(acc, (OUT == kOutSlab || OUT == kOutSlabBF16) ? wgrad_dst<OUT>(slab, tile, s, S) : tt.out,
                           wm * 128, wn * 64, lane, tt.accumulate);
 }
 
@@ -556,7 +592,7 @@ __device__ __forceinline__ bf16x8_t qtr_frag(const uint8_t* img, uint32_t k, uin
     return __builtin_bit_cast(bf16x8_t, both);
 }
 
-template <int OUT, int QS, bool BATCH>
+template <int OUT, int QS, bool BATCH, int FMT = kFmtBF16>
 __global__ __launch_bounds__(kQThreads, 2)
 void wgrad_quarter_kernel(const WgradModules mods, int64_t T, int64_t chunk, int S, int64_t seq, int kps, int n_tiles,
                           const int32_t* __restrict__ tile_tab, const int32_t* __restrict__ order,
@@ -658,14 +694,116 @@ void wgrad_quarter_kernel(const WgradModules mods, int64_t T, int64_t chunk, int
             for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
                 for (int nb = 0; nb < 2; ++nb)
-                    acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[nb], af[mb], acc[mb][nb], 0, 0, 0);
+                    acc[mb][nb] = mfma16<FMT>(bfr[nb], af[mb], acc[mb][nb]);
         }
     }
-    wgrad_store_t<OUT, 2>(acc, (OUT == kOutSlab || OUT == kOutSlabBF16) ? wgrad_dst<OUT>(slab, tile, s, S) : tt.out,
+    wgrad_store_t<OUT, 2, FMT>(acc, (OUT == kOutSlab || OUT == kOutSlabBF16) ? wgrad_dst<OUT>(slab, tile, s, S) : tt.out,
                           qm * 128 + wm * 64, qn * 128 + wn * 64, lane, tt.accumulate);
 }
 
-__device__ __forceinline__ float bf16_round(float v) { return bf16_bits_to_f32(f32_to_bf16_bits(v)); }
+// ------------------------------------------------------------------------------------------------
+// fp32 operands (the reference's --dtype fp32, fine_tune.py:955-959): exact f32 products on
+// v_mfma_f32_32x32x2_f32 (1/16 of the bf16 rate, cdna_hip_programming "FP32-input MFMA"). A workgroup
+// of 4 waves owns one 128x128 quarter of a tile for one split of T, as wgrad_quarter_kernel (same
+// XCD-contiguous logical ids, slabs and reduce); each wave 64x64 = 2x2 accumulators. The operand
+// lane maps of the f32 form (A[i = l&31][k = l>>5], B[k = l>>5][j = l&31]) are rows of the K-major
+// slices themselves: lanes 0-31 read 32 consecutive floats of row t, lanes 32-63 of row t+1, so the
+// fragments come straight from global memory (128-B coalesced pieces, L1/L2-shared by the waves and
+// quarters that read the same slice) with no LDS image and no transpose. x is A and g is B, so the
+// accumulators hold C^T as in the 16-bit kernels and wgrad_store_t is shared. kUnroll row pairs are
+// loaded ahead of the MFMAs that consume them.
+// ------------------------------------------------------------------------------------------------
+constexpr int kF32Threads = 256;
+constexpr int kF32Unroll = 8;                              // row pairs (K = 2 each) per loaded batch
+
+template <int OUT, bool BATCH>
+__global__ __launch_bounds__(kF32Threads, 2)
+void wgrad_f32_kernel(const WgradModules mods, int64_t T, int64_t chunk, int S, int64_t seq, int kps, int n_tiles,
+                      const int32_t* __restrict__ tile_tab, const int32_t* __restrict__ order,
+                      float* __restrict__ slab) {
+    const int total = n_tiles * S * 4;
+    const int b = blockIdx.x;
+    const int q8 = total >> 3, r8 = total & 7, xcd = b & 7;
+    const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+    const int qd = L & 3;
+    const int ts = L >> 2;
+    const int s = ts / n_tiles;
+    const int li = ts - s * n_tiles;
+    const int tile = order != nullptr ? order[li] : li;
+    const int qm = qd >> 1, qn = qd & 1;
+    int mi = 0, r, c, ti;
+    if (BATCH) {
+        mi = tile_tab[4 * tile]; r = tile_tab[4 * tile + 1]; c = tile_tab[4 * tile + 2]; ti = tile_tab[4 * tile + 3];
+    } else {
+        r = tile_tab[2 * tile]; c = tile_tab[2 * tile + 1]; ti = tile;
+    }
+    const smt_wgrad_module& m = mods.m[mi];
+    const int64_t ldg = m.ld_grad_out, ldx = m.ld_x;
+    const float* gb = static_cast<const float*>(m.grad_out) + (int64_t)r * kTile;
+    const float* xb = static_cast<const float*>(m.x) + (int64_t)c * m.x_block_stride;
+    int64_t t_begin, t_end;
+    wgrad_span(s, T, chunk, seq, kps, t_begin, t_end);
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int m0 = qm * 128 + (wave >> 1) * 64;            // the wave's origin in the tile (rows: g)
+    const int n0 = qn * 128 + (wave & 1) * 64;             // (columns: x)
+    const int kr = lane >> 5, cl = lane & 31;
+
+    f32x16_t acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    typedef float Frags[kF32Unroll][2];
+    auto load = [&](Frags& ga, Frags& xa, int64_t t0) {    // kF32Unroll row pairs from row t0 on
+        // buffer loads over this batch's rows: 32-bit lane offsets, and the descriptor's range check
+        // reads the rows past the split's end as zeros (no per-load branch); the second 32-column
+        // half of a fragment is the same address + 128 B
+        const int64_t nrows = (t_end - t0 < 2 * kF32Unroll) ? (t_end - t0) : 2 * kF32Unroll;
+        const __amdgpu_buffer_rsrc_t rg = uniform_rsrc(gb + t0 * ldg, nrows * ldg * 4);
+        const __amdgpu_buffer_rsrc_t rx = uniform_rsrc(xb + t0 * ldx, nrows * ldx * 4);
+        int og = (int)((kr * ldg + m0 + cl) * 4), ox = (int)((kr * ldx + n0 + cl) * 4);
+        const int sg = (int)(2 * ldg * 4), sx = (int)(2 * ldx * 4);
+#pragma unroll
+        for (int u = 0; u < kF32Unroll; ++u) {
+            ga[u][0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rg, og, 0, 0));
+            ga[u][1] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rg, og + 128, 0, 0));
+            xa[u][0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, ox, 0, 0));
+            xa[u][1] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, ox + 128, 0, 0));
+            og += sg;
+            ox += sx;
+        }
+    };
+    auto compute = [&](const Frags& ga, const Frags& xa) {
+#pragma unroll
+        for (int u = 0; u < kF32Unroll; ++u)
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb)
+                    acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[u][nb], ga[u][mb], acc[mb][nb], 0, 0, 0);
+    };
+    // two register batches: the next batch's loads are in flight under the current batch's MFMAs
+    constexpr int kStep = 2 * kF32Unroll;
+    Frags g0, x0, g1, x1;
+    if (t_begin < t_end) load(g0, x0, t_begin);
+    for (int64_t t0 = t_begin; t0 < t_end; t0 += 2 * kStep) {
+        const bool more1 = t0 + kStep < t_end;
+        if (more1) load(g1, x1, t0 + kStep);
+        compute(g0, x0);
+        if (!more1) break;
+        if (t0 + 2 * kStep < t_end) load(g0, x0, t0 + 2 * kStep);
+        compute(g1, x1);
+    }
+    void* out = static_cast<uint8_t*>(m.grad_tiles) + (int64_t)ti * kTileElems * 4;
+    wgrad_store_t<OUT, 2, kFmtF32>(acc, OUT == kOutSlab ? wgrad_dst<OUT>(slab, tile, s, S) : out, m0, n0, lane,
+                                   m.accumulate);
+}
 
 // Sum the S partial slabs of one tile in order s = 0..S-1 (deterministic) and write the tile (this
 // workgroup's 1024 of its elements). kps > 0 (reference rounding, wgrad_span): the slabs come in
@@ -673,7 +811,7 @@ __device__ __forceinline__ float bf16_round(float v) { return bf16_bits_to_f32(f
 // the samples are summed in order in fp32 and the sum is rounded to bf16 once more (smt.py:397-404:
 // bf16 matmul per sample, then torch.sum(dim=0) of the bf16 partials, accumulated in fp32), before
 // the optional accumulation into the output (autograd's add into .grad).
-template <bool OUT_F32, bool SLAB16 = false>
+template <bool OUT_F32, bool SLAB16 = false, int FMT = kFmtBF16>
 __device__ __forceinline__ void wgrad_reduce_tile(const float* __restrict__ slab, int S, int kps, int tile,
                                                   void* __restrict__ tile_out, int accumulate) {
     const int e = (((blockIdx.x & 63) << 8) + threadIdx.x) * 4;
@@ -687,11 +825,11 @@ __device__ __forceinline__ void wgrad_reduce_tile(const float* __restrict__ slab
 #pragma unroll 8
         for (int s = 0; s < S; ++s) {                      // unrolled: several slab loads in flight
             const uint2 v = *reinterpret_cast<const uint2*>(s16 + (int64_t)s * kTileElems);
-            sum.x += bf16_bits_to_f32(v.x & 0xffffu); sum.y += bf16_bits_to_f32(v.x >> 16);
-            sum.z += bf16_bits_to_f32(v.y & 0xffffu); sum.w += bf16_bits_to_f32(v.y >> 16);
+            sum.x += from16<FMT>(v.x & 0xffffu); sum.y += from16<FMT>(v.x >> 16);
+            sum.z += from16<FMT>(v.y & 0xffffu); sum.w += from16<FMT>(v.y >> 16);
         }
-        sum.x = bf16_round(sum.x); sum.y = bf16_round(sum.y);
-        sum.z = bf16_round(sum.z); sum.w = bf16_round(sum.w);
+        sum.x = round_op<FMT>(sum.x); sum.y = round_op<FMT>(sum.y);
+        sum.z = round_op<FMT>(sum.z); sum.w = round_op<FMT>(sum.w);
     } else if (kps <= 0) {
         sum = *reinterpret_cast<const float4*>(src);
 #pragma unroll 4
@@ -708,11 +846,11 @@ __device__ __forceinline__ void wgrad_reduce_tile(const float* __restrict__ slab
                 const float4 v = *reinterpret_cast<const float4*>(src + (int64_t)(s0 + j) * kTileElems);
                 part.x += v.x; part.y += v.y; part.z += v.z; part.w += v.w;
             }
-            sum.x += bf16_round(part.x); sum.y += bf16_round(part.y);
-            sum.z += bf16_round(part.z); sum.w += bf16_round(part.w);
+            sum.x += round_op<FMT>(part.x); sum.y += round_op<FMT>(part.y);
+            sum.z += round_op<FMT>(part.z); sum.w += round_op<FMT>(part.w);
         }
-        sum.x = bf16_round(sum.x); sum.y = bf16_round(sum.y);
-        sum.z = bf16_round(sum.z); sum.w = bf16_round(sum.w);
+        sum.x = round_op<FMT>(sum.x); sum.y = round_op<FMT>(sum.y);
+        sum.z = round_op<FMT>(sum.z); sum.w = round_op<FMT>(sum.w);
     }
     const int64_t o = e;
     void* out = tile_out;
@@ -727,24 +865,24 @@ __device__ __forceinline__ void wgrad_reduce_tile(const float* __restrict__ slab
         uint2* dst = reinterpret_cast<uint2*>(static_cast<uint16_t*>(out) + o);
         if (accumulate) {
             const uint2 a = *dst;
-            sum.x += bf16_bits_to_f32(a.x & 0xffffu);
-            sum.y += bf16_bits_to_f32(a.x >> 16);
-            sum.z += bf16_bits_to_f32(a.y & 0xffffu);
-            sum.w += bf16_bits_to_f32(a.y >> 16);
+            sum.x += from16<FMT>(a.x & 0xffffu);
+            sum.y += from16<FMT>(a.x >> 16);
+            sum.z += from16<FMT>(a.y & 0xffffu);
+            sum.w += from16<FMT>(a.y >> 16);
         }
         uint2 w;
-        w.x = (uint32_t)f32_to_bf16_bits(sum.x) | ((uint32_t)f32_to_bf16_bits(sum.y) << 16);
-        w.y = (uint32_t)f32_to_bf16_bits(sum.z) | ((uint32_t)f32_to_bf16_bits(sum.w) << 16);
+        w.x = (uint32_t)to16<FMT>(sum.x) | ((uint32_t)to16<FMT>(sum.y) << 16);
+        w.y = (uint32_t)to16<FMT>(sum.z) | ((uint32_t)to16<FMT>(sum.w) << 16);
         *dst = w;
     }
 }
 
 // 64 workgroups x 256 threads x 4 elements per tile; tile i's output = out + i tiles
-template <bool OUT_F32, bool SLAB16 = false>
+template <bool OUT_F32, bool SLAB16 = false, int FMT = kFmtBF16>
 __global__ __launch_bounds__(256)
 void wgrad_reduce_kernel(const float* __restrict__ slab, int S, int kps, void* __restrict__ out, int accumulate) {
     const int tile = blockIdx.x >> 6;
-    wgrad_reduce_tile<OUT_F32, SLAB16>(slab, S, kps, tile, static_cast<uint8_t*>(out) + (int64_t)tile * kTileElems * (OUT_F32 ? 4 : 2),
+    wgrad_reduce_tile<OUT_F32, SLAB16, FMT>(slab, S, kps, tile, static_cast<uint8_t*>(out) + (int64_t)tile * kTileElems * (OUT_F32 ? 4 : 2),
                                accumulate);
 }
 
@@ -762,13 +900,13 @@ void wgrad_reduce_mx_batch_kernel(const float* __restrict__ slab, int S, const W
 }
 
 // the same over a batch: each tile's output and accumulate flag from its module (wgrad_tile)
-template <bool OUT_F32, bool SLAB16 = false>
+template <bool OUT_F32, bool SLAB16 = false, int FMT = kFmtBF16>
 __global__ __launch_bounds__(256)
 void wgrad_reduce_batch_kernel(const float* __restrict__ slab, int S, int kps, const WgradModules mods,
                                const int32_t* __restrict__ tile_tab) {
     const int tile = blockIdx.x >> 6;
     const WgradTile tt = wgrad_tile<true, OUT_F32 ? 4 : 2>(mods, tile_tab, tile);
-    wgrad_reduce_tile<OUT_F32, SLAB16>(slab, S, kps, tile, tt.out, tt.accumulate);
+    wgrad_reduce_tile<OUT_F32, SLAB16, FMT>(slab, S, kps, tile, tt.out, tt.accumulate);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1947,7 +2085,7 @@ extern "C" {
 
 const char* smt_last_error(void) { return g_err; }
 
-int smt_abi_version(void) { return 10; }
+int smt_abi_version(void) { return 11; }
 
 size_t smt_wgrad_workspace_bytes(int64_t T, int32_t n_tiles) {
     if (T <= 0 || n_tiles <= 0) return 0;
@@ -1963,10 +2101,12 @@ namespace {
 // Launch the tile wgrad of `n_tiles` tiles (one module, or a batch) and, when split, its reduce.
 // max_ld: the largest leading dimension of any operand (the LDS-DMA kernels' 32-bit buffer offsets
 // need chunk * ld * 2 < 2^31, otherwise the register-staged kernel, which addresses with 64 bits).
-template <bool BATCH>
-int wgrad_launch(const WgradModules& mods, int64_t T, int64_t max_ld, const int32_t* tab, const int32_t* order,
-                 int32_t n_tiles, int32_t out_dtype, void* workspace, size_t workspace_bytes, hipStream_t stream,
-                 int64_t seq = 0) {
+// FMT: the operands' format (kFmtBF16 / kFmtF16: the 16-bit kernels; kFmtF32: wgrad_f32_kernel, on
+// the same split, slabs and reduce, so the workspace sizes do not depend on the format).
+template <bool BATCH, int FMT>
+int wgrad_launch_fmt(const WgradModules& mods, int64_t T, int64_t max_ld, const int32_t* tab, const int32_t* order,
+                     int32_t n_tiles, int32_t out_dtype, void* workspace, size_t workspace_bytes, hipStream_t stream,
+                     int64_t seq) {
     const WgradSplit sp = seq > 0 ? wgrad_split_seq(T, seq, n_tiles) : wgrad_split(T, n_tiles);
     const bool use_slab = sp.S > 1 || sp.seq > 0;       // reference rounding always reduces
     const dim3 grid(n_tiles * sp.S), block(kWgThreads);
@@ -1976,9 +2116,10 @@ int wgrad_launch(const WgradModules& mods, int64_t T, int64_t max_ld, const int3
     const bool dma = sp.chunk * max_ld * 2 < (int64_t)0x7fffffff;
     const bool quarter = dma && sp.quarter;
     // reference rounding with one workgroup per sample piece (kps == 1): the LDS-DMA kernels round
-    // each sample's partial to bf16 themselves and write half-size slabs (SMT_WGRAD_SLAB16=0: fp32)
+    // each sample's partial to the 16-bit operand format themselves and write half-size slabs
+    // (SMT_WGRAD_SLAB16=0: fp32)
     static const bool slab16_ok = [] { const char* e = getenv("SMT_WGRAD_SLAB16"); return !(e && atoi(e) == 0); }();
-    const bool slab16 = slab16_ok && dma && sp.seq > 0 && sp.kps == 1;
+    const bool slab16 = FMT != kFmtF32 && slab16_ok && dma && sp.seq > 0 && sp.kps == 1;
     float* slab = nullptr;
     if (use_slab) {
         const size_t need = (size_t)n_tiles * sp.S * kTileElems * sizeof(float);
@@ -1987,50 +2128,90 @@ int wgrad_launch(const WgradModules& mods, int64_t T, int64_t max_ld, const int3
         if (!aligned16(workspace)) return fail(SMT_E_ALIGN, "smt_tile_wgrad: workspace not 16-byte aligned");
         slab = static_cast<float*>(workspace);
     }
+    if constexpr (FMT == kFmtF32) {
+        const dim3 fgrid(n_tiles * sp.S * 4), fblock(kF32Threads);
+        if (!use_slab) hipLaunchKernelGGL((wgrad_f32_kernel<kOutF32, BATCH>), fgrid, fblock, 0, stream, mods, T,
+                                          sp.chunk, sp.S, sp.seq, sp.kps, n_tiles, tab, order, slab);
+        else hipLaunchKernelGGL((wgrad_f32_kernel<kOutSlab, BATCH>), fgrid, fblock, 0, stream, mods, T, sp.chunk,
+                                sp.S, sp.seq, sp.kps, n_tiles, tab, order, slab);
+        const int rc = check_launch("wgrad_f32_kernel");
+        if (rc || !use_slab) return rc;
+    } else {
 #define SMT_WGRAD_LAUNCH(OUT)                                                                                     \
     do {                                                                                                          \
-        if (!dma) hipLaunchKernelGGL((wgrad_partial_kernel<OUT, BATCH>), grid, block, 0, stream, mods, T, sp.chunk, \
-                                     sp.S, sp.seq, sp.kps, n_tiles, tab, order, slab);                           \
-        else if (quarter) hipLaunchKernelGGL((wgrad_quarter_kernel<OUT, kQSlots, BATCH>), qgrid, qblock, 0, stream,  \
-                                     mods, T, sp.chunk, sp.S, sp.seq, sp.kps, n_tiles, tab, order, slab);        \
-        else hipLaunchKernelGGL((wgrad_dma_kernel<OUT, kDmaSlotsDefault, BATCH>), grid, block, 0, stream, mods, T,   \
-                                sp.chunk, sp.S, sp.seq, sp.kps, n_tiles, tab, order, slab);                      \
+        if (!dma) hipLaunchKernelGGL((wgrad_partial_kernel<OUT, BATCH, FMT>), grid, block, 0, stream, mods, T,    \
+                                     sp.chunk, sp.S, sp.seq, sp.kps, n_tiles, tab, order, slab);                  \
+        else if (quarter) hipLaunchKernelGGL((wgrad_quarter_kernel<OUT, kQSlots, BATCH, FMT>), qgrid, qblock, 0,   \
+                                     stream, mods, T, sp.chunk, sp.S, sp.seq, sp.kps, n_tiles, tab, order, slab); \
+        else hipLaunchKernelGGL((wgrad_dma_kernel<OUT, kDmaSlotsDefault, BATCH, FMT>), grid, block, 0, stream,     \
+                                mods, T, sp.chunk, sp.S, sp.seq, sp.kps, n_tiles, tab, order, slab);              \
     } while (0)
-    if (!use_slab) {
-        if (out_dtype == SMT_DTYPE_FP32) SMT_WGRAD_LAUNCH(kOutF32);
-        else SMT_WGRAD_LAUNCH(kOutBF16);
-        return check_launch("wgrad kernel");
-    }
-    if (slab16) {
-        // the LDS-DMA kernels only (dma is true here)
-        if (quarter) hipLaunchKernelGGL((wgrad_quarter_kernel<kOutSlabBF16, kQSlots, BATCH>), qgrid, qblock, 0, stream,
-                                        mods, T, sp.chunk, sp.S, sp.seq, sp.kps, n_tiles, tab, order, slab);
-        else hipLaunchKernelGGL((wgrad_dma_kernel<kOutSlabBF16, kDmaSlotsDefault, BATCH>), grid, block, 0, stream, mods, T,
-                                sp.chunk, sp.S, sp.seq, sp.kps, n_tiles, tab, order, slab);
-    } else {
-        SMT_WGRAD_LAUNCH(kOutSlab);
-    }
+        if (!use_slab) {
+            if (out_dtype == SMT_DTYPE_FP32) SMT_WGRAD_LAUNCH(kOutF32);
+            else SMT_WGRAD_LAUNCH(kOutBF16);
+            return check_launch("wgrad kernel");
+        }
+        if (slab16) {
+            // the LDS-DMA kernels only (dma is true here)
+            if (quarter) hipLaunchKernelGGL((wgrad_quarter_kernel<kOutSlabBF16, kQSlots, BATCH, FMT>), qgrid, qblock, 0,
+                                            stream, mods, T, sp.chunk, sp.S, sp.seq, sp.kps, n_tiles, tab, order, slab);
+            else hipLaunchKernelGGL((wgrad_dma_kernel<kOutSlabBF16, kDmaSlotsDefault, BATCH, FMT>), grid, block, 0,
+                                    stream, mods, T, sp.chunk, sp.S, sp.seq, sp.kps, n_tiles, tab, order, slab);
+        } else {
+            SMT_WGRAD_LAUNCH(kOutSlab);
+        }
 #undef SMT_WGRAD_LAUNCH
-    int rc = check_launch("wgrad kernel");
-    if (rc) return rc;
+        const int rc = check_launch("wgrad kernel");
+        if (rc) return rc;
+    }
     const dim3 rgrid(n_tiles * 64), rblock(256);
     const int kps = sp.seq > 0 ? sp.kps : 0;
 #define SMT_WGRAD_REDUCE(F32, S16)                                                                                 \
     do {                                                                                                          \
-        if (BATCH) hipLaunchKernelGGL((wgrad_reduce_batch_kernel<F32, S16>), rgrid, rblock, 0, stream, slab, sp.S,  \
-                                      kps, mods, tab);                                                            \
-        else hipLaunchKernelGGL((wgrad_reduce_kernel<F32, S16>), rgrid, rblock, 0, stream, slab, sp.S, kps,          \
+        if (BATCH) hipLaunchKernelGGL((wgrad_reduce_batch_kernel<F32, S16, FMT>), rgrid, rblock, 0, stream, slab,  \
+                                      sp.S, kps, mods, tab);                                                      \
+        else hipLaunchKernelGGL((wgrad_reduce_kernel<F32, S16, FMT>), rgrid, rblock, 0, stream, slab, sp.S, kps,   \
                                 mods.m[0].grad_tiles, mods.m[0].accumulate);                                      \
     } while (0)
-    if (out_dtype == SMT_DTYPE_FP32) {
-        if (slab16) SMT_WGRAD_REDUCE(true, true);
-        else SMT_WGRAD_REDUCE(true, false);
+    if constexpr (FMT == kFmtF32) {
+        SMT_WGRAD_REDUCE(true, false);
     } else {
-        if (slab16) SMT_WGRAD_REDUCE(false, true);
-        else SMT_WGRAD_REDUCE(false, false);
+        if (out_dtype == SMT_DTYPE_FP32) {
+            if (slab16) SMT_WGRAD_REDUCE(true, true);
+            else SMT_WGRAD_REDUCE(true, false);
+        } else {
+            if (slab16) SMT_WGRAD_REDUCE(false, true);
+            else SMT_WGRAD_REDUCE(false, false);
+        }
     }
 #undef SMT_WGRAD_REDUCE
     return check_launch("wgrad_reduce_kernel");
+}
+
+// The operand format from SMT_DTYPE_* (checked by the entry points against out_dtype).
+template <bool BATCH>
+int wgrad_launch(const WgradModules& mods, int64_t T, int64_t max_ld, const int32_t* tab, const int32_t* order,
+                 int32_t n_tiles, int32_t out_dtype, void* workspace, size_t workspace_bytes, hipStream_t stream,
+                 int64_t seq = 0, int32_t operand_dtype = SMT_DTYPE_BF16) {
+    switch (operand_dtype) {
+        case SMT_DTYPE_FP16:
+            return wgrad_launch_fmt<BATCH, kFmtF16>(mods, T, max_ld, tab, order, n_tiles, out_dtype, workspace,
+                                                    workspace_bytes, stream, seq);
+        case SMT_DTYPE_FP32:
+            return wgrad_launch_fmt<BATCH, kFmtF32>(mods, T, max_ld, tab, order, n_tiles, out_dtype, workspace,
+                                                    workspace_bytes, stream, seq);
+        default:
+            return wgrad_launch_fmt<BATCH, kFmtBF16>(mods, T, max_ld, tab, order, n_tiles, out_dtype, workspace,
+                                                     workspace_bytes, stream, seq);
+    }
+}
+
+// out_dtype allowed for an operand format: the operand dtype itself (the reference's grad dtype,
+// smt.py:382-385) or fp32 (the engine's sink)
+bool wgrad_dtypes_ok(int32_t operand_dtype, int32_t out_dtype) {
+    if (out_dtype == SMT_DTYPE_FP32) return operand_dtype == SMT_DTYPE_BF16 || operand_dtype == SMT_DTYPE_FP16 ||
+                                            operand_dtype == SMT_DTYPE_FP32;
+    return (operand_dtype == SMT_DTYPE_BF16 || operand_dtype == SMT_DTYPE_FP16) && out_dtype == operand_dtype;
 }
 
 // argument checks shared by the single-module and batched entry points
@@ -2090,8 +2271,9 @@ int wgrad_batch_entry(const char* fn, const smt_wgrad_module* modules, int32_t n
     if (n_tiles == 0) return SMT_OK;
     if (n_modules == 0 || n_modules > SMT_WGRAD_MAX_MODULES || !modules)
         return fail(SMT_E_INVALID, "%s: %d modules (1..%d)", fn, n_modules, SMT_WGRAD_MAX_MODULES);
-    if (out_dtype != SMT_DTYPE_BF16 && out_dtype != SMT_DTYPE_FP32)
-        return fail(SMT_E_INVALID, "%s: out_dtype %d not supported", fn, out_dtype);
+    const int32_t operand_dtype = modules[0].operand_dtype;
+    if (!wgrad_dtypes_ok(operand_dtype, out_dtype))
+        return fail(SMT_E_INVALID, "%s: operand dtype %d with out_dtype %d not supported", fn, operand_dtype, out_dtype);
     if (!tile_tab_dev) return fail(SMT_E_INVALID, "%s: null tile table", fn);
     if (T == 0) return fail(SMT_E_INVALID, "%s: T = 0 (use smt_tile_wgrad per module)", fn);
     if (seq < 0 || (seq > 0 && T % seq))
@@ -2102,12 +2284,15 @@ int wgrad_batch_entry(const char* fn, const smt_wgrad_module* modules, int32_t n
     for (int i = 0; i < n_modules; ++i) {
         const int rc = check_wgrad_module(fn, modules[i]);
         if (rc) return rc;
+        if (modules[i].operand_dtype != operand_dtype)
+            return fail(SMT_E_INVALID, "%s: modules of one launch need one operand dtype (%d, %d)", fn,
+                        modules[i].operand_dtype, operand_dtype);
         mods.m[i] = modules[i];
         mods.m[i].accumulate = modules[i].accumulate ? 1 : 0;
         max_ld = std::max(max_ld, std::max(modules[i].ld_grad_out, modules[i].ld_x));
     }
     return wgrad_launch<true>(mods, T, max_ld, tile_tab_dev, order_dev, n_tiles, out_dtype, workspace, workspace_bytes,
-                              stream, seq);
+                              stream, seq, operand_dtype);
 }
 
 }  // namespace

@@ -504,7 +504,10 @@ class linearZ(torch.autograd.Function):
     packed copy of the union of their blocks, or the input itself when the union covers it. Under
     the "views" activation policy the input is always saved as is (the reference's own choice), and
     under "selective" a norm's / SwiGLU's output is not saved at all (rebuilt in the backward). The
-    tile gradients are bit-identical every way (same operands, same kernel, same order).
+    tile gradients are bit-identical every way (same operands, same kernel, same order). The packed
+    copies are of 16-bit inputs; an fp32 model (the reference's --dtype fp32) keeps its input as is.
+    Operands may be bf16, fp16 or fp32 (``fine_tune.py:955-959``): the tile gradients are computed in
+    that dtype's arithmetic (per-sample partials rounded to it, smt.py:397-404) by the same launches.
 
     If ``selected_weight`` carries an engine gradient sink (``_smt_grad_sink``), the fp32 tile
     gradients are written straight into the engine's packed buffer and ``None`` is returned for
@@ -559,7 +562,7 @@ class linearZ(torch.autograd.Function):
             saved = None
             ctx.packed = True
         elif (policy != "views" and ctx.needs_input_grad[1] and len(tiles) and input.device.type == "cuda"
-                and getattr(weight, "_smt_cb_group", None) is not None
+                and input.element_size() == 2 and getattr(weight, "_smt_cb_group", None) is not None
                 and len(weight._smt_cb_group.col_blocks) < in_blocks
                 and all(c in weight._smt_cb_group.pos for c in tiles.column_blocks())):
             # one packed copy of the group's union of column blocks, shared with the other members
@@ -568,7 +571,7 @@ class linearZ(torch.autograd.Function):
             saved = grp.packed_input(input, x2d, ctx.sink)
             ctx.packed = grp.pos
         elif (policy != "views" and ctx.needs_input_grad[1] and len(tiles) and input.device.type == "cuda"
-                and (getattr(weight, "_smt_cb_group", None) is None
+                and input.element_size() == 2 and (getattr(weight, "_smt_cb_group", None) is None
                      or not all(c in weight._smt_cb_group.pos for c in tiles.column_blocks()))
                 and 2 * len(tiles.column_blocks()) <= in_blocks):
             cb_dev, _ = tiles.packed_tables(input.device)

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
     out = subprocess.run(["nm", "-D", "--defined-only", _hip.lib_path()], capture_output=True, text=True).stdout
     for name in declared_functions():
         assert re.search(rf"\bT {name}$", out, re.M), name
-    assert lib.smt_abi_version() == 10
+    assert lib.smt_abi_version() == 11
 
 
 def test_library_carries_gfx950_code_object():
