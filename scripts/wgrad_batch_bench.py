@@ -17,6 +17,8 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from sparse_matrix_tuning_amd import _hip  # noqa: E402
 
+DTYPE = torch.bfloat16
+
 # (name, out_features, in_features) of one LLaMA-3-8B decoder layer, in backward order
 LAYER = [("down", 4096, 14336), ("up", 14336, 4096), ("gate", 14336, 4096), ("o", 4096, 4096),
          ("v", 1024, 4096), ("k", 1024, 4096), ("q", 4096, 4096)]
@@ -41,8 +43,8 @@ def make_batches(T, tiles_per_module, batch_tiles, n_layers, dev, gen, pattern="
                 rc = [(p // cb, p % cb) for p in perm]
             cols = sorted({c for _r, c in rc})
             pos = {c: i for i, c in enumerate(cols)}
-            g = torch.randn(T, out_f, device=dev, dtype=torch.bfloat16)      # this module's output gradient
-            x = torch.randn(len(cols), T, 256, device=dev, dtype=torch.bfloat16)   # packed column blocks
+            g = torch.randn(T, out_f, device=dev, dtype=DTYPE)      # this module's output gradient
+            x = torch.randn(len(cols), T, 256, device=dev, dtype=DTYPE)   # packed column blocks
             out = torch.zeros(n * 256, 256, device=dev, dtype=torch.float32)
             ktiles = [(r, pos[c]) for r, c in rc]
             keys = {("g", g.data_ptr(), r) for r, _c in rc} | {("x", x.data_ptr(), c) for _r, c in ktiles}
@@ -67,7 +69,11 @@ def main():
     ap.add_argument("--g-width", type=int, default=None, help="override every module's out features")
     ap.add_argument("--seq-len", type=int, default=0, help="reference rounding: T / seq_len samples")
     ap.add_argument("--tag", default=os.environ.get("SMT_HIP_LIB", "default"))
+    ap.add_argument("--dtype", default="bf16", choices=("bf16", "fp16", "fp32"),
+                    help="operand dtype (the reference's --dtype; fp32 runs wgrad_f32_kernel)")
     args = ap.parse_args()
+    global DTYPE
+    DTYPE = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[args.dtype]
     dev = torch.device("cuda")
     gen = torch.Generator().manual_seed(1234)
     torch.manual_seed(0)
@@ -79,8 +85,9 @@ def main():
         items = [(m[0], m[1], m[2], False) for m in mods]
         n = sum(len(m[3]) for m in mods)
         keys = set().union(*[m[4] for m in mods])
-        distinct = len(keys) * args.T * 512 + n * 65536 * 4
-        per_tile = n * (2 * args.T * 512 + 65536 * 4)
+        eb = torch.tensor([], dtype=DTYPE).element_size()
+        distinct = len(keys) * args.T * 256 * eb + n * 65536 * 4
+        per_tile = n * (2 * args.T * 256 * eb + 65536 * 4)
         prepared.append((items, tab, order, n, distinct, per_tile))
 
     def run_all():
@@ -109,7 +116,7 @@ def main():
     distinct = sum(p[4] for p in prepared)
     per_tile = sum(p[5] for p in prepared)
     tiles = sum(p[3] for p in prepared)
-    print(json.dumps({"tag": os.path.basename(args.tag), "env": {k: v for k, v in os.environ.items()
+    print(json.dumps({"tag": os.path.basename(args.tag), "dtype": args.dtype, "env": {k: v for k, v in os.environ.items()
                                                                     if k.startswith("SMT_WGRAD")},
                       "seq_len": args.seq_len, "T": args.T, "launches": launches,
                       "tiles_per_launch": round(tiles / launches, 1),

@@ -747,8 +747,15 @@ def row_scatter(weight: torch.Tensor, rows_dev: torch.Tensor, rows: torch.Tensor
 def column_gather(x2d: torch.Tensor, cols_dev: torch.Tensor, n_cols: int, ld_out: int) -> torch.Tensor:
     """[T, ld_out] with out[:, j] = x2d[:, cols[j]] for j < n_cols and zeros after (smt.py:225-233)."""
     dev = _require_device(x2d, cols_dev)
-    if x2d.dim() != 2 or x2d.stride(1) != 1 or x2d.element_size() != 2:
-        raise ValueError("column_gather: x must be a 2-D row-major 16-bit tensor")
+    if x2d.dim() != 2 or x2d.stride(1) != 1 or x2d.element_size() not in (2, 4):
+        raise ValueError("column_gather: x must be a 2-D row-major 16- or 32-bit tensor")
+    if x2d.element_size() == 4:
+        # an fp32 column c is the 16-bit column pair (2c, 2c + 1) of the same rows: the same kernel
+        # over the rows viewed as 16-bit words, with the pairs as its column list
+        c = cols_dev[:n_cols].to(torch.int32)
+        pairs = torch.stack((2 * c, 2 * c + 1), 1).reshape(-1).contiguous()
+        out16 = column_gather(x2d.view(torch.int16), pairs, 2 * int(n_cols), 2 * int(ld_out))
+        return out16.view(x2d.dtype)
     out = torch.empty(x2d.shape[0], ld_out, dtype=x2d.dtype, device=dev)
     rc = load().smt_column_gather(_ptr(x2d), x2d.stride(0), x2d.shape[1], x2d.shape[0], _ptr(cols_dev), int(n_cols),
                                   _ptr(out), ld_out, _stream(dev))

@@ -131,3 +131,28 @@ def test_reference_fwbw_demo_geometry(dtype):
     e = _rel(sel.grad, restated)
     print(f"{dtype}: tile grads vs the restatement {e:.2e}")
     assert e <= (1e-5 if dtype == torch.float32 else 1e-3)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.float32])
+def test_channel_module_in_dtype(dtype):
+    """LinearLayer_ChannelSparsity (smt.py:185-296) with the model in fp16 / fp32: the partial input
+    gather (an fp32 column is a 16-bit column pair), the channel gradient through the tile kernels of
+    that dtype, against the restatement (oracle.linearchannel_*) and fp64."""
+    torch.manual_seed(31)
+    W = (torch.randn(512, 512) * 0.05).to(dtype)
+    idx = [3, 100, 7, 511, 256]
+    x = torch.randn(2, 96, 512).to(dtype)
+    g = torch.randn(2, 96, 512).to(dtype)
+    mod = smt.LinearLayer_ChannelSparsity(nn.Parameter(W.to(DEV)), index_list=idx)
+    assert mod.selected_weight.dtype == dtype
+    xd = x.to(DEV).requires_grad_(True)
+    y = mod(xd)
+    y.backward(g.to(DEV))
+    y_ref, partial = ref.linearchannel_forward(x, W, idx)
+    gi_ref, gw_ref = ref.linearchannel_backward(g, partial, W)
+    tol = 1e-5 if dtype == torch.float32 else 2e-3
+    assert _rel(y, y_ref) <= tol and _rel(xd.grad, gi_ref) <= tol
+    truth = ref.channel_grads_fp64(g, x, idx)
+    gw = mod.selected_weight.grad
+    assert gw.dtype == dtype and gw.shape == (len(idx), 512)
+    assert _rel(gw, truth) <= max(tol, 1.1 * _rel(gw_ref, truth)), (_rel(gw, truth), _rel(gw_ref, truth))
