@@ -80,7 +80,7 @@ extern "C" {
 
 /* One 256x256 tile of a flat tile-major parameter buffer and where it lives in W. */
 typedef struct smt_tile_desc {
-    void* weight;                   /* W base (bf16, row-major) or NULL: no scatter   */
+    void* weight;                   /* W base (row-major, the AdamW step's param_dtype) or NULL: no scatter */
     int64_t ld_weight;              /* W row stride in elements                       */
     int32_t row_block;              /* index[0] of smt.py:318                         */
     int32_t col_block;              /* index[1] of smt.py:318                         */
@@ -113,9 +113,15 @@ typedef struct smt_adamw_args {
     float bias_correction1;         /* 1 - beta1^step (1.0 if bias_correction off) */
     float bias_correction2;         /* 1 - beta2^step                              */
     float max_grad_norm;            /* <= 0: no clipping                           */
-    float grad_scale;               /* multiplies every gradient (1/world for DP average) */
+    float grad_scale;               /* multiplies every gradient (1/world for DP average; with fp16
+                                       loss scaling also 1/loss_scale)                       */
     int32_t mode;                   /* SMT_ADAM_*                                  */
-    int32_t grad_dtype;             /* SMT_DTYPE_BF16 or SMT_DTYPE_FP32            */
+    int32_t grad_dtype;             /* SMT_DTYPE_FP32 (any param_dtype), or SMT_DTYPE_BF16 / _FP16
+                                       equal to param_dtype                                  */
+    int32_t param_dtype;            /* ABI v12: SMT_DTYPE_BF16, _FP16 or _FP32, the dtype of the
+                                       parameter (and W) values written -- the reference's
+                                       --dtype (fine_tune.py:955-959, deepspeed_helpers.py:53-61) */
+    int32_t reserved;               /* 0                                           */
 } smt_adamw_args;
 
 typedef struct smt_adamw_tensor {
@@ -123,7 +129,7 @@ typedef struct smt_adamw_tensor {
     float* master;                  /* n fp32 master values                       */
     float* exp_avg;
     float* exp_avg_sq;
-    void* param;                    /* n bf16 parameter values (written)          */
+    void* param;                    /* n parameter values of args->param_dtype (written) */
     int64_t n;
 } smt_adamw_tensor;                 /* all five buffers 16-byte aligned          */
 
@@ -247,13 +253,13 @@ int smt_sq_norm(const float* x, int64_t n, double* partials_dev, int32_t n_parti
                 double* out_dev, hipStream_t stream);
 
 /*
- * Fused clip + AdamW + bf16 cast (+ scatter into W) over flat tile-major buffers of
+ * Fused clip + AdamW + cast to args->param_dtype (+ scatter into W) over flat tile-major buffers of
  * n_tiles*65536 elements (tiles_dev != NULL) or n_elems plain elements (tiles_dev == NULL).
  * grad_sq_norm_dev: device fp64 squared global norm of the effective gradient (grad * grad_scale,
  * over every parameter the clip covers), or NULL for no clipping.
  */
 int smt_adamw_step(const void* grad, float* master, float* exp_avg, float* exp_avg_sq,
-                   void* param_bf16, const smt_tile_desc* tiles_dev, int32_t n_tiles,
+                   void* param, const smt_tile_desc* tiles_dev, int32_t n_tiles,
                    int64_t n_elems, const double* grad_sq_norm_dev,
                    const smt_adamw_args* args, hipStream_t stream);
 

@@ -391,6 +391,67 @@ def fused_adam_step(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.
 
 
 # ------------------------------------------------------------------------------------------------
+# fp16 training (the reference's --dtype fp16: deepspeed_helpers.py:53-55 sets
+# "fp16": {"enabled": True, "loss_scale_window": 100}); DeepSpeed 0.16.5 internals, external and
+# restated from its published code (runtime/fp16/loss_scaler.py DynamicLossScaler,
+# runtime/zero/stage_1_and_2.py step / unscale_and_clip_grads): parity unpinned by the reference
+# ------------------------------------------------------------------------------------------------
+class RefDynamicLossScaler:
+    """DeepSpeed's dynamic loss scale with its fp16 config defaults (loss_scale 0 = dynamic,
+    initial_scale_power 16, loss_scale_window 1000 (the reference: 100), hysteresis 2,
+    consecutive_hysteresis False, min_loss_scale 1)."""
+
+    def __init__(self, init_scale=2.0 ** 16, scale_window=1000, min_scale=1.0, delayed_shift=2,
+                 consecutive_hysteresis=False, scale_factor=2.0):
+        self.cur_scale = float(init_scale)
+        self.cur_iter = 0
+        self.last_overflow_iter = -1
+        self.scale_factor = scale_factor
+        self.scale_window = scale_window
+        self.min_scale = min_scale
+        self.delayed_shift = delayed_shift
+        self.cur_hysteresis = delayed_shift
+        self.consecutive_hysteresis = consecutive_hysteresis
+
+    def update_scale(self, overflow: bool) -> None:
+        if overflow:
+            if self.delayed_shift == 1 or self.cur_hysteresis == 1:
+                if self.cur_scale == self.min_scale:
+                    raise RuntimeError("Current loss scale already at minimum - cannot decrease scale anymore.")
+                self.cur_scale = max(self.cur_scale / self.scale_factor, self.min_scale)
+            else:
+                self.cur_hysteresis -= 1
+            self.last_overflow_iter = self.cur_iter
+        else:
+            if self.consecutive_hysteresis:
+                self.cur_hysteresis = self.delayed_shift
+            if (self.cur_iter - self.last_overflow_iter) % self.scale_window == 0:
+                if not self.consecutive_hysteresis:
+                    self.cur_hysteresis = self.delayed_shift
+                self.cur_scale *= self.scale_factor
+        self.cur_iter += 1
+
+
+def fp16_step_scales(scaler: RefDynamicLossScaler, grads_scaled: List[torch.Tensor], max_norm: float):
+    """One ZeRO-1/2 fp16 step's bookkeeping: overflow = any inf/nan in the (loss-scaled) gradients;
+    the scaler updates FIRST, then the gradients are unscaled and clipped with the scale it now holds
+    (combined_scale = max(1, (||g_scaled|| / scale + 1e-6) / max_norm) * scale). Returns (overflow,
+    multiplier for the scaled gradients; None on overflow: the step is skipped)."""
+    overflow = any(not torch.isfinite(g.double()).all().item() for g in grads_scaled)
+    scaler.update_scale(overflow)
+    if overflow:
+        return True, None
+    scale = scaler.cur_scale
+    combined = scale
+    if max_norm > 0:
+        total = torch.sqrt(sum((g.double() ** 2).sum() for g in grads_scaled)).item()
+        clip = (total / scale + 1e-6) / max_norm
+        if clip > 1:
+            combined = clip * scale
+    return False, 1.0 / combined
+
+
+# ------------------------------------------------------------------------------------------------
 # module-level restatement (smt.py:83-134, 302-413) for end-to-end CPU checks
 # ------------------------------------------------------------------------------------------------
 class RefLinearZ(torch.autograd.Function):

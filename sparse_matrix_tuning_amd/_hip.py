@@ -24,7 +24,7 @@ SCORE_MEAN_ABS, SCORE_ABS_MEAN, SCORE_L1, SCORE_L2 = 0, 1, 2, 3
 ADAM_DEEPSPEED, ADAM_TORCH = 0, 1
 
 _DT = {torch.bfloat16: DTYPE_BF16, torch.float32: DTYPE_FP32, torch.float16: DTYPE_FP16}
-ABI_VERSION = 11            # include/smt_hip.h: smt_wgrad_module.operand_dtype (v11)
+ABI_VERSION = 12            # include/smt_hip.h: smt_adamw_args.param_dtype (v12), smt_wgrad_module.operand_dtype (v11)
 
 # Every function the headers declare (include/smt_hip.h, smt_model_ops.h, smt_attention.h); tests check the
 # library exports each of them.
@@ -86,7 +86,8 @@ class AdamWArgs(ctypes.Structure):
                 ("eps", ctypes.c_float), ("weight_decay", ctypes.c_float),
                 ("bias_correction1", ctypes.c_float), ("bias_correction2", ctypes.c_float),
                 ("max_grad_norm", ctypes.c_float), ("grad_scale", ctypes.c_float),
-                ("mode", ctypes.c_int32), ("grad_dtype", ctypes.c_int32)]
+                ("mode", ctypes.c_int32), ("grad_dtype", ctypes.c_int32),
+                ("param_dtype", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 class AdamWTensor(ctypes.Structure):
@@ -641,20 +642,36 @@ def sq_norm(x: torch.Tensor, out: Optional[torch.Tensor] = None, n_partials: int
     return out
 
 
+_PARAM_DTYPES = (torch.bfloat16, torch.float16, torch.float32)
+
+
+def _adamw_dtypes(fn: str, grad_dtype: torch.dtype, param_dtype: torch.dtype) -> None:
+    """smt_adamw_*: fp32 gradients of a bf16 / fp16 / fp32 parameter, or bf16 / fp16 gradients of a
+    parameter of the same dtype (ABI v12; the reference's --dtype, fine_tune.py:955-959)."""
+    if param_dtype not in _PARAM_DTYPES:
+        raise ValueError(f"{fn}: parameters must be bf16, fp16 or fp32, not {param_dtype}")
+    if grad_dtype != torch.float32 and grad_dtype != param_dtype:
+        raise ValueError(f"{fn}: {grad_dtype} gradients of a {param_dtype} parameter (fp32, or the parameter's dtype)")
+
+
 def adamw_step(grad: torch.Tensor, master: torch.Tensor, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor,
-               param_bf16: torch.Tensor, args: AdamWArgs, tiles: Optional[torch.Tensor] = None,
+               param: torch.Tensor, args: AdamWArgs, tiles: Optional[torch.Tensor] = None,
                n_tiles: int = 0, grad_sq_norm: Optional[torch.Tensor] = None) -> None:
-    dev = _require_device(grad, master, exp_avg, exp_avg_sq, param_bf16, tiles, grad_sq_norm)
+    """Fused clip + AdamW over flat buffers; the updated values are written into ``param`` (bf16, fp16
+    or fp32) and, with ``tiles``, scattered into the W each descriptor names (W of ``param``'s dtype)."""
+    dev = _require_device(grad, master, exp_avg, exp_avg_sq, param, tiles, grad_sq_norm)
     for t in (master, exp_avg, exp_avg_sq):
         if t.dtype != torch.float32 or not t.is_contiguous():
             raise ValueError("adamw_step: master/exp_avg/exp_avg_sq must be contiguous fp32")
-    if param_bf16.dtype != torch.bfloat16 or not param_bf16.is_contiguous() or not grad.is_contiguous():
-        raise ValueError("adamw_step: param must be contiguous bf16 and grad contiguous")
+    if not param.is_contiguous() or not grad.is_contiguous():
+        raise ValueError("adamw_step: param and grad must be contiguous")
+    _adamw_dtypes("adamw_step", grad.dtype, param.dtype)
     n = master.numel()
-    if not (grad.numel() == n == exp_avg.numel() == exp_avg_sq.numel() == param_bf16.numel()):
+    if not (grad.numel() == n == exp_avg.numel() == exp_avg_sq.numel() == param.numel()):
         raise ValueError("adamw_step: buffer sizes differ")
     args.grad_dtype = _DT[grad.dtype]
-    rc = load().smt_adamw_step(_ptr(grad), _ptr(master), _ptr(exp_avg), _ptr(exp_avg_sq), _ptr(param_bf16),
+    args.param_dtype = _DT[param.dtype]
+    rc = load().smt_adamw_step(_ptr(grad), _ptr(master), _ptr(exp_avg), _ptr(exp_avg_sq), _ptr(param),
                                _ptr(tiles), int(n_tiles), n, _ptr(grad_sq_norm), ctypes.byref(args), _stream(dev))
     _check(rc, "smt_adamw_step")
 
@@ -663,19 +680,21 @@ ADAM_MULTI_BLOCK = 2048
 
 
 def adamw_multi(tensors, args: AdamWArgs, grad_sq_norm: Optional[torch.Tensor] = None) -> None:
-    """One ``smt_adamw_multi`` launch over ``tensors`` = [(grad, master, exp_avg, exp_avg_sq, param_bf16)]
-    (all on one device, one gradient dtype, every buffer contiguous and 16-byte aligned)."""
+    """One ``smt_adamw_multi`` launch over ``tensors`` = [(grad, master, exp_avg, exp_avg_sq, param)]
+    (all on one device, one gradient dtype and one parameter dtype, every buffer contiguous and 16-byte
+    aligned)."""
     if not tensors:
         return
     dev = _require_device(*[t for row in tensors for t in row], grad_sq_norm)
-    gdt = tensors[0][0].dtype
+    gdt, pdt = tensors[0][0].dtype, tensors[0][4].dtype
+    _adamw_dtypes("adamw_multi", gdt, pdt)
     rows, starts = [], [0]
     for grad, master, m, v, p in tensors:
         for t in (master, m, v):
             if t.dtype != torch.float32 or not t.is_contiguous():
                 raise ValueError("adamw_multi: master/exp_avg/exp_avg_sq must be contiguous fp32")
-        if p.dtype != torch.bfloat16 or not p.is_contiguous() or not grad.is_contiguous() or grad.dtype != gdt:
-            raise ValueError("adamw_multi: param must be contiguous bf16, grads contiguous and of one dtype")
+        if (p.dtype != pdt or not p.is_contiguous() or not grad.is_contiguous() or grad.dtype != gdt):
+            raise ValueError("adamw_multi: params of one dtype, grads of one dtype, all contiguous")
         n = master.numel()
         if not (grad.numel() == n == m.numel() == v.numel() == p.numel()):
             raise ValueError("adamw_multi: buffer sizes differ")
@@ -687,6 +706,7 @@ def adamw_multi(tensors, args: AdamWArgs, grad_sq_norm: Optional[torch.Tensor] =
     table_dev = _device_table(rows, AdamWTensor, dev)
     starts_dev = torch.tensor(starts, dtype=torch.int64).to(dev)
     args.grad_dtype = _DT[gdt]
+    args.param_dtype = _DT[pdt]
     rc = load().smt_adamw_multi(_ptr(table_dev), _ptr(starts_dev), len(tensors), starts[-1], _ptr(grad_sq_norm),
                                 ctypes.byref(args), _stream(dev))
     _check(rc, "smt_adamw_multi")
@@ -701,13 +721,14 @@ def tile_scatter_t(descs: torch.Tensor, n_tiles: int, tiles: torch.Tensor) -> No
     _check(rc, "smt_tile_scatter_t")
 
 
-def tile_descs(entries: Sequence[tuple], device: torch.device) -> torch.Tensor:
-    """entries: (weight tensor or None, row_block, col_block, flat_offset) -> device smt_tile_desc[]."""
+def tile_descs(entries: Sequence[tuple], device: torch.device, dtype: torch.dtype = torch.bfloat16) -> torch.Tensor:
+    """entries: (weight tensor or None, row_block, col_block, flat_offset) -> device smt_tile_desc[];
+    every W is row-major of ``dtype`` (the parameter dtype of the AdamW step that scatters into it)."""
     descs = []
     for w, r, c, off in entries:
         if w is not None:
-            if w.dtype != torch.bfloat16 or w.stride(1) != 1:
-                raise ValueError("tile_descs: W must be bf16 row-major")
+            if w.dtype != dtype or w.stride(1) != 1:
+                raise ValueError(f"tile_descs: W must be {dtype} row-major")
             descs.append(TileDesc(w.data_ptr(), w.stride(0), int(r), int(c), int(off)))
         else:
             descs.append(TileDesc(None, 0, int(r), int(c), int(off)))

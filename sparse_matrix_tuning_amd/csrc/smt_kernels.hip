@@ -1555,9 +1555,52 @@ struct AdamStep {
     }
 };
 
-template <int GDT>
-__device__ __forceinline__ void adam8(const void* grad, float* master, float* m, float* v, uint16_t* param,
-                                      int64_t f, float gscale, const AdamStep& st, uint4* packed) {
+// the updated values in the parameter dtype (ABI v12: the reference's --dtype, fine_tune.py:955-959):
+// 8 elements are 16 B of bf16 / fp16 (a) or 32 B of fp32 (a, b)
+struct Packed8 {
+    uint4 a, b;
+};
+
+template <int PDT>
+__device__ __forceinline__ uint16_t param16(float f) {
+    return PDT == SMT_DTYPE_FP16 ? f32_to_half_bits(f) : f32_to_bf16_bits(f);
+}
+
+template <int PDT>
+__device__ __forceinline__ void pack8(const float (&p)[8], Packed8& out) {
+    if (PDT == SMT_DTYPE_FP32) {
+        out.a = make_uint4(__float_as_uint(p[0]), __float_as_uint(p[1]), __float_as_uint(p[2]), __float_as_uint(p[3]));
+        out.b = make_uint4(__float_as_uint(p[4]), __float_as_uint(p[5]), __float_as_uint(p[6]), __float_as_uint(p[7]));
+    } else {
+        uint32_t w[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            w[j] = (uint32_t)param16<PDT>(p[2 * j]) | ((uint32_t)param16<PDT>(p[2 * j + 1]) << 16);
+        out.a = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
+
+// 8 consecutive elements at element i of a parameter-dtype buffer
+template <int PDT>
+__device__ __forceinline__ void store8(void* base, int64_t i, const Packed8& v) {
+    if (PDT == SMT_DTYPE_FP32) {
+        uint4* d = reinterpret_cast<uint4*>(static_cast<float*>(base) + i);
+        d[0] = v.a;
+        d[1] = v.b;
+    } else {
+        *reinterpret_cast<uint4*>(static_cast<uint16_t*>(base) + i) = v.a;
+    }
+}
+
+template <int PDT>
+__device__ __forceinline__ void store1(void* base, int64_t i, float p) {
+    if (PDT == SMT_DTYPE_FP32) static_cast<float*>(base)[i] = p;
+    else static_cast<uint16_t*>(base)[i] = param16<PDT>(p);
+}
+
+template <int GDT, int PDT>
+__device__ __forceinline__ void adam8(const void* grad, float* master, float* m, float* v, void* param,
+                                      int64_t f, float gscale, const AdamStep& st, Packed8* packed) {
     float g[8];
     load8<GDT>(grad, f, g);
     float4* P = reinterpret_cast<float4*>(master + f);
@@ -1572,12 +1615,8 @@ __device__ __forceinline__ void adam8(const void* grad, float* master, float* m,
     P[0] = make_float4(pp[0], pp[1], pp[2], pp[3]); P[1] = make_float4(pp[4], pp[5], pp[6], pp[7]);
     M[0] = make_float4(mm[0], mm[1], mm[2], mm[3]); M[1] = make_float4(mm[4], mm[5], mm[6], mm[7]);
     V[0] = make_float4(vv[0], vv[1], vv[2], vv[3]); V[1] = make_float4(vv[4], vv[5], vv[6], vv[7]);
-    uint32_t w[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-        w[j] = (uint32_t)f32_to_bf16_bits(pp[2 * j]) | ((uint32_t)f32_to_bf16_bits(pp[2 * j + 1]) << 16);
-    *packed = make_uint4(w[0], w[1], w[2], w[3]);
-    *reinterpret_cast<uint4*>(param + f) = *packed;
+    pack8<PDT>(pp, *packed);
+    store8<PDT>(param, f, *packed);
 }
 
 // norm_sq: squared global norm of the EFFECTIVE gradient (after grad_scale), fp64.
@@ -1592,10 +1631,10 @@ __device__ __forceinline__ float clip_scale(const double* norm_sq, float max_nor
     return s;
 }
 
-template <int GDT>
+template <int GDT, int PDT>
 __global__ __launch_bounds__(256)
 void adamw_tiles_kernel(const void* __restrict__ grad, float* __restrict__ master, float* __restrict__ m,
-                        float* __restrict__ v, uint16_t* __restrict__ param,
+                        float* __restrict__ v, void* __restrict__ param,
                         const smt_tile_desc* __restrict__ tiles, const double* __restrict__ norm_sq,
                         smt_adamw_args a) {
     const int tile = blockIdx.x >> 5;
@@ -1604,35 +1643,34 @@ void adamw_tiles_kernel(const void* __restrict__ grad, float* __restrict__ maste
     const int64_t f = d.flat_offset + local;
     const AdamStep st{a.lr, a.beta1, a.beta2, a.eps, a.weight_decay, a.bias_correction1, a.bias_correction2, a.mode};
     const float gscale = clip_scale(norm_sq, a.max_grad_norm, a.grad_scale);
-    uint4 packed;
-    adam8<GDT>(grad, master, m, v, param, f, gscale, st, &packed);
+    Packed8 packed;
+    adam8<GDT, PDT>(grad, master, m, v, param, f, gscale, st, &packed);
     if (d.weight != nullptr) {
         const int row = local >> 8;
         const int col = local & 255;
-        uint16_t* w = static_cast<uint16_t*>(d.weight) +
-                      ((int64_t)d.row_block * kTile + row) * d.ld_weight + (int64_t)d.col_block * kTile + col;
-        *reinterpret_cast<uint4*>(w) = packed;
+        store8<PDT>(d.weight, ((int64_t)d.row_block * kTile + row) * d.ld_weight + (int64_t)d.col_block * kTile + col,
+                    packed);
     }
 }
 
-template <int GDT>
+template <int GDT, int PDT>
 __global__ __launch_bounds__(256)
 void adamw_flat_kernel(const void* __restrict__ grad, float* __restrict__ master, float* __restrict__ m,
-                       float* __restrict__ v, uint16_t* __restrict__ param, int64_t n,
+                       float* __restrict__ v, void* __restrict__ param, int64_t n,
                        const double* __restrict__ norm_sq, smt_adamw_args a) {
     const int64_t f = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
     if (f >= n) return;
     const AdamStep st{a.lr, a.beta1, a.beta2, a.eps, a.weight_decay, a.bias_correction1, a.bias_correction2, a.mode};
     const float gscale = clip_scale(norm_sq, a.max_grad_norm, a.grad_scale);
     if (f + 8 <= n) {
-        uint4 packed;
-        adam8<GDT>(grad, master, m, v, param, f, gscale, st, &packed);
+        Packed8 packed;
+        adam8<GDT, PDT>(grad, master, m, v, param, f, gscale, st, &packed);
     } else {
         for (int64_t i = f; i < n; ++i) {
             float pp = master[i], mm = m[i], vv = v[i];
             st.apply(load_elem<GDT>(grad, i) * gscale, pp, mm, vv);
             master[i] = pp; m[i] = mm; v[i] = vv;
-            param[i] = f32_to_bf16_bits(pp);
+            store1<PDT>(param, i, pp);
         }
     }
 }
@@ -1640,7 +1678,7 @@ void adamw_flat_kernel(const void* __restrict__ grad, float* __restrict__ master
 // Multi-tensor flat AdamW: one launch over every dense parameter of the warm-up full fine-tune
 // (DeepSpeed FusedAdam's multi_tensor_apply, external). Workgroup w covers 2048 elements of the
 // tensor t with block_start[t] <= w < block_start[t+1] (binary search over the n+1 prefix).
-template <int GDT>
+template <int GDT, int PDT>
 __global__ __launch_bounds__(256)
 void adamw_multi_kernel(const smt_adamw_tensor* __restrict__ tensors, const int64_t* __restrict__ block_start,
                         int32_t n_tensors, const double* __restrict__ norm_sq, smt_adamw_args a) {
@@ -1655,16 +1693,15 @@ void adamw_multi_kernel(const smt_adamw_tensor* __restrict__ tensors, const int6
     if (f >= d.n) return;
     const AdamStep st{a.lr, a.beta1, a.beta2, a.eps, a.weight_decay, a.bias_correction1, a.bias_correction2, a.mode};
     const float gscale = clip_scale(norm_sq, a.max_grad_norm, a.grad_scale);
-    uint16_t* param = static_cast<uint16_t*>(d.param);
     if (f + 8 <= d.n) {
-        uint4 packed;
-        adam8<GDT>(d.grad, d.master, d.exp_avg, d.exp_avg_sq, param, f, gscale, st, &packed);
+        Packed8 packed;
+        adam8<GDT, PDT>(d.grad, d.master, d.exp_avg, d.exp_avg_sq, d.param, f, gscale, st, &packed);
     } else {
         for (int64_t i = f; i < d.n; ++i) {
             float pp = d.master[i], mm = d.exp_avg[i], vv = d.exp_avg_sq[i];
             st.apply(load_elem<GDT>(d.grad, i) * gscale, pp, mm, vv);
             d.master[i] = pp; d.exp_avg[i] = mm; d.exp_avg_sq[i] = vv;
-            param[i] = f32_to_bf16_bits(pp);
+            store1<PDT>(d.param, i, pp);
         }
     }
 }
@@ -2081,11 +2118,32 @@ WgradSplit wgrad_split_seq(int64_t T, int64_t seq, int32_t n_tiles) {
 // ================================================================================================
 // C ABI
 // ================================================================================================
+// AdamW launches per (grad dtype, parameter dtype), dispatched by smt_adamw_step / _multi below
+template <int GDT, int PDT>
+static void adamw_launch(bool tiled, int64_t blocks, const void* grad, float* master, float* exp_avg,
+                         float* exp_avg_sq, void* param, const smt_tile_desc* tiles_dev, int64_t n_elems,
+                         const double* grad_sq_norm_dev, const smt_adamw_args& a, hipStream_t stream) {
+    if (tiled)
+        hipLaunchKernelGGL((adamw_tiles_kernel<GDT, PDT>), dim3((unsigned)blocks), dim3(256), 0, stream, grad, master,
+                           exp_avg, exp_avg_sq, param, tiles_dev, grad_sq_norm_dev, a);
+    else
+        hipLaunchKernelGGL((adamw_flat_kernel<GDT, PDT>), dim3((unsigned)blocks), dim3(256), 0, stream, grad, master,
+                           exp_avg, exp_avg_sq, param, n_elems, grad_sq_norm_dev, a);
+}
+
+template <int GDT, int PDT>
+static void adamw_multi_launch(int64_t n_blocks, const smt_adamw_tensor* tensors_dev, const int64_t* block_start_dev,
+                               int32_t n_tensors, const double* grad_sq_norm_dev, const smt_adamw_args& a,
+                               hipStream_t stream) {
+    hipLaunchKernelGGL((adamw_multi_kernel<GDT, PDT>), dim3((unsigned)n_blocks), dim3(256), 0, stream, tensors_dev,
+                       block_start_dev, n_tensors, grad_sq_norm_dev, a);
+}
+
 extern "C" {
 
 const char* smt_last_error(void) { return g_err; }
 
-int smt_abi_version(void) { return 11; }
+int smt_abi_version(void) { return 12; }
 
 size_t smt_wgrad_workspace_bytes(int64_t T, int32_t n_tiles) {
     if (T <= 0 || n_tiles <= 0) return 0;
@@ -2517,61 +2575,71 @@ int smt_sq_norm(const float* x, int64_t n, double* partials_dev, int32_t n_parti
     return check_launch("sq_norm_final_kernel");
 }
 
-int smt_adamw_step(const void* grad, float* master, float* exp_avg, float* exp_avg_sq, void* param_bf16,
+// (grad dtype, parameter dtype) pairs of the AdamW kernels: bf16 / fp16 gradients of a parameter of
+// the same dtype, or fp32 gradients (the engine's packed tile buffer) of any parameter dtype
+static bool adamw_dtypes_ok(int gdt, int pdt) {
+    const bool p_ok = pdt == SMT_DTYPE_BF16 || pdt == SMT_DTYPE_FP16 || pdt == SMT_DTYPE_FP32;
+    return p_ok && (gdt == SMT_DTYPE_FP32 || ((gdt == SMT_DTYPE_BF16 || gdt == SMT_DTYPE_FP16) && gdt == pdt));
+}
+
+static int adamw_args_ok(const char* fn, const smt_adamw_args* args) {
+    if (!args) return fail(SMT_E_INVALID, "%s: null args", fn);
+    if (!adamw_dtypes_ok(args->grad_dtype, args->param_dtype))
+        return fail(SMT_E_INVALID, "%s: grad_dtype %d with param_dtype %d not supported", fn, args->grad_dtype,
+                    args->param_dtype);
+    if (args->mode != SMT_ADAM_DEEPSPEED && args->mode != SMT_ADAM_TORCH)
+        return fail(SMT_E_INVALID, "%s: mode %d", fn, args->mode);
+    if (!(args->bias_correction1 > 0.f) || !(args->bias_correction2 > 0.f))
+        return fail(SMT_E_INVALID, "%s: bias corrections must be > 0", fn);
+    return SMT_OK;
+}
+
+// F(GDT, PDT) for the runtime pair (adamw_dtypes_ok checked)
+#define SMT_ADAMW_DISPATCH(gdt, pdt, F)                                                                      \
+    do {                                                                                                    \
+        if ((gdt) == SMT_DTYPE_FP32) {                                                                       \
+            if ((pdt) == SMT_DTYPE_FP32) F(SMT_DTYPE_FP32, SMT_DTYPE_FP32);                                   \
+            else if ((pdt) == SMT_DTYPE_FP16) F(SMT_DTYPE_FP32, SMT_DTYPE_FP16);                              \
+            else F(SMT_DTYPE_FP32, SMT_DTYPE_BF16);                                                          \
+        } else if ((gdt) == SMT_DTYPE_FP16) {                                                                \
+            F(SMT_DTYPE_FP16, SMT_DTYPE_FP16);                                                               \
+        } else {                                                                                            \
+            F(SMT_DTYPE_BF16, SMT_DTYPE_BF16);                                                               \
+        }                                                                                                   \
+    } while (0)
+
+int smt_adamw_step(const void* grad, float* master, float* exp_avg, float* exp_avg_sq, void* param,
                    const smt_tile_desc* tiles_dev, int32_t n_tiles, int64_t n_elems, const double* grad_sq_norm_dev,
                    const smt_adamw_args* args, hipStream_t stream) {
-    if (!args) return fail(SMT_E_INVALID, "smt_adamw_step: null args");
-    if (args->grad_dtype != SMT_DTYPE_BF16 && args->grad_dtype != SMT_DTYPE_FP32)
-        return fail(SMT_E_INVALID, "smt_adamw_step: grad_dtype %d not supported", args->grad_dtype);
-    if (args->mode != SMT_ADAM_DEEPSPEED && args->mode != SMT_ADAM_TORCH)
-        return fail(SMT_E_INVALID, "smt_adamw_step: mode %d", args->mode);
-    if (!(args->bias_correction1 > 0.f) || !(args->bias_correction2 > 0.f))
-        return fail(SMT_E_INVALID, "smt_adamw_step: bias corrections must be > 0");
+    if (int rc = adamw_args_ok("smt_adamw_step", args)) return rc;
     const bool tiled = tiles_dev != nullptr;
     if (tiled ? n_tiles < 0 : n_elems < 0) return fail(SMT_E_INVALID, "smt_adamw_step: negative size");
     if ((tiled && n_tiles == 0) || (!tiled && n_elems == 0)) return SMT_OK;
-    if (!grad || !master || !exp_avg || !exp_avg_sq || !param_bf16) return fail(SMT_E_INVALID, "smt_adamw_step: null buffer");
-    if (!aligned16(grad) || !aligned16(master) || !aligned16(exp_avg) || !aligned16(exp_avg_sq) || !aligned16(param_bf16))
+    if (!grad || !master || !exp_avg || !exp_avg_sq || !param) return fail(SMT_E_INVALID, "smt_adamw_step: null buffer");
+    if (!aligned16(grad) || !aligned16(master) || !aligned16(exp_avg) || !aligned16(exp_avg_sq) || !aligned16(param))
         return fail(SMT_E_ALIGN, "smt_adamw_step: buffers must be 16-byte aligned");
     const smt_adamw_args a = *args;
-    uint16_t* p = static_cast<uint16_t*>(param_bf16);
-    if (tiled) {
-        dim3 grid(n_tiles * 32);
-        if (a.grad_dtype == SMT_DTYPE_FP32)
-            hipLaunchKernelGGL(adamw_tiles_kernel<SMT_DTYPE_FP32>, grid, dim3(256), 0, stream, grad, master, exp_avg, exp_avg_sq, p, tiles_dev, grad_sq_norm_dev, a);
-        else
-            hipLaunchKernelGGL(adamw_tiles_kernel<SMT_DTYPE_BF16>, grid, dim3(256), 0, stream, grad, master, exp_avg, exp_avg_sq, p, tiles_dev, grad_sq_norm_dev, a);
-        return check_launch("adamw_tiles_kernel");
-    }
-    const int64_t blocks = (n_elems + 2047) / 2048;
+    const int64_t blocks = tiled ? (int64_t)n_tiles * 32 : (n_elems + 2047) / 2048;
     if (blocks > 0x7fffffffLL) return fail(SMT_E_INVALID, "smt_adamw_step: too many elements");
-    if (a.grad_dtype == SMT_DTYPE_FP32)
-        hipLaunchKernelGGL(adamw_flat_kernel<SMT_DTYPE_FP32>, dim3((unsigned)blocks), dim3(256), 0, stream, grad, master, exp_avg, exp_avg_sq, p, n_elems, grad_sq_norm_dev, a);
-    else
-        hipLaunchKernelGGL(adamw_flat_kernel<SMT_DTYPE_BF16>, dim3((unsigned)blocks), dim3(256), 0, stream, grad, master, exp_avg, exp_avg_sq, p, n_elems, grad_sq_norm_dev, a);
-    return check_launch("adamw_flat_kernel");
+#define SMT_ADAMW_STEP(G, P) \
+    adamw_launch<G, P>(tiled, blocks, grad, master, exp_avg, exp_avg_sq, param, tiles_dev, n_elems, grad_sq_norm_dev, a, stream)
+    SMT_ADAMW_DISPATCH(a.grad_dtype, a.param_dtype, SMT_ADAMW_STEP);
+#undef SMT_ADAMW_STEP
+    return check_launch(tiled ? "adamw_tiles_kernel" : "adamw_flat_kernel");
 }
 
 int smt_adamw_multi(const smt_adamw_tensor* tensors_dev, const int64_t* block_start_dev, int32_t n_tensors,
                     int64_t n_blocks, const double* grad_sq_norm_dev, const smt_adamw_args* args, hipStream_t stream) {
-    if (!args) return fail(SMT_E_INVALID, "smt_adamw_multi: null args");
-    if (args->grad_dtype != SMT_DTYPE_BF16 && args->grad_dtype != SMT_DTYPE_FP32)
-        return fail(SMT_E_INVALID, "smt_adamw_multi: grad_dtype %d not supported", args->grad_dtype);
-    if (args->mode != SMT_ADAM_DEEPSPEED && args->mode != SMT_ADAM_TORCH)
-        return fail(SMT_E_INVALID, "smt_adamw_multi: mode %d", args->mode);
-    if (!(args->bias_correction1 > 0.f) || !(args->bias_correction2 > 0.f))
-        return fail(SMT_E_INVALID, "smt_adamw_multi: bias corrections must be > 0");
+    if (int rc = adamw_args_ok("smt_adamw_multi", args)) return rc;
     if (n_tensors < 0 || n_blocks < 0) return fail(SMT_E_INVALID, "smt_adamw_multi: negative size");
     if (n_tensors == 0 || n_blocks == 0) return SMT_OK;
     if (!tensors_dev || !block_start_dev) return fail(SMT_E_INVALID, "smt_adamw_multi: null table");
     if (n_blocks > 0x7fffffffLL) return fail(SMT_E_INVALID, "smt_adamw_multi: too many elements");
     const smt_adamw_args a = *args;
-    if (a.grad_dtype == SMT_DTYPE_FP32)
-        hipLaunchKernelGGL(adamw_multi_kernel<SMT_DTYPE_FP32>, dim3((unsigned)n_blocks), dim3(256), 0, stream,
-                           tensors_dev, block_start_dev, n_tensors, grad_sq_norm_dev, a);
-    else
-        hipLaunchKernelGGL(adamw_multi_kernel<SMT_DTYPE_BF16>, dim3((unsigned)n_blocks), dim3(256), 0, stream,
-                           tensors_dev, block_start_dev, n_tensors, grad_sq_norm_dev, a);
+#define SMT_ADAMW_MULTI(G, P) \
+    adamw_multi_launch<G, P>(n_blocks, tensors_dev, block_start_dev, n_tensors, grad_sq_norm_dev, a, stream)
+    SMT_ADAMW_DISPATCH(a.grad_dtype, a.param_dtype, SMT_ADAMW_MULTI);
+#undef SMT_ADAMW_MULTI
     return check_launch("adamw_multi_kernel");
 }
 

@@ -45,6 +45,52 @@ import torch.distributed as dist
 from . import _hip, dgrad
 from .smt.smt import LinearLayer_ChannelSparsity, LinearLayer_MatrixSparsity
 
+# the reference's --dtype bf16 | fp16 | fp32 (fine_tune.py:955-959, deepspeed_helpers.py:53-61)
+PARAM_DTYPES = (torch.bfloat16, torch.float16, torch.float32)
+
+
+class DynamicLossScale:
+    """fp16 loss scaling as DeepSpeed 0.16.5 runs it for the reference's ``--dtype fp16``
+    (deepspeed_helpers.py:53-55: ``"fp16": {"enabled": True, "loss_scale_window": 100}``; external,
+    restated from DeepSpeed's published DynamicLossScaler / ZeRO-1/2 step, parity unpinned).
+
+    ``scale`` starts at 2**initial_scale_power. A step whose gradients hold an inf / nan is skipped:
+    once ``hysteresis`` such steps have used up the tolerance, each halves the scale (never below
+    ``min_loss_scale``; an overflow AT the minimum raises). Every ``loss_scale_window``-th iteration
+    counted from the last overflow doubles it and restores the tolerance. ``loss_scale`` > 0 in the
+    config is a static scale (never updated)."""
+
+    def __init__(self, fp16_cfg: dict):
+        static = float(fp16_cfg.get("loss_scale", 0) or 0)
+        self.dynamic = static == 0
+        self.scale = static if not self.dynamic else 2.0 ** int(fp16_cfg.get("initial_scale_power", 16))
+        self.window = int(fp16_cfg.get("loss_scale_window", 1000))
+        self.min_scale = float(fp16_cfg.get("min_loss_scale", 1))
+        self.hysteresis = int(fp16_cfg.get("hysteresis", 2))
+        self.consecutive = bool(fp16_cfg.get("consecutive_hysteresis", False))
+        self.tolerance = self.hysteresis
+        self.iteration = 0
+        self.last_overflow = -1
+
+    def update(self, overflow: bool) -> None:
+        if not self.dynamic:
+            return
+        if overflow:
+            if self.hysteresis != 1 and self.tolerance != 1:
+                self.tolerance -= 1                     # tolerated: the scale stays
+            elif self.scale == self.min_scale:
+                raise RuntimeError("fp16 loss scale already at its minimum: cannot decrease it further")
+            else:
+                self.scale = max(self.scale / 2.0, self.min_scale)
+            self.last_overflow = self.iteration
+        else:
+            if self.consecutive:
+                self.tolerance = self.hysteresis
+            if (self.iteration - self.last_overflow) % self.window == 0:
+                self.tolerance = self.hysteresis
+                self.scale *= 2.0
+        self.iteration += 1
+
 TILE_ELEMS = _hip.TILE_ELEMS
 
 
@@ -86,12 +132,12 @@ class SMTFusedAdam(torch.optim.Optimizer):
             for p in group["params"]:
                 if p.grad is None:
                     continue
-                if p.dtype != torch.bfloat16:
-                    raise NotImplementedError("SMTFusedAdam: bf16 parameters only")
+                if p.dtype not in PARAM_DTYPES:
+                    raise NotImplementedError(f"SMTFusedAdam: bf16, fp16 or fp32 parameters, not {p.dtype}")
                 st = self.state[p]
                 if not st:
                     st["step"] = 0
-                    st["master"] = p.detach().float()
+                    st["master"] = p.detach().to(torch.float32, copy=True)
                     st["exp_avg"] = torch.zeros_like(st["master"])
                     st["exp_avg_sq"] = torch.zeros_like(st["master"])
                 st["step"] += 1
@@ -692,7 +738,8 @@ class _TileGroup:
         n_tiles = sum(len(m.tiles) for m in modules)
         self.n_tiles = n_tiles
         n = n_tiles * TILE_ELEMS
-        self.param = torch.empty(n, dtype=torch.bfloat16, device=device)
+        self.dtype = modules[0].weight.dtype           # the model's dtype: bf16, fp16 or fp32
+        self.param = torch.empty(n, dtype=self.dtype, device=device)
         self.grad = torch.zeros(n, dtype=torch.float32, device=device)
         ranges, off = [], 0
         for m in modules:
@@ -721,7 +768,7 @@ class _TileGroup:
         self.master = self.param.float()
         self.exp_avg = torch.zeros_like(self.master)
         self.exp_avg_sq = torch.zeros_like(self.master)
-        self.descs = _hip.tile_descs(descs, device) if descs else None
+        self.descs = _hip.tile_descs(descs, device, self.dtype) if descs else None
         self.n_tdescs = len(tdescs)
         self.tdescs = _hip.tile_descs(tdescs, device) if tdescs else None
         self.fp8_modules = [(m, m.weight._smt_fp8) for m in modules if getattr(m.weight, "_smt_fp8", None) is not None]
@@ -774,6 +821,19 @@ class SMTEngine:
             gas = max(1, int(total) // (int(micro) * self.world)) if (micro and total) else 1
         self.gradient_accumulation_steps = int(gas)
         self.max_grad_norm = float(cfg.get("gradient_clipping", 0.0) or 0.0)
+        # the reference's --dtype (deepspeed_helpers.py:53-61): "fp16": {"enabled": true, ...} trains an
+        # fp16 model under a dynamic loss scale, "bf16" a bf16 model; neither: whatever the model holds
+        # (fp32 with "fp16": {"enabled": false}). DeepSpeed casts the model itself; here it must come in
+        # that dtype already
+        fp16 = cfg.get("fp16") or {}
+        bf16 = cfg.get("bf16") or cfg.get("bfloat16") or {}
+        model_dtypes = {p.dtype for p in model.parameters() if p.is_floating_point()}
+        if fp16.get("enabled", False) and model_dtypes != {torch.float16}:
+            raise ValueError(f"fp16 enabled in the config, but the model holds {model_dtypes}: convert it first (model.half())")
+        if bf16.get("enabled", False) and model_dtypes != {torch.bfloat16}:
+            raise ValueError(f"bf16 enabled in the config, but the model holds {model_dtypes}: convert it first")
+        self.loss_scaler = DynamicLossScale(fp16) if fp16.get("enabled", False) else None
+        self.skipped_steps = 0
         # this engine's own modes; linearZ reads them through the modules' gradient sinks, so they
         # end with the engine. "wgrad_rounding": "reference" rounds the tile gradients as
         # smt.py:397-404 does (per-sample bf16 partials), "single" sums in fp32 over the whole batch;
@@ -830,8 +890,11 @@ class SMTEngine:
                 mods = [owner[id(p)] for p in group["params"] if id(p) in owner]
                 dense = [p for p in group["params"] if id(p) not in owner and p.requires_grad]
                 if mods:
-                    if any(m.weight.dtype != torch.bfloat16 for m in mods):
-                        raise NotImplementedError("SMT engine: bf16 models only")
+                    dts = {m.weight.dtype for m in mods}
+                    if len(dts) != 1 or not dts <= set(PARAM_DTYPES):
+                        raise NotImplementedError(f"SMT engine: one model dtype of bf16, fp16, fp32 (got {dts})")
+                    if cfg.get("fp8_linears", False) and dts != {torch.bfloat16}:
+                        raise NotImplementedError("SMT engine: fp8 linears need a bf16 model")
                     self.tile_groups.append(_TileGroup(group, mods, self.device, self,
                                                        self.reduce_bucket_size if self.exchange else None))
                 if dense:
@@ -918,7 +981,11 @@ class SMTEngine:
                 tg.buckets.arm()                # tile buckets all-reduce while backward runs
             if self.dense_buckets is not None:
                 self.dense_buckets.arm()
-        loss.backward()
+        if self.loss_scaler is not None:
+            # DeepSpeed's fp16 backward: (loss.float() * scale).backward(); unscaled in step()
+            (loss.float() * self.loss_scaler.scale).backward()
+        else:
+            loss.backward()
         if self.wgrad_batcher is not None:
             self.wgrad_batcher.callback_queued = False
             self.wgrad_batcher.flush()          # (the end-of-backward callback already did, normally)
@@ -941,6 +1008,19 @@ class SMTEngine:
     def _grad_scale(self) -> float:
         return 1.0 / self.world
 
+    def _grad_sq_norm(self, gs: float) -> torch.Tensor:
+        """Squared global norm of the DP-averaged gradients (tile and dense), fp64 on the device."""
+        self._norm_sq.zero_()
+        for tg in self.tile_groups:
+            self._norm_sq += _hip.sq_norm(tg.grad) * (gs * gs)
+        dense_grads = [p.grad for _g, ps in self.dense_groups for p in ps if p.grad is not None]
+        if dense_grads:
+            # fp32-accumulated per-tensor norms (DeepSpeed takes fp32 norms of the gradients): the
+            # default for bf16 inputs returns each norm ROUNDED TO bf16 (~0.2 % off the clip)
+            norms = torch._foreach_norm(dense_grads, 2.0, dtype=torch.float32)
+            self._norm_sq += torch.stack([n.double() for n in norms]).pow(2).sum()
+        return self._norm_sq
+
     def step(self):
         boundary = self.is_gradient_accumulation_boundary()
         self.micro_steps += 1
@@ -948,18 +1028,25 @@ class SMTEngine:
             return
         gs = self._grad_scale()
         norm = None
-        if self.max_grad_norm > 0:
-            # squared global norm of the effective (DP-averaged) gradient, kept on the device
-            self._norm_sq.zero_()
-            for tg in self.tile_groups:
-                self._norm_sq += _hip.sq_norm(tg.grad) * (gs * gs)
-            dense_grads = [p.grad for _g, ps in self.dense_groups for p in ps if p.grad is not None]
-            if dense_grads:
-                # fp32-accumulated per-tensor norms (DeepSpeed takes fp32 norms of the gradients): the
-                # default for bf16 inputs returns each norm ROUNDED TO bf16 (~0.2 % off the clip)
-                norms = torch._foreach_norm(dense_grads, 2.0, dtype=torch.float32)
-                self._norm_sq += torch.stack([n.double() for n in norms]).pow(2).sum()
-            norm = self._norm_sq
+        if self.loss_scaler is not None:
+            # fp16 (DeepSpeed ZeRO-1/2 step, restated): an inf / nan anywhere in the loss-scaled gradients
+            # skips the step (one host read of the norm); the scale is updated FIRST, and the gradients
+            # are unscaled (and the clip computed) with the scale it then holds
+            norm = self._grad_sq_norm(gs)
+            overflow = not bool(torch.isfinite(norm).item())
+            self.loss_scaler.update(overflow)
+            if overflow:
+                self.skipped_steps += 1
+                self.global_steps += 1
+                self.zero_grad()
+                return                                  # no update, no optimizer step count, no LR step
+            inv = 1.0 / self.loss_scaler.scale
+            gs *= inv
+            norm *= inv * inv
+            if self.max_grad_norm <= 0:
+                norm = None
+        elif self.max_grad_norm > 0:
+            norm = self._grad_sq_norm(gs)
         for tg in self.tile_groups:
             tg.step += 1
             args = self.optimizer._args(tg.group, tg.step, self.max_grad_norm, gs)
@@ -972,6 +1059,7 @@ class SMTEngine:
                 fw.refresh(m.weight, rb, cb, group=False)
             for g, cb in tg.fp8_groups:
                 g.refresh(cb)
+        dense_scale = 1.0 if self.loss_scaler is None else 1.0 / self.loss_scaler.scale
         for group, params in self.dense_groups:
             # one multi-tensor launch per (group, step count, grad dtype): the warm-up's full fine-tune
             batches = {}
@@ -980,7 +1068,7 @@ class SMTEngine:
                     continue
                 st = self._dense_state.get(id(p))
                 if st is None:
-                    st = {"step": 0, "master": p.detach().float()}
+                    st = {"step": 0, "master": p.detach().to(torch.float32, copy=True)}
                     st["exp_avg"] = torch.zeros_like(st["master"])
                     st["exp_avg_sq"] = torch.zeros_like(st["master"])
                     self._dense_state[id(p)] = st
@@ -988,7 +1076,8 @@ class SMTEngine:
                 batches.setdefault((st["step"], p.grad.dtype), []).append(
                     (p.grad.contiguous(), st["master"], st["exp_avg"], st["exp_avg_sq"], p.data))
             for (step, _dt), rows in batches.items():
-                _hip.adamw_multi(rows, self.optimizer._args(group, step, self.max_grad_norm, 1.0), grad_sq_norm=norm)
+                _hip.adamw_multi(rows, self.optimizer._args(group, step, self.max_grad_norm, dense_scale),
+                                 grad_sq_norm=norm)
             for p in params:
                 p.grad = None
         self.global_steps += 1

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
     out = subprocess.run(["nm", "-D", "--defined-only", _hip.lib_path()], capture_output=True, text=True).stdout
     for name in declared_functions():
         assert re.search(rf"\bT {name}$", out, re.M), name
-    assert lib.smt_abi_version() == 11
+    assert lib.smt_abi_version() == 12
 
 
 def test_library_carries_gfx950_code_object():
@@ -42,7 +42,7 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(_hip.TileDesc) == 32
     assert ctypes.sizeof(_hip.AccumEntry) == 40
     assert ctypes.sizeof(_hip.ScoreEntry) == 48
-    assert ctypes.sizeof(_hip.AdamWArgs) == 44
+    assert ctypes.sizeof(_hip.AdamWArgs) == 52          # ABI v12: param_dtype + reserved
     assert ctypes.sizeof(_hip.RopeTensor) == 72
     assert ctypes.sizeof(_hip.AdamWTensor) == 48
     assert ctypes.sizeof(_hip.WgradModule) == 56
@@ -64,6 +64,19 @@ def test_validation_errors_without_gpu():
     assert lib.smt_adamw_multi(None, None, 0, 0, None, ctypes.byref(args), None) == 0      # nothing to do
     assert lib.smt_adamw_multi(None, None, 3, 5, None, ctypes.byref(args), None) == -1
     assert b"null table" in lib.smt_last_error()
+    # parameter dtypes (ABI v12): 16-bit gradients only of a parameter of their own dtype
+    args.grad_dtype, args.param_dtype = _hip.DTYPE_BF16, _hip.DTYPE_FP16
+    assert lib.smt_adamw_step(None, None, None, None, None, None, 0, 8, None, ctypes.byref(args), None) == -1
+    assert b"param_dtype" in lib.smt_last_error()
+    args.grad_dtype, args.param_dtype = _hip.DTYPE_FP16, _hip.DTYPE_FP32
+    assert lib.smt_adamw_multi(None, None, 3, 5, None, ctypes.byref(args), None) == -1
+    assert b"param_dtype" in lib.smt_last_error()
+    args.param_dtype = 7
+    assert lib.smt_adamw_step(None, None, None, None, None, None, 0, 8, None, ctypes.byref(args), None) == -1
+    for g, p in ((_hip.DTYPE_FP32, _hip.DTYPE_FP32), (_hip.DTYPE_FP32, _hip.DTYPE_FP16), (_hip.DTYPE_FP16, _hip.DTYPE_FP16)):
+        args.grad_dtype, args.param_dtype = g, p
+        assert lib.smt_adamw_step(None, None, None, None, None, None, 0, 8, None, ctypes.byref(args), None) == -1
+        assert b"null buffer" in lib.smt_last_error()
     assert lib.smt_tile_gather(None, 256, 3, None, 1, None, None) == -1
     assert lib.smt_sq_norm(None, 10, None, 0, None, None) == -1
     assert lib.smt_wgrad_workspace_bytes(32768, 27) == 27 * 9 * 65536 * 4
