@@ -226,3 +226,61 @@ def test_mini_llama_trains_through_the_engine_in_dtype(dtype):
         if isinstance(mod, smt.LinearLayer_MatrixSparsity):
             assert mod.selected_weight.dtype == dtype
             assert torch.equal(ref.gather_tiles(mod.weight.detach().cpu(), mod.index_list), mod.selected_weight.detach().cpu())
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.float32])
+def test_reference_flow_in_dtype(dtype):
+    """fine_tune.py's whole flow in the reference's fp16 / fp32: full fine-tuning warm-up steps through
+    the engine (dense fused AdamW on fp16 / fp32 parameters; fp16 under the loss scale) with the GPU
+    harvest, then selection, freeze, conversion and SMT steps. The harvest equals the restatement's
+    CPU accumulation of the same gradients bit for bit (in fp16 these are the LOSS-SCALED gradients,
+    what DeepSpeed's safe_get_full_grad returns between backward and step), and the selection the
+    restatement's on them. A small initial scale keeps the warm-up free of overflow steps here (an
+    overflow step's inf gradients would enter the harvest, as in the reference)."""
+    import bench
+    cfg = dict(bench.MODELS["mini"])
+    cfg["num_hidden_layers"] = 2
+    bench.MODELS["_td"] = cfg
+    try:
+        torch.manual_seed(21)
+        model = bench.build_model("_td", DEV).to(dtype)
+    finally:
+        del bench.MODELS["_td"]
+    from sparse_matrix_tuning_amd import trainer
+    from sparse_matrix_tuning_amd.engine import safe_get_full_grad
+    ds = {"gradient_clipping": 1.0, "fp16": ({"enabled": True, "loss_scale_window": 100, "initial_scale_power": 10}
+                                             if dtype == torch.float16 else {"enabled": False})}
+    dims = trainer.get_targeted_module_dims(model)
+    n_att, n_mlp = trainer.block_budgets(trainer.count_total_blocks(model), 0.1, 0.1)
+    opt = SMTFusedAdam(model.parameters(), lr=1e-4, betas=(0.9, 0.95))
+    engine, _, _, _ = initialize(model=model, optimizer=opt, config=ds)
+    harvester = trainer.GradHarvester(model, n_mlp, n_att)
+    mlp_ref, att_ref = {}, {}
+    for b in bench.batches(3, 2, 128, bench.MODELS["mini"]["vocab_size"], 0, DEV):
+        engine.backward(engine(**b, use_cache=False).loss)
+        harvester.harvest()
+        named = [(n, safe_get_full_grad(p)) for n, p in model.named_parameters()]
+        assert all(g is None or g.dtype == dtype for _n, g in named)
+        ref.harvest([(n, g) for n, g in named if g is not None], mlp_ref, att_ref, n_mlp, n_att)
+        engine.step()
+    assert engine.skipped_steps == 0 and all(p.dtype == dtype for p in model.parameters())
+    for k in mlp_ref:
+        assert torch.equal(harvester.warmup_grads[k].cpu(), mlp_ref[k])
+    for k in att_ref:
+        assert torch.equal(harvester.attention_warmup_grads[k].cpu(), att_ref[k])
+    want_att = ref.select_submatrix(att_ref, dims, n_att)
+    want_mlp = ref.select_submatrix(mlp_ref, dims, n_mlp, calculate_strategy="abs_mean")
+    engine, _opt, _sched, sel_mlp, sel_att = trainer.select_and_convert(
+        engine, harvester, dims, n_att, n_mlp, calculate_strategy="abs_mean", smt_lr=1e-4,
+        num_training_steps=10, ds_config=ds)
+    assert list(sel_mlp.items()) == list(want_mlp.items())
+    assert list(dict(sel_att).items()) == list(dict(want_att).items())
+    assert engine.tile_groups and all(tg.param.dtype == dtype for tg in engine.tile_groups)
+    for b in bench.batches(3, 2, 128, bench.MODELS["mini"]["vocab_size"], 0, DEV, offset=7):
+        loss = engine(**b, use_cache=False).loss
+        engine.backward(loss)
+        engine.step()
+        assert torch.isfinite(loss).item()
+    for mod in model.modules():
+        if isinstance(mod, smt.LinearLayer_MatrixSparsity):
+            assert torch.equal(ref.gather_tiles(mod.weight.detach().cpu(), mod.index_list), mod.selected_weight.detach().cpu())
