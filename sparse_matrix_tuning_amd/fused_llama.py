@@ -279,12 +279,13 @@ def fused_decoder_layer_forward(self, hidden_states, attention_mask=None, positi
         # the MLP residual add fused with the NEXT layer's input RMSNorm (one add+norm pass instead of
         # an add and a norm): the layer still returns h = residual + mlp_out, with the normalised h
         # attached for the next layer, which uses it only if it receives this very tensor unchanged
+        # (fp8 attention: the norm also emits the next q/k/v's e4m3 rows, and its backward the
+        # down_proj data gradient's, as the next layer's own input norm would)
         qn = _attn_quant(nxt.self_attn, H)
-        if not qn[0]:
-            n1 = nxt.input_layernorm
-            h, y = FusedAddRMSNormFn.apply(hidden_states, residual, n1.weight, n1.variance_epsilon, *qn)
-            h.__dict__["_smt_normed"] = (n1.weight, qn, y, h._version)
-            return h
+        n1 = nxt.input_layernorm
+        h, y = FusedAddRMSNormFn.apply(hidden_states, residual, n1.weight, n1.variance_epsilon, *qn)
+        h.__dict__["_smt_normed"] = (n1.weight, qn, y, h._version)
+        return h
     return residual + hidden_states
 
 

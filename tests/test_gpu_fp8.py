@@ -556,3 +556,48 @@ def test_rmsnorm_bwd_add_quant_matches_bwd_then_quant(H):
     dx, q, s = f8.rmsnorm_bwd_add_quant(dy, x, w, rstd, dres)
     assert torch.equal(dx, dx_ref)
     assert torch.equal(s, s_ref) and torch.equal(q.view(torch.uint8), q_ref.view(torch.uint8))
+
+
+def test_fp8_layer_tail_fusion_matches_separate_add():
+    """The MLP residual add fused with the next layer's input RMSNorm on the fp8 path (the norm also
+    emits the next q/k/v's e4m3 rows; its backward the down_proj data gradient's): loss and gradient
+    identical to the separate add + norm, and the tail is used (one more fused add+norm per layer)."""
+    import bench
+    from sparse_matrix_tuning_amd import fused_llama as fl
+    from sparse_matrix_tuning_amd.engine import attach_fp8_weights
+    cfg = dict(bench.MODELS["mini"], hidden_size=1024, intermediate_size=2048, num_attention_heads=8,
+               num_key_value_heads=2, num_hidden_layers=3)
+    bench.MODELS["_n"] = cfg
+    try:
+        model = bench.build_model("_n", DEV)
+    finally:
+        del bench.MODELS["_n"]
+    fl.patch_llama(model)
+    for p in model.parameters():
+        p.requires_grad_(False)
+    model.model.embed_tokens.weight.requires_grad_(True)
+    assert attach_fp8_weights(model) > 0
+    ids = torch.randint(0, 4096, (2, 256), generator=torch.Generator().manual_seed(3)).to(DEV)
+    out = []
+    real = fl.FusedAddRMSNormFn.apply
+    for tail in (False, True):
+        old = fl._LAYER_TAIL
+        fl._LAYER_TAIL = tail
+        calls = [0]
+
+        def counting(*a, **k):
+            calls[0] += 1
+            return real(*a, **k)
+        fl.FusedAddRMSNormFn.apply = counting
+        try:
+            model.model.embed_tokens.weight.grad = None
+            loss = model(input_ids=ids, labels=ids, use_cache=False).loss
+            loss.backward()
+            out.append((loss.detach().clone(), model.model.embed_tokens.weight.grad.clone(), calls[0]))
+        finally:
+            fl._LAYER_TAIL = old
+            del fl.FusedAddRMSNormFn.apply          # the inherited autograd.Function.apply again
+    (l0, g0, c0), (l1, g1, c1) = out
+    assert (c0, c1) == (3, 5)
+    assert torch.equal(l0, l1), (l0.item(), l1.item())
+    assert torch.equal(g0, g1)
