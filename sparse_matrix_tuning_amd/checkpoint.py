@@ -6,9 +6,9 @@ lost. Here an SMT checkpoint is what is needed to resume bit-for-bi
 base model:
 
 * ``smt_meta.json``: format tag, per-module ``(name, index_list, weight shape)`` in selection
-  order, the optimizer param-group hyper-parameters, step counters, the LR-scheduler state, and a
-  fingerprint of every frozen parameter (SMT modules' W with their tile blocks masked out);
-* ``smt_state.safetensors``: the bf16 tiles of every module and, per engine tile group, the fp32
+  order, the optimizer param-group hyper-parameters, step counters, the LR-scheduler state, the fp16
+  loss scale's state (the reference's ``--dtype fp16``), and a fingerprint of every frozen parameter (SMT modules' W with their tile blocks masked out);
+* ``smt_state.safetensors``: the tiles of every module (in the model's dtype) and, per engine tile group, the fp32
   master / exp_avg / exp_avg_sq (0.8 GB at the LLaMA-3-8B operating point);
 * ``smt_frozen.safetensors`` (``include_frozen=True``, the default, as DeepSpeed's
   ``save_checkpoint`` also saves the module): every other weight of the model as it is now. The
@@ -135,8 +135,10 @@ def _write_checkpoint(engine, save_dir: str, client_state: Optional[dict], inclu
         tensors[f"master/{gi}"] = tg.master.cpu()
         tensors[f"exp_avg/{gi}"] = tg.exp_avg.cpu()
         tensors[f"exp_avg_sq/{gi}"] = tg.exp_avg_sq.cpu()
+    scaler = getattr(engine, "loss_scaler", None)
     meta = {"format": FORMAT, "modules": modules, "groups": groups, "global_steps": engine.global_steps,
-            "micro_steps": engine.micro_steps,
+            "micro_steps": engine.micro_steps, "skipped_steps": getattr(engine, "skipped_steps", 0),
+            "loss_scaler": scaler.state_dict() if scaler is not None else None,
             "lr_scheduler": engine.lr_scheduler.state_dict() if engine.lr_scheduler is not None else None,
             "client_state": client_state or {}, "frozen_fingerprints": _frozen_fingerprints(model),
             "includes_frozen": bool(include_frozen), "save_id": save_id}
@@ -247,6 +249,15 @@ def load_optimizer_state(engine, load_dir: str) -> dict:
             tg.group[k] = tuple(v) if isinstance(v, list) else v
     engine.global_steps = int(meta["global_steps"])
     engine.micro_steps = int(meta["micro_steps"])
+    engine.skipped_steps = int(meta.get("skipped_steps", 0))
+    saved_scaler = meta.get("loss_scaler")
+    scaler = getattr(engine, "loss_scaler", None)
+    if (saved_scaler is None) != (scaler is None):
+        raise ValueError("the checkpoint was saved " + ("with" if saved_scaler is not None else "without")
+                         + " an fp16 loss scale and this engine runs " + ("with" if scaler is not None else "without")
+                         + " one: resume with the same \"fp16\" config")
+    if scaler is not None:
+        scaler.load_state_dict(saved_scaler)     # the dynamic scale's schedule continues where it stopped
     if engine.lr_scheduler is not None and meta.get("lr_scheduler") is not None:
         engine.lr_scheduler.load_state_dict(meta["lr_scheduler"])
     return meta.get("client_state", {})

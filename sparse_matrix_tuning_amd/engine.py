@@ -72,6 +72,16 @@ class DynamicLossScale:
         self.iteration = 0
         self.last_overflow = -1
 
+    _STATE = ("dynamic", "scale", "window", "min_scale", "hysteresis", "consecutive", "tolerance", "iteration",
+              "last_overflow")
+
+    def state_dict(self) -> dict:
+        return {k: getattr(self, k) for k in self._STATE}
+
+    def load_state_dict(self, state: dict) -> None:
+        for k in self._STATE:
+            setattr(self, k, state[k])
+
     def update(self, overflow: bool) -> None:
         if not self.dynamic:
             return

@@ -237,3 +237,66 @@ def test_fp8_group_resume_is_bit_identical(tmp_path):
         assert torch.equal(ta.master, tc.master) and torch.equal(ta.exp_avg_sq, tc.exp_avg_sq)
     for (na, pa), (nc, pc) in zip(a.module.named_parameters(), c.module.named_parameters()):
         assert na == nc and torch.equal(pa, pc), na
+
+
+FP16_CFG = {"gradient_clipping": 1.0, "fp16": {"enabled": True, "loss_scale_window": 2, "initial_scale_power": 24}}
+
+
+def _engine16(net, convert=True, cfg=FP16_CFG):
+    if convert:
+        smt.freeze_unselected_matrix_layer(net, SEL_MLP, SEL_ATT)
+        smt.convert_linear_layer_to_matrix_sparsity(net, SEL_MLP, SEL_ATT)
+    groups = smt.get_optimizer_sparse_grouped_parameters(net, 0.01, 2e-3)
+    opt = SMTFusedAdam(groups, lr=2e-3, betas=(0.9, 0.95))
+    sched = torch.optim.lr_scheduler.LambdaLR(opt, linear_lr_lambda(1, 10))
+    eng, _, _, _ = initialize(model=net, optimizer=opt, config=cfg, lr_scheduler=sched)
+    return eng
+
+
+def _step16(eng, i):
+    x = torch.randn(2, 32, 512, generator=torch.Generator().manual_seed(100 + i)).half().to(DEV)
+    loss = (eng(x).float() ** 2).mean()
+    eng.backward(loss)
+    eng.step()
+
+
+def test_fp16_resume_keeps_the_loss_scale(tmp_path):
+    """The reference's --dtype fp16 under the engine: an fp16 run interrupted after steps that
+    overflowed and resumed from its checkpoint continues the dynamic loss scale's schedule (scale,
+    tolerance, iteration, last overflow) and is bit-identical to the uninterrupted run; resuming
+    it without the fp16 config is refused."""
+    def base16():
+        return _base().half()
+    base_sd = {k: v.clone() for k, v in base16().state_dict().items()}
+    a = _engine16(base16())
+    for i in range(8):
+        _step16(a, i)
+    b = _engine16(base16())
+    for i in range(4):
+        _step16(b, i)
+    assert b.skipped_steps >= 1                           # the first steps overflow at 2**24
+    b.save_checkpoint(str(tmp_path), tag="s4")
+    saved = dict(b.loss_scaler.state_dict())
+    del b
+    net = base16()
+    net.load_state_dict(base_sd)
+    checkpoint.restore_model(net, str(tmp_path / "s4"))
+    c = _engine16(net, convert=False)
+    c.load_checkpoint(str(tmp_path), tag="s4")
+    assert c.loss_scaler.state_dict() == saved
+    for i in range(4, 8):
+        _step16(c, i)
+    torch.cuda.synchronize()
+    assert c.loss_scaler.state_dict() == a.loss_scaler.state_dict()
+    assert c.skipped_steps == a.skipped_steps and c.global_steps == a.global_steps == 8
+    for ta, tc in zip(a.tile_groups, c.tile_groups):
+        assert ta.step == tc.step
+        assert torch.equal(ta.master, tc.master) and torch.equal(ta.exp_avg_sq, tc.exp_avg_sq)
+    for (na, pa), (nc, pc) in zip(a.module.named_parameters(), c.module.named_parameters()):
+        assert na == nc and pa.dtype == torch.float16 and torch.equal(pa, pc), na
+    net = base16()
+    net.load_state_dict(base_sd)
+    checkpoint.restore_model(net, str(tmp_path / "s4"))
+    d = _engine16(net, convert=False, cfg={"gradient_clipping": 1.0})
+    with pytest.raises(ValueError, match="loss scale"):
+        d.load_checkpoint(str(tmp_path), tag="s4")
