@@ -18,6 +18,9 @@ all-reduces of the dense warm-up gradients and the tile gradients run (identitie
 
 ``--fp8``: the SMT phase on the fp8 path (e4m3 decoder GEMMs, MX-fp8 tile weight gradients).
 
+``--dtype fp16``: the reference's --dtype fp16 (an fp16 model, transformers' own ops, the engine under
+DeepSpeed's dynamic loss scale; the fp16 config of deepspeed_helpers.py:53-55).
+
 Writes the post-warm-up weights, the selection, the tile optimizer state and the SMT modules'
 weights after the SMT step (rank 0).
 """
@@ -41,6 +44,7 @@ def main():
     ap.add_argument("--fp8", action="store_true", help="SMT phase on the fp8 path (MX-fp8 tile gradients)")
     ap.add_argument("--pg", default=None, help="process-group backend (default: gloo when WORLD_SIZE > 1)")
     ap.add_argument("--exchange", default="auto", choices=("auto", "always"), help="the engine's dp_exchange")
+    ap.add_argument("--dtype", default="bf16", choices=("bf16", "fp16"))
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -63,7 +67,10 @@ def main():
     cfg["num_hidden_layers"] = 2
     bench.MODELS["_dp"] = cfg
     model = bench.build_model("_dp", dev)
-    patch_llama(model)
+    if args.dtype == "fp16":
+        model = model.half()                             # the fused LLaMA ops are bf16-only
+    else:
+        patch_llama(model)
     model.train()
     vocab = cfg["vocab_size"]
 
@@ -80,15 +87,19 @@ def main():
     ds = {"gradient_clipping": 1.0, "train_micro_batch_size_per_gpu": micro, "train_batch_size": 4,
           "reduce_bucket_size": 300000,                 # several buckets on this small model
           "dp_exchange": args.exchange}
+    if args.dtype == "fp16":
+        ds["fp16"] = {"enabled": True, "loss_scale_window": 100, "initial_scale_power": 12}
     dims = trainer.get_targeted_module_dims(model)
     n_att, n_mlp = trainer.block_budgets(trainer.count_total_blocks(model), 0.05, 0.05)
     opt = SMTFusedAdam(model.parameters(), lr=1e-3, betas=(0.9, 0.95))
     engine, opt, _, _ = initialize(model=model, optimizer=opt, config=ds)
     harvester = trainer.GradHarvester(model, n_mlp, n_att)
+    warm_grads = {}
     for b in halves(1000):
         engine.backward(engine(**b, use_cache=False).loss)
         if engine.is_gradient_accumulation_boundary():
             harvester.harvest()                          # the DP-averaged (accumulated) gradients
+            warm_grads = {n: p.grad.float().cpu() for n, p in model.named_parameters() if p.grad is not None}
         engine.step()
     warm = {n: p.detach().cpu().clone() for n, p in model.named_parameters()}
     dense_issued = engine.dense_buckets.issued if engine.dense_buckets is not None else 0
@@ -109,7 +120,12 @@ def main():
            "buckets": len(tg.buckets.buckets) if tg.buckets is not None else 0,
            "tile_issued": tg.buckets.issued if tg.buckets is not None else 0, "dense_issued": dense_issued,
            "backend": dist.get_backend() if dist.is_initialized() else None,
-           "world": dist.get_world_size() if dist.is_initialized() else 1}
+           "world": dist.get_world_size() if dist.is_initialized() else 1,
+           "loss_scale": engine.loss_scaler.state_dict() if engine.loss_scaler is not None else None,
+           # the last step's DP-averaged (accumulated) tile gradient, still loss-scaled in fp16
+           "grad": tg.grad.cpu() / (dist.get_world_size() if dist.is_initialized() else 1),
+           "skipped": engine.skipped_steps,
+           "warm_grads": warm_grads if args.dtype == "fp16" else {}}
     if rank == 0:
         torch.save(out, args.out)
     if dist.is_initialized():

@@ -132,3 +132,49 @@ def test_rccl_world1_exchange_bit_identical_to_no_process_group(tmp_path):
         assert torch.equal(rccl[k], plain[k]), k
     for n in plain["W"]:
         assert torch.equal(rccl["W"][n], plain["W"][n]), n
+
+
+def test_dp2_fp16_matches_gradient_accumulation(tmp_path):
+    """The equivalence in the reference's --dtype fp16 (fp16 model, transformers' ops, the dynamic loss
+    scale). Not bit for bit: accumulation halves each micro-step's loss BEFORE the fp16 backward
+    (the engine's gas scaling, as DeepSpeed's), the exchange averages after it, and fp16 gradients this
+    small are subnormal in places, so the two round differently. Asserted: the warm-up's exchanged
+    dense gradients (the loss-scaled fp16 gradients the bucketed all-reduce averaged) within 2e-3
+    (relative, per parameter) of the accumulated ones; the same loss-scale state and skipped steps (the
+    overflow decision is taken on the exchanged gradients, the same on every rank); the same selection.
+    After AdamW the states drift apart further: its first steps move every weight by ~lr times the
+    gradient's sign, which turns a flipped sign of a near-zero gradient into a 2 lr difference, so the
+    warm-up weights are compared elementwise (< 1 % differ, each within 2.5 lr) and the SMT step's tile
+    gradient, computed on those weights, within 1e-2."""
+    outs = {}
+    for mode in ("acc", "dp"):
+        out = str(tmp_path / f"{mode}16.pt")
+        if mode == "dp":
+            cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                   "--master-addr", "127.0.0.1", "--master-port", str(_port()), WORKER, "--mode", "dp",
+                   "--dtype", "fp16", "--out", out]
+        else:
+            cmd = [sys.executable, WORKER, "--mode", mode, "--dtype", "fp16", "--out", out]
+        _run(cmd, tmp_path)
+        outs[mode] = torch.load(out, weights_only=True)
+    dp, acc = outs["dp"], outs["acc"]
+    assert dp["buckets"] > 1 and dp["loss_scale"] is not None
+    assert dp["loss_scale"] == acc["loss_scale"] and dp["skipped"] == acc["skipped"]
+    assert sorted(dp["warm_grads"]) == sorted(acc["warm_grads"]) and acc["warm_grads"]
+    worst = 0.0
+    for n, ga in acc["warm_grads"].items():
+        gd = dp["warm_grads"][n]
+        worst = max(worst, ((gd - ga).double().norm() / ga.double().norm().clamp_min(1e-30)).item())
+    print(f"\nfp16 dp vs accumulation: warm-up dense gradients within {worst:.2e} (relative, worst parameter)")
+    assert worst <= 2e-3, worst
+    lr = 1e-3
+    for n in acc["warm"]:
+        a, d = acc["warm"][n].float(), dp["warm"][n].float()
+        assert acc["warm"][n].dtype == torch.float16
+        assert (a != d).float().mean().item() < 0.01, n
+        assert (a - d).abs().max().item() <= 2.5 * lr, n
+    assert dp["sel_mlp"] == acc["sel_mlp"] and dp["sel_att"] == acc["sel_att"]
+    g_dp, g_acc = dp["grad"].double(), acc["grad"].double()
+    rel = ((g_dp - g_acc).norm() / g_acc.norm()).item()
+    print(f"fp16 dp vs accumulation: SMT-step tile gradient {rel:.2e} relative")
+    assert rel <= 1e-2, rel
