@@ -642,8 +642,11 @@ class linearZ(torch.autograd.Function):
             dev = g2.device
             if getattr(ctx, "recompute", None) is not None:
                 cb_dev, table = tiles.packed_tables(dev)
-                x2 = _recompute_blocks(ctx.recompute, cb_dev)
-                ctx.recompute = None
+                rec, ctx.recompute = ctx.recompute, None
+                # rebuilt on the wgrad stream, like the forward's block copies: its only consumer is
+                # the tile-gradient launch there, so the data-gradient GEMMs do not wait for it
+                x2 = _off_stream(ctx.sink, lambda: _recompute_blocks(rec, cb_dev),
+                                 *[t for t in rec[1] if t is not None])
             elif ctx.packed:
                 x2 = saved
                 table = tiles.packed_tables(dev, ctx.packed if isinstance(ctx.packed, dict) else None)[1]

@@ -158,3 +158,40 @@ def test_selective_policy_detects_in_place_change():
             out.float().sum().backward()
     finally:
         smt.set_activation_policy(old)
+
+
+def test_selective_policy_through_the_engine_bit_identical():
+    """Under the engine the rebuilt blocks are made on the wgrad stream (beside the data-gradient
+    GEMMs, like the forward's block copies): two SMT steps with "activation_policy": "selective" give
+    the same loss, tile optimizer state and W as with "resident", bit for bit."""
+    from sparse_matrix_tuning_amd.engine import SMTFusedAdam, initialize
+
+    def run(policy):
+        model = _model()
+        fl.patch_llama(model)
+        try:
+            groups = smt.get_optimizer_sparse_grouped_parameters(model, 0.0, smt_lr=1e-3)
+            opt = SMTFusedAdam(groups, lr=1e-3, betas=(0.9, 0.95))
+            eng, _, _, _ = initialize(model=model, optimizer=opt,
+                                      config={"gradient_clipping": 1.0, "activation_policy": policy})
+            assert eng.wgrad_stream is not None
+            losses = []
+            for i in range(2):
+                ids = torch.randint(1, CFG["vocab_size"], (2, 1024), generator=torch.Generator().manual_seed(20 + i)).to(DEV)
+                loss = eng(input_ids=ids, labels=ids, use_cache=False).loss
+                eng.backward(loss)
+                eng.step()
+                losses.append(loss.detach())
+            torch.cuda.synchronize()
+            tg = eng.tile_groups[0]
+            W = {n: m.weight.detach().clone() for n, m in model.named_modules()
+                 if isinstance(m, smt.LinearLayer_MatrixSparsity)}
+            return losses, tg.master.clone(), tg.exp_avg_sq.clone(), W
+        finally:
+            fl.unpatch_llama(model)
+
+    lr_, mr, vr, Wr = run("resident")
+    ls_, ms, vs, Ws = run("selective")
+    assert all(torch.equal(a, b) for a, b in zip(lr_, ls_))
+    assert torch.equal(mr, ms) and torch.equal(vr, vs)
+    assert Wr.keys() == Ws.keys() and all(torch.equal(Wr[n], Ws[n]) for n in Wr)
