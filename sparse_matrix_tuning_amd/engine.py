@@ -6,7 +6,8 @@
 returns an engine with that surface, designed for the SMT phase on one GPU per process:
 
 * Every trainable ``selected_weight`` of the model's SMT modules is re-pointed into ONE flat
-  bf16 buffer (tile-major, 65536 elements per tile). fp32 master / exp_avg / exp_avg_sq and an
+  buffer of the model's dtype (tile-major, 65536 elements per tile; bf16, or the reference's fp16 /
+  fp32, fine_tune.py:955-959). fp32 master / exp_avg / exp_avg_sq and an
   fp32 gradient buffer of the same length sit beside it (57.1 M params at the LLaMA-3-8B
   operating point: 0.92 GB).
 * ``linearZ.backward`` writes each module's tile gradients straight into that fp32 buffer through
@@ -19,8 +20,10 @@ returns an engine with that surface, designed for the SMT phase on one GPU per p
   the optimizer kernels.
 * ``step()`` = one ``smt_sq_norm`` (global norm for ``gradient_clipping``) + one fused
   ``smt_adamw_step`` launch per parameter group that clips, updates fp32 master/moments, writes the
-  bf16 tiles AND scatters them into the frozen ``W`` — so the modules skip the per-forward
-  write-back of smt.py:332-341. No host synchronisation anywhere in the step.
+  tiles AND scatters them into the frozen ``W`` — so the modules skip the per-forward
+  write-back of smt.py:332-341. No host synchronisation anywhere in the step, except under the
+  reference's fp16 (DeepSpeed's dynamic loss scale, :class:`DynamicLossScale`): one read of the
+  gradient norm decides whether the step overflowed and is skipped.
 
 * Data gradients ``grad_input = g @ W`` of every frozen linear (SMT modules, untouched ``nn.Linear``
   such as o_proj and lm_head) run against a transposed copy W^T as the TN product g @ (W^T)^T,
@@ -29,7 +32,7 @@ returns an engine with that surface, designed for the SMT phase on one GPU per p
   The AdamW epilogue's scatter is followed by one transposed scatter into the W^T copies.
 
 Other trainable parameters (the full fine-tuning warm-up, fine_tune.py:160-190) take the dense
-path: autograd bf16 grads, one all-reduce per parameter, and the same fused AdamW kernel in flat
+path: autograd grads in the model's dtype, bucketed all-reduces (``DenseGradBuckets``), and the same fused AdamW kernel in flat
 mode over per-parameter fp32 masters. The ZeRO partitioning of the reference is not reproduced:
 at 288 GB per GPU the 57 M-parameter tile optimizer state is simply replicated.
 """
