@@ -110,3 +110,19 @@ def test_engine_checks_the_config_dtype_against_the_model():
     assert eng.loss_scaler is not None and eng.loss_scaler.scale == 65536.0 and eng.loss_scaler.window == 100
     eng, _, _, _ = initialize(model=nn.Linear(8, 8), optimizer=None, config={"fp16": {"enabled": False}})
     assert eng.loss_scaler is None                    # the reference's fp32 (fp16 disabled)
+
+
+def test_loss_scale_state_round_trip():
+    """The state a checkpoint carries (checkpoint.py meta "loss_scaler") restores the schedule: the
+    restored scaler and the original stay equal under the same later overflows."""
+    import json
+    a = DynamicLossScale({"enabled": True, "loss_scale_window": 3, "initial_scale_power": 10})
+    for o in (True, False, True, True, False, False):
+        a.update(o)
+    b = DynamicLossScale({"enabled": True})
+    b.load_state_dict(json.loads(json.dumps(a.state_dict())))      # through the JSON meta file
+    assert b.state_dict() == a.state_dict()
+    for o in (False, False, False, True, False, True, True):
+        a.update(o)
+        b.update(o)
+        assert b.state_dict() == a.state_dict()
