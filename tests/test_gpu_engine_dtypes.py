@@ -284,3 +284,47 @@ def test_reference_flow_in_dtype(dtype):
     for mod in model.modules():
         if isinstance(mod, smt.LinearLayer_MatrixSparsity):
             assert torch.equal(ref.gather_tiles(mod.weight.detach().cpu(), mod.index_list), mod.selected_weight.detach().cpu())
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.float32])
+def test_channel_path_through_the_engine_in_dtype(dtype):
+    """The channel (activation-selected rows) path, fine_tune.py:406-709, in the reference's fp16 /
+    fp32: harvest -> select -> convert -> engine with DeepSpeed's dtype config. The selected rows are
+    dense parameters of the model's dtype for the engine (fp16 under the loss scale); 4 steps run
+    with finite losses, and the rows written back into W are the rows' values in that dtype."""
+    import bench
+    import numpy as np
+    from sparse_matrix_tuning_amd import trainer
+    cfg = dict(bench.MODELS["mini"])
+    cfg["num_hidden_layers"] = 2
+    cfg["num_key_value_heads"] = cfg["num_attention_heads"]
+    bench.MODELS["_tcd"] = cfg
+    try:
+        model = bench.build_model("_tcd", DEV).to(dtype)
+    finally:
+        del bench.MODELS["_tcd"]
+    ds = {"gradient_clipping": 1.0, "fp16": ({"enabled": True, "loss_scale_window": 100}
+                                             if dtype == torch.float16 else {"enabled": False})}
+    h = trainer.ActivationHarvester(model, num_mlp_channel=0, num_attention_channel=24)
+    ids = torch.randint(0, 4096, (2, 128), generator=torch.Generator().manual_seed(7)).to(DEV)
+    h.collect({"input_ids": ids})
+    engine, _opt, _sched, sel_mlp, sel_att = trainer.select_and_convert_channels(
+        model, h, num_attention_channel=24, num_mlp_channel=0, ft_learning_rate=1e-3, num_training_steps=10,
+        ds_config=ds)
+    assert sum(len(v) for v in sel_att.values()) == 24
+    assert (engine.loss_scaler is not None) == (dtype == torch.float16)
+    mods = {n: m for n, m in model.named_modules() if isinstance(m, smt.LinearLayer_ChannelSparsity)}
+    assert mods and all(m.selected_weight.dtype == dtype for m in mods.values())
+    before = {n: m.selected_weight.detach().clone() for n, m in mods.items()}
+    losses = []
+    for _ in range(4):
+        o = engine(input_ids=ids, labels=ids, use_cache=False)
+        engine.backward(o.loss)
+        engine.step()
+        losses.append(o.loss.item())
+    assert all(np.isfinite(losses)), losses
+    assert engine.global_steps - engine.skipped_steps >= 2
+    assert any(not torch.equal(before[n], m.selected_weight.detach()) for n, m in mods.items())
+    for n, m in mods.items():
+        m(torch.zeros(1, 1, m.weight.shape[1], dtype=dtype, device=DEV))     # the per-forward write-back
+        assert torch.equal(m.weight.detach()[m.index_list].cpu(), m.selected_weight.detach().cpu())
