@@ -28,8 +28,12 @@ returns an engine with that surface, designed for the SMT phase on one GPU per p
 * Data gradients ``grad_input = g @ W`` of every frozen linear (SMT modules, untouched ``nn.Linear``
   such as o_proj and lm_head) run against a transposed copy W^T as the TN product g @ (W^T)^T,
   the layout hipBLASLt runs 13-19 % faster on the LLaMA-3-8B shapes (``transposed_dgrad`` config
-  key, default on; +2 bytes per frozen weight element, 15 GB at 8B, still below the warm-up peak).
-  The AdamW epilogue's scatter is followed by one transposed scatter into the W^T copies.
+  key; +2 bytes per frozen weight element, 14 GB at 8B). The AdamW epilogue's scatter is followed by
+  one transposed scatter into the W^T copies. ``"auto"`` (the default) follows the memory policy the
+  caller chose: copies when activations stay resident, none when the model recomputes its layers
+  (``gradient_checkpointing_enable()`` before ``initialize``, as fine_tune.py:192 runs the SMT
+  phase), where memory is the point; ``true`` / ``false`` force it. :meth:`SMTEngine.set_transposed_dgrad`
+  switches it between steps.
 
 Other trainable parameters (the full fine-tuning warm-up, fine_tune.py:160-190) take the dense
 path: autograd grads in the model's dtype, bucketed all-reduces (``DenseGradBuckets``), and the same fused AdamW kernel in flat
@@ -283,6 +287,30 @@ def attach_transposed_weights(model: torch.nn.Module, joint_qkv: bool = True) ->
             if type(m) is torch.nn.Linear:
                 m.forward = _frozen_linear_forward.__get__(m, type(m))
     return added
+
+
+def drop_transposed_weights(model: torch.nn.Module) -> None:
+    """Undo :func:`attach_transposed_weights` only (the W^T copies and the joint q/k/v marks); plain
+    frozen ``nn.Linear`` forwards go back to ``F.linear`` unless they carry fp8 copies."""
+    for m in model.modules():
+        if "_smt_joint_qkv_grad" in m.__dict__:
+            del m.__dict__["_smt_joint_qkv_grad"]
+        w = getattr(m, "weight", None)
+        if isinstance(w, torch.Tensor) and hasattr(w, "_smt_weight_t"):
+            delattr(w, "_smt_weight_t")
+            if type(m) is torch.nn.Linear and "forward" in m.__dict__ and getattr(w, "_smt_fp8", None) is None:
+                del m.__dict__["forward"]
+
+
+def transposed_dgrad_wanted(cfg: dict, model: torch.nn.Module) -> bool:
+    """The engine's ``transposed_dgrad`` key: ``"auto"`` (default) = copies unless the model recomputes
+    its layers (the reference's memory policy, fine_tune.py:192); ``true`` / ``false`` force it."""
+    v = cfg.get("transposed_dgrad", "auto")
+    if isinstance(v, str):
+        if v != "auto":
+            raise ValueError(f"transposed_dgrad {v!r}: 'auto', true or false")
+        return not bool(getattr(model, "is_gradient_checkpointing", False))
+    return bool(v)
 
 
 def attach_channel_gather_groups(model: torch.nn.Module) -> int:
@@ -762,7 +790,7 @@ class _TileGroup:
         self.reported = [False] * len(modules)          # wrote its tile gradients in this accumulation window
         # bucket_elems None: one rank, no exchange; <= 0: one bucket for the whole buffer
         self.buckets = TileGradBuckets(self.grad, ranges, bucket_elems) if bucket_elems is not None else None
-        descs, tdescs, off = [], [], 0
+        descs, off = [], 0
         for idx, m in enumerate(modules):
             k = len(m.tiles)
             view = self.param[off * TILE_ELEMS:(off + k) * TILE_ELEMS].view(k * 256, 256)
@@ -772,18 +800,15 @@ class _TileGroup:
                 self.grad[off * TILE_ELEMS:(off + k) * TILE_ELEMS].view(k * 256, 256), engine, self, self.buckets, idx)
             m.writeback_on_forward = False                      # the AdamW epilogue scatters into W
             m.sync_weight()                                     # W (and W^T) consistent with the tiles now
-            wt = getattr(m.weight, "_smt_weight_t", None)
             for i, (r, c) in enumerate(m.tiles):
                 descs.append((m.weight.data, r, c, (off + i) * TILE_ELEMS))
-                if wt is not None:
-                    tdescs.append((wt, r, c, (off + i) * TILE_ELEMS))
             off += k
+        self.device = device
         self.master = self.param.float()
         self.exp_avg = torch.zeros_like(self.master)
         self.exp_avg_sq = torch.zeros_like(self.master)
         self.descs = _hip.tile_descs(descs, device, self.dtype) if descs else None
-        self.n_tdescs = len(tdescs)
-        self.tdescs = _hip.tile_descs(tdescs, device) if tdescs else None
+        self.build_transposed_descs()
         self.fp8_modules = [(m, m.weight._smt_fp8) for m in modules if getattr(m.weight, "_smt_fp8", None) is not None]
         # grouped fp8 copies: the joint transposed copy is re-quantised once per step over the union of
         # the column blocks its tile-carrying members touch
@@ -793,6 +818,18 @@ class _TileGroup:
                 union.setdefault(id(fw.group), (fw.group, set()))[1].update(m.tiles.column_blocks())
         self.fp8_groups = [(g, torch.tensor(sorted(cbs), dtype=torch.int32).to(device)) for g, cbs in union.values()]
         self.step = 0
+
+    def build_transposed_descs(self) -> None:
+        """The epilogue's second scatter: each tile into its module's W^T copy, where one exists."""
+        tdescs, off = [], 0
+        for m in self.modules:
+            wt = getattr(m.weight, "_smt_weight_t", None)
+            for i, (r, c) in enumerate(m.tiles):
+                if wt is not None:
+                    tdescs.append((wt, r, c, (off + i) * TILE_ELEMS))
+            off += len(m.tiles)
+        self.n_tdescs = len(tdescs)
+        self.tdescs = _hip.tile_descs(tdescs, self.device) if tdescs else None
 
     def begin_window(self) -> None:
         self.reported = [False] * len(self.modules)
@@ -885,7 +922,7 @@ class SMTEngine:
             if owner and cfg.get("fp8_linears", False):
                 # config 5: e4m3 copies of the decoder-layer weights (re-quantised after each step)
                 self.fp8_bytes = attach_fp8_weights(model)
-            if (owner or channel_rows) and cfg.get("transposed_dgrad", True):
+            if (owner or channel_rows) and transposed_dgrad_wanted(cfg, model):
                 # SMT phase: every linear weight is frozen (tiles change only through the epilogue;
                 # the channel path's rows through LinearLayer_ChannelSparsity.sync_weight, which keeps
                 # W^T in step)
@@ -974,6 +1011,20 @@ class SMTEngine:
         self._wgrad_events.append(ev)
         if len(self._wgrad_events) > self.wgrad_max_lag:
             cur.wait_event(self._wgrad_events.popleft())
+
+    def set_transposed_dgrad(self, on: bool) -> int:
+        """Attach (``on``) or drop the W^T copies of the frozen linears' data-gradient GEMMs on a live
+        engine, between steps (the bench measures the recompute policy both ways). Tiles are written
+        into a copy when it is attached, so W^T always equals W. Returns the bytes the copies take."""
+        if on and not self.transposed_bytes:
+            joint = self.config.get("joint_qkv_dgrad", os.environ.get("SMT_JOINT_QKV", "1") != "0")
+            self.transposed_bytes = attach_transposed_weights(self.module, joint_qkv=joint)
+        elif not on and self.transposed_bytes:
+            drop_transposed_weights(self.module)
+            self.transposed_bytes = 0
+        for tg in self.tile_groups:
+            tg.build_transposed_descs()
+        return self.transposed_bytes
 
     def is_gradient_accumulation_boundary(self) -> bool:
         return (self.micro_steps + 1) % self.gradient_accumulation_steps == 0

@@ -99,3 +99,22 @@ def test_dp_exchange_always_at_world_one_gloo():
     res = q.get(timeout=120)
     p.join(timeout=60)
     assert res is True, res
+
+
+def test_transposed_dgrad_key():
+    """``transposed_dgrad``: "auto" (default) keeps W^T copies for resident activations and none when
+    the model recomputes its layers (fine_tune.py:192); booleans force it; other strings raise."""
+    from sparse_matrix_tuning_amd.engine import transposed_dgrad_wanted
+
+    class M:
+        is_gradient_checkpointing = False
+    m = M()
+    assert transposed_dgrad_wanted({}, m) is True
+    m.is_gradient_checkpointing = True
+    assert transposed_dgrad_wanted({}, m) is False
+    assert transposed_dgrad_wanted({"transposed_dgrad": "auto"}, m) is False
+    assert transposed_dgrad_wanted({"transposed_dgrad": True}, m) is True
+    assert transposed_dgrad_wanted({"transposed_dgrad": False}, M()) is False
+    assert transposed_dgrad_wanted({}, torch.nn.Linear(2, 2)) is True       # no checkpointing attribute
+    with pytest.raises(ValueError):
+        transposed_dgrad_wanted({"transposed_dgrad": "always"}, m)

@@ -302,6 +302,50 @@ def test_transposed_dgrad_matches_plain_dgrad():
     assert not hasattr(W, "_smt_weight_t") and "forward" not in net.lin.__dict__
 
 
+def test_transposed_dgrad_auto_follows_recompute_and_toggles_live():
+    """``transposed_dgrad: "auto"`` (the default): an engine created on a model that recomputes its
+    layers (fine_tune.py:192, where memory is the point) keeps no W^T copies; one on a resident model
+    does. ``set_transposed_dgrad`` attaches / drops them between steps, and the AdamW epilogue's
+    transposed scatter follows (W^T == W after every step)."""
+    import bench
+    from sparse_matrix_tuning_amd.fused_llama import patch_llama
+    sel_mlp = {("gate_proj", 1): [(0, 0), (2, 1)]}
+    sel_att = {("q_proj", 0): [(0, 1)], ("v_proj", 3): [(0, 0)]}
+
+    def make(ckpt):
+        model = bench.build_model("mini", DEV)
+        patch_llama(model)
+        if ckpt:
+            model.gradient_checkpointing_enable()
+        model.train()
+        smt.freeze_unselected_matrix_layer(model, sel_mlp, sel_att)
+        smt.convert_linear_layer_to_matrix_sparsity(model, sel_mlp, sel_att)
+        opt = SMTFusedAdam(smt.get_optimizer_sparse_grouped_parameters(model, 0.0, 1e-3), lr=1e-3, betas=(0.9, 0.95))
+        return model, initialize(model=model, optimizer=opt, config={"gradient_clipping": 1.0})[0]
+
+    def copies(model):
+        return [m for m in model.modules() if isinstance(getattr(m, "weight", None), torch.Tensor)
+                and getattr(m.weight, "_smt_weight_t", None) is not None]
+
+    model, eng = make(ckpt=False)
+    assert eng.transposed_bytes > 0 and copies(model)
+    model, eng = make(ckpt=True)
+    assert eng.transposed_bytes == 0 and not copies(model) and eng.tile_groups[0].tdescs is None
+    b = bench.batches(3, 2, 128, bench.MODELS["mini"]["vocab_size"], 0, DEV)
+    losses = []
+    for i, on in enumerate((True, False, True)):
+        added = eng.set_transposed_dgrad(on)
+        assert (added > 0) == on and bool(copies(model)) == on
+        loss = eng(**b[i], use_cache=False).loss
+        eng.backward(loss)
+        eng.step()
+        losses.append(loss.item())
+        torch.cuda.synchronize()
+        for m in copies(model):
+            assert torch.equal(m.weight._smt_weight_t, m.weight.detach().t()), i
+    assert all(l == l for l in losses)
+
+
 def test_engine_sink_grads_are_fp32_and_exact():
     torch.manual_seed(9)
     W = nn.Parameter((torch.randn(512, 768) * 0.05).bfloat16().to(DEV))
