@@ -113,6 +113,14 @@ def parse():
                     help="after the recompute point, also time this many steps with the same per-layer recompute "
                          "but the last half of the decoder layers resident (reported under "
                          "'grad_ckpt_half_resident_mode'; default: min(--steps, 20); 0 disables)")
+    ap.add_argument("--no-transposed-steps", type=int, default=None,
+                    help="after the recompute point, time this many steps of the same per-layer recompute without "
+                         "the W^T copies of the data-gradient GEMMs (the engine's transposed_dgrad 'auto' default "
+                         "under recompute; reported under 'grad_ckpt_no_transposed_mode' and in memory_vs_full_ft; "
+                         "default: min(--steps, 20); 0 disables)")
+    ap.add_argument("--transposed-dgrad", default="on", choices=("on", "off"),
+                    help="the headline engine's W^T copies of the frozen linears' data-gradient GEMMs (engine key "
+                         "transposed_dgrad; default on: the resident headline keeps them)")
     ap.add_argument("--ref-rounding-steps", type=int, default=None,
                     help="after the selective point, also time this many steps with the other tile-gradient rounding "
                          "than the engine's (default engine: the reference's per-sample bf16 partials, smt.py:397-404; "
@@ -165,6 +173,8 @@ def parse():
         args.half_resident_steps = min(args.steps, 20)
     if args.ref_rounding_steps is None:
         args.ref_rounding_steps = min(args.steps, 20)
+    if args.no_transposed_steps is None:
+        args.no_transposed_steps = min(args.steps, 20)
     if args.raw_harvest_steps is None:
         args.raw_harvest_steps = min(args.steps, 20)
     return args
@@ -810,6 +820,26 @@ def cpu_baseline(seconds: float, tiles_one_layer: dict, model_name: str, gpu: di
             "units": units}
 
 
+def memory_vs_full_ft(ckpt_mode, no_t_mode, full_ft_gb, harvest_gb, ckpt_copies=True):
+    """The reference's one published figure for this path: SMT cuts the GPU memory footprint of full
+    fine-tuning by 67 % (README.md:5). Same activation policy on both sides (every layer recomputed,
+    fine_tune.py:192); the harvest accumulators, which the reference keeps on the host, are taken out of
+    the full fine-tuning peak. One point per W^T setting, tokens/s beside each; ``reduction`` is the
+    engine's default at this policy (transposed_dgrad "auto": no copies when layers are recomputed)."""
+    points = []
+    for mode, copies in ((ckpt_mode, ckpt_copies), (no_t_mode, False)):
+        if mode is not None:
+            points.append({"transposed_dgrad": copies, "smt_peak_gb": mode["peak_hbm_gb"],
+                           "reduction": round(1.0 - mode["peak_hbm_gb"] / full_ft_gb, 4),
+                           "tokens_per_s": mode["value"], "median_ms_per_step": mode["median_ms_per_step"]})
+    default = points[-1]
+    return {"policy": "every layer recomputed (fine_tune.py:192) in both",
+            "smt_peak_gb": default["smt_peak_gb"], "full_ft_peak_gb": round(full_ft_gb, 2),
+            "harvest_accumulators_gb": round(harvest_gb, 2), "reduction": default["reduction"],
+            "default_transposed_dgrad": default["transposed_dgrad"], "points": points,
+            "reference_claim": {"reduction": 0.67, "source": "README.md:5", "gpu": "unspecified"}}
+
+
 def _median(xs):
     xs = sorted(xs)
     n = len(xs)
@@ -922,8 +952,11 @@ def main():
     # ---- warm-up: full fine-tuning + gradient harvest (fine_tune.py:710-775) ----
     ds_config = {"gradient_clipping": 1.0, "train_micro_batch_size_per_gpu": B, "train_batch_size": B * world,
                  "dp_exchange": "always" if pg1 else "auto"}
+    # the headline keeps activations resident, so its engine keeps the W^T copies of the data-gradient
+    # GEMMs (the model still recomputes its layers from the warm-up when the engine is built, which
+    # the "auto" default would read as the reference's memory policy)
     smt_config = dict(ds_config, fp8_linears=bool(args.fp8), overlap_wgrad=not args.no_overlap_wgrad,
-                      wgrad_batch_tiles=args.wgrad_batch_tiles)
+                      wgrad_batch_tiles=args.wgrad_batch_tiles, transposed_dgrad=args.transposed_dgrad == "on")
     from sparse_matrix_tuning_amd.smt.smt import _NO_DECAY
     groups = [{"params": [p for n, p in model.named_parameters() if not any(nd in n.lower() for nd in _NO_DECAY)],
                "weight_decay": 0.0},
@@ -1127,7 +1160,7 @@ def main():
         log(f"{alt} rounding: {alt_round_mode['value']} tokens/s (median step x{alt_round_mode['median_step_vs_headline']})")
 
     # ---- the reference's memory policy (per-layer recompute), same engine and tiles ----
-    ckpt_mode = half_mode = None
+    ckpt_mode = half_mode = no_t_mode = None
     if args.ref_mode_steps > 0 and not args.grad_ckpt:
         engine.module.gradient_checkpointing_enable()
         ref_batches = batches(1 + args.ref_mode_steps, B, S, vocab, rank, device, offset=50000)
@@ -1156,6 +1189,21 @@ def main():
             trainer.set_resident_layers(engine.module, 0)
             log(f"recompute policy, {n_half} layers resident: {half_mode['value']} tokens/s at "
                 f"{half_mode['peak_hbm_gb']} GB")
+        # the same recompute without the W^T copies: every data gradient then runs
+        # g @ W on hipBLASLt's NN layout, and the 14 GB of copies are gone. This is what an engine built
+        # on a recomputing model gets by default (transposed_dgrad "auto", fine_tune.py:192)
+        if args.no_transposed_steps > 0 and not args.fp8 and engine.transposed_bytes:
+            copies_gb = engine.transposed_bytes / 1e9
+            engine.set_transposed_dgrad(False)
+            torch.cuda.empty_cache()
+            no_t_mode = policy_point(args.no_transposed_steps, 45000, "grad_ckpt")
+            no_t_mode["transposed_dgrad"] = False
+            no_t_mode["transposed_copies_dropped_gb"] = round(copies_gb, 2)
+            no_t_mode["median_step_vs_with_copies"] = round(no_t_mode["median_ms_per_step"] /
+                                                            ckpt_mode["median_ms_per_step"], 4)
+            engine.set_transposed_dgrad(True)
+            log(f"recompute policy without W^T copies: {no_t_mode['value']} tokens/s at "
+                f"{no_t_mode['peak_hbm_gb']} GB (median step x{no_t_mode['median_step_vs_with_copies']})")
         engine.module.gradient_checkpointing_disable()
 
     # ---- the raw harvest's selection (no per-layer scaling), swapped in at the end ----
@@ -1274,6 +1322,7 @@ def main():
                        "activations": "recomputed per layer (fine_tune.py:192)" if args.grad_ckpt else
                                       "resident in HBM (MI355X default; the reference's recompute policy: grad_ckpt_mode)",
                        "grad_ckpt": bool(args.grad_ckpt), "full_ft_steps": args.full_ft_steps,
+                       "transposed_dgrad": args.transposed_dgrad == "on",
                        "wgrad_rounding": WGRAD_ROUNDING_NOTE.get(headline_rounding, headline_rounding),
                        "fused_llama_ops": not args.eager_ops,
                        "attention": "sdpa" if (args.eager_ops or args.sdpa_attention) else "smt_flash",
@@ -1291,13 +1340,9 @@ def main():
             # full fine-tuning by 67 % (README.md:5). Same activation policy on both sides (every layer
             # recomputed, fine_tune.py:192); the harvest accumulators, which the reference keeps on
             # the host, are taken out of the full fine-tuning peak
-            "memory_vs_full_ft": None if (ckpt_mode is None or resident or args.fp8) else {
-                "policy": "every layer recomputed (fine_tune.py:192) in both",
-                "smt_peak_gb": ckpt_mode["peak_hbm_gb"],
-                "full_ft_peak_gb": round(warm_peak - harvest_gb, 2),
-                "harvest_accumulators_gb": round(harvest_gb, 2),
-                "reduction": round(1.0 - ckpt_mode["peak_hbm_gb"] / (warm_peak - harvest_gb), 4),
-                "reference_claim": {"reduction": 0.67, "source": "README.md:5", "gpu": "unspecified"}},
+            "memory_vs_full_ft": None if (ckpt_mode is None or resident or args.fp8) else memory_vs_full_ft(
+                ckpt_mode, no_t_mode, warm_peak - harvest_gb, harvest_gb, args.transposed_dgrad == "on"),
+            "grad_ckpt_no_transposed_mode": no_t_mode,
             "selective_mode": selective_mode,
             "views_mode": views_mode,
             "wgrad_rounding_alt_mode": alt_round_mode,

@@ -1,6 +1,10 @@
 """Data-gradient GEMM layouts of the LLaMA-3-8B SMT step (T = 32768), interleaved rounds in one
 process (DVFS noise): g @ W with W [out, in] row-major (hipBLASLt NN) vs g @ Wt^T with a transposed
-copy Wt = W^T [in, out] row-major (hipBLASLt TN, the forward's layout). Prints one JSON line per shape."""
+copy Wt = W^T [in, out] row-major (hipBLASLt TN, the forward's layout). Also the forward from the
+transposed copy alone (``fwd_from_wt``: F.linear(x, Wt.t()), W a strided view of Wt, hipBLASLt NN), the
+"single copy" storage. Prints one JSON line per shape, then one line pricing the
+three storages per step of the reference's recompute policy (every decoder linear's forward twice,
+its data gradient once; the LM head's forward and data gradient once): W only, W + W^T copy, W^T only."""
 import json
 import statistics
 
@@ -21,8 +25,13 @@ def timed(fn, iters):
     return e0.elapsed_time(e1) / iters
 
 
+# per decoder layer: q, o (q/o shape), k, v, gate, up, down; 32 layers
+PER_LAYER = {"q/o": 2, "k/v": 2, "gate/up": 2, "down": 1}
+
+
 def main():
     torch.manual_seed(0)
+    rows = {}
     for name, (fin, fout) in SHAPES.items():
         iters = 2 if name == "lm_head" else 10
         x = torch.randn(T, fin, device="cuda", dtype=torch.bfloat16)
@@ -30,7 +39,8 @@ def main():
         Wt = W.t().contiguous()
         g = torch.randn(T, fout, device="cuda", dtype=torch.bfloat16)
         fns = {"fwd": lambda: torch.matmul(x, W.t()), "dgrad_nn": lambda: torch.matmul(g, W),
-               "dgrad_tn": lambda: torch.matmul(g, Wt.t())}
+               "dgrad_tn": lambda: torch.matmul(g, Wt.t()),
+               "fwd_from_wt": lambda: torch.nn.functional.linear(x, Wt.t())}
         for f in fns.values():
             f()
         torch.cuda.synchronize()
@@ -47,7 +57,16 @@ def main():
         same = torch.equal(torch.matmul(g[:256], W), torch.matmul(g[:256], Wt.t()))
         out["dgrad_bitwise_equal_on_256_rows"] = bool(same)
         print(json.dumps(out), flush=True)
+        rows[name] = out
         del x, W, Wt, g
+    cost = {}
+    for store, fwd, dg in (("W only", "fwd", "dgrad_nn"), ("W + W^T copy", "fwd", "dgrad_tn"),
+                           ("W^T only (single copy)", "fwd_from_wt", "dgrad_tn")):
+        ms = 32 * sum(n * (2 * rows[k][fwd + "_ms"] + rows[k][dg + "_ms"]) for k, n in PER_LAYER.items())
+        ms += rows["lm_head"][fwd + "_ms"] + rows["lm_head"][dg + "_ms"]
+        cost[store] = round(ms, 1)
+    print(json.dumps({"recompute_step_gemm_ms": cost, "note": "decoder linears: 2 forwards (forward + "
+                      "per-layer recompute) + 1 data gradient; LM head: 1 + 1; weight gradients excluded"}), flush=True)
 
 
 if __name__ == "__main__":
