@@ -5,8 +5,10 @@
  * Auxiliary to the SMT hot path (smt_hip.h): it replaces the attention of the HF transformers LLaMA
  * decoder that carries the SMT modules (the reference trains that model through
  * AutoModelForCausalLM, deepspeed/fine_tune.py:150-155; transformers' sdpa attention dispatches to
- * aotriton on this torch build). Causal, grouped-query (Hq = G * Hkv), head_dim 128, bf16 in / out,
- * fp32 softmax statistics.
+ * aotriton on this torch build). Causal, grouped-query (Hq = G * Hkv), head_dim 128, 16-bit in / out
+ * (shape->dtype: SMT_DTYPE_BF16 or, since ABI v13, SMT_DTYPE_FP16 -- the reference's --dtype,
+ * fine_tune.py:955-959), fp32 softmax statistics; P and dS are rounded to that format for their
+ * products.
  *
  * Tensors are addressed by element strides (d-stride 1, rows 16-byte aligned):
  *   q, o, dq, do   element (b, h, s, d) at base + b*sb + h*sh + s*ss + d,  h < Hq
@@ -35,7 +37,7 @@ typedef struct smt_attn_tensor {
 typedef struct smt_attn_shape {
     int32_t B, Hq, Hkv, S;
     float scale;                    /* softmax scale, usually 1/sqrt(128) */
-    int32_t pad_;
+    int32_t dtype;                  /* ABI v13 (was padding, 0): SMT_DTYPE_BF16 (0) or SMT_DTYPE_FP16 (2) */
 } smt_attn_shape;
 
 const char* smt_attn_last_error(void);

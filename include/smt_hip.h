@@ -134,6 +134,9 @@ typedef struct smt_adamw_tensor {
 } smt_adamw_tensor;                 /* all five buffers 16-byte aligned          */
 
 const char* smt_last_error(void);
+/* 13: the fused LLaMA ops (smt_model_ops.h) and the flash attention (smt_attention.h) take the
+ *     model's 16-bit dtype, bf16 or fp16 (the reference's --dtype fp16, fine_tune.py:955-959);
+ * 12: smt_adamw_args.param_dtype; 11: smt_wgrad_module.operand_dtype. */
 int smt_abi_version(void);
 
 /* Workspace bytes smt_tile_wgrad needs for T rows and n_tiles tiles. */

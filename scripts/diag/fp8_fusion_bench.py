@@ -32,11 +32,11 @@ def main():
     st = torch.cuda.current_stream().cuda_stream
 
     def fwd_unfused():
-        lib.smt_swiglu_fwd(g.data_ptr(), u.data_ptr(), h.data_ptr(), g.numel(), st)
+        lib.smt_swiglu_fwd(g.data_ptr(), u.data_ptr(), h.data_ptr(), g.numel(), 0, st)
         f8.quant_rows(h)
 
     def bwd_unfused():
-        lib.smt_swiglu_bwd(g.data_ptr(), u.data_ptr(), dh.data_ptr(), dg.data_ptr(), du.data_ptr(), g.numel(), st)
+        lib.smt_swiglu_bwd(g.data_ptr(), u.data_ptr(), dh.data_ptr(), dg.data_ptr(), du.data_ptr(), g.numel(), 0, st)
         f8.quant_rows_cat([dg, du])
 
     fns = {"fwd_unfused": fwd_unfused,

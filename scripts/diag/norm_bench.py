@@ -43,11 +43,11 @@ def main():
     P = _hip._ptr
 
     def bwd():
-        rc = lib.smt_rmsnorm_bwd_add(P(dy), H, P(x), H, P(w), P(rstd), P(dres), H, P(dx), H, T, H, st)
+        rc = lib.smt_rmsnorm_bwd_add(P(dy), H, P(x), H, P(w), P(rstd), P(dres), H, P(dx), H, T, H, 0, st)
         assert rc == 0
 
     def fwd():
-        rc = lib.smt_add_rmsnorm_fwd(P(x), H, P(dres), H, P(w), P(h), H, P(y), H, P(rs), T, H, 1e-5, st)
+        rc = lib.smt_add_rmsnorm_fwd(P(x), H, P(dres), H, P(w), P(h), H, P(y), H, P(rs), T, H, 1e-5, 0, st)
         assert rc == 0
 
     from sparse_matrix_tuning_amd import fused_llama as fl

@@ -1,8 +1,9 @@
 """The SMT step of LLaMA-3-8B in the reference's other --dtype (fine_tune.py:955-959): fp16 under
 DeepSpeed's dynamic loss scale or fp32, through SMTEngine with DeepSpeed's config for the dtype
-(deepspeed_helpers.py:53-61), every layer recomputed (fine_tune.py:192). The fused LLaMA kernels are
-bf16-only, so the model runs transformers' own ops; the SMT modules, the tile weight gradients, the
-fused AdamW and the loss scale are this build's. 436 + 436 tiles drawn at random (seeded) over the
+(deepspeed_helpers.py:53-61), every layer recomputed (fine_tune.py:192). bf16 and fp16 models run the
+fused LLaMA kernels, smt_flash and the fused LM head + loss (ABI v13: one template body per 16-bit
+format; ``--eager-ops`` keeps transformers' own ops), fp32 models transformers' ops; the SMT modules,
+the tile weight gradients, the fused AdamW and the loss scale are this build's. 436 + 436 tiles drawn at random (seeded) over the
 attention (q/k/v) and MLP candidate blocks of every layer, as SMT(0.71 %) selects them.
 
     python scripts/dtype_step_bench.py --dtype fp16 --steps 10
@@ -46,11 +47,16 @@ def main():
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--seq", type=int, default=2048)
     ap.add_argument("--tiles", type=int, default=436, help="per pool (attention, MLP)")
+    ap.add_argument("--eager-ops", action="store_true", help="transformers' own ops even for bf16 / fp16")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     dtype = DTYPES[args.dtype]
     model = bench.build_model("llama3-8b", dev).to(dtype)
+    fused = dtype != torch.float32 and not args.eager_ops
+    if fused:
+        from sparse_matrix_tuning_amd.fused_llama import patch_llama
+        patch_llama(model)
     dims = trainer.get_targeted_module_dims(model)
     L = bench.MODELS["llama3-8b"]["num_hidden_layers"]
     sel_att = random_selection(dims, L, args.tiles, ("q_proj", "k_proj", "v_proj"), 1)
@@ -96,7 +102,9 @@ def main():
            "median_ms_per_step": round(med * 1e3, 2), "median_tokens_per_s": round(tok / med, 1),
            "peak_hbm_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 2), "dtype": args.dtype,
            "tiles": n_tiles, "tile_param_dtype": str(engine.tile_groups[0].param.dtype),
-           "activations": "recomputed per layer (fine_tune.py:192); transformers' own ops",
+           "activations": "recomputed per layer (fine_tune.py:192)",
+           "ops": "fused LLaMA kernels + smt_flash + fused LM head/loss" if fused else "transformers' own ops",
+           "transposed_copies_gb": round(engine.transposed_bytes / 1e9, 2),
            "skipped_steps": engine.skipped_steps,
            "loss_scale": engine.loss_scaler.state_dict() if engine.loss_scaler is not None else None,
            "losses": [round(float(x), 4) for x in losses]}

@@ -24,7 +24,8 @@ SCORE_MEAN_ABS, SCORE_ABS_MEAN, SCORE_L1, SCORE_L2 = 0, 1, 2, 3
 ADAM_DEEPSPEED, ADAM_TORCH = 0, 1
 
 _DT = {torch.bfloat16: DTYPE_BF16, torch.float32: DTYPE_FP32, torch.float16: DTYPE_FP16}
-ABI_VERSION = 12            # include/smt_hip.h: smt_adamw_args.param_dtype (v12), smt_wgrad_module.operand_dtype (v11)
+ABI_VERSION = 13            # include/smt_hip.h: 16-bit dtype of the model ops / attention (v13),
+                            # smt_adamw_args.param_dtype (v12), smt_wgrad_module.operand_dtype (v11)
 
 # Every function the headers declare (include/smt_hip.h, smt_model_ops.h, smt_attention.h); tests check the
 # library exports each of them.
@@ -112,7 +113,7 @@ class AttnTensor(ctypes.Structure):
 
 class AttnShape(ctypes.Structure):
     _fields_ = [("B", ctypes.c_int32), ("Hq", ctypes.c_int32), ("Hkv", ctypes.c_int32), ("S", ctypes.c_int32),
-                ("scale", ctypes.c_float), ("pad_", ctypes.c_int32)]
+                ("scale", ctypes.c_float), ("dtype", ctypes.c_int32)]       # ABI v13: SMT_DTYPE_BF16 / _FP16
 
 
 ACC_CHUNK = 4096
@@ -159,19 +160,22 @@ _SIGS = {
     "smt_attn_bwd_kmask": (ctypes.c_int, [ctypes.POINTER(AttnTensor)] * 5 + [_P, _P] + [ctypes.POINTER(AttnTensor)] * 3
                            + [_P, _I64, ctypes.POINTER(AttnShape), _P]),
     "smt_model_ops_last_error": (ctypes.c_char_p, []),
-    "smt_rmsnorm_fwd": (ctypes.c_int, [_P, _I64, _P, _P, _I64, _P, _I64, _I32, ctypes.c_float, _P]),
+    "smt_rmsnorm_fwd": (ctypes.c_int, [_P, _I64, _P, _P, _I64, _P, _I64, _I32, ctypes.c_float, _I32, _P]),
     "smt_rmsnorm_bwd_waves": (ctypes.c_int, [_I64]),
-    "smt_add_rmsnorm_fwd": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _P, _I64, _P, _I64, _P, _I64, _I32, ctypes.c_float, _P]),
-    "smt_rmsnorm_bwd_add": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _P, _P, _I64, _P, _I64, _I64, _I32, _P]),
-    "smt_rmsnorm_bwd": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _P, _P, _I64, _P, _P, _I64, _I32, _P]),
-    "smt_rmsnorm_bwd_add_dw": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _P, _P, _I64, _P, _I64, _P, _P, _I64, _I32, _P]),
-    "smt_rope_fwd": (ctypes.c_int, [ctypes.POINTER(RopeTensor), ctypes.POINTER(RopeTensor), _P, _P, _I64, _I64, _I64, _I32, _I32, _P]),
-    "smt_rope_bwd": (ctypes.c_int, [ctypes.POINTER(RopeTensor), ctypes.POINTER(RopeTensor), _P, _P, _I64, _I64, _I64, _I32, _I32, _P]),
-    "smt_swiglu_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _P]),
-    "smt_colblock_recompute": (ctypes.c_int, [_I32, _P, _I64, _P, _I64, _P, _P, _I64, _P, _I32, _P, _P]),
-    "smt_swiglu_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I64, _P]),
-    "smt_ce_fwd": (ctypes.c_int, [_P, _I64, _P, _I64, _I64, _I64, _P, _P, _P]),
-    "smt_ce_bwd": (ctypes.c_int, [_P, _I64, _P, _P, _P, _I64, _I64, _I64, _P, _I64, _P]),
+    "smt_add_rmsnorm_fwd": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _P, _I64, _P, _I64, _P, _I64, _I32, ctypes.c_float,
+                                           _I32, _P]),
+    "smt_rmsnorm_bwd_add": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _P, _P, _I64, _P, _I64, _I64, _I32, _I32, _P]),
+    "smt_rmsnorm_bwd": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _P, _P, _I64, _P, _P, _I64, _I32, _I32, _P]),
+    "smt_rmsnorm_bwd_add_dw": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _P, _P, _I64, _P, _I64, _P, _P, _I64, _I32, _I32, _P]),
+    "smt_rope_fwd": (ctypes.c_int, [ctypes.POINTER(RopeTensor), ctypes.POINTER(RopeTensor), _P, _P, _I64, _I64, _I64, _I32,
+                                    _I32, _I32, _P]),
+    "smt_rope_bwd": (ctypes.c_int, [ctypes.POINTER(RopeTensor), ctypes.POINTER(RopeTensor), _P, _P, _I64, _I64, _I64, _I32,
+                                    _I32, _I32, _P]),
+    "smt_swiglu_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _I32, _P]),
+    "smt_colblock_recompute": (ctypes.c_int, [_I32, _P, _I64, _P, _I64, _P, _P, _I64, _P, _I32, _P, _I32, _P]),
+    "smt_swiglu_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I64, _I32, _P]),
+    "smt_ce_fwd": (ctypes.c_int, [_P, _I64, _P, _I64, _I64, _I64, _P, _P, _I32, _P]),
+    "smt_ce_bwd": (ctypes.c_int, [_P, _I64, _P, _P, _P, _I64, _I64, _I64, _P, _I64, _I32, _P]),
     "smt_fp8_last_error": (ctypes.c_char_p, []),
     "smt_quant_rows_e4m3": (ctypes.c_int, [_P, _I64, _I64, _I32, _P, _I32, _P, _I64, _P, _P]),
     "smt_quant_cols_t_e4m3": (ctypes.c_int, [_P, _I64, _I32, _I32, _P, _I32, _P, _I64, _P, _P]),
@@ -185,6 +189,15 @@ _SIGS = {
     "smt_swiglu_bwd_quant_e4m3_packed": (ctypes.c_int, [_P, _P, _P, _I64, _I32, _P, _I64, _P, _P, _P, _I64, _P, _P,
                                                          _I64, _P]),
 }
+
+
+def dtype_code16(dtype: torch.dtype, what: str) -> int:
+    """SMT_DTYPE_* of a 16-bit model dtype (the model ops and the attention, ABI v13)."""
+    if dtype == torch.bfloat16:
+        return DTYPE_BF16
+    if dtype == torch.float16:
+        return DTYPE_FP16
+    raise RuntimeError(f"{what}: bf16 or fp16 tensors only (got {dtype})")
 
 
 def lib_path() -> str:
@@ -449,8 +462,10 @@ def colblock_recompute(op: int, a2d: torch.Tensor, col_blocks: torch.Tensor, b2d
     rebuilt from those operands (bit-identical to gathering the producer's output)."""
     dev = _require_device(a2d, col_blocks, b2d, weight, rstd)
     for t in (a2d, b2d):
-        if t is not None and (t.dim() != 2 or t.stride(1) != 1 or t.dtype != torch.bfloat16):
-            raise ValueError("colblock_recompute: operands must be 2-D row-major bf16")
+        if t is not None and (t.dim() != 2 or t.stride(1) != 1 or t.dtype not in (torch.bfloat16, torch.float16)):
+            raise ValueError("colblock_recompute: operands must be 2-D row-major bf16 / fp16")
+    if b2d is not None and b2d.dtype != a2d.dtype or weight is not None and weight.dtype != a2d.dtype:
+        raise ValueError("colblock_recompute: operands of one dtype")
     if b2d is not None and b2d.shape != a2d.shape:
         raise ValueError("colblock_recompute: gate and up shapes differ")
     if rstd is not None and (rstd.dtype != torch.float32 or rstd.numel() != a2d.shape[0] or not rstd.is_contiguous()):
@@ -463,7 +478,7 @@ def colblock_recompute(op: int, a2d: torch.Tensor, col_blocks: torch.Tensor, b2d
                                        b2d.stride(0) if b2d is not None else 0,
                                        _ptr(weight) if weight is not None else None,
                                        _ptr(rstd) if rstd is not None else None, a2d.shape[0], _ptr(col_blocks), n_cb,
-                                       _ptr(out), _stream(dev))
+                                       _ptr(out), dtype_code16(a2d.dtype, "colblock_recompute"), _stream(dev))
     _check(rc, "smt_colblock_recompute")
     return out
 
@@ -713,10 +728,11 @@ def adamw_multi(tensors, args: AdamWArgs, grad_sq_norm: Optional[torch.Tensor] =
 
 
 def tile_scatter_t(descs: torch.Tensor, n_tiles: int, tiles: torch.Tensor) -> None:
-    """Transposed write-back of bf16 tiles into the W^T copies the descriptors point at."""
+    """Transposed write-back of 16-bit (bf16 / fp16) tiles into the W^T copies the descriptors point at
+    (the kernel moves 16-bit values: one instance for both formats)."""
     dev = _require_device(descs, tiles)
-    if tiles.dtype != torch.bfloat16 or not tiles.is_contiguous():
-        raise ValueError("tile_scatter_t: tiles must be contiguous bf16")
+    if tiles.dtype not in (torch.bfloat16, torch.float16) or not tiles.is_contiguous():
+        raise ValueError("tile_scatter_t: tiles must be contiguous bf16 / fp16")
     rc = load().smt_tile_scatter_t(_ptr(descs), int(n_tiles), _ptr(tiles), _stream(dev))
     _check(rc, "smt_tile_scatter_t")
 

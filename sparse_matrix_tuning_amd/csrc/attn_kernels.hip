@@ -1,4 +1,5 @@
-// Causal grouped-query flash attention for gfx950 (CDNA4), head_dim 128, bf16 I/O, fp32 softmax.
+// Causal grouped-query flash attention for gfx950 (CDNA4), head_dim 128, bf16 or fp16 I/O (the model's
+// dtype, smt_attn_shape.dtype; ABI v13), fp32 softmax.
 // C ABI: include/smt_attention.h. Replaces transformers' sdpa attention (aotriton on this torch
 // build) in the LLaMA decoder that carries the SMT modules.
 //
@@ -24,6 +25,7 @@
 #include <utility>
 
 #include "smt_attention.h"
+#include "smt_hip.h"
 
 namespace {
 
@@ -45,6 +47,8 @@ int check_launch(const char* what) {
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
 typedef short s16x8_t __attribute__((ext_vector_type(8)));
@@ -86,8 +90,15 @@ __device__ __forceinline__ bf16x8_t tr_frag(const uint8_t* img, TrLane tl, uint3
     return __builtin_bit_cast(bf16x8_t, both);
 }
 
+// Fragments travel as bf16x8_t bit containers whatever the format; F = SMT_DTYPE_BF16 (0) or
+// SMT_DTYPE_FP16 (2) picks the MFMA (v_mfma_f32_32x32x16_bf16 / _f16, the same lane maps) and the
+// roundings of P, dS and the outputs.
+template <int F>
 __device__ __forceinline__ f32x16_t mfma(bf16x8_t a, bf16x8_t b, f32x16_t c) {
-    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+    if constexpr (F == SMT_DTYPE_FP16)
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c,
+                                                      0, 0, 0);
+    else return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
 // Two-lane fp32 arithmetic of the softmax. PK: packed (v_pk_fma_f32 / v_pk_add_f32 / v_pk_mul_f32,
@@ -112,9 +123,21 @@ __device__ __forceinline__ f32x2_t add2(f32x2_t a, f32x2_t b) {
     return f32x2_t{a.x + b.x, a.y + b.y};
 }
 
-__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+template <int F>
+__device__ __forceinline__ uint32_t pk16(float a, float b) {        // two fp32 -> two 16-bit values (RNE)
     f32x2_t v = {a, b};
-    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
+    if constexpr (F == SMT_DTYPE_FP16) return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2_t));
+    else return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
+}
+template <int F>
+__device__ __forceinline__ float lo16(uint32_t w) {                  // the low / high 16-bit value of a word
+    if constexpr (F == SMT_DTYPE_FP16) return (float)__builtin_bit_cast(_Float16, (uint16_t)(w & 0xffffu));
+    else return __uint_as_float(w << 16);
+}
+template <int F>
+__device__ __forceinline__ float hi16(uint32_t w) {
+    if constexpr (F == SMT_DTYPE_FP16) return (float)__builtin_bit_cast(_Float16, (uint16_t)(w >> 16));
+    else return __uint_as_float(w & 0xffff0000u);
 }
 
 __device__ __forceinline__ float other_half_max(float x) {
@@ -128,10 +151,11 @@ __device__ __forceinline__ float halves_sum(float x) {
 
 // C-layout probabilities of one 32-column tile (16 fp32 per lane: column = lane's n, rows
 // (i&3)+8(i>>2)+4hi) -> two B fragments for k-steps of 16 rows, rows 8hi..8hi+7 per lane.
+template <int F>
 __device__ __forceinline__ void pack_b_frags(const float (&p)[16], bf16x8_t& f0, bf16x8_t& f1) {
     uint32_t w[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) w[i] = pk_bf16(p[2 * i], p[2 * i + 1]);
+    for (int i = 0; i < 8; ++i) w[i] = pk16<F>(p[2 * i], p[2 * i + 1]);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         auto a = __builtin_amdgcn_permlane32_swap(w[4 * h + 0], w[4 * h + 2], false, false);
@@ -297,7 +321,7 @@ __device__ __forceinline__ float max3f(float a, float b, float c) {
 // one wave per SIMD over 64 rows (two builds), all slower.
 // ------------------------------------------------------------------------------------------------
 
-template <bool KMASK>
+template <bool KMASK, int F>
 struct FwdLean {
     const FwdArgs& a;
     uint8_t* lds;
@@ -339,7 +363,7 @@ struct FwdLean {
             }
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int j = 0; j < 2; ++j) sc[j] = mfma(kf[ks % 3][j], qf[ks], ks ? sc[j] : f32x16_t{});
+            for (int j = 0; j < 2; ++j) sc[j] = mfma<F>(kf[ks % 3][j], qf[ks], ks ? sc[j] : f32x16_t{});
             __builtin_amdgcn_sched_barrier(0);
         }
         // the first two V fragments of the PV product, in flight during the softmax
@@ -404,14 +428,14 @@ struct FwdLean {
                 for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
         }
         bf16x8_t pf[4];
-        pack_b_frags(*reinterpret_cast<const float(*)[16]>(&x[0]), pf[0], pf[1]);
-        pack_b_frags(*reinterpret_cast<const float(*)[16]>(&x[16]), pf[2], pf[3]);
+        pack_b_frags<F>(*reinterpret_cast<const float(*)[16]>(&x[0]), pf[0], pf[1]);
+        pack_b_frags<F>(*reinterpret_cast<const float(*)[16]>(&x[16]), pf[2], pf[3]);
         // V^T fragments two MFMAs ahead (n = 4 dt + kst)
 #pragma unroll
         for (int n = 0; n < 16; ++n) {
             if (n + 2 < 16) vf[(n + 2) % 3] = tr_frag(V, tl, 16 * ((n + 2) & 3), 32 * ((n + 2) >> 2));
             __builtin_amdgcn_sched_barrier(0);
-            o[n >> 2] = mfma(vf[n % 3], pf[n & 3], o[n >> 2]);
+            o[n >> 2] = mfma<F>(vf[n % 3], pf[n & 3], o[n >> 2]);
             __builtin_amdgcn_sched_barrier(0);
         }
     }
@@ -474,8 +498,8 @@ struct FwdLean {
                 for (int g = 0; g < 4; ++g) {
                     const int d = 32 * dt + 8 * g + 4 * hi;
                     uint2 w;
-                    w.x = pk_bf16(o[dt][4 * g] * inv, o[dt][4 * g + 1] * inv);
-                    w.y = pk_bf16(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
+                    w.x = pk16<F>(o[dt][4 * g] * inv, o[dt][4 * g + 1] * inv);
+                    w.y = pk16<F>(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
                     *reinterpret_cast<uint2*>(op + d) = w;
                 }
             if (hi == 0)
@@ -485,7 +509,7 @@ struct FwdLean {
     }
 };
 
-template <bool KMASK>
+template <bool KMASK, int F>
 __global__ __launch_bounds__(64 * kFwdWaves, 2)
 void attn_fwd_kernel(FwdArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * 2 * kTileB];      // K/V ring: 2 x 32 KiB
@@ -499,7 +523,7 @@ void attn_fwd_kernel(FwdArgs a) {
     const int grp = L / per_group;
     const int rem = L - grp * per_group;
     const int hk = grp % a.Hkv;
-    FwdLean<KMASK> fl(a, lds);
+    FwdLean<KMASK, F> fl(a, lds);
     fl.run(grp / a.Hkv, hk * G + rem % G, hk, nqb - 1 - rem / G);
 }
 
@@ -529,7 +553,7 @@ struct DqArgs {
 // fp32, the causal test only on the wave's diagonal tile, scheduling fences that bound the fragment
 // reads hoisted ahead. Measured and removed (git history): one wave per SIMD with AGPR
 // accumulators, and dQ as a GEMM over a materialised dS, both slower.
-template <bool KMASK>
+template <bool KMASK, int F>
 struct DqLean {
     const DqArgs& a;
     uint8_t* lds;
@@ -557,16 +581,16 @@ struct DqLean {
         const uint32_t lr = opaque(lo_row);
         constexpr int KH = KI + 32 * kRowB, VH = VI + 32 * kRowB;     // keys 32..63 of the tile
         f32x16_t s[2], dp[2];
-        s[0] = mfma(rowx<KI>(lds, lr, 0), qf[0], f32x16_t{});
-        s[1] = mfma(rowx<KH>(lds, lr, 0), qf[0], f32x16_t{});
-        dp[0] = mfma(rowx<VI>(lds, lr, 0), df[0], f32x16_t{});
-        dp[1] = mfma(rowx<VH>(lds, lr, 0), df[0], f32x16_t{});
+        s[0] = mfma<F>(rowx<KI>(lds, lr, 0), qf[0], f32x16_t{});
+        s[1] = mfma<F>(rowx<KH>(lds, lr, 0), qf[0], f32x16_t{});
+        dp[0] = mfma<F>(rowx<VI>(lds, lr, 0), df[0], f32x16_t{});
+        dp[1] = mfma<F>(rowx<VH>(lds, lr, 0), df[0], f32x16_t{});
 #pragma unroll
         for (int ks = 1; ks < 8; ++ks) {
-            s[0] = mfma(rowx<KI>(lds, lr, ks), qf[ks], s[0]);
-            s[1] = mfma(rowx<KH>(lds, lr, ks), qf[ks], s[1]);
-            dp[0] = mfma(rowx<VI>(lds, lr, ks), df[ks], dp[0]);
-            dp[1] = mfma(rowx<VH>(lds, lr, ks), df[ks], dp[1]);
+            s[0] = mfma<F>(rowx<KI>(lds, lr, ks), qf[ks], s[0]);
+            s[1] = mfma<F>(rowx<KH>(lds, lr, ks), qf[ks], s[1]);
+            dp[0] = mfma<F>(rowx<VI>(lds, lr, ks), df[ks], dp[0]);
+            dp[1] = mfma<F>(rowx<VH>(lds, lr, ks), df[ks], dp[1]);
             if (ks & 1) __builtin_amdgcn_sched_barrier(0);
         }
         float pr[32];
@@ -603,13 +627,13 @@ struct DqLean {
             pr[i + 1] = r.y;
         }
         bf16x8_t sf[4];
-        pack_b_frags(*reinterpret_cast<const float(*)[16]>(&pr[0]), sf[0], sf[1]);
-        pack_b_frags(*reinterpret_cast<const float(*)[16]>(&pr[16]), sf[2], sf[3]);
+        pack_b_frags<F>(*reinterpret_cast<const float(*)[16]>(&pr[0]), sf[0], sf[1]);
+        pack_b_frags<F>(*reinterpret_cast<const float(*)[16]>(&pr[16]), sf[2], sf[3]);
         const uint32_t t0 = opaque(lo_t0), t4 = opaque(lo_t4);
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) {
 #pragma unroll
-            for (int kst = 0; kst < 4; ++kst) dq[dt] = mfma(trx<KI>(lds, t0, t4, kst, dt), sf[kst], dq[dt]);
+            for (int kst = 0; kst < 4; ++kst) dq[dt] = mfma<F>(trx<KI>(lds, t0, t4, kst, dt), sf[kst], dq[dt]);
             __builtin_amdgcn_sched_barrier(0);
         }
     }
@@ -659,8 +683,8 @@ struct DqLean {
                 const u32x4_t dv = __builtin_bit_cast(u32x4_t, df[ks]);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    part += __uint_as_float(ov[j] << 16) * __uint_as_float(dv[j] << 16);
-                    part += __uint_as_float(ov[j] & 0xffff0000u) * __uint_as_float(dv[j] & 0xffff0000u);
+                    part += lo16<F>(ov[j]) * lo16<F>(dv[j]);
+                    part += hi16<F>(ov[j]) * hi16<F>(dv[j]);
                 }
             }
             dlt = halves_sum(part);
@@ -699,15 +723,15 @@ struct DqLean {
                 for (int g = 0; g < 4; ++g) {
                     const int d = 32 * dt + 8 * g + 4 * hi;
                     uint2 w;
-                    w.x = pk_bf16(dq[dt][4 * g] * a.scale, dq[dt][4 * g + 1] * a.scale);
-                    w.y = pk_bf16(dq[dt][4 * g + 2] * a.scale, dq[dt][4 * g + 3] * a.scale);
+                    w.x = pk16<F>(dq[dt][4 * g] * a.scale, dq[dt][4 * g + 1] * a.scale);
+                    w.y = pk16<F>(dq[dt][4 * g + 2] * a.scale, dq[dt][4 * g + 3] * a.scale);
                     *reinterpret_cast<uint2*>(out + d) = w;
                 }
         }
     }
 };
 
-template <bool KMASK>
+template <bool KMASK, int F>
 __global__ __launch_bounds__(64 * kDqWaves, 8 / kDqWaves)
 void attn_dq_kernel(DqArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * 2 * kTileB];      // 64 KiB
@@ -721,7 +745,7 @@ void attn_dq_kernel(DqArgs a) {
     const int grp = L / per_group;
     const int rem = L - grp * per_group;
     const int hk = grp % a.Hkv;
-    DqLean<KMASK> dl(a, lds);
+    DqLean<KMASK, F> dl(a, lds);
     dl.run(grp / a.Hkv, hk * G + rem % G, hk, nqb - 1 - rem / G);
 }
 
@@ -771,7 +795,7 @@ struct DkvArgs {
 // measured 2.17, 2.21, 2.21 ms for the whole backward: profiles/r03_attn_bwd_variants.jsonl)
 constexpr int kDkvLeanRing = 2;
 static_assert(kDkvLeanRing >= 2 && kDkvLeanRing * kSliceBuf + kVImg <= 160 * 1024, "dK/dV lean ring");
-template <bool KMASK>
+template <bool KMASK, int F>
 struct DkvLean {
     const DkvArgs& a;
     uint8_t* lds;
@@ -822,12 +846,12 @@ struct DkvLean {
         // ring slot SLOT at [SLOT * kSliceBuf, ...): Q rows, dO rows, lse[32], delta[32]; V image after the ring
         constexpr int QI = SLOT * kSliceBuf, DI = QI + kSliceB;
         const uint32_t lr = opaque(lo_row), lv = opaque(lo_v);
-        s = mfma(rowx<QI>(lds, lr, 0), kf[0], f32x16_t{});
-        dp = mfma(rowx<DI>(lds, lr, 0), rowx<0>(lds, lv, 0), f32x16_t{});
+        s = mfma<F>(rowx<QI>(lds, lr, 0), kf[0], f32x16_t{});
+        dp = mfma<F>(rowx<DI>(lds, lr, 0), rowx<0>(lds, lv, 0), f32x16_t{});
 #pragma unroll
         for (int ks = 1; ks < 8; ++ks) {
-            s = mfma(rowx<QI>(lds, lr, ks), kf[ks], s);
-            dp = mfma(rowx<DI>(lds, lr, ks), rowx<0>(lds, lv, ks), dp);
+            s = mfma<F>(rowx<QI>(lds, lr, ks), kf[ks], s);
+            dp = mfma<F>(rowx<DI>(lds, lr, ks), rowx<0>(lds, lv, ks), dp);
             if (ks & 1) __builtin_amdgcn_sched_barrier(0);    // bound the reads hoisted ahead (VGPRs)
         }
     }
@@ -876,15 +900,15 @@ struct DkvLean {
             }
         }
         bf16x8_t pf[2], sf[2];
-        pack_b_frags(pr, pf[0], pf[1]);
-        pack_b_frags(dsv, sf[0], sf[1]);
+        pack_b_frags<F>(pr, pf[0], pf[1]);
+        pack_b_frags<F>(dsv, sf[0], sf[1]);
         const uint32_t t0 = opaque(lo_t0), t4 = opaque(lo_t4);
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
             for (int kq = 0; kq < 2; ++kq) {
-                dvt[dt] = mfma(trx<DI>(lds, t0, t4, kq, dt), pf[kq], dvt[dt]);
-                dkt[dt] = mfma(trx<QI>(lds, t0, t4, kq, dt), sf[kq], dkt[dt]);
+                dvt[dt] = mfma<F>(trx<DI>(lds, t0, t4, kq, dt), pf[kq], dvt[dt]);
+                dkt[dt] = mfma<F>(trx<QI>(lds, t0, t4, kq, dt), sf[kq], dkt[dt]);
                 if (kq) __builtin_amdgcn_sched_barrier(0);
             }
     }
@@ -970,18 +994,18 @@ struct DkvLean {
                 for (int g = 0; g < 4; ++g) {
                     const int d = 32 * dt + 8 * g + 4 * hi;
                     uint2 w;
-                    w.x = pk_bf16(dkt[dt][4 * g] * a.scale, dkt[dt][4 * g + 1] * a.scale);
-                    w.y = pk_bf16(dkt[dt][4 * g + 2] * a.scale, dkt[dt][4 * g + 3] * a.scale);
+                    w.x = pk16<F>(dkt[dt][4 * g] * a.scale, dkt[dt][4 * g + 1] * a.scale);
+                    w.y = pk16<F>(dkt[dt][4 * g + 2] * a.scale, dkt[dt][4 * g + 3] * a.scale);
                     *reinterpret_cast<uint2*>(dkr + d) = w;
-                    w.x = pk_bf16(dvt[dt][4 * g], dvt[dt][4 * g + 1]);
-                    w.y = pk_bf16(dvt[dt][4 * g + 2], dvt[dt][4 * g + 3]);
+                    w.x = pk16<F>(dvt[dt][4 * g], dvt[dt][4 * g + 1]);
+                    w.y = pk16<F>(dvt[dt][4 * g + 2], dvt[dt][4 * g + 3]);
                     *reinterpret_cast<uint2*>(dvr + d) = w;
                 }
         }
     }
 };
 
-template <bool KMASK>
+template <bool KMASK, int F>
 __global__ __launch_bounds__(kDkvWaves * 64, 2)
 void attn_dkdv_kernel(DkvArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kVImg + kDkvLeanRing * kSliceBuf];
@@ -993,7 +1017,7 @@ void attn_dkdv_kernel(DkvArgs a) {
 #pragma nounroll
     for (int i = 0; i < t.n; ++i) {
         if (i) __syncthreads();
-        DkvLean<KMASK> dl(a, lds);
+        DkvLean<KMASK, F> dl(a, lds);
         dl.run(t.b, t.hk, t.blk[1 - i]);
     }
 }
@@ -1012,8 +1036,22 @@ int check_shape(const smt_attn_shape* s, const char* fn) {
     if (s->B <= 0 || s->Hq <= 0 || s->Hkv <= 0 || s->S <= 0 || s->Hq % s->Hkv)
         return fail(-1, "%s: bad shape B=%d Hq=%d Hkv=%d S=%d", fn, s->B, s->Hq, s->Hkv, s->S);
     if (!(s->scale > 0.f)) return fail(-1, "%s: scale must be > 0", fn);
+    if (s->dtype != SMT_DTYPE_BF16 && s->dtype != SMT_DTYPE_FP16)
+        return fail(-1, "%s: dtype %d is not a 16-bit format (SMT_DTYPE_BF16 / SMT_DTYPE_FP16)", fn, (int)s->dtype);
     return 0;
 }
+
+// the (key mask, format) instance of a kernel template
+#define SMT_ATTN_LAUNCH(kernel, kmask, dtype, grid, block, stream, args)                                         \
+    do {                                                                                                      \
+        if ((dtype) == SMT_DTYPE_FP16) {                                                                      \
+            if (kmask) hipLaunchKernelGGL((kernel<true, SMT_DTYPE_FP16>), grid, block, 0, stream, args);     \
+            else hipLaunchKernelGGL((kernel<false, SMT_DTYPE_FP16>), grid, block, 0, stream, args);          \
+        } else {                                                                                              \
+            if (kmask) hipLaunchKernelGGL((kernel<true, SMT_DTYPE_BF16>), grid, block, 0, stream, args);     \
+            else hipLaunchKernelGGL((kernel<false, SMT_DTYPE_BF16>), grid, block, 0, stream, args);          \
+        }                                                                                                     \
+    } while (0)
 
 Tns tns(const smt_attn_tensor* t) { return Tns{static_cast<const uint16_t*>(t->ptr), t->sb, t->sh, t->ss}; }
 
@@ -1045,8 +1083,7 @@ int smt_attn_fwd_kmask(const smt_attn_tensor* q, const smt_attn_tensor* k, const
     const int64_t nqb = (shape->S + kFwdQB - 1) / kFwdQB;
     const int64_t blocks = nqb * shape->Hq * shape->B;
     if (blocks > 0x7fffffffLL) return fail(-1, "%s: too many blocks", fn);
-    if (key_mask) hipLaunchKernelGGL(attn_fwd_kernel<true>, dim3((unsigned)blocks), dim3(64 * kFwdWaves), 0, stream, a);
-    else hipLaunchKernelGGL(attn_fwd_kernel<false>, dim3((unsigned)blocks), dim3(64 * kFwdWaves), 0, stream, a);
+    SMT_ATTN_LAUNCH(attn_fwd_kernel, key_mask, shape->dtype, dim3((unsigned)blocks), dim3(64 * kFwdWaves), stream, a);
     return check_launch("attn_fwd_kernel");
 }
 
@@ -1081,8 +1118,7 @@ int smt_attn_bwd_kmask(const smt_attn_tensor* q, const smt_attn_tensor* k, const
     qa.B = B; qa.Hq = Hq; qa.Hkv = Hkv; qa.S = S; qa.sl2 = sl2; qa.scale = shape->scale;
     const int64_t nqb = (S + kDqQB - 1) / kDqQB;
     const dim3 qgrid((unsigned)(nqb * Hq * B)), qblock(64 * kDqWaves);
-    if (key_mask) hipLaunchKernelGGL(attn_dq_kernel<true>, qgrid, qblock, 0, stream, qa);
-    else hipLaunchKernelGGL(attn_dq_kernel<false>, qgrid, qblock, 0, stream, qa);
+    SMT_ATTN_LAUNCH(attn_dq_kernel, key_mask, shape->dtype, qgrid, qblock, stream, qa);
     if ((rc = check_launch("attn_dq_kernel"))) return rc;
 
     DkvArgs ka;
@@ -1094,8 +1130,7 @@ int smt_attn_bwd_kmask(const smt_attn_tensor* q, const smt_attn_tensor* k, const
     ka.B = B; ka.Hq = Hq; ka.Hkv = Hkv; ka.S = S; ka.sl2 = sl2; ka.scale = shape->scale;
     const int64_t nkb = (S + kKB - 1) / kKB;
     const dim3 grid((unsigned)(((nkb + 1) / 2) * Hkv * B));
-    if (key_mask) hipLaunchKernelGGL(attn_dkdv_kernel<true>, grid, dim3(kDkvWaves * 64), 0, stream, ka);
-    else hipLaunchKernelGGL(attn_dkdv_kernel<false>, grid, dim3(kDkvWaves * 64), 0, stream, ka);
+    SMT_ATTN_LAUNCH(attn_dkdv_kernel, key_mask, shape->dtype, grid, dim3(kDkvWaves * 64), stream, ka);
     return check_launch("attn_dkdv_kernel");
 }
 

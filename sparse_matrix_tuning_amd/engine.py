@@ -196,7 +196,7 @@ def _frozen_linear_forward(self, x):
 
 
 def _transposable(w: torch.Tensor) -> bool:
-    return (w.dim() == 2 and w.device.type == "cuda" and w.dtype == torch.bfloat16 and not w.requires_grad
+    return (w.dim() == 2 and w.device.type == "cuda" and w.dtype in (torch.bfloat16, torch.float16) and not w.requires_grad
             and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0)
 
 
@@ -656,7 +656,9 @@ class DenseGradBuckets:
     earlier bucket are complete, as one asynchronous all-reduce (sum) of the flat buffer.
     :meth:`finish` issues the rest (a parameter without a gradient contributes zeros on every rank),
     waits, and divides each flat buffer by the world size in place: ``p.grad`` then holds the
-    DP-averaged value. A gradient accumulated into a parameter again after its bucket was issued
+    DP-averaged value. fp16 buckets (the reference's ``--dtype fp16``: loss-scaled gradients) are
+    divided BEFORE the sum instead, as DeepSpeed's ZeRO-2 reduction does, so that ranks whose
+    gradients are each finite cannot overflow fp16 in the sum. A gradient accumulated into a parameter again after its bucket was issued
     would be lost, so that raises (as :class:`TileGradBuckets` does)."""
 
     def __init__(self, params: List[torch.Tensor], bucket_elems: int, world: int):
@@ -740,6 +742,8 @@ class DenseGradBuckets:
         for p in params:
             if id(p) not in self.seen:          # no gradient on this rank in this step: zeros
                 self._pack(p)
+        if self.flats[b].dtype == torch.float16 and self.world > 1:
+            self.flats[b].div_(float(self.world))         # average, then sum: no fp16 overflow in the sum
         self.works[b] = dist.all_reduce(self.flats[b], async_op=True)
         self.issued += 1
         dp_trace()("dense_issue", bucket=b, numel=self.flats[b].numel())
@@ -759,7 +763,8 @@ class DenseGradBuckets:
             w.wait()
             if tr.f is not None:
                 tr("dense_waited", bucket=b)
-            self.flats[b].div_(float(self.world))          # p.grad are views of it
+            if self.flats[b].dtype != torch.float16:
+                self.flats[b].div_(float(self.world))      # p.grad are views of it
         self.works, self.flats = [], []
         self.armed = False
 
@@ -829,7 +834,7 @@ class _TileGroup:
                     tdescs.append((wt, r, c, (off + i) * TILE_ELEMS))
             off += len(m.tiles)
         self.n_tdescs = len(tdescs)
-        self.tdescs = _hip.tile_descs(tdescs, self.device) if tdescs else None
+        self.tdescs = _hip.tile_descs(tdescs, self.device, self.dtype) if tdescs else None
 
     def begin_window(self) -> None:
         self.reported = [False] * len(self.modules)
@@ -949,6 +954,13 @@ class SMTEngine:
                                                        self.reduce_bucket_size if self.exchange else None))
                 if dense:
                     self.dense_groups.append((group, dense))
+        if self.loss_scaler is not None and self.tile_groups and self.wgrad_rounding == "single":
+            # fp16 overflow is detected from inf / nan in the tile gradients: the reference rounding
+            # makes every per-sample fp16 partial (and the fp16 sum) overflow to inf exactly where the
+            # reference's fp16 gradients do (smt.py:397-404); fp32 single-rounded sums would stay
+            # finite past 65504 and the loss-scale schedule would diverge from DeepSpeed's
+            raise ValueError("fp16 (dynamic loss scale) needs wgrad_rounding 'reference' (the reference's fp16 "
+                             "per-sample partials); 'single' would hide fp16 overflows from the loss scale")
         self._set_mx_unions()
         self._norm_sq = torch.zeros(1, dtype=torch.float64, device=self.device)
         # tile-gradient kernels on a stream of their own (overlap_wgrad, default on): joined before

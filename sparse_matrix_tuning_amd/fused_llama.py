@@ -5,7 +5,7 @@ The SMT step trains ``transformers`` ``LlamaForCausalLM`` (the reference loads i
 SwiGLU each run as chains of 4-8 elementwise kernels, several in fp32; on MI355X those chains are
 27 % of an SMT step (profiles/r01_bench_step_breakdown.txt). :func:`patch_llama` swaps them for
 one-pass HIP kernels (``csrc/llama_kernels.hip``, C ABI ``include/smt_model_ops.h``) wrapped in
-autograd Functions. Every intermediate bf16 rounding of the eager chain is reproduced, so results
+autograd Functions. Every intermediate 16-bit rounding of the eager chain is reproduced, so results
 match the eager model up to reduction order / exp ulps (tests/test_gpu_fused_llama.py).
 
 It also routes the decoder's attention to a gfx950 causal flash attention (forward + backward,
@@ -17,7 +17,10 @@ The causal-LM loss (transformers ``ForCausalLMLoss``: ``logits.float()`` then cr
 two row kernels over the bf16 logits (``smt_ce_fwd`` / ``smt_ce_bwd``), so the 16.8 GB fp32 logits
 copy, its log-softmax and its fp32 gradient are never materialised (tests/test_gpu_cross_entropy.py).
 
-Only bf16 CUDA tensors take the fused path; anything else raises (no silent fallback).
+The model's dtype is bf16 or, since ABI v13, fp16 (the reference's ``--dtype fp16``,
+``fine_tune.py:955-959``): every kernel is one template body for both formats, rounding where the eager
+chain rounds to the model's dtype (tests/test_gpu_fused_fp16.py). fp32 models and mixed dtypes raise
+(no silent fallback); the fp8 producer fusions stay bf16-only.
 """
 from __future__ import annotations
 
@@ -35,9 +38,18 @@ def _stream(t):
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
-def _need(t: torch.Tensor, what: str):
-    if t.device.type != "cuda" or t.dtype != torch.bfloat16:
-        raise RuntimeError(f"fused {what}: bf16 ROCm tensors only (got {t.dtype} on {t.device})")
+def _need(t: torch.Tensor, what: str, like: torch.Tensor = None):
+    """A ROCm tensor of the model's 16-bit dtype: bf16, or fp16 (the reference's --dtype fp16,
+    fine_tune.py:955-959; ABI v13) -- and, with ``like``, the same dtype as it."""
+    if t.device.type != "cuda" or t.dtype not in (torch.bfloat16, torch.float16):
+        raise RuntimeError(f"fused {what}: bf16 / fp16 ROCm tensors only (got {t.dtype} on {t.device})")
+    if like is not None and t.dtype != like.dtype:
+        raise RuntimeError(f"fused {what}: {t.dtype} beside {like.dtype} (one model dtype)")
+
+
+def _dt(t: torch.Tensor) -> int:
+    """SMT_DTYPE_* of a 16-bit tensor, the kernels' format argument."""
+    return _hip.dtype_code16(t.dtype, "fused op")
 
 
 def _tag(out, op, a2d, b2d=None, w=None, rstd=None):
@@ -61,14 +73,14 @@ class FusedRMSNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, eps):
         _need(x, "rmsnorm")
-        _need(weight, "rmsnorm")
+        _need(weight, "rmsnorm", like=x)
         x2 = _rows2d(x)
         rows, H = x2.shape
         y = torch.empty((rows, H), dtype=x.dtype, device=x.device)
         rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
         w = weight.contiguous()
         rc = _hip.load().smt_rmsnorm_fwd(x2.data_ptr(), x2.stride(0), w.data_ptr(), y.data_ptr(), y.stride(0),
-                                         rstd.data_ptr(), rows, H, float(eps), _stream(x))
+                                         rstd.data_ptr(), rows, H, float(eps), _dt(x), _stream(x))
         _hip._check(rc, "smt_rmsnorm_fwd")
         ctx.save_for_backward(x2, w, rstd)
         ctx.shape = x.shape
@@ -98,13 +110,13 @@ def _rmsnorm_bwd(x2, w, rstd, dy, need_dw: bool, dres=None):
         dr2 = _rows2d(dres)
         rc = lib.smt_rmsnorm_bwd_add_dw(dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0), w.data_ptr(),
                                         rstd.data_ptr(), dr2.data_ptr(), dr2.stride(0), dx.data_ptr(), dx.stride(0),
-                                        partial.data_ptr(), dw.data_ptr(), rows, H, _stream(x2))
+                                        partial.data_ptr(), dw.data_ptr(), rows, H, _dt(x2), _stream(x2))
         _hip._check(rc, "smt_rmsnorm_bwd_add_dw")
         return dx, dw
     rc = lib.smt_rmsnorm_bwd(dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0), w.data_ptr(),
                              rstd.data_ptr(), dx.data_ptr(), dx.stride(0),
                              None if partial is None else partial.data_ptr(),
-                             None if dw is None else dw.data_ptr(), rows, H, _stream(x2))
+                             None if dw is None else dw.data_ptr(), rows, H, _dt(x2), _stream(x2))
     _hip._check(rc, "smt_rmsnorm_bwd")
     if dres is not None:
         dx = dx + _rows2d(dres)
@@ -156,7 +168,7 @@ class FusedRMSNormResFn(torch.autograd.Function):
         dx = torch.empty_like(x2)
         rc = _hip.load().smt_rmsnorm_bwd_add(dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0), w.data_ptr(),
                                              rstd.data_ptr(), dr2.data_ptr(), dr2.stride(0), dx.data_ptr(), H, rows, H,
-                                             _stream(x2))
+                                             _dt(x2), _stream(x2))
         _hip._check(rc, "smt_rmsnorm_bwd_add")
         return dx.view(ctx.shape), None, None, None, None
 
@@ -169,7 +181,7 @@ class FusedAddRMSNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, eps, quant=False, need_y=True):
         for t, n in ((x, "x"), (residual, "residual"), (weight, "weight")):
-            _need(t, "add+rmsnorm " + n)
+            _need(t, "add+rmsnorm " + n, like=x)
         x2, r2 = _rows2d(x), _rows2d(residual)
         rows, H = x2.shape
         if quant:
@@ -189,7 +201,7 @@ class FusedAddRMSNormFn(torch.autograd.Function):
         w = weight.contiguous()
         rc = _hip.load().smt_add_rmsnorm_fwd(x2.data_ptr(), x2.stride(0), r2.data_ptr(), r2.stride(0), w.data_ptr(),
                                              h.data_ptr(), H, y.data_ptr(), H, rstd.data_ptr(), rows, H, float(eps),
-                                             _stream(x))
+                                             _dt(x), _stream(x))
         _hip._check(rc, "smt_add_rmsnorm_fwd")
         ctx.save_for_backward(h, w, rstd)
         ctx.shape = x.shape
@@ -217,7 +229,7 @@ class FusedAddRMSNormFn(torch.autograd.Function):
             dy2, dh2 = _rows2d(dy), _rows2d(dh)
             dx = torch.empty_like(h)
             rc = lib.smt_rmsnorm_bwd_add(dy2.data_ptr(), dy2.stride(0), h.data_ptr(), H, w.data_ptr(), rstd.data_ptr(),
-                                         dh2.data_ptr(), dh2.stride(0), dx.data_ptr(), H, rows, H, _stream(h))
+                                         dh2.data_ptr(), dh2.stride(0), dx.data_ptr(), H, rows, H, _dt(h), _stream(h))
             _hip._check(rc, "smt_rmsnorm_bwd_add")
             dx = dx.view(ctx.shape)
         return dx, dx, dw, None, None, None
@@ -322,7 +334,7 @@ def _rope_launch(fn_name, q, k, cos, sin, q_layout=None, k_layout=None, in_place
     dq, dk = _rope_desc(q, qo), _rope_desc(k, ko)
     lib = _hip.load()
     rc = getattr(lib, fn_name)(ctypes.byref(dq), ctypes.byref(dk), cos.data_ptr(), sin.data_ptr(), cos.stride(0),
-                               cos.stride(1), B, S, D, _stream(q))
+                               cos.stride(1), B, S, D, _dt(q), _stream(q))
     _hip._check(rc, fn_name)
     return qo, ko
 
@@ -338,7 +350,7 @@ class FusedRoPEFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, cos, sin):
         for t, n in ((q, "q"), (k, "k"), (cos, "cos"), (sin, "sin")):
-            _need(t, "rope " + n)
+            _need(t, "rope " + n, like=q)
         qo, ko = _rope_launch("smt_rope_fwd", q, k, cos, sin)
         ctx.save_for_backward(cos, sin)
         # grads go back in q/k's own layout, so the transpose/view backward of q_proj's output is free
@@ -350,9 +362,9 @@ class FusedRoPEFn(torch.autograd.Function):
         cos, sin = ctx.saved_tensors
         ql, kl = ctx.layouts
         if dqo is None:
-            dqo = torch.zeros(ql[0], dtype=torch.bfloat16, device=cos.device)
+            dqo = torch.zeros(ql[0], dtype=cos.dtype, device=cos.device)
         if dko is None:
-            dko = torch.zeros(kl[0], dtype=torch.bfloat16, device=cos.device)
+            dko = torch.zeros(kl[0], dtype=cos.dtype, device=cos.device)
         # the flash attention's joint [dq | dk | dv] gradient (FlashAttnFn joint): rotate the q / k
         # slices in place, so q_proj and k_proj receive slices of the one buffer (dgrad's joint GEMM)
         joint = (getattr(dqo, "_smt_joint", False) and getattr(dko, "_smt_joint", False)
@@ -381,7 +393,7 @@ class FusedSwiGLUFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, gate, up, quant_out=False, need_bf16_out=True):
         _need(gate, "swiglu")
-        _need(up, "swiglu")
+        _need(up, "swiglu", like=gate)
         from .fp8 import swiglu_group
         ctx.fp8 = swiglu_group(gate, up)
         g = gate.contiguous()
@@ -397,7 +409,7 @@ class FusedSwiGLUFn(torch.autograd.Function):
             h._smt_q8 = (h._version, q, sq)
             return h
         h = torch.empty_like(g)
-        rc = _hip.load().smt_swiglu_fwd(g.data_ptr(), u.data_ptr(), h.data_ptr(), g.numel(), _stream(g))
+        rc = _hip.load().smt_swiglu_fwd(g.data_ptr(), u.data_ptr(), h.data_ptr(), g.numel(), _dt(g), _stream(g))
         _hip._check(rc, "smt_swiglu_fwd")
         return _tag(h, _hip.RECOMPUTE_SWIGLU, _rows2d(g), _rows2d(u))
 
@@ -417,7 +429,7 @@ class FusedSwiGLUFn(torch.autograd.Function):
         dg = torch.empty_like(g)
         du = torch.empty_like(u)
         rc = _hip.load().smt_swiglu_bwd(g.data_ptr(), u.data_ptr(), dh.data_ptr(), dg.data_ptr(), du.data_ptr(),
-                                        g.numel(), _stream(g))
+                                        g.numel(), _dt(g), _stream(g))
         _hip._check(rc, "smt_swiglu_bwd")
         return dg, du, None, None
 
@@ -457,9 +469,9 @@ def fused_mlp_forward(self, x):
 # causal-LM cross entropy
 # ------------------------------------------------------------------------------------------------
 class FusedCrossEntropyFn(torch.autograd.Function):
-    """``F.cross_entropy(logits.float(), labels, ignore_index, reduction=sum) / denom`` over bf16
-    logits ``[N, V]`` without the fp32 copy: one pass for the row log-sum-exp, one for the bf16
-    gradient. ``denom``: fp32 device scalar (valid-label count for the mean, or num_items_in_batch)."""
+    """``F.cross_entropy(logits.float(), labels, ignore_index, reduction=sum) / denom`` over 16-bit
+    (bf16 / fp16) logits ``[N, V]`` without the fp32 copy: one pass for the row log-sum-exp, one for the
+    gradient in the logits' dtype. ``denom``: fp32 device scalar (valid-label count for the mean, or num_items_in_batch)."""
 
     @staticmethod
     def forward(ctx, logits2d, labels, ignore_index, denom):
@@ -473,7 +485,7 @@ class FusedCrossEntropyFn(torch.autograd.Function):
         lse = torch.empty(N, dtype=torch.float32, device=logits2d.device)
         rows = torch.empty(N, dtype=torch.float32, device=logits2d.device)
         rc = _hip.load().smt_ce_fwd(logits2d.data_ptr(), logits2d.stride(0), labels.data_ptr(), N, V,
-                                    int(ignore_index), lse.data_ptr(), rows.data_ptr(), _stream(logits2d))
+                                    int(ignore_index), lse.data_ptr(), rows.data_ptr(), _dt(logits2d), _stream(logits2d))
         _hip._check(rc, "smt_ce_fwd")
         ctx.save_for_backward(logits2d, labels, lse, denom)
         ctx.ignore_index = int(ignore_index)
@@ -487,7 +499,7 @@ class FusedCrossEntropyFn(torch.autograd.Function):
         dlogits = torch.empty_like(logits2d)
         rc = _hip.load().smt_ce_bwd(logits2d.data_ptr(), logits2d.stride(0), labels.data_ptr(), lse.data_ptr(),
                                     scale.data_ptr(), N, V, ctx.ignore_index, dlogits.data_ptr(), dlogits.stride(0),
-                                    _stream(logits2d))
+                                    _dt(logits2d), _stream(logits2d))
         _hip._check(rc, "smt_ce_bwd")
         return dlogits, None, None, None
 
@@ -552,9 +564,9 @@ class FusedLMHeadLossFn(torch.autograd.Function):
     before its one rounding. tests/test_gpu_cross_entropy.py checks both."""
 
     @staticmethod
-    def forward(ctx, hidden, weight, weight_t, labels, ignore_index, denom, chunk_rows):
+    def forward(ctx, hidden, weight, weight_t, labels, ignore_index, denom, chunk_rows, grad_enabled=True):
         _need(hidden, "lm head loss")
-        _need(weight, "lm head loss")
+        _need(weight, "lm head loss", like=hidden)
         h2 = _rows2d(hidden)
         N, H = h2.shape
         V = weight.shape[0]
@@ -565,10 +577,13 @@ class FusedLMHeadLossFn(torch.autograd.Function):
         labels = labels.to(device=hidden.device, dtype=torch.int64).contiguous()
         if labels.numel() != N:
             raise ValueError(f"lm head loss: {labels.numel()} labels for {N} rows")
-        need_dh = bool(ctx.needs_input_grad[0])
-        need_dw = bool(ctx.needs_input_grad[1])
+        # needs_input_grad reflects requires_grad even under torch.no_grad() (an evaluation forward with
+        # labels): the caller passes the grad mode it ran under (inside forward it is always off)
+        need_dh = bool(ctx.needs_input_grad[0]) and grad_enabled
+        need_dw = bool(ctx.needs_input_grad[1]) and grad_enabled
         lib = _hip.load()
         stream = _stream(hidden)
+        dt = _dt(hidden)
         lse = torch.empty(N, dtype=torch.float32, device=hidden.device)
         rows = torch.empty(N, dtype=torch.float32, device=hidden.device)
         dh = torch.empty((N, H), dtype=hidden.dtype, device=hidden.device) if need_dh else None
@@ -583,11 +598,11 @@ class FusedLMHeadLossFn(torch.autograd.Function):
             hc = h2[r0:r0 + c]
             torch.mm(hc, weight.t(), out=lg)
             rc = lib.smt_ce_fwd(lg.data_ptr(), lg.stride(0), labels[r0:].data_ptr(), c, V, int(ignore_index),
-                                lse[r0:].data_ptr(), rows[r0:].data_ptr(), stream)
+                                lse[r0:].data_ptr(), rows[r0:].data_ptr(), dt, stream)
             _hip._check(rc, "smt_ce_fwd")
             if need_dh or need_dw:
                 rc = lib.smt_ce_bwd(lg.data_ptr(), lg.stride(0), labels[r0:].data_ptr(), lse[r0:].data_ptr(),
-                                    scale.data_ptr(), c, V, int(ignore_index), lg.data_ptr(), lg.stride(0), stream)
+                                    scale.data_ptr(), c, V, int(ignore_index), lg.data_ptr(), lg.stride(0), dt, stream)
                 _hip._check(rc, "smt_ce_bwd")
             if need_dh:
                 torch.mm(lg, w_dgrad, out=dh[r0:r0 + c])
@@ -611,7 +626,7 @@ class FusedLMHeadLossFn(torch.autograd.Function):
         scale = dloss.float()
         gh = torch.mul(dh, scale).view(ctx.shape) if dh is not None else None
         gw = torch.mul(dw, scale) if dw is not None else None
-        return gh, gw, None, None, None, None, None
+        return gh, gw, None, None, None, None, None, None
 
 
 def fused_lm_head_loss(hidden, lm_head: nn.Linear, labels, num_items_in_batch=None, ignore_index=-100,
@@ -624,13 +639,14 @@ def fused_lm_head_loss(hidden, lm_head: nn.Linear, labels, num_items_in_batch=No
         denom = torch.as_tensor(num_items_in_batch, device=hidden.device).to(torch.float32)
     wt = getattr(lm_head.weight, "_smt_weight_t", None)
     return FusedLMHeadLossFn.apply(hidden, lm_head.weight, wt, shift, ignore_index, denom,
-                                   LM_HEAD_CHUNK_ROWS if chunk_rows is None else chunk_rows)
+                                   LM_HEAD_CHUNK_ROWS if chunk_rows is None else chunk_rows, torch.is_grad_enabled())
 
 
 def _fusable_lm_head(head) -> bool:
     w = getattr(head, "weight", None)
     return (type(head) is nn.Linear and head.bias is None and isinstance(w, torch.Tensor)
-            and w.device.type == "cuda" and w.dtype == torch.bfloat16 and getattr(w, "_smt_fp8", None) is None)
+            and w.device.type == "cuda" and w.dtype in (torch.bfloat16, torch.float16)
+            and getattr(w, "_smt_fp8", None) is None)
 
 
 def fused_causal_lm_forward(self, input_ids=None, attention_mask=None, position_ids=None, past_key_values=None,
@@ -704,7 +720,7 @@ class FlashAttnFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, scale, key_mask=None, joint=False):
         for t, n in ((q, "q"), (k, "k"), (v, "v")):
-            _need(t, "flash attention " + n)
+            _need(t, "flash attention " + n, like=q)
         B, Hq, S, D = q.shape
         Hkv = k.shape[1]
         if D != 128 or k.shape != (B, Hkv, S, D) or v.shape != k.shape or Hq % Hkv or S % 4:
@@ -717,7 +733,7 @@ class FlashAttnFn(torch.autograd.Function):
         o = torch.empty(B, S, Hq, D, dtype=q.dtype, device=q.device)
         lse = torch.empty(B, Hq, S, dtype=torch.float32, device=q.device)
         ov = o.transpose(1, 2)
-        shape = _hip.AttnShape(B, Hq, Hkv, S, float(scale), 0)
+        shape = _hip.AttnShape(B, Hq, Hkv, S, float(scale), _dt(q))
         km, km_ld = None, 0
         if key_mask is not None:
             if key_mask.S != S or key_mask.bits.shape[0] != B or key_mask.bits.device != q.device:
@@ -753,7 +769,9 @@ class FlashAttnFn(torch.autograd.Function):
             dk = torch.empty_strided(k.shape, k.stride(), dtype=k.dtype, device=k.device)
             dv = torch.empty_strided(v.shape, v.stride(), dtype=v.dtype, device=v.device)
         delta = torch.empty(B, Hq, S, dtype=torch.float32, device=q.device)
-        shape = _hip.AttnShape(B, Hq, Hkv, S, ctx.scale, 0)
+        if do.dtype != q.dtype:
+            do = do.to(q.dtype)
+        shape = _hip.AttnShape(B, Hq, Hkv, S, ctx.scale, _dt(q))
         T = _attn_tensor
         rc = _hip.load().smt_attn_bwd_kmask(ctypes.byref(T(q)), ctypes.byref(T(k)), ctypes.byref(T(v)),
                                             ctypes.byref(T(o.transpose(1, 2))), ctypes.byref(T(do.transpose(1, 2))),

@@ -319,7 +319,7 @@ class TileIndex:
         t = self._dev.get(key)
         if t is None:
             t = _hip.tile_descs([(weight_t, r, c, i * _hip.TILE_ELEMS) for i, (r, c) in enumerate(self.index_list)],
-                                weight_t.device)
+                                weight_t.device, weight_t.dtype)
             self._dev[key] = t
         return t
 
@@ -905,17 +905,21 @@ class ChannelGatherGroup:
             off += ch.padded
         self.width = off
         self.table = _hip.index_table(cols, device)
+        # (weakref to the input, its version, weakref to the joint buffer): weak references only, as
+        # ColumnBlockGroup holds its copy, so the joint buffer lives exactly as long as a member's
+        # saved view of it (until the last member's backward), whoever else keeps the input alive
+        self._cache = None
 
     def partial(self, input: torch.Tensor, x2: torch.Tensor, member: int) -> torch.Tensor:
         """Member ``member``'s ``[T, padded]`` partial input: a view of the joint gather of ``input``,
-        made by the first member that asks for it (cached on the input tensor while its version holds)."""
-        cache = input.__dict__.get("_smt_cgather")
-        if cache is None or cache[0] is not self or cache[1] != input._version:
+        made by the first member that asks for it (reused while the input and its version hold)."""
+        c = self._cache
+        joint = c[2]() if (c is not None and c[0]() is input and c[1] == input._version) else None
+        if joint is None:
             joint = _hip.column_gather(x2, self.table, self.width, self.width)
-            cache = (self, input._version, joint)
-            input.__dict__["_smt_cgather"] = cache
+            self._cache = (weakref.ref(input), input._version, weakref.ref(joint))
         off, width = self.offsets[member]
-        return cache[2][:, off:off + width]
+        return joint[:, off:off + width]
 
 
 class LinearLayer_ChannelSparsity(torch.nn.Module):

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
     out = subprocess.run(["nm", "-D", "--defined-only", _hip.lib_path()], capture_output=True, text=True).stdout
     for name in declared_functions():
         assert re.search(rf"\bT {name}$", out, re.M), name
-    assert lib.smt_abi_version() == 12
+    assert lib.smt_abi_version() == 13
 
 
 def test_library_carries_gfx950_code_object():
@@ -98,13 +98,26 @@ def test_validation_errors_without_gpu():
     assert b"whole number" in lib.smt_last_error()
     assert lib.smt_tile_wgrad_batch_seq(mods, 1, 4096, 0, tab, None, 8, 0, None, 0, None) == -1
     # selective activation policy (ABI v9): column blocks rebuilt from the producer's operands
-    assert lib.smt_colblock_recompute(7, None, 0, None, 0, None, None, 8, None, 1, None, None) == -1
+    bf16 = _hip.DTYPE_BF16
+    assert lib.smt_colblock_recompute(7, None, 0, None, 0, None, None, 8, None, 1, None, bf16, None) == -1
     assert b"unknown op" in lib.smt_model_ops_last_error()
-    assert lib.smt_colblock_recompute(0, None, 0, None, 0, None, None, 0, None, 1, None, None) == 0     # no rows
-    assert lib.smt_colblock_recompute(1, tab, 512, None, 0, None, None, 8, tab, 1, tab, None) == -1
+    assert lib.smt_colblock_recompute(0, None, 0, None, 0, None, None, 0, None, 1, None, bf16, None) == 0   # no rows
+    assert lib.smt_colblock_recompute(1, tab, 512, None, 0, None, None, 8, tab, 1, tab, bf16, None) == -1
     assert b"null up" in lib.smt_model_ops_last_error()
-    assert lib.smt_colblock_recompute(0, tab, 512, None, 0, None, None, 8, tab, 1, tab, None) == -1
+    assert lib.smt_colblock_recompute(0, tab, 512, None, 0, None, None, 8, tab, 1, tab, bf16, None) == -1
     assert b"null weight" in lib.smt_model_ops_last_error()
+    # ABI v13: the model ops and the attention take the model's 16-bit dtype; anything else is refused
+    # before a launch (fp32 = SMT_DTYPE_FP32 and an unknown code)
+    for bad in (_hip.DTYPE_FP32, 7):
+        assert lib.smt_swiglu_fwd(tab, tab, tab, 8, bad, None) == -1
+        assert b"not a 16-bit format" in lib.smt_model_ops_last_error()
+        assert lib.smt_ce_fwd(tab, 8, tab, 1, 8, -100, tab, tab, bad, None) == -1
+        assert b"not a 16-bit format" in lib.smt_model_ops_last_error()
+        shape = _hip.AttnShape(1, 8, 2, 64, 0.088, bad)
+        t = _hip.AttnTensor(tab, 0, 0, 0)
+        assert lib.smt_attn_fwd(ctypes.byref(t), ctypes.byref(t), ctypes.byref(t), ctypes.byref(t), tab,
+                                ctypes.byref(shape), None) == -1
+        assert b"not a 16-bit format" in lib.smt_attn_last_error()
     # channel path (ABI v3)
     assert lib.smt_row_gather(None, 256, 2, 256, None, 4, None, 256, None) == -1
     assert lib.smt_row_gather(None, 256, 2, 256, None, 0, None, 256, None) == 0       # no rows: no-op

@@ -249,3 +249,41 @@ def test_gloo_dense_buckets_mixed_dtypes():
     for p in procs:
         p.join(timeout=60)
     assert res == {r: True for r in range(world)}
+
+
+def _fp16_headroom_worker(rank, world, port, q):
+    """loss-scaled fp16 gradients that are finite on every rank but whose cross-rank SUM
+    exceeds 65504. The dense buckets divide fp16 buckets by the world size before the all-reduce (as
+    DeepSpeed's ZeRO-2 reduction does), so the average comes back finite and exact."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from sparse_matrix_tuning_amd.engine import DenseGradBuckets
+    p16 = torch.nn.Parameter(torch.zeros(64, dtype=torch.float16))
+    p32 = torch.nn.Parameter(torch.zeros(8))
+    buckets = DenseGradBuckets([p16, p32], bucket_elems=16, world=world)
+    buckets.arm()
+    big = 40000.0 + 64.0 * rank                       # fp16-exact, as are their halves and their mean
+    ((p16.float() * big).sum() + (p32 * (rank + 1.0)).sum()).backward()
+    buckets.finish()
+    want16 = sum(40000.0 + 64.0 * r for r in range(world)) / world      # any two sum past 65504
+    ok = p16.grad.dtype == torch.float16 and bool(torch.isfinite(p16.grad).all())
+    ok &= torch.equal(p16.grad.float(), torch.full((64,), want16))
+    ok &= torch.equal(p32.grad, torch.full((8,), sum(r + 1.0 for r in range(world)) / world))   # fp32: sum, then divide
+    buckets.remove()
+    q.put((rank, bool(ok)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_dense_fp16_buckets_average_without_overflow():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fp16_headroom_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {r: True for r in range(world)}

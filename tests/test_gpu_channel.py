@@ -465,3 +465,29 @@ def test_channel_qkv_share_one_column_gather():
             assert torch.equal(a, b)
     for a, b in zip(rows_s, rows_p):
         assert torch.equal(a, b)
+
+
+def test_channel_joint_gather_freed_after_backward_while_input_lives():
+    """the joint partial-input buffer of a ChannelGatherGroup is held by weak references
+    only, so it is freed with the members' backward even while something else keeps the q/k/v input
+    alive (here: the test itself)."""
+    import gc
+    from sparse_matrix_tuning_amd.engine import SMTFusedAdam, initialize
+    torch.manual_seed(37)
+    net = nn.Module()
+    net.attn = nn.Module()
+    for name in ("q_proj", "k_proj", "v_proj"):
+        W = nn.Parameter((torch.randn(512, 512) * 0.05).bfloat16().to(DEV), requires_grad=False)
+        setattr(net.attn, name, smt.LinearLayer_ChannelSparsity(W, index_list=[3, 77, 400]))
+    mods = [net.attn.q_proj, net.attn.k_proj, net.attn.v_proj]
+    engine, *_ = initialize(model=net, optimizer=SMTFusedAdam([m.selected_weight for m in mods], lr=1e-2), config={})
+    assert engine.channel_gather_groups == 1
+    grp = mods[0].weight._smt_cgather[0]
+    xi = torch.randn(2, 64, 512).bfloat16().to(DEV).requires_grad_(True)      # kept alive throughout
+    loss = sum(m(xi).float().pow(2).mean() for m in mods)
+    assert grp._cache is not None and grp._cache[2]() is not None           # alive while backward needs it
+    engine.backward(loss)
+    del loss
+    gc.collect()
+    assert grp._cache[0]() is xi and grp._cache[2]() is None               # the input lives, the buffer is gone
+    assert "_smt_cgather" not in xi.__dict__

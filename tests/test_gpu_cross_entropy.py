@@ -208,6 +208,8 @@ def test_lm_head_loss_never_holds_the_full_logits():
     full = B * S * V * 2
 
     def peak(fn):
+        import gc
+        gc.collect()                # garbage of earlier tests freed mid-measurement would lower the peak
         torch.cuda.synchronize()
         base = torch.cuda.memory_allocated()
         torch.cuda.reset_peak_memory_stats()
@@ -232,6 +234,28 @@ def test_lm_head_loss_without_grad_is_the_loss_only():
         lf = fl.fused_lm_head_loss(h, _Head(w.clone(), wt), labels, chunk_rows=40)
     assert not lf.requires_grad
     assert abs(lf.item() - lu.item()) <= 1e-6 * abs(lu.item())
+
+
+def test_lm_head_loss_trainable_head_under_no_grad_skips_the_gradients():
+    """``needs_input_grad`` reflects requires_grad even under ``torch.no_grad()``. With a
+    trainable head (the warm-up) an evaluation forward with labels must still compute the loss only:
+    no dlogits, no dW GEMMs, no fp32 ``[V, H]`` accumulator (here 131 MB)."""
+    B, S, H, V = 2, 64, 1024, 32000
+    h, w, wt, labels = _head_operands(B, S, H, V, seed=4, transposed=False)
+    lu, _ = _unfused_head(h, w, wt, labels)
+    head = torch.nn.Linear(H, V, bias=False, device=DEV, dtype=torch.bfloat16)
+    with torch.no_grad():
+        head.weight.copy_(w)
+    assert head.weight.requires_grad
+    torch.cuda.synchronize()
+    base = torch.cuda.memory_allocated(DEV)
+    torch.cuda.reset_peak_memory_stats(DEV)
+    with torch.no_grad():
+        lf = fl.fused_lm_head_loss(h.detach(), head, labels)
+    torch.cuda.synchronize()
+    extra = torch.cuda.max_memory_allocated(DEV) - base
+    assert not lf.requires_grad and abs(lf.item() - lu.item()) <= 1e-6 * abs(lu.item())
+    assert extra < V * H * 4 // 4, extra                     # far below the fp32 accumulator
 
 
 def test_patched_model_fuses_the_head():

@@ -187,6 +187,28 @@ def test_engine_fp16_loss_scaling_matches_restatement(window):
         assert torch.equal(ref.gather_tiles(mod.weight.detach().cpu(), mod.index_list), mod.selected_weight.detach().cpu())
 
 
+def test_fp16_engine_refuses_single_rounding():
+    """under fp16's dynamic loss scale an overflow is detected from inf / nan in the tile
+    gradients. The reference rounding overflows exactly where the reference's fp16 per-sample partials
+    do; the single fp32 rounding would not, so an fp16 engine refuses it (explicitly or by default)."""
+    net, _m = _tile_net(torch.float16)
+    opt = SMTFusedAdam([m.selected_weight for m in net.layers], lr=1e-3)
+    with pytest.raises(ValueError, match="reference"):
+        initialize(model=net, optimizer=opt, config={"fp16": {"enabled": True}, "wgrad_rounding": "single"})
+    old = smt.set_wgrad_rounding("single")
+    try:
+        net, _m = _tile_net(torch.float16, seed=9)
+        with pytest.raises(ValueError, match="reference"):
+            initialize(model=net, optimizer=SMTFusedAdam([m.selected_weight for m in net.layers], lr=1e-3),
+                       config={"fp16": {"enabled": True}})
+    finally:
+        smt.set_wgrad_rounding(old)
+    net, _m = _tile_net(torch.float16, seed=10)
+    eng, *_ = initialize(model=net, optimizer=SMTFusedAdam([m.selected_weight for m in net.layers], lr=1e-3),
+                         config={"fp16": {"enabled": True}})
+    assert eng.wgrad_rounding == "reference"
+
+
 @pytest.mark.parametrize("dtype", [torch.float16, torch.float32])
 def test_mini_llama_trains_through_the_engine_in_dtype(dtype):
     """A converted 2-layer mini-LLaMA in fp16 / fp32 through SMTEngine (the reference's --dtype with

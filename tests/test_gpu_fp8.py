@@ -237,7 +237,7 @@ def test_swiglu_bwd_quant_matches_swiglu_bwd_then_cat_quant(rows, cols):
     dh = (torch.randn(rows, cols, device=DEV) * 1e-3).bfloat16()
     dg_ref, du_ref = torch.empty_like(g), torch.empty_like(u)
     rc = _hip.load().smt_swiglu_bwd(g.data_ptr(), u.data_ptr(), dh.data_ptr(), dg_ref.data_ptr(), du_ref.data_ptr(),
-                                    g.numel(), torch.cuda.current_stream().cuda_stream)
+                                    g.numel(), _hip.DTYPE_BF16, torch.cuda.current_stream().cuda_stream)
     assert rc == 0
     q_ref, s_ref = f8.quant_rows_cat([dg_ref, du_ref])
     q, s, dg, du = f8.swiglu_bwd_quant(g, u, dh, True, True)
@@ -445,7 +445,7 @@ def test_swiglu_fwd_quant_matches_swiglu_then_quant(rows, cols):
     g = (torch.randn(rows, cols, device=DEV) * 3).bfloat16()
     u = torch.randn(rows, cols, device=DEV).bfloat16()
     h_ref = torch.empty_like(g)
-    assert _hip.load().smt_swiglu_fwd(g.data_ptr(), u.data_ptr(), h_ref.data_ptr(), g.numel(),
+    assert _hip.load().smt_swiglu_fwd(g.data_ptr(), u.data_ptr(), h_ref.data_ptr(), g.numel(), _hip.DTYPE_BF16,
                                       torch.cuda.current_stream().cuda_stream) == 0
     q_ref, s_ref = f8.quant_rows(h_ref)
     q, s, h = f8.swiglu_fwd_quant(g, u, True)
@@ -488,10 +488,10 @@ def test_rmsnorm_quant_matches_rmsnorm_then_quant(H, residual, need_y):
     if residual:
         h_ref = torch.empty_like(x)
         assert lib.smt_add_rmsnorm_fwd(x.data_ptr(), H, r.data_ptr(), H, w.data_ptr(), h_ref.data_ptr(), H,
-                                       y_ref.data_ptr(), H, rstd_ref.data_ptr(), rows, H, 1e-5, st) == 0
+                                       y_ref.data_ptr(), H, rstd_ref.data_ptr(), rows, H, 1e-5, _hip.DTYPE_BF16, st) == 0
     else:
         assert lib.smt_rmsnorm_fwd(x.data_ptr(), H, w.data_ptr(), y_ref.data_ptr(), H, rstd_ref.data_ptr(), rows, H,
-                                   1e-5, st) == 0
+                                   1e-5, _hip.DTYPE_BF16, st) == 0
     q_ref, s_ref = f8.quant_rows(y_ref)
     h, y, rstd, q, s = f8.rmsnorm_quant(x, r, w, 1e-5, need_y)
     assert torch.equal(rstd, rstd_ref)
@@ -550,7 +550,7 @@ def test_rmsnorm_bwd_add_quant_matches_bwd_then_quant(H):
     rstd = (torch.rand(rows, device=DEV) + 0.5)
     dx_ref = torch.empty_like(x)
     assert _hip.load().smt_rmsnorm_bwd_add(dy.data_ptr(), H, x.data_ptr(), H, w.data_ptr(), rstd.data_ptr(),
-                                           dres.data_ptr(), H, dx_ref.data_ptr(), H, rows, H,
+                                           dres.data_ptr(), H, dx_ref.data_ptr(), H, rows, H, _hip.DTYPE_BF16,
                                            torch.cuda.current_stream().cuda_stream) == 0
     q_ref, s_ref = f8.quant_rows(dx_ref)
     dx, q, s = f8.rmsnorm_bwd_add_quant(dy, x, w, rstd, dres)
