@@ -308,10 +308,16 @@ def test_transposed_dgrad_auto_follows_recompute_and_toggles_live():
     does. ``set_transposed_dgrad`` attaches / drops them between steps, and the AdamW epilogue's
     transposed scatter follows (W^T == W after every step)."""
     import bench
-    from sparse_matrix_tuning_amd.fused_llama import patch_llama
+    from sparse_matrix_tuning_amd.fused_llama import patch_llama, unpatch_llama
     sel_mlp = {("gate_proj", 1): [(0, 0), (2, 1)]}
     sel_att = {("q_proj", 0): [(0, 1)], ("v_proj", 3): [(0, 0)]}
+    try:
+        _transposed_auto_and_toggle(bench, patch_llama, sel_mlp, sel_att)
+    finally:
+        unpatch_llama()                     # module-level RoPE back to transformers' (later host runs)
 
+
+def _transposed_auto_and_toggle(bench, patch_llama, sel_mlp, sel_att):
     def make(ckpt):
         model = bench.build_model("mini", DEV)
         patch_llama(model)
