@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 6, session d: the last-arriver slab sum MEASURED. Kernel-variant builds of
 # the same sources (scripts/diag/build_variant.py): la1 = last arriver, chunk-major schedule; la2 = last
-# arriver, tile-major schedule; default = wgrad_dma_kernel<kOutSlabBF16> + wgrad_reduce_batch_kernel.
+# arriver, tile-major schedule (the variant code is in git history at 6eb62e0, removed after this run); default = wgrad_dma_kernel<kOutSlabBF16> + wgrad_reduce_batch_kernel.
 # Bench-shaped batched reference-rounding launches (T 32768 = 16 x 2048), alternating builds, then
 # FETCH_SIZE / WRITE_SIZE passes per build. Then the fp16 session c steps (fp16 tests, suite, dtype bench).
 set -o pipefail

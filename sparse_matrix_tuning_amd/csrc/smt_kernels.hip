@@ -564,223 +564,6 @@ void wgrad_dma_kernel(const WgradModules mods, int64_t T, int64_t chunk, int S, 
                           wm * 128, wn * 64, lane, tt.accumulate);
 }
 
-#ifndef SMT_WGRAD_LAST_ARRIVER
-#define SMT_WGRAD_LAST_ARRIVER 0
-#endif
-#if SMT_WGRAD_LAST_ARRIVER
-// ------------------------------------------------------------------------------------------------
-// EXPERIMENT (built only with -DSMT_WGRAD_LAST_ARRIVER=1 or 2 by
-// scripts/diag/build_variant.py, never in the library build): the reference rounding's per-sample
-// partials summed by each tile's LAST-ARRIVING workgroup instead of by wgrad_reduce_batch_kernel.
-// One workgroup per (tile, sample) as wgrad_dma_kernel<kOutSlabBF16> (kps == 1). Each stores its
-// bf16-rounded partial write-through (16-B sc1 buffer stores), every wave drains its stores
-// (vmcnt(0)), a workgroup barrier, then ONE lane adds 1 to the tile's agent-scope counter; the
-// workgroup whose add returns S - 1 sums the S partials in sample order with 16-B sc1 buffer loads,
-// exactly as wgrad_reduce_tile's SLAB16 branch (bit-identical tiles), and writes the tile; it also
-// resets the counter for the next launch (MI355X_MICROARCH "Valid forms", the table's first row:
-// hipMalloc'd memory, one workgroup per CU, 16-B sc1 stores and loads). Schedule: 1 = the default
-// chunk-major order (every tile's last sample in the last round); 2 = tile-major (a tile's samples
-// are consecutive ids, so tiles complete, and their last arrivers sum, round after round).
-// ------------------------------------------------------------------------------------------------
-typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-
-template <bool BATCH, int FMT, bool OUT_F32>
-__global__ __launch_bounds__(kWgThreads, 1)
-void wgrad_dma_la_kernel(const WgradModules mods, int64_t T, int64_t chunk, int S, int64_t seq, int n_tiles,
-                         const int32_t* __restrict__ tile_tab, const int32_t* __restrict__ order,
-                         uint16_t* __restrict__ slab, int* __restrict__ counters) {
-    constexpr int SLOTS = kDmaSlotsDefault, AHEAD = SLOTS - 2;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[SLOTS * kDmaSlotBytes];
-    const int total = n_tiles * S;
-    const int b = blockIdx.x;
-    const int q8 = total >> 3, r8 = total & 7, xcd = b & 7;
-    const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
-#if SMT_WGRAD_LAST_ARRIVER == 2
-    const int li = L / S, s = L - li * S;                  // tile-major
-#else
-    const int s = L / n_tiles, li = L - s * n_tiles;       // chunk-major
-#endif
-    const int tile = order != nullptr ? order[li] : li;
-    const WgradTile tt = wgrad_tile<BATCH, OUT_F32 ? 4 : 2>(mods, tile_tab, tile);
-    const int64_t ldg = tt.ldg, ldx = tt.ldx;
-    int64_t t_begin, t_end;
-    wgrad_span(s, T, chunk, seq, 1, t_begin, t_end);
-    const int rows = (t_end > t_begin) ? (int)(t_end - t_begin) : 0;
-    const int nst = (rows + kDmaBK - 1) / kDmaBK;
-    const __amdgpu_buffer_rsrc_t rg = uniform_rsrc(tt.g + t_begin * ldg, (int64_t)rows * ldg * 2);
-    const __amdgpu_buffer_rsrc_t rx = uniform_rsrc(tt.x + t_begin * ldx, (int64_t)rows * ldx * 2);
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave >> 2;
-    const int wn = wave & 3;
-    int voff_g[2], voff_x[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const int k = 4 * wave + 2 * j + (lane >> 5);
-        const int lb = (16 * (lane & 31)) ^ ((k & 3) << 6);
-        voff_g[j] = (int)(k * ldg * 2) + lb;
-        voff_x[j] = (int)(k * ldx * 2) + lb;
-    }
-    const int step_g = (int)(kDmaBK * ldg * 2), step_x = (int)(kDmaBK * ldx * 2);
-    const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(lds));
-    auto issue = [&](int st) {
-        const uint32_t slot = lds0 + (uint32_t)((st % SLOTS) * kDmaSlotBytes);
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const uint32_t row0 = (uint32_t)(4 * wave + 2 * j) * kRowBytes;
-            dma16(rg, __builtin_amdgcn_readfirstlane(slot + row0), voff_g[j] + st * step_g);
-            dma16(rx, __builtin_amdgcn_readfirstlane(slot + kDmaImg + row0), voff_x[j] + st * step_x);
-        }
-    };
-    f32x16_t acc[4][2];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-    const int gi = lane >> 4;
-    const int q = (lane >> 2) & 3;
-    const int p = lane & 3;
-    const uint32_t feat_byte = 2u * (16u * (gi & 1) + 4u * p);
-    const uint32_t krow = 8u * (gi >> 1) + q;
-#pragma unroll
-    for (int i = 0; i < AHEAD; ++i)
-        if (i < nst) issue(i);
-    for (int st = 0; st < nst; ++st) {
-        if (st + AHEAD < nst) {
-            issue(st + AHEAD);
-            wait_vm_stages(AHEAD);
-        } else {
-            wait_vm_stages(nst - 1 - st);
-        }
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        const uint8_t* A = lds + (st % SLOTS) * kDmaSlotBytes;
-        const uint8_t* B = A + kDmaImg;
-#pragma unroll
-        for (int ks = 0; ks < kDmaBK / 16; ++ks) {
-            bf16x8_t af[4], bfr[2];
-#pragma unroll
-            for (int mb = 0; mb < 4; ++mb)
-                af[mb] = tr_frag(A, ks * 16 + krow, 2u * (wm * 128 + mb * 32) + feat_byte);
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb)
-                bfr[nb] = tr_frag(B, ks * 16 + krow, 2u * (wn * 64 + nb * 32) + feat_byte);
-#pragma unroll
-            for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-                for (int nb = 0; nb < 2; ++nb)
-                    acc[mb][nb] = mfma16<FMT>(bfr[nb], af[mb], acc[mb][nb]);
-        }
-    }
-    // 1. this sample's partial rounded to the 16-bit format, stored write-through (the kOutSlabBF16
-    //    layout and lane pairing of wgrad_store_t)
-    const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(slab + (int64_t)(tile * S + s) * kTileElems, (int64_t)kTileElems * 2);
-    {
-        const int r = lane & 31, h = lane >> 5;
-#pragma unroll
-        for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb) {
-                const int m = wm * 128 + mb * 32 + r;
-                const int n0 = wn * 64 + nb * 32;
-                const f32x16_t& a = acc[mb][nb];
-#pragma unroll
-                for (int g = 0; g < 4; g += 2) {
-                    uint32_t lo0 = to16<FMT>(a[4 * g]) | ((uint32_t)to16<FMT>(a[4 * g + 1]) << 16);
-                    uint32_t lo1 = to16<FMT>(a[4 * g + 2]) | ((uint32_t)to16<FMT>(a[4 * g + 3]) << 16);
-                    uint32_t hi0 = to16<FMT>(a[4 * g + 4]) | ((uint32_t)to16<FMT>(a[4 * g + 5]) << 16);
-                    uint32_t hi1 = to16<FMT>(a[4 * g + 6]) | ((uint32_t)to16<FMT>(a[4 * g + 7]) << 16);
-                    const auto s0 = __builtin_amdgcn_permlane32_swap(lo0, hi0, false, false);
-                    const auto s1 = __builtin_amdgcn_permlane32_swap(lo1, hi1, false, false);
-                    const u32x4_t w = {s0[0], s1[0], s0[1], s1[1]};
-                    __builtin_amdgcn_raw_buffer_store_b128(w, rs, (int)((m * kTile + n0 + 8 * (g + h)) * 2), 0, 16);
-                }
-            }
-    }
-    // 2. every wave's stores drained, then one agent-scope arrival for the workgroup
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    volatile int* flag = reinterpret_cast<volatile int*>(lds);
-    if (tid == 0) {
-        const int old = __hip_atomic_fetch_add(counters + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = old == S - 1;
-        if (last) __hip_atomic_store(counters + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *flag = last;
-    }
-    __syncthreads();
-    if (*flag == 0) return;
-    // 3. the last arriver: the S partials summed in sample order in fp32 and rounded once more
-    //    (smt.py:397-404; wgrad_reduce_tile's SLAB16 branch), then the tile written / accumulated
-    const __amdgpu_buffer_rsrc_t ra = uniform_rsrc(slab + (int64_t)tile * S * kTileElems, (int64_t)S * kTileElems * 2);
-#pragma unroll 1
-    for (int k = 0; k < kTileElems / (8 * kWgThreads); ++k) {
-        const int e = (k * kWgThreads + tid) * 8;
-        float sum[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) sum[j] = 0.f;
-#pragma unroll 8
-        for (int s2 = 0; s2 < S; ++s2) {
-            const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(ra, (int)(((int64_t)s2 * kTileElems + e) * 2), 0, 16);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                sum[2 * j] += from16<FMT>(v[j] & 0xffffu);
-                sum[2 * j + 1] += from16<FMT>(v[j] >> 16);
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) sum[j] = round_op<FMT>(sum[j]);
-        if (OUT_F32) {
-            float4* dst = reinterpret_cast<float4*>(static_cast<float*>(tt.out) + e);
-            float4 a0 = make_float4(sum[0], sum[1], sum[2], sum[3]), a1 = make_float4(sum[4], sum[5], sum[6], sum[7]);
-            if (tt.accumulate) {
-                const float4 o0 = dst[0], o1 = dst[1];
-                a0.x += o0.x; a0.y += o0.y; a0.z += o0.z; a0.w += o0.w;
-                a1.x += o1.x; a1.y += o1.y; a1.z += o1.z; a1.w += o1.w;
-            }
-            dst[0] = a0;
-            dst[1] = a1;
-        } else {
-            uint4* dst = reinterpret_cast<uint4*>(static_cast<uint16_t*>(tt.out) + e);
-            if (tt.accumulate) {
-                const uint4 o = *dst;
-                const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    sum[2 * j] += from16<FMT>(ow[j] & 0xffffu);
-                    sum[2 * j + 1] += from16<FMT>(ow[j] >> 16);
-                }
-            }
-            uint32_t w[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) w[j] = (uint32_t)to16<FMT>(sum[2 * j]) | ((uint32_t)to16<FMT>(sum[2 * j + 1]) << 16);
-            *dst = make_uint4(w[0], w[1], w[2], w[3]);
-        }
-    }
-}
-
-// Per-device tile counters of the experiment (hipMalloc'd, zeroed once; each launch's last arrivers
-// reset theirs). One launch at a time per device: concurrent launches on two streams would share them.
-int* la_counters(int n_tiles, hipStream_t stream) {
-    static int* buf[64] = {};
-    static int cap[64] = {};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-    if (cap[dev] < n_tiles) {
-        const int want = n_tiles > 8192 ? n_tiles : 8192;
-        if (buf[dev]) (void)hipFree(buf[dev]);
-        buf[dev] = nullptr;
-        cap[dev] = 0;
-        if (hipMalloc(&buf[dev], (size_t)want * sizeof(int)) != hipSuccess) return nullptr;
-        if (hipMemsetAsync(buf[dev], 0, (size_t)want * sizeof(int), stream) != hipSuccess) return nullptr;
-        cap[dev] = want;
-    }
-    return buf[dev];
-}
-#endif  // SMT_WGRAD_LAST_ARRIVER
-
 // ------------------------------------------------------------------------------------------------
 // Quarter-tile variant for modules with few tiles (the HBM-bound regime: no two tiles share an
 // operand slice). A 256-thread workgroup owns one 128x128 quarter of a tile for one chunk of T rows
@@ -2427,19 +2210,6 @@ int wgrad_launch_fmt(const WgradModules& mods, int64_t T, int64_t max_ld, const 
             return check_launch("wgrad kernel");
         }
         if (slab16) {
-#if SMT_WGRAD_LAST_ARRIVER
-            if (!quarter) {                                // the experiment: no reduce launch
-                int* cnt = la_counters(n_tiles, stream);
-                if (!cnt) return fail(SMT_E_LAUNCH, "smt_tile_wgrad: last-arriver counters");
-                if (out_dtype == SMT_DTYPE_FP32)
-                    hipLaunchKernelGGL((wgrad_dma_la_kernel<BATCH, FMT, true>), grid, block, 0, stream, mods, T, sp.chunk,
-                                       sp.S, sp.seq, n_tiles, tab, order, reinterpret_cast<uint16_t*>(slab), cnt);
-                else
-                    hipLaunchKernelGGL((wgrad_dma_la_kernel<BATCH, FMT, false>), grid, block, 0, stream, mods, T, sp.chunk,
-                                       sp.S, sp.seq, n_tiles, tab, order, reinterpret_cast<uint16_t*>(slab), cnt);
-                return check_launch("wgrad_dma_la_kernel");
-            }
-#endif
             // the LDS-DMA kernels only (dma is true here)
             if (quarter) hipLaunchKernelGGL((wgrad_quarter_kernel<kOutSlabBF16, kQSlots, BATCH, FMT>), qgrid, qblock, 0,
                                             stream, mods, T, sp.chunk, sp.S, sp.seq, sp.kps, n_tiles, tab, order, slab);
