@@ -7,7 +7,7 @@ OUT=gpurun_out/${PROFILE_TAG:-r02}
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 # the kernel alone (wgrad stream joined), as bench.py measures the roofline: the averages must agree
-SHORT="--steps 3 --warmup 1 --cpu-baseline-seconds 0 --ref-mode-steps 0 --selective-steps 0 --views-steps 0 --ref-rounding-steps 0 --raw-harvest-steps 0 --no-overlap-wgrad --roofline-steps 0 ${BENCH_ARGS:-}"
+SHORT="--steps 3 --warmup 1 --cpu-baseline-seconds 0 --ref-mode-steps 0 --selective-steps 0 --views-steps 0 --ref-rounding-steps 0 --raw-harvest-steps 0 --half-resident-steps 0 --no-transposed-steps 0 --no-overlap-wgrad --roofline-steps 0 ${BENCH_ARGS:-}"
 if [ -z "$SKIP_BENCH" ]; then
   timeout -k 10 800 python3 bench.py ${BENCH_ARGS:-} --out $OUT/bench.json > $OUT/bench.log 2>&1 || exit 11
 fi

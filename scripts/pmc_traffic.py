@@ -28,7 +28,8 @@ def main(fetch_csv, write_csv, out_json):
     f, fn = per_dispatch(fetch_csv, "FETCH_SIZE")
     w, wn = per_dispatch(write_csv, "WRITE_SIZE")
     # one smt_tile_wgrad call = one main kernel (wgrad_dma / wgrad_quarter) + a wgrad_reduce when split
-    main_k = lambda n: "wgrad_dma" in n or "wgrad_quarter" in n or "wgrad_partial" in n
+    main_k = lambda n: ("wgrad_dma" in n or "wgrad_quarter" in n or "wgrad_partial" in n or "wgrad_mx_kernel" in n
+                        or "wgrad_mx_quarter" in n)
     every = lambda names: [d for d, n in names.items() if "wgrad_" in n]
     calls = lambda names: max(1, sum(1 for n in names.values() if main_k(n)))
     fetch_kib = sum(f[d] for d in every(fn)) / calls(fn)
