@@ -58,3 +58,21 @@ def test_nccl_ranks_beyond_devices_refused():
                        capture_output=True, text=True, timeout=120)
     assert r.returncode != 0
     assert "need 2 GPUs" in r.stderr
+
+
+def test_memory_vs_full_ft_reports_both_transposed_settings():
+    """the reference's one published figure (README.md:5, 67 % less GPU memory than
+    full fine-tuning) reported at the recompute policy with and without the W^T copies, tokens/s beside
+    each; the headline ``reduction`` is the engine's default at that policy (no copies)."""
+    ck = {"peak_hbm_gb": 49.02, "value": 28510.0, "median_ms_per_step": 1145.25}
+    nt = {"peak_hbm_gb": 34.26, "value": 29109.5, "median_ms_per_step": 1125.11}
+    m = bench.memory_vs_full_ft(ck, nt, 133.99, 25.77)
+    assert [p["transposed_dgrad"] for p in m["points"]] == [True, False]
+    assert m["default_transposed_dgrad"] is False and m["smt_peak_gb"] == 34.26
+    assert m["reduction"] == round(1 - 34.26 / 133.99, 4) and m["reduction"] > m["reference_claim"]["reduction"]
+    assert m["points"][0]["reduction"] == round(1 - 49.02 / 133.99, 4)
+    assert m["points"][1]["tokens_per_s"] == 29109.5
+    only = bench.memory_vs_full_ft(ck, None, 133.99, 25.77)          # --no-transposed-steps 0
+    assert len(only["points"]) == 1 and only["default_transposed_dgrad"] is True
+    off = bench.memory_vs_full_ft(nt, None, 133.99, 25.77, ckpt_copies=False)   # --transposed-dgrad off
+    assert off["points"][0]["transposed_dgrad"] is False
