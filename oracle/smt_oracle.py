@@ -129,8 +129,10 @@ def block_stat_fp64(grad: torch.Tensor, d1: int, d2: int, strategy: str) -> torc
 
 def select_submatrix(grads: Dict[Hashable, torch.Tensor], targeted_module_dims, n=660,
                      selection_strategy="no_restriction", calculate_strategy="mean_abs",
-                     stat=block_stat):
-    """smt_helper.py:40-146, including the heap loop of 111-119 and its UnboundLocalError paths."""
+                     stat=block_stat, stable=False):
+    """smt_helper.py:40-146, including the heap loop of 111-119 and its UnboundLocalError paths.
+    ``norm_dist`` calls ``torch.argsort(descending=True)`` on the CPU as smt_helper.py:86 does (ATen's
+    std::sort: equal values in its own order); ``stable=True`` only shows where index order differs."""
     block_means = {}
     for key, grad in grads.items():
         d1 = int(targeted_module_dims[key[0]][0] / Block_dimension)
@@ -144,7 +146,7 @@ def select_submatrix(grads: Dict[Hashable, torch.Tensor], targeted_module_dims, 
         if not block_means:
             raise UnboundLocalError("indices")
         for key, block_mean in block_means.items():
-            indices = torch.argsort(block_mean.view(-1), descending=True, stable=True)
+            indices = torch.argsort(block_mean.view(-1), descending=True, stable=stable)
             for idx in indices[:n]:
                 ranked_blocks[key].append(((idx // block_mean.shape[1]).item(), (idx % block_mean.shape[1]).item()))
         return ranked_blocks
@@ -183,7 +185,7 @@ def select_channel(activation: Dict[Hashable, torch.Tensor], n=660, selection_st
     if selection_strategy == "norm_dist":
         if not column_means:
             raise UnboundLocalError("indices")          # `del indices` with nothing bound (smt_helper.py:194)
-        return {key: torch.argsort(cm, descending=True, stable=True)[:n].tolist() for key, cm in column_means.items()}
+        return {key: torch.argsort(cm, descending=True)[:n].tolist() for key, cm in column_means.items()}
     top_columns = []
     for key, column_mean in column_means.items():
         for idx in range(column_mean.shape[0]):
@@ -286,7 +288,7 @@ def channel_stat_fp64(act: torch.Tensor, strategy: str) -> torch.Tensor:
 def rank_channels(column_means: Dict[Hashable, torch.Tensor], n: int, selection_strategy="no_restriction"):
     """smt_helper.py:186-230 (the heap / argsort half of select_channel) on given fp32 statistics."""
     if selection_strategy == "norm_dist":
-        return {key: torch.argsort(cm, descending=True, stable=True)[:n].tolist() for key, cm in column_means.items()}
+        return {key: torch.argsort(cm, descending=True)[:n].tolist() for key, cm in column_means.items()}
     top = []
     for key, cm in column_means.items():
         for idx in range(cm.shape[0]):

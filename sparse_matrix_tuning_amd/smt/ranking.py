@@ -30,7 +30,6 @@ order-independent worst-case bound.
 from __future__ import annotations
 
 import heapq
-import math
 import time
 from collections import defaultdict
 from typing import Callable, Dict, Hashable, List, Optional, Sequence
@@ -311,11 +310,174 @@ def top_n(entries: Sequence[KeyScores], n: int) -> List[tuple]:
     return result
 
 
+# ------------------------------------------------------------------------------------------------
+# ATen's CPU argsort(descending=True), ties included
+# ------------------------------------------------------------------------------------------------
+# The reference's norm_dist ranks with torch.argsort(v, descending=True) on CPU tensors (the
+# harvests are .cpu(), fine_tune.py:733, 657; smt_helper.py:86, 191). With stable=False, ATen's CPU
+# sort kernel (aten/src/ATen/native/cpu/SortingKernel.cpp, torch 2.x) runs std::sort over
+# (value, index) pairs with KeyValueCompDesc: lhs before rhs iff lhs is NaN and rhs is not, or
+# lhs > rhs. std::sort is libstdc++'s introsort (bits/stl_algo.h): median-of-three pivot moved to
+# the front, unguarded Hoare partition, recursion on the right part, heap sort past 2*floor(log2 n)
+# levels, then one insertion sort over the 16-element runs. That algorithm is deterministic, so
+# equal values come out in one definite order, which is restated below and pinned against this
+# host's torch.argsort and a g++ std::sort / std::partial_sort (tests/test_aten_argsort.py).
+_S_THRESHOLD = 16
+
+
+def _before(a, b) -> bool:
+    x, y = a[0], b[0]
+    return (x != x and y == y) or x > y
+
+
+def _unguarded_linear_insert(a: list, last: int) -> None:
+    val = a[last]
+    nxt = last - 1
+    while _before(val, a[nxt]):
+        a[last] = a[nxt]
+        last = nxt
+        nxt -= 1
+    a[last] = val
+
+
+def _insertion_sort(a: list, first: int, last: int) -> None:
+    for i in range(first + 1, last):
+        if _before(a[i], a[first]):
+            val = a[i]
+            a[first + 1:i + 1] = a[first:i]
+            a[first] = val
+        else:
+            _unguarded_linear_insert(a, i)
+
+
+def _push_heap(a: list, first: int, hole: int, top: int, value) -> None:
+    while hole > top:
+        parent = (hole - 1) // 2
+        if not _before(a[first + parent], value):
+            break
+        a[first + hole] = a[first + parent]
+        hole = parent
+    a[first + hole] = value
+
+
+def _adjust_heap(a: list, first: int, hole: int, length: int, value) -> None:
+    top = second = hole
+    while second < (length - 1) // 2:
+        second = 2 * (second + 1)
+        if _before(a[first + second], a[first + second - 1]):
+            second -= 1
+        a[first + hole] = a[first + second]
+        hole = second
+    if (length & 1) == 0 and second == (length - 2) // 2:
+        second = 2 * (second + 1)
+        a[first + hole] = a[first + second - 1]
+        hole = second - 1
+    _push_heap(a, first, hole, top, value)
+
+
+def _pop_heap(a: list, first: int, last: int, result: int) -> None:
+    value = a[result]
+    a[result] = a[first]
+    _adjust_heap(a, first, 0, last - first, value)
+
+
+def _partial_sort(a: list, first: int, middle: int, last: int) -> None:
+    length = middle - first
+    if length >= 2:                                      # make_heap
+        parent = (length - 2) // 2
+        while True:
+            _adjust_heap(a, first, parent, length, a[first + parent])
+            if parent == 0:
+                break
+            parent -= 1
+    for i in range(middle, last):                        # heap_select
+        if _before(a[i], a[first]):
+            _pop_heap(a, first, middle, i)
+    while middle - first > 1:                            # sort_heap
+        middle -= 1
+        _pop_heap(a, first, middle, middle)
+
+
+def _move_median_to_first(a: list, result: int, x: int, y: int, z: int) -> None:
+    if _before(a[x], a[y]):
+        if _before(a[y], a[z]):
+            m = y
+        elif _before(a[x], a[z]):
+            m = z
+        else:
+            m = x
+    elif _before(a[x], a[z]):
+        m = x
+    elif _before(a[y], a[z]):
+        m = z
+    else:
+        m = y
+    a[result], a[m] = a[m], a[result]
+
+
+def _introsort_loop(a: list, first: int, last: int, depth: int) -> None:
+    while last - first > _S_THRESHOLD:
+        if depth == 0:
+            _partial_sort(a, first, last, last)
+            return
+        depth -= 1
+        _move_median_to_first(a, first, first + 1, first + (last - first) // 2, last - 1)
+        lo, hi = first + 1, last                         # unguarded partition around a[first]
+        while True:
+            while _before(a[lo], a[first]):
+                lo += 1
+            hi -= 1
+            while _before(a[first], a[hi]):
+                hi -= 1
+            if not lo < hi:
+                break
+            a[lo], a[hi] = a[hi], a[lo]
+            lo += 1
+        _introsort_loop(a, lo, last, depth)
+        last = lo
+
+
+def aten_argsort_desc(values, heap_only: bool = False) -> np.ndarray:
+    """``torch.argsort(torch.tensor(values, dtype=float32), descending=True)`` as ATen's CPU kernel
+    computes it (std::sort, see above), equal values included. ``heap_only``: std::partial_sort over
+    the whole range instead (the introsort's depth-limit fallback, for the tests)."""
+    a = [(v, i) for i, v in enumerate(np.asarray(values, dtype=np.float32).reshape(-1).tolist())]
+    n = len(a)
+    if heap_only:
+        _partial_sort(a, 0, n, n)
+    elif n > 1:
+        _introsort_loop(a, 0, n, 2 * (n.bit_length() - 1))
+        if n > _S_THRESHOLD:
+            _insertion_sort(a, 0, _S_THRESHOLD)
+            for i in range(_S_THRESHOLD, n):
+                _unguarded_linear_insert(a, i)
+        else:
+            _insertion_sort(a, 0, n)
+    return np.fromiter((i for _v, i in a), dtype=np.int64, count=n)
+
+
+def _ties_decide(e: KeyScores, top: np.ndarray, rest: np.ndarray) -> bool:
+    """Do two EXACT values, one of them in ``top``, compare equal? Then ``order[:n]`` depends on the
+    sort's tie order. A tie that involves an inexact value shows as overlapping intervals instead,
+    which the caller re-scores; once everything it depends on is decided, no such tie is left."""
+    t = top[e.exact[top]]
+    if not t.size:
+        return False
+    v = e.nominal[t]
+    if np.unique(v).size < v.size:
+        return True
+    r = rest[e.exact[rest]]
+    return bool(r.size and np.isin(e.nominal[r], v).any())
+
+
 def top_n_per_key(entries: Sequence[KeyScores], n: int) -> List[List[int]]:
-    """``norm_dist``: per key the ``n`` best flat indices by descending value, ties in index order
-    (the reference's ``argsort(descending=True)`` leaves tie order unspecified; smt_helper.py:86-94)."""
+    """``norm_dist``: per key ``torch.argsort(values, descending=True)[:n]`` (smt_helper.py:86-94,
+    191-195): the order is decided from the intervals; where equal values make the result depend on
+    the sort's tie order, the key is re-scored exactly and ATen's CPU sort restated
+    (:func:`aten_argsort_desc`) gives it."""
     t0 = time.perf_counter()
     report = _new_report("norm_dist", n, entries)
+    report["tie_sorted_keys"] = []
     out = []
     for e in entries:
         for _ in range(e.size + 3):
@@ -327,10 +489,21 @@ def top_n_per_key(entries: Sequence[KeyScores], n: int) -> List[List[int]]:
                     e.make_exact()
                     report["rescored_keys"].append(e.key)
                     continue
-                order = np.asarray(sorted(idx.tolist(), key=lambda i: -val[i] if val[i] == val[i] else -math.inf))
-            else:
-                order = np.lexsort((idx, -val))
+                order = aten_argsort_desc(e.nominal)
+                out.append([int(i) for i in order[:n]])
+                break
+            order = np.lexsort((idx, -val))
             top, rest = order[:n], order[n:]        # Python slicing, as indices[:n] of smt_helper.py:93
+            if _ties_decide(e, top, rest):
+                # equal values at stake: ATen's std::sort order over the key's exact values
+                if not e.all_exact:
+                    before = int(e.exact.sum())
+                    e.make_exact()
+                    report["rescored_keys"].append(e.key)
+                    report["rescored_elements"] += int(e.exact.sum()) - before
+                report["tie_sorted_keys"].append(e.key)
+                out.append([int(i) for i in aten_argsort_desc(e.nominal)[:n]])
+                break
             if e.all_exact or not top.size:
                 out.append([int(i) for i in top])
                 break

@@ -141,6 +141,19 @@ def test_channel_selection_bit_exact_vs_golden():
         assert got == case["expected"], (case["pool"], case["strategy"], case["n"], case["selection_strategy"])
 
 
+def test_channel_norm_dist_ties_follow_aten_sort_on_gpu():
+    """Equal channel statistics under norm_dist come out in the order of ATen's unstable CPU argsort
+    (smt_helper.py:191; tests/test_aten_argsort.py), from the GPU scan's intervals and the re-score."""
+    from tests.golden.make_golden import digest, tie_channel_inputs
+    spec = json.load(open(os.path.join(GOLDEN, "norm_dist_ties_expected.json")))["channel"]
+    act = tie_channel_inputs()
+    assert digest(act) == spec["inputs_sha256"]
+    for case in spec["cases"]:
+        out = smt_helper.select_channel_based_on_activation(act, case["n"], selection_strategy="norm_dist",
+                                                            calculate_strategy=case["strategy"])
+        assert [[k[0], k[1], list(v)] for k, v in out.items()] == case["expected"], (case["strategy"], case["n"])
+
+
 def test_channel_selection_kat2_on_gpu():
     """SURVEY §4 KAT-2 through the product (reference-format CPU fp32 dict)."""
     act = {

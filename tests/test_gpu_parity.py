@@ -115,6 +115,25 @@ def test_selection_bit_exact_vs_golden():
         assert got == case["expected"], (case["pool"], case["strategy"], case["n"], case["selection_strategy"])
 
 
+def test_norm_dist_ties_follow_aten_sort_on_gpu():
+    """Runs of equal block statistics (copied blocks, all-zero blocks) under norm_dist: the product's
+    order is the reference's unstable CPU argsort (smt_helper.py:86), not index order
+    (tests/test_aten_argsort.py); at least 10 of the fixture's cases differ from index order."""
+    from sparse_matrix_tuning_amd.smt import ranking
+    from tests.golden.make_golden import digest, tie_inputs
+    spec = json.load(open(os.path.join(GOLDEN, "norm_dist_ties_expected.json")))
+    grads = tie_inputs()
+    assert digest(grads) == spec["inputs_sha256"]
+    dev = {k: v.to(DEV) for k, v in grads.items()}
+    tie_sorted = 0
+    for case in spec["cases"]:
+        out = smt_helper.select_submatrix_based_on_grads(dev, spec["dims"], case["n"], selection_strategy="norm_dist",
+                                                         calculate_strategy=case["strategy"])
+        assert [[k[0], k[1], [list(t) for t in v]] for k, v in out.items()] == case["expected"], (case["strategy"], case["n"])
+        tie_sorted += bool(ranking.LAST_REPORT["tie_sorted_keys"])
+    assert tie_sorted >= 10
+
+
 def test_selection_kat1_on_gpu():
     grads = {('gate_proj', 1): torch.zeros(11008, 4096), ('up_proj', 1): torch.zeros(11008, 4096),
              ('down_proj', 2): torch.ones(4096, 11008)}
