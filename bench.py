@@ -561,7 +561,7 @@ def pmc_traffic(args, rounding):
     if args.wgrad_batch_tiles <= 0:
         cands = ("r02_wgrad_pmc.json", "r01_wgrad_pmc.json")
     elif rounding == "reference":             # the per-sample slabs of smt_tile_wgrad_batch_seq
-        cands = ("r05_end_wgrad_pmc.json", "r05_k_wgrad_pmc.json", "r05_p_wgrad_pmc.json", "r04_s_wgrad_pmc.json", "r04_e_wgrad_pmc.json", "r04_final_wgrad_pmc.json")
+        cands = ("r06_g_wgrad_pmc.json", "r05_end_wgrad_pmc.json", "r05_k_wgrad_pmc.json", "r05_p_wgrad_pmc.json", "r04_s_wgrad_pmc.json", "r04_e_wgrad_pmc.json", "r04_final_wgrad_pmc.json")
     else:
         cands = ("r03_final_wgrad_pmc.json", "r02_final_wgrad_pmc.json", "r02_wgrad_batch_pmc.json")
     for cand in cands:
