@@ -1,6 +1,7 @@
 """The SMT step of LLaMA-3-8B in the reference's other --dtype (fine_tune.py:955-959): fp16 under
 DeepSpeed's dynamic loss scale or fp32, through SMTEngine with DeepSpeed's config for the dtype
-(deepspeed_helpers.py:53-61), every layer recomputed (fine_tune.py:192). bf16 and fp16 models run the
+(deepspeed_helpers.py:53-61), every layer recomputed (fine_tune.py:192; ``--resident`` keeps them, the
+headline's policy). bf16 and fp16 models run the
 fused LLaMA kernels, smt_flash and the fused LM head + loss (ABI v13: one template body per 16-bit
 format; ``--eager-ops`` keeps transformers' own ops), fp32 models transformers' ops; the SMT modules,
 the tile weight gradients, the fused AdamW and the loss scale are this build's. 436 + 436 tiles drawn at random (seeded) over the
@@ -48,6 +49,8 @@ def main():
     ap.add_argument("--seq", type=int, default=2048)
     ap.add_argument("--tiles", type=int, default=436, help="per pool (attention, MLP)")
     ap.add_argument("--eager-ops", action="store_true", help="transformers' own ops even for bf16 / fp16")
+    ap.add_argument("--resident", action="store_true",
+                    help="keep every layer's activations (the headline's policy) instead of recomputing them")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -63,8 +66,9 @@ def main():
     sel_mlp = random_selection(dims, L, args.tiles, ("gate_proj", "up_proj", "down_proj"), 2)
     smt.freeze_unselected_matrix_layer(model, sel_mlp, sel_att)
     smt.convert_linear_layer_to_matrix_sparsity(model, sel_mlp, sel_att)
-    model.gradient_checkpointing_enable()
-    trainer.make_gradient_checkpointing_compatible(model)
+    if not args.resident:
+        model.gradient_checkpointing_enable()
+        trainer.make_gradient_checkpointing_compatible(model)
     model.train()
     ds = {"gradient_clipping": 1.0, "train_micro_batch_size_per_gpu": args.batch, "train_batch_size": args.batch}
     if args.dtype == "fp16":
@@ -102,7 +106,7 @@ def main():
            "median_ms_per_step": round(med * 1e3, 2), "median_tokens_per_s": round(tok / med, 1),
            "peak_hbm_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 2), "dtype": args.dtype,
            "tiles": n_tiles, "tile_param_dtype": str(engine.tile_groups[0].param.dtype),
-           "activations": "recomputed per layer (fine_tune.py:192)",
+           "activations": "resident" if args.resident else "recomputed per layer (fine_tune.py:192)",
            "ops": "fused LLaMA kernels + smt_flash + fused LM head/loss" if fused else "transformers' own ops",
            "transposed_copies_gb": round(engine.transposed_bytes / 1e9, 2),
            "skipped_steps": engine.skipped_steps,
