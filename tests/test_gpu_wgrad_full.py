@@ -254,3 +254,62 @@ def test_reference_rounding_rejects_partial_samples():
     out = torch.empty(256, 256, dtype=torch.bfloat16, device=DEV)
     with pytest.raises(ValueError):
         _hip.tile_wgrad(go, x, table, out, seq_len=3000)
+
+
+@pytest.mark.parametrize("seq,n", [(100, 3), (100, 20), (1377, 3), (1377, 20), (33, 64)])
+def test_ragged_sequence_lengths(seq, n):
+    """Batches padded to a length that is not a multiple of the 32-row LDS-DMA stage (the collator
+    pads to the batch's longest sample, helper.py:194-204): every sample's span starts off a stage
+    boundary. Quarter-tile (3 tiles) and full-tile (20, 64) kernels, reference rounding vs
+    oracle.linearz_tile_grads (<= 1e-3), and the single rounding (ragged T) vs fp64 truth."""
+    Bo = 3
+    out_f, in_f = 2048, 2048
+    To = Bo * seq
+    g = torch.Generator(device=DEV).manual_seed(seq + n)
+    x = torch.randn(To, in_f, generator=g, device=DEV).bfloat16()
+    go = (torch.randn(To, out_f, generator=g, device=DEV) * 1e-2).bfloat16()
+    tiles = _tiles(out_f, in_f, n, seed=seq * 7 + n)
+    table = _hip.tile_table(tiles, DEV)
+    order = _hip.order_table(tiles, DEV)
+    ref_out = torch.empty(n * 256, 256, dtype=torch.bfloat16, device=DEV)
+    _hip.tile_wgrad(go, x, table, ref_out, order=order, seq_len=seq)
+    single = torch.empty(n * 256, 256, dtype=torch.float32, device=DEV)
+    _hip.tile_wgrad(go, x, table, single, order=order)
+    torch.cuda.synchronize()
+    pick = sorted({0, n // 2, n - 1})
+    sel = [tiles[i] for i in pick]
+    gs = torch.cat([go[:, r * 256:(r + 1) * 256] for r, _c in sel], 1).view(Bo, seq, -1).cpu()
+    xs = torch.cat([x[:, c * 256:(c + 1) * 256] for _r, c in sel], 1).view(Bo, seq, -1).cpu()
+    want = ref.linearz_tile_grads(gs, xs, [(k, k) for k in range(len(sel))])
+    for k, i in enumerate(pick):
+        r, c = tiles[i]
+        assert _rel(ref_out[i * 256:(i + 1) * 256].cpu(), want[k * 256:(k + 1) * 256]) <= 1e-3, (tiles[i], "reference")
+        assert _rel(single[i * 256:(i + 1) * 256], _truth(go, x, r, c)) <= 1e-5, (tiles[i], "single")
+
+
+def test_register_staged_kernel_past_32bit_buffer_offsets():
+    """A split whose rows span >= 2 GiB of an operand (chunk * ld * 2 >= 2^31: here 80000 rows of
+    the 14336-wide down_proj input in one split) cannot use the LDS-DMA kernels' 32-bit buffer
+    offsets; the launch takes the register-staged kernel, which addresses with 64 bits. Single
+    rounding (fp32 out) vs fp64 truth <= 1e-5, reference rounding (one 80000-row sample, bf16 out)
+    vs oracle.linearz_tile_grads <= 1e-3."""
+    To, (out_f, in_f), n = 80000, SHAPES["down_proj"], 436
+    g = torch.Generator(device=DEV).manual_seed(80)
+    x = torch.randn(To, in_f, generator=g, device=DEV).bfloat16()
+    go = (torch.randn(To, out_f, generator=g, device=DEV) * 1e-2).bfloat16()
+    tiles = _tiles(out_f, in_f, n, seed=81)
+    table, order = _hip.tile_table(tiles, DEV), _hip.order_table(tiles, DEV)
+    single = torch.empty(n * 256, 256, dtype=torch.float32, device=DEV)
+    _hip.tile_wgrad(go, x, table, single, order=order)
+    refr = torch.empty(n * 256, 256, dtype=torch.bfloat16, device=DEV)
+    _hip.tile_wgrad(go, x, table, refr, order=order, seq_len=To)
+    torch.cuda.synchronize()
+    pick = [0, n // 2, n - 1]
+    sel = [tiles[i] for i in pick]
+    gs = torch.cat([go[:, r * 256:(r + 1) * 256] for r, _c in sel], 1).view(1, To, -1).cpu()
+    xs = torch.cat([x[:, c * 256:(c + 1) * 256] for _r, c in sel], 1).view(1, To, -1).cpu()
+    want = ref.linearz_tile_grads(gs, xs, [(k, k) for k in range(len(sel))])
+    for k, i in enumerate(pick):
+        r, c = tiles[i]
+        assert _rel(single[i * 256:(i + 1) * 256], _truth(go, x, r, c)) <= 1e-5, tiles[i]
+        assert _rel(refr[i * 256:(i + 1) * 256].cpu(), want[k * 256:(k + 1) * 256]) <= 1e-3, tiles[i]
