@@ -177,3 +177,21 @@ def test_norm_dist_tie_goldens_on_host():
                         "L1": lambda: torch.norm(s, p=1, dim=0), "L2": lambda: torch.norm(s, p=2, dim=0)}[case["strategy"]]().numpy()
         out = smt_helper.rank_channels(stats, case["n"], "norm_dist")
         assert [[k[0], k[1], list(v)] for k, v in out.items()] == case["expected"], case
+
+
+def test_near_tie_channel_fixture_norm_dist_on_host():
+    """The near-tie channel fixture holds an exact tie under norm_dist (two channels of one key with
+    equal ATen means; ATen's sort puts the larger index first): the oracle's unstable argsort and
+    the product's host ranking on ATen's statistics both give the committed order."""
+    from tests.golden.make_golden import near_tie_channel_inputs
+    spec = json.load(open(os.path.join(GOLDEN, "near_tie_expected.json")))["channel"]
+    act = near_tie_channel_inputs()
+    cases = [c for c in spec["cases"] if c["selection_strategy"] == "norm_dist"]
+    assert cases
+    for case in cases:
+        out = ref.select_channel(act, case["n"], selection_strategy="norm_dist", calculate_strategy=case["strategy"])
+        assert [[k[0], k[1], list(v)] for k, v in out.items()] == case["expected"], (case["strategy"], case["n"])
+        if case["strategy"] in ("mean_abs", "abs_mean"):
+            stats = {k: torch.mean(torch.sum(a.abs(), dim=0).abs(), dim=0).numpy() for k, a in act.items()}
+            got = smt_helper.rank_channels(stats, case["n"], "norm_dist")
+            assert [[k[0], k[1], list(v)] for k, v in got.items()] == case["expected"], (case["strategy"], case["n"])
